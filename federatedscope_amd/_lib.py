@@ -1,0 +1,87 @@
+"""ctypes binding of libfsagg.so (the C ABI declared in include/fsagg.h).
+
+The HIP library is the only compute path of this package: importing it on a
+machine where the library is missing raises immediately — there is no CPU or
+PyTorch fallback anywhere in ``federatedscope_amd``.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('FSAGG_LIB',
+                          os.path.join(_HERE, 'lib', 'libfsagg.so'))
+
+FSAGG_F32, FSAGG_F16, FSAGG_BF16, FSAGG_F64, FSAGG_I64 = range(5)
+
+_c_p = ctypes.c_void_p
+_c_i = ctypes.c_int
+_c_i64 = ctypes.c_int64
+_c_f = ctypes.c_float
+_c_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/fsagg.h one for one
+SIGNATURES = {
+    'fsagg_version': (_c_i, []),
+    'fsagg_last_error': (ctypes.c_char_p, []),
+    'fsagg_weighted_sum_f32': (_c_i, [_c_p, _c_p, _c_p, _c_i, _c_i64, _c_p,
+                                      _c_p, _c_p]),
+    'fsagg_weighted_sum_typed': (_c_i, [_c_p, _c_i, _c_p, _c_i, _c_i64, _c_p,
+                                        _c_p]),
+    'fsagg_online_inc_f32': (_c_i, [_c_p, _c_p, _c_f, _c_f, _c_f, _c_i64,
+                                    _c_p]),
+    'fsagg_add_f32': (_c_i, [_c_p, _c_p, _c_p, _c_i64, _c_p]),
+    'fsagg_coord_median_f32': (_c_i, [_c_p, _c_i, _c_i64, _c_p, _c_p, _c_p]),
+    'fsagg_trimmed_mean_f32': (_c_i, [_c_p, _c_i, _c_i64, _c_i, _c_f, _c_p,
+                                      _c_p, _c_p]),
+    'fsagg_pairdist_workspace_bytes': (_c_sz, [_c_i, _c_i64, _c_i]),
+    'fsagg_pairdist_f32': (_c_i, [_c_p, _c_i, _c_i64, _c_p, _c_i, _c_p, _c_p,
+                                  _c_sz, _c_p]),
+    'fsagg_rownorm_workspace_bytes': (_c_sz, [_c_i, _c_i64]),
+    'fsagg_row_sqnorm_f32': (_c_i, [_c_p, _c_i, _c_i64, _c_p, _c_p, _c_sz,
+                                    _c_p]),
+    'fsagg_fill_uniform_f32': (_c_i, [_c_p, _c_i, _c_i64, _c_i64,
+                                      ctypes.c_uint64, _c_i64, _c_p]),
+}
+
+_lib = None
+
+
+class FsaggError(RuntimeError):
+    pass
+
+
+def load(path=None):
+    """Load libfsagg.so (once).  Raises FsaggError if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise FsaggError(
+            'libfsagg.so not found at %s — build it with '
+            '`python -c "import __graft_entry__ as g; g.build()"` '
+            '(make -C federatedscope_amd/csrc).  federatedscope_amd has no '
+            'CPU fallback.' % p)
+    # torch first: its bundled libamdhip64.so.7 then satisfies our NEEDED
+    # entry, so the library and torch share one HIP runtime (one set of
+    # streams / device pointers).
+    import torch  # noqa: F401
+    lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what=''):
+    if rc != 0:
+        msg = load().fsagg_last_error()
+        raise FsaggError('%s failed (%d): %s' %
+                         (what, rc, msg.decode() if msg else ''))
+    return rc
+
+
+def exported_symbols():
+    return list(SIGNATURES.keys())

@@ -1,0 +1,198 @@
+"""Device plumbing shared by the drop-in aggregators.
+
+Every aggregator in this package runs its reduction on an MI355X through
+libfsagg (federatedscope_amd/ops.py).  This mixin owns:
+
+* the compute device (a GPU — there is no CPU path: without one the
+  aggregators raise instead of silently computing elsewhere);
+* cached bucket layouts and the persistent device client stack (reused
+  across rounds; sized for HBM, grown on demand);
+* the general weighted-average driver that mirrors
+  ClientsAvgAggregator._para_weighted_avg (clients_avg_aggregator.py:60-100)
+  including its per-key "skip missing client" rule and dtype rules;
+* conversion of the flat device result back to a state_dict on the device
+  the client updates came from (host dicts in → host dicts out, as the
+  reference's CPU aggregators return).
+"""
+from collections import OrderedDict
+
+import torch
+
+from ... import ops
+from ...layout import BucketLayout, ClientStack
+from ..auxiliaries.utils import param2tensor
+
+
+def compute_device(device=None):
+    if not torch.cuda.is_available():
+        raise RuntimeError(
+            'federatedscope_amd aggregators run on an AMD GPU (libfsagg); no '
+            'GPU is visible and there is no CPU fallback')
+    if device is not None:
+        d = torch.device(device)
+        if d.type == 'cuda':
+            return torch.device('cuda', d.index if d.index is not None else
+                                torch.cuda.current_device())
+    return torch.device('cuda', torch.cuda.current_device())
+
+
+def fedavg_weights(sizes, ignore_weight=False, use_ss=False):
+    """The reference's per-client weights, as Python doubles
+    (clients_avg_aggregator.py:64-84)."""
+    total = 0
+    for s in sizes:
+        total += s
+    n = len(sizes)
+    if ignore_weight:
+        return [1.0 / n] * n
+    if use_ss:
+        return [1.0] * n
+    return [s / total for s in sizes]
+
+
+def _first_device(model):
+    for v in model.values():
+        if isinstance(v, torch.Tensor):
+            return v.device
+    return torch.device('cpu')
+
+
+class DeviceEngine:
+    """Mixin: call ``_engine_init(device)`` from the constructor."""
+
+    def _engine_init(self, device=None):
+        self._dev_req = device
+        self._dev = None
+        self._layouts = {}
+        self._stacks = {}
+
+    @property
+    def compute_device(self):
+        if self._dev is None:
+            self._dev = compute_device(self._dev_req)
+        return self._dev
+
+    # -- layouts and stacks -------------------------------------------------
+    def _layout(self, template, as_float=False):
+        if as_float:
+            template = OrderedDict(
+                (k, _as_float_proto(v)) for k, v in template.items())
+        sig = tuple((k, tuple(param2tensor(v).shape), param2tensor(v).dtype)
+                    for k, v in template.items())
+        lay = self._layouts.get(sig)
+        if lay is None:
+            lay = BucketLayout(template)
+            self._layouts[sig] = lay
+        return lay
+
+    def _stack(self, layout, models, as_float=False):
+        """Pack the fp32 keys of each client dict into a device row."""
+        key = layout.signature()
+        st = self._stacks.get(key)
+        if st is None or st.capacity < len(models):
+            st = ClientStack(layout, max(len(models), 1), self.compute_device)
+            st.slab.zero_()
+            self._stacks[key] = st
+        for i, m in enumerate(models):
+            if as_float:
+                m = OrderedDict((k, param2tensor(v).float())
+                                for k, v in m.items())
+            st.load(i, m)
+        return st
+
+    def _bucket(self, layout, model, as_float=False):
+        """A single model (e.g. the server's init model) as a device bucket;
+        every layout key must be present."""
+        flat = torch.zeros(layout.numel, dtype=torch.float32,
+                           device=self.compute_device)
+        src = OrderedDict()
+        for k in layout.keys:
+            if k not in model:
+                raise KeyError(k)
+            v = param2tensor(model[k])
+            src[k] = v.float() if as_float else v
+        layout.pack_device(src, flat)
+        return flat
+
+    # -- result emission -----------------------------------------------------
+    @staticmethod
+    def _emit(layout, flat, keys, out_device, extra=None):
+        """Views of ``flat`` per key, on ``out_device`` (one copy)."""
+        if out_device.type != 'cuda' or out_device != flat.device:
+            flat = flat.to(out_device)
+        views = layout.unpack(flat)
+        out = OrderedDict()
+        for k in keys:
+            if k in views:
+                out[k] = views[k]
+            elif extra is not None and k in extra:
+                out[k] = extra[k].to(out_device)
+        return out
+
+    # -- the FedAvg core ----------------------------------------------------
+    def _weighted_avg_device(self, models, weights, as_float=False,
+                             base_model=None, prescale=None, staged=None):
+        """Weighted average with the reference's per-key semantics.
+
+        Returns (layout, flat fp32 bucket on the GPU, {non-fp32 key: tensor},
+        key order).  ``models`` is the client_feedback list of
+        (sample_size, dict); ``weights`` the per-client Python doubles."""
+        dicts = [m for _, m in models]
+        template = dicts[0]
+        n = len(dicts)
+        if staged is not None:
+            layout, stack = staged
+        else:
+            layout = self._layout(template, as_float=as_float)
+            stack = self._stack(layout, dicts, as_float=as_float)
+        out = torch.empty(layout.numel, dtype=torch.float32,
+                          device=self.compute_device)
+        base = None
+        if base_model is not None:
+            base = self._bucket(layout, base_model, as_float=as_float)
+        ops.weighted_sum(stack.rows(list(range(n))), weights, out,
+                         prescale=prescale, base=base)
+        # keys some clients lack: reduce over the clients that have them,
+        # weights NOT renormalised (clients_avg_aggregator.py:74-75)
+        for k in layout.keys:
+            have = [i for i in range(n) if k in dicts[i]]
+            if len(have) == n:
+                continue
+            o, m = layout.offsets[k], layout.numels[k]
+            ops.weighted_sum(
+                stack.rows(have, key=k), [weights[i] for i in have],
+                out[o:o + m],
+                prescale=None if prescale is None else
+                [prescale[i] for i in have],
+                base=None if base is None else base[o:o + m])
+        extra = OrderedDict()
+        for k, dt in layout.other.items():
+            have = [i for i in range(n) if k in dicts[i]]
+            ts = [param2tensor(dicts[i][k]).to(self.compute_device)
+                  .contiguous() for i in have]
+            o = torch.empty(ts[0].shape, dtype=ops.typed_out_dtype(dt),
+                            device=self.compute_device)
+            ops.weighted_sum_typed(ts, [weights[i] for i in have], o)
+            if base_model is not None:
+                raise NotImplementedError(
+                    'init + update for non-fp32 key %r' % k)
+            extra[k] = o
+        return layout, out, extra, list(template.keys())
+
+    def _stage_all(self, models, as_float=True):
+        """Pack every client (robust rules need all keys in all clients)."""
+        dicts = [m for _, m in models]
+        layout = self._layout(dicts[0], as_float=as_float)
+        for i, d in enumerate(dicts):
+            for k in layout.keys:
+                if k not in d:
+                    raise KeyError('client %d lacks key %r' % (i, k))
+        stack = self._stack(layout, dicts, as_float=as_float)
+        return layout, stack
+
+
+def _as_float_proto(v):
+    t = param2tensor(v)
+    if isinstance(t, torch.Tensor) and t.dtype != torch.float32:
+        return torch.empty(t.shape, dtype=torch.float32)
+    return t

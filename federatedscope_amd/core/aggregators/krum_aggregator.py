@@ -1,0 +1,61 @@
+"""Krum / multi-Krum (federatedscope/core/aggregators/krum_aggregator.py:6-90).
+
+Device path: all client updates are staged as fp32 rows; fsagg_pairdist_f32
+computes the per-key L2 distances for every pair and the n×n matrix (sum over
+keys, +inf diagonal) in one pass over the stack; the n×n matrix (≤ 200² floats)
+comes back to the host where the score/sort/select logic runs with the same
+torch CPU ops as the reference (:75-87); the selected clients are then
+averaged in ascending-score order with init + avg fused into the kernel.
+"""
+import torch
+
+from ... import ops
+from ._engine import _first_device, fedavg_weights
+from .clients_avg_aggregator import ClientsAvgAggregator
+
+
+def krum_scores(D, byzantine_node_num):
+    """_calculate_score's tail (krum_aggregator.py:75-77), on the host."""
+    model_num = D.shape[0]
+    closest_num = model_num - byzantine_node_num - 2
+    sorted_distance = torch.sort(D)[0]
+    return torch.sum(sorted_distance[:, :closest_num], axis=-1)
+
+
+class KrumAggregator(ClientsAvgAggregator):
+    def __init__(self, model=None, device='cpu', config=None):
+        super().__init__(model, device, config)
+        self.byzantine_node_num = config.aggregator.byzantine_node_num
+        self.krum_agg_num = config.aggregator.BFT_args.krum_agg_num
+        assert 2 * self.byzantine_node_num + 2 < config.federate.client_num, \
+            "it should be satisfied that 2*byzantine_node_num + 2 < client_num"
+
+    def aggregate(self, agg_info):
+        models = agg_info["client_feedback"]
+        out_dev = _first_device(models[0][1])
+        layout, flat, keys = self._krum_device(models, self.krum_agg_num)
+        return self._emit(layout, flat, keys, out_dev)
+
+    def distance_matrix(self, models):
+        """D (host fp32 [n, n]) as _calculate_score fills it (:58-73)."""
+        layout, stack = self._stage_all(models)
+        rows = stack.rows(list(range(len(models))))
+        return ops.pairdist(rows, layout.segments()).cpu(), layout, stack
+
+    def _calculate_score(self, models):
+        D, _, _ = self.distance_matrix([(0, m) for m in models])
+        return krum_scores(D, self.byzantine_node_num)
+
+    def _krum_device(self, models, agg_num):
+        D, layout, stack = self.distance_matrix(models)
+        scores = krum_scores(D, self.byzantine_node_num)
+        index_order = torch.sort(scores)[1].numpy()
+        sel = [int(i) for i in index_order[:agg_num]]
+        self.last_selection = sel
+        sizes = [models[i][0] for i in sel]
+        weights = fedavg_weights(sizes, self.cfg.federate.ignore_weight)
+        base = self._bucket(layout, self.model.state_dict(), as_float=True)
+        out = torch.empty(layout.numel, dtype=torch.float32,
+                          device=self.compute_device)
+        ops.weighted_sum(stack.rows(sel), weights, out, base=base)
+        return layout, out, list(models[0][1].keys())

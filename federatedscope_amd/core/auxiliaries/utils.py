@@ -1,0 +1,58 @@
+"""Helpers the aggregation path shares with the reference.
+
+Mirrors federatedscope/core/auxiliaries/utils.py:95-111 (param2tensor,
+merge_param_dict).  The gRPC wire format ships tensors as base64-encoded
+pickles (federatedscope/core/message.py:8-9,118-120); they are decoded here
+with a restricted unpickler that only admits torch's tensor-rebuild helpers,
+so a crafted message cannot execute code.
+"""
+import base64
+import collections
+import io
+import pickle
+
+import torch
+
+
+def _storage_from_bytes(b):
+    return torch.load(io.BytesIO(b), weights_only=True)
+
+
+class _TensorUnpickler(pickle.Unpickler):
+    _ALLOWED = {
+        ('torch._utils', '_rebuild_tensor_v2'): torch._utils._rebuild_tensor_v2,
+        ('torch.storage', '_load_from_bytes'): _storage_from_bytes,
+        ('collections', 'OrderedDict'): collections.OrderedDict,
+    }
+
+    def find_class(self, module, name):
+        fn = self._ALLOWED.get((module, name))
+        if fn is None:
+            raise pickle.UnpicklingError(
+                'refusing to unpickle %s.%s in a model update' % (module, name))
+        return fn
+
+
+def b64_to_tensor(s):
+    return _TensorUnpickler(io.BytesIO(base64.b64decode(s))).load()
+
+
+def param2tensor(param):
+    """list → FloatTensor, int → long, float → float, str → decoded tensor;
+    tensors pass through (utils.py:95-105)."""
+    if isinstance(param, list):
+        param = torch.FloatTensor(param)
+    elif isinstance(param, int):
+        param = torch.tensor(param, dtype=torch.long)
+    elif isinstance(param, float):
+        param = torch.tensor(param, dtype=torch.float)
+    elif isinstance(param, str):
+        param = b64_to_tensor(param)
+    return param
+
+
+def merge_param_dict(raw_param, filtered_param):
+    """Overlay the aggregate onto the model state_dict (utils.py:108-111)."""
+    for key in filtered_param.keys():
+        raw_param[key] = filtered_param[key]
+    return raw_param

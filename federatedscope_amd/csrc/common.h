@@ -1,0 +1,59 @@
+// Shared helpers for libfsagg (gfx950 only).  Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/fsagg.h"
+
+namespace fsagg {
+
+// thread-local last error (fsagg_last_error)
+void set_error(const char *fmt, ...);
+
+inline hipStream_t as_stream(fsagg_stream_t s) {
+  return reinterpret_cast<hipStream_t>(s);
+}
+
+inline bool aligned16(const void *p) {
+  return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+}
+
+// Check the launch status once, after the kernel is enqueued.
+int check_launch(const char *what);
+
+constexpr int kWave = 64;
+
+// Grid size for a streaming kernel: enough workgroups to fill 256 CUs a few
+// times over, never more than the work needs.
+inline unsigned stream_grid(int64_t work_items, int block, int64_t cap) {
+  int64_t g = (work_items + block - 1) / block;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return static_cast<unsigned>(g);
+}
+
+// IEEE single ops that the compiler may not contract into an FMA.  The
+// library is also compiled with -ffp-contract=off; these make the intent
+// explicit at the call sites that the bit-exact contract depends on.
+__device__ __forceinline__ float mul_rn(float a, float b) {
+  return __fmul_rn(a, b);
+}
+__device__ __forceinline__ float add_rn(float a, float b) {
+  return __fadd_rn(a, b);
+}
+
+// Order-preserving float <-> uint32 key (total order, -0 < +0).
+__device__ __forceinline__ uint32_t f2key(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+  uint32_t u = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+  return __uint_as_float(u);
+}
+
+}  // namespace fsagg

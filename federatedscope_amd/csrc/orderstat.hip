@@ -1,0 +1,350 @@
+// Coordinate-wise order statistics over client buckets (gfx950):
+// median (median_aggregator.py:43-52) and trimmed mean
+// (trimmedmean_aggregator.py:44-57, Bulyan's stage 2 bulyan_aggregator.py:92-105).
+//
+// One lane owns one coordinate (column of the n×P client stack).  The lane
+// loads its n values with coalesced 4-B loads (64 consecutive coordinates per
+// wave-instruction, one row at a time), maps them to order-preserving uint32
+// keys and sorts them in registers with a bitonic network that is generated
+// at compile time as straight-line min/max code (NMAX ∈ {4..256}; padding
+// keys 0xFFFFFFFF sort last) for n <= 64.  For 64 < n <= 256 the keys stay
+// in registers and the two needed ranks are found together by a 32-step
+// radix (bit-by-bit) select — branch-free counting over the register file;
+// the straight-line bitonic network beyond 64 keys is too large for the
+// compiler.  n > 256 uses the same radix select re-reading the column from
+// L2.
+//
+// Algorithmic bytes per coordinate: 4·n read + 4 (base) read + 4 written.
+#include <utility>
+
+#include "common.h"
+
+namespace fsagg {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr uint32_t kPad = 0xFFFFFFFFu;
+
+// ---- compile-time bitonic network --------------------------------------
+template <int N, int SIZE, int STRIDE, int I>
+__device__ __forceinline__ void cmpx(uint32_t (&k)[N]) {
+  constexpr int J = I ^ STRIDE;
+  if constexpr (J > I) {
+    constexpr bool up = (I & SIZE) == 0;
+    const uint32_t a = k[I], b = k[J];
+    const uint32_t lo = a < b ? a : b;
+    const uint32_t hi = a < b ? b : a;
+    k[I] = up ? lo : hi;
+    k[J] = up ? hi : lo;
+  }
+}
+
+template <int N, int SIZE, int STRIDE, int... I>
+__device__ __forceinline__ void stage(uint32_t (&k)[N],
+                                      std::integer_sequence<int, I...>) {
+  (cmpx<N, SIZE, STRIDE, I>(k), ...);
+}
+
+template <int N, int SIZE, int STRIDE>
+__device__ __forceinline__ void merge_level(uint32_t (&k)[N]) {
+  stage<N, SIZE, STRIDE>(k, std::make_integer_sequence<int, N>{});
+  if constexpr (STRIDE > 1) merge_level<N, SIZE, STRIDE / 2>(k);
+}
+
+template <int N, int SIZE>
+__device__ __forceinline__ void sort_from(uint32_t (&k)[N]) {
+  merge_level<N, SIZE, SIZE / 2>(k);
+  if constexpr (SIZE < N) sort_from<N, SIZE * 2>(k);
+}
+
+template <int N>
+__device__ __forceinline__ void bitonic_sort(uint32_t (&k)[N]) {
+  sort_from<N, 2>(k);
+}
+
+// read k[idx] for a runtime idx without dynamic register indexing
+template <int N, int... I>
+__device__ __forceinline__ uint32_t pick(const uint32_t (&k)[N], int idx,
+                                         std::integer_sequence<int, I...>) {
+  uint32_t r = 0;
+  ((r = (I == idx) ? k[I] : r), ...);
+  return r;
+}
+
+// Σ key2f(k[j]) for lo <= j < hi, in float64, ascending order
+template <int N, int... I>
+__device__ __forceinline__ double mid_sum(const uint32_t (&k)[N], int lo,
+                                          int hi,
+                                          std::integer_sequence<int, I...>) {
+  double s = 0.0;
+  ((s += (I >= lo && I < hi) ? double(key2f(k[I])) : 0.0), ...);
+  return s;
+}
+
+// The reference computes cat([T, -top_k, -bottom_k]).sum(): for a column that
+// holds ±inf/NaN with k >= 1 an infinity is always among the excluded values,
+// so the fp32 sum is inf - inf = NaN; with k == 0 it is Σall (inf or NaN).
+template <int N, int... I>
+__device__ __forceinline__ float nonfinite_sum(const uint32_t (&k)[N], int n,
+                                               int kk, bool nan,
+                                               std::integer_sequence<int, I...>) {
+  if (kk > 0 || nan) return __builtin_nanf("");
+  float s = 0.0f;
+  ((s = (I < n) ? add_rn(s, key2f(k[I])) : s), ...);
+  return s;
+}
+
+enum Mode { kMedian = 0, kTrimmed = 1 };
+
+template <int N, int MODE>
+__global__ __launch_bounds__(kBlock) void orderstat_reg_kernel(
+    const float *const *__restrict__ rows, int n, int64_t numel, int kk,
+    float divisor, const float *__restrict__ base, float *__restrict__ out) {
+  const int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (p >= numel) return;
+  uint32_t k[N];
+  bool nan = false, nonfinite = false;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    if (j < n) {
+      const float x = rows[j][p];
+      nan |= __builtin_isnan(x);
+      nonfinite |= !__builtin_isfinite(x);
+      k[j] = f2key(x);
+    } else {
+      k[j] = kPad;
+    }
+  }
+  bitonic_sort<N>(k);
+  using Seq = std::make_integer_sequence<int, N>;
+  float r;
+  if constexpr (MODE == kMedian) {
+    const float lo = key2f(pick<N>(k, (n - 1) / 2, Seq{}));
+    const float hi = key2f(pick<N>(k, n / 2, Seq{}));
+    // (median(T) - median(-T)) / 2, literally
+    r = __fdiv_rn(lo - (-hi), 2.0f);
+    if (nan) r = __builtin_nanf("");
+  } else {
+    float s;
+    if (!nonfinite) {
+      s = float(mid_sum<N>(k, kk, n - kk, Seq{}));
+    } else {
+      s = nonfinite_sum<N>(k, n, kk, nan, Seq{});
+    }
+    r = __fdiv_rn(s, divisor);
+  }
+  if (base) r = add_rn(base[p], r);
+  out[p] = r;
+}
+
+// ---- 64 < n <= 256: register-resident radix select ----------------------
+template <int N, int MODE>
+__global__ __launch_bounds__(kBlock) void orderstat_radix_kernel(
+    const float *const *__restrict__ rows, int n, int64_t numel, int kk,
+    float divisor, const float *__restrict__ base, float *__restrict__ out) {
+  const int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (p >= numel) return;
+  uint32_t k[N];
+  bool nan = false, nonfinite = false;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    if (j < n) {
+      const float x = rows[j][p];
+      nan |= __builtin_isnan(x);
+      nonfinite |= !__builtin_isfinite(x);
+      k[j] = f2key(x);
+    } else {
+      k[j] = kPad;
+    }
+  }
+  const int r1 = MODE == kMedian ? (n - 1) / 2 : kk;
+  const int r2 = MODE == kMedian ? n / 2 : n - kk - 1;
+  // p = the key of rank r: the largest prefix with #(key <= prefix|lowbits) <= r
+  uint32_t p1 = 0, p2 = 0;
+#pragma unroll 1
+  for (int bit = 31; bit >= 0; --bit) {
+    const uint32_t m = (1u << bit) - 1u;
+    const uint32_t c1 = p1 | m, c2 = p2 | m;
+    int n1 = 0, n2 = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      n1 += k[j] <= c1;
+      n2 += k[j] <= c2;
+    }
+    if (n1 <= r1) p1 |= 1u << bit;
+    if (n2 <= r2) p2 |= 1u << bit;
+  }
+  float r;
+  if constexpr (MODE == kMedian) {
+    r = __fdiv_rn(key2f(p1) - (-key2f(p2)), 2.0f);
+    if (nan) r = __builtin_nanf("");
+  } else {
+    float s;
+    if (!nonfinite) {
+      const uint32_t klo = p1, khi = p2;
+      int below = 0, eq_lo = 0, inside = 0;
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        below += k[j] < klo;
+        eq_lo += k[j] == klo;
+        const bool in = k[j] > klo && k[j] < khi;
+        inside += in;
+        acc += in ? double(key2f(k[j])) : 0.0;
+      }
+      const int keep = n - 2 * kk;
+      if (klo == khi) {
+        acc = double(key2f(klo)) * keep;
+      } else {
+        const int lo_kept = min(below + eq_lo, n - kk) - kk;
+        const int hi_kept = keep - lo_kept - inside;
+        acc += double(key2f(klo)) * lo_kept + double(key2f(khi)) * hi_kept;
+      }
+      s = float(acc);
+    } else if (kk > 0 || nan) {
+      s = __builtin_nanf("");
+    } else {
+      s = 0.0f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) s = j < n ? add_rn(s, key2f(k[j])) : s;
+    }
+    r = __fdiv_rn(s, divisor);
+  }
+  if (base) r = add_rn(base[p], r);
+  out[p] = r;
+}
+
+// ---- generic n: radix select (binary search on the key bits) -----------
+__device__ __forceinline__ uint32_t select_rank(const float *const *rows,
+                                                int n, int64_t p, int rank) {
+  // smallest key v such that #(key <= v) > rank
+  uint32_t prefix = 0;
+  for (int bit = 31; bit >= 0; --bit) {
+    const uint32_t cand = prefix | ((1u << bit) - 1u);  // all lower bits set
+    int cnt = 0;
+    for (int j = 0; j < n; ++j) cnt += f2key(rows[j][p]) <= cand;
+    if (cnt <= rank) prefix |= 1u << bit;
+  }
+  return prefix;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void orderstat_generic_kernel(
+    const float *const *__restrict__ rows, int n, int64_t numel, int kk,
+    float divisor, const float *__restrict__ base, float *__restrict__ out) {
+  const int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (p >= numel) return;
+  bool nan = false, nonfinite = false;
+  for (int j = 0; j < n; ++j) {
+    const float x = rows[j][p];
+    nan |= __builtin_isnan(x);
+    nonfinite |= !__builtin_isfinite(x);
+  }
+  float r;
+  if constexpr (MODE == kMedian) {
+    const float lo = key2f(select_rank(rows, n, p, (n - 1) / 2));
+    const float hi = key2f(select_rank(rows, n, p, n / 2));
+    r = __fdiv_rn(lo - (-hi), 2.0f);
+    if (nan) r = __builtin_nanf("");
+  } else {
+    const uint32_t klo = select_rank(rows, n, p, kk);
+    const uint32_t khi = select_rank(rows, n, p, n - kk - 1);
+    float s;
+    if (!nonfinite) {
+      // kept ranks [kk, n-kk): strictly inside (klo, khi) plus tie copies
+      double acc = 0.0;
+      int below = 0, eq_lo = 0, inside = 0;
+      for (int j = 0; j < n; ++j) {
+        const float x = rows[j][p];
+        const uint32_t key = f2key(x);
+        below += key < klo;
+        eq_lo += key == klo;
+        const bool in = key > klo && key < khi;
+        inside += in;
+        if (in) acc += double(x);
+      }
+      const int keep = n - 2 * kk;
+      if (klo == khi) {
+        acc = double(key2f(klo)) * keep;
+      } else {
+        const int lo_kept = min(below + eq_lo, n - kk) - kk;
+        const int hi_kept = keep - lo_kept - inside;
+        acc += double(key2f(klo)) * lo_kept + double(key2f(khi)) * hi_kept;
+      }
+      s = float(acc);
+    } else {
+      // Σall − Σtop − Σbottom in fp32: with k >= 1 an infinity is always
+      // among the excluded values, so inf - inf (or a NaN) gives NaN;
+      // with k == 0 the result is Σall itself.
+      float all = 0.0f;
+      for (int j = 0; j < n; ++j) all = add_rn(all, rows[j][p]);
+      s = (kk == 0 && !nan) ? all : __builtin_nanf("");
+    }
+    r = __fdiv_rn(s, divisor);
+  }
+  if (base) r = add_rn(base[p], r);
+  out[p] = r;
+}
+
+template <int MODE>
+int launch(const float *const *rows, int n, int64_t numel, int kk,
+           float divisor, const float *base, float *out, hipStream_t s) {
+  const unsigned grid = unsigned((numel + kBlock - 1) / kBlock);
+#define FSAGG_OS(NN)                                                        \
+  hipLaunchKernelGGL((orderstat_reg_kernel<NN, MODE>), dim3(grid),         \
+                     dim3(kBlock), 0, s, rows, n, numel, kk, divisor, base, \
+                     out)
+  if (n <= 4) FSAGG_OS(4);
+  else if (n <= 8) FSAGG_OS(8);
+  else if (n <= 16) FSAGG_OS(16);
+  else if (n <= 32) FSAGG_OS(32);
+  else if (n <= 64) FSAGG_OS(64);
+#define FSAGG_RX(NN)                                                        \
+  hipLaunchKernelGGL((orderstat_radix_kernel<NN, MODE>), dim3(grid),       \
+                     dim3(kBlock), 0, s, rows, n, numel, kk, divisor, base, \
+                     out)
+  else if (n <= 96) FSAGG_RX(96);
+  else if (n <= 128) FSAGG_RX(128);
+  else if (n <= 160) FSAGG_RX(160);
+  else if (n <= 192) FSAGG_RX(192);
+  else if (n <= 224) FSAGG_RX(224);
+  else if (n <= 256) FSAGG_RX(256);
+  else
+    hipLaunchKernelGGL((orderstat_generic_kernel<MODE>), dim3(grid),
+                       dim3(kBlock), 0, s, rows, n, numel, kk, divisor, base,
+                       out);
+#undef FSAGG_OS
+#undef FSAGG_RX
+  return check_launch(MODE == kMedian ? "fsagg_coord_median_f32"
+                                      : "fsagg_trimmed_mean_f32");
+}
+
+}  // namespace
+}  // namespace fsagg
+
+using namespace fsagg;
+
+extern "C" int fsagg_coord_median_f32(const float *const *rows, int n,
+                                      int64_t numel, const float *base,
+                                      float *out, fsagg_stream_t stream) {
+  if (!rows || !out || n < 1 || numel < 0) {
+    set_error("fsagg_coord_median_f32: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  if (numel == 0) return FSAGG_OK;
+  return launch<kMedian>(rows, n, numel, 0, 2.0f, base, out,
+                         as_stream(stream));
+}
+
+extern "C" int fsagg_trimmed_mean_f32(const float *const *rows, int n,
+                                      int64_t numel, int k, float divisor,
+                                      const float *base, float *out,
+                                      fsagg_stream_t stream) {
+  if (!rows || !out || n < 1 || numel < 0 || k < 0 || 2 * k >= n) {
+    set_error("fsagg_trimmed_mean_f32: invalid argument (n=%d k=%d)", n, k);
+    return FSAGG_EINVAL;
+  }
+  if (numel == 0) return FSAGG_OK;
+  return launch<kTrimmed>(rows, n, numel, k, divisor, base, out,
+                          as_stream(stream));
+}

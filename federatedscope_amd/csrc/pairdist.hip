@@ -1,0 +1,322 @@
+// Krum pairwise distances and per-client norms (gfx950).
+//
+// Krum (krum_aggregator.py:41-77) needs, for every client pair (a, b) and
+// every state_dict key, Σ_p (x_a[p] - x_b[p])^2 over the key's elements; the
+// distance is the SUM over keys of the per-key L2 norms.  That is a Gram-like
+// reduction over the coordinates (K = P, M = N = n) with a difference-square
+// inner op; it is done on the VALU (exact fp32 differences, no MFMA: the
+// ‖a‖²+‖b‖²−2a·b rewrite cancels catastrophically for near-identical
+// honest clients, which is exactly the regime Krum must rank).
+//
+// Work decomposition
+//   * the flat bucket is cut into chunks of ≤ chl coordinates that never
+//     straddle a key (a per-key chunk prefix is built on the device);
+//     one workgroup per chunk (× tile-pair groups when n > 184);
+//   * the chunk streams through LDS in stages of `sub` coordinates, stored
+//     coordinate-major ([coord][client], row pitch ldsp) so one lane reads
+//     its 8 + 8 client values with four ds_read_b128;
+//   * each lane owns an 8×8 client-pair tile (64 fp32 accumulators) and a
+//     k-slice of the stage's coordinates; at the end of the chunk the
+//     k-slices are summed through LDS in a fixed order → partial[chunk][pair];
+//   * a final kernel sums each key's chunks in fp64 (fixed order), takes the
+//     per-key sqrt, rounds to fp32 and accumulates the keys in fp32 in key
+//     order (the reference's `distance += torch.dist(...)`).
+// Deterministic: no atomics anywhere.
+#include "common.h"
+
+namespace fsagg {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kTS = 8;                       // pair tile side
+constexpr int kRedPitch = kTS * kTS + 1;     // 65: LDS pitch of a reduction slot
+constexpr int kLdsFloats = kBlock * kRedPitch;  // 16640 floats = 65 KiB
+
+struct PairPlan {
+  int nt;       // tiles per side
+  int ntp;      // upper-triangular tile pairs
+  int groups;   // grid.y
+  int tpg;      // tile pairs per group
+  int ks;       // k-slices per tile pair
+  int ldsp;     // LDS pitch (floats) of one staged coordinate
+  int sub;      // coordinates per stage
+  int64_t chl;  // coordinates per chunk
+  int64_t max_chunks;
+};
+
+PairPlan make_plan(int n, int64_t numel, int nseg) {
+  PairPlan pl;
+  pl.nt = (n + kTS - 1) / kTS;
+  pl.ntp = pl.nt * (pl.nt + 1) / 2;
+  pl.groups = (pl.ntp + kBlock - 1) / kBlock;
+  pl.tpg = (pl.ntp + pl.groups - 1) / pl.groups;
+  pl.ks = kBlock / pl.tpg;
+  pl.ldsp = pl.nt * kTS + 4;
+  pl.sub = kLdsFloats / pl.ldsp;
+  int64_t chl = (numel + 1023) / 1024;
+  if (chl < 2048) chl = 2048;
+  pl.chl = chl;
+  pl.max_chunks = numel / chl + nseg + 1;
+  return pl;
+}
+
+inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+__global__ void chunk_prefix_kernel(const int64_t *__restrict__ seg_off,
+                                    int nseg, int64_t chl, int *prefix) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  int acc = 0;
+  prefix[0] = 0;
+  for (int s = 0; s < nseg; ++s) {
+    const int64_t len = seg_off[s + 1] - seg_off[s];
+    acc += int((len + chl - 1) / chl);
+    prefix[s + 1] = acc;
+  }
+}
+
+__device__ __forceinline__ void tp_to_tiles(int tp, int nt, int &ti, int &tj) {
+  int r = 0, base = 0;
+  while (tp >= base + (nt - r)) {
+    base += nt - r;
+    ++r;
+  }
+  ti = r;
+  tj = r + (tp - base);
+}
+
+__global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
+    const float *const *__restrict__ rows, int n, PairPlan pl,
+    const int64_t *__restrict__ seg_off, int nseg,
+    const int *__restrict__ prefix, float *__restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) float lds[kLdsFloats];
+  const int c = blockIdx.x;
+  const int total = prefix[nseg];
+  if (c >= total) return;
+  // segment s: largest s with prefix[s] <= c
+  int lo = 0, hi = nseg;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (prefix[mid] <= c) lo = mid;
+    else hi = mid;
+  }
+  const int s = lo;
+  const int64_t start = seg_off[s] + int64_t(c - prefix[s]) * pl.chl;
+  int64_t end = start + pl.chl;
+  if (end > seg_off[s + 1]) end = seg_off[s + 1];
+
+  const int tid = threadIdx.x;
+  const int tpl = tid % pl.tpg;
+  const int ksl = tid / pl.tpg;
+  const int tp = blockIdx.y * pl.tpg + tpl;
+  const bool active = ksl < pl.ks && tpl < pl.tpg && tp < pl.ntp;
+  int ti = 0, tj = 0;
+  if (active) tp_to_tiles(tp, pl.nt, ti, tj);
+
+  // zero the staging area once: padded client rows stay zero
+  for (int q = tid; q < kLdsFloats; q += kBlock) lds[q] = 0.0f;
+  __syncthreads();
+
+  float acc[kTS][kTS];
+#pragma unroll
+  for (int u = 0; u < kTS; ++u)
+#pragma unroll
+    for (int v = 0; v < kTS; ++v) acc[u][v] = 0.0f;
+
+  for (int64_t cs = start; cs < end; cs += pl.sub) {
+    const int len = int(end - cs < pl.sub ? end - cs : pl.sub);
+    // stage [n][len] → lds[coord][client]
+    const int items = n * len;
+    for (int q = tid; q < items; q += kBlock) {
+      const int r = q / len;
+      const int cc = q - r * len;
+      lds[cc * pl.ldsp + r] = rows[r][cs + cc];
+    }
+    __syncthreads();
+    if (active) {
+      for (int cc = ksl; cc < len; cc += pl.ks) {
+        const float4 *col = reinterpret_cast<const float4 *>(lds + cc * pl.ldsp);
+        const float4 a0 = col[ti * 2], a1 = col[ti * 2 + 1];
+        const float4 b0 = col[tj * 2], b1 = col[tj * 2 + 1];
+        const float a[kTS] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const float b[kTS] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int u = 0; u < kTS; ++u)
+#pragma unroll
+          for (int v = 0; v < kTS; ++v) {
+            const float d = a[u] - b[v];
+            acc[u][v] = __builtin_fmaf(d, d, acc[u][v]);
+          }
+      }
+    }
+    __syncthreads();
+  }
+
+  // sum the k-slices of each tile pair in slice order
+  if (ksl < pl.ks) {
+    float *slot = lds + (ksl * pl.tpg + tpl) * kRedPitch;
+#pragma unroll
+    for (int u = 0; u < kTS; ++u)
+#pragma unroll
+      for (int v = 0; v < kTS; ++v) slot[u * kTS + v] = acc[u][v];
+  }
+  __syncthreads();
+  const int outs = pl.tpg * kTS * kTS;
+  for (int o = tid; o < outs; o += kBlock) {
+    const int l = o / (kTS * kTS);
+    const int e = o - l * (kTS * kTS);
+    const int gtp = blockIdx.y * pl.tpg + l;
+    if (gtp >= pl.ntp) continue;
+    float sum = 0.0f;
+    for (int k = 0; k < pl.ks; ++k) sum += lds[(k * pl.tpg + l) * kRedPitch + e];
+    partial[(int64_t(c) * pl.ntp + gtp) * (kTS * kTS) + e] = sum;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void pairdist_final_kernel(
+    const float *__restrict__ partial, int n, PairPlan pl, int nseg,
+    const int *__restrict__ prefix, float *__restrict__ D) {
+  const int q = blockIdx.x * kBlock + threadIdx.x;
+  if (q >= n * n) return;
+  const int a = q / n, b = q - (q / n) * n;
+  if (a == b) {
+    D[q] = __builtin_inff();
+    return;
+  }
+  const int i = a < b ? a : b, j = a < b ? b : a;
+  const int ti = i / kTS, tj = j / kTS, u = i % kTS, v = j % kTS;
+  const int tp = ti * pl.nt - ti * (ti - 1) / 2 + (tj - ti);
+  const int e = u * kTS + v;
+  float dist = 0.0f;
+  for (int s = 0; s < nseg; ++s) {
+    double sq = 0.0;
+    for (int c = prefix[s]; c < prefix[s + 1]; ++c)
+      sq += double(partial[(int64_t(c) * pl.ntp + tp) * (kTS * kTS) + e]);
+    dist = add_rn(dist, float(sqrt(sq)));
+  }
+  D[q] = dist;
+}
+
+// ---- per-row squared norms (fp64, deterministic) -------------------------
+inline int rownorm_blocks(int n, int64_t numel) {
+  int64_t b = (numel + kBlock * 16 - 1) / (kBlock * 16);
+  int64_t cap = (2048 + n - 1) / n;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return int(b);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(kBlock) void rownorm_partial_kernel(
+    const float *const *__restrict__ rows, int64_t numel, int nblk,
+    double *__restrict__ partial) {
+  __shared__ double red[kBlock / kWave];
+  const int row = blockIdx.y;
+  const int64_t chunk = (numel + nblk - 1) / nblk;
+  const int64_t lo = int64_t(blockIdx.x) * chunk;
+  int64_t hi = lo + chunk;
+  if (hi > numel) hi = numel;
+  const float *x = rows[row];
+  double acc = 0.0;
+  for (int64_t p = lo + threadIdx.x; p < hi; p += kBlock) {
+    const double d = double(x[p]);
+    acc += d * d;
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < kBlock / kWave; ++w) t += red[w];
+    partial[int64_t(row) * nblk + blockIdx.x] = t;
+  }
+}
+
+__global__ void rownorm_final_kernel(const double *__restrict__ partial, int n,
+                                     int nblk, double *__restrict__ sq) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= n) return;
+  double t = 0.0;
+  for (int b = 0; b < nblk; ++b) t += partial[int64_t(row) * nblk + b];
+  sq[row] = t;
+}
+
+}  // namespace
+}  // namespace fsagg
+
+using namespace fsagg;
+
+extern "C" size_t fsagg_pairdist_workspace_bytes(int n, int64_t numel,
+                                                 int nseg) {
+  if (n < 1 || nseg < 1) return 0;
+  const PairPlan pl = make_plan(n, numel, nseg);
+  return align256(sizeof(int) * size_t(nseg + 1)) +
+         align256(sizeof(float) * size_t(pl.max_chunks) * size_t(pl.ntp) *
+                  kTS * kTS);
+}
+
+extern "C" int fsagg_pairdist_f32(const float *const *rows, int n,
+                                  int64_t numel, const int64_t *seg_off,
+                                  int nseg, float *D, void *workspace,
+                                  size_t workspace_bytes,
+                                  fsagg_stream_t stream) {
+  if (!rows || !seg_off || !D || n < 2 || nseg < 1 || numel < 0) {
+    set_error("fsagg_pairdist_f32: invalid argument (n=%d nseg=%d)", n, nseg);
+    return FSAGG_EINVAL;
+  }
+  const size_t need = fsagg_pairdist_workspace_bytes(n, numel, nseg);
+  if (!workspace || workspace_bytes < need) {
+    set_error("fsagg_pairdist_f32: workspace %zu < %zu bytes", workspace_bytes,
+              need);
+    return FSAGG_ESPACE;
+  }
+  const PairPlan pl = make_plan(n, numel, nseg);
+  hipStream_t s = as_stream(stream);
+  int *prefix = static_cast<int *>(workspace);
+  float *partial = reinterpret_cast<float *>(
+      static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)));
+  hipLaunchKernelGGL(chunk_prefix_kernel, dim3(1), dim3(1), 0, s, seg_off,
+                     nseg, pl.chl, prefix);
+  if (numel > 0)
+    hipLaunchKernelGGL(pairdist_chunk_kernel,
+                       dim3(unsigned(pl.max_chunks), unsigned(pl.groups)),
+                       dim3(kBlock), 0, s, rows, n, pl, seg_off, nseg, prefix,
+                       partial);
+  hipLaunchKernelGGL(pairdist_final_kernel,
+                     dim3(unsigned((n * n + kBlock - 1) / kBlock)),
+                     dim3(kBlock), 0, s, partial, n, pl, nseg, prefix, D);
+  return check_launch("fsagg_pairdist_f32");
+}
+
+extern "C" size_t fsagg_rownorm_workspace_bytes(int n, int64_t numel) {
+  if (n < 1) return 0;
+  return sizeof(double) * size_t(n) * size_t(rownorm_blocks(n, numel));
+}
+
+extern "C" int fsagg_row_sqnorm_f32(const float *const *rows, int n,
+                                    int64_t numel, double *sq, void *workspace,
+                                    size_t workspace_bytes,
+                                    fsagg_stream_t stream) {
+  if (!rows || !sq || n < 1 || numel < 0) {
+    set_error("fsagg_row_sqnorm_f32: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  const size_t need = fsagg_rownorm_workspace_bytes(n, numel);
+  if (!workspace || workspace_bytes < need) {
+    set_error("fsagg_row_sqnorm_f32: workspace %zu < %zu bytes",
+              workspace_bytes, need);
+    return FSAGG_ESPACE;
+  }
+  const int nblk = rownorm_blocks(n, numel);
+  hipStream_t s = as_stream(stream);
+  double *partial = static_cast<double *>(workspace);
+  hipLaunchKernelGGL(rownorm_partial_kernel, dim3(unsigned(nblk), unsigned(n)),
+                     dim3(kBlock), 0, s, rows, numel, nblk, partial);
+  hipLaunchKernelGGL(rownorm_final_kernel, dim3(unsigned((n + 63) / 64)),
+                     dim3(64), 0, s, partial, n, nblk, sq);
+  return check_launch("fsagg_row_sqnorm_f32");
+}

@@ -1,0 +1,404 @@
+// FedAvg-family weighted sum over client buckets (gfx950).
+//
+// Semantics: ClientsAvgAggregator._para_weighted_avg
+// (federatedscope/core/aggregators/clients_avg_aggregator.py:60-100): per
+// element, acc = x0*w0, then acc = acc + xi*wi in client-list order, every
+// multiply and add rounded to fp32 separately (ATen CPU semantics; no FMA).
+//
+// HBM layout: each client's update is one flat fp32 bucket (a row); the
+// kernel reads a row table so stacked slabs, per-client tensors and Krum's
+// selected subsets all stream without a gather copy.  Bytes per element:
+// 4·n read + 4 written (+4 read for the fused `base` add) — the whole kernel
+// is HBM-bound (0.5 FLOP/B), so the design goal is pure streaming:
+//   * each thread owns V f4 columns of the bucket (16 B/lane, 1 KiB per
+//     wave-instruction per row, fully coalesced);
+//   * the client loop issues U rows' loads before consuming any of them, so
+//     U·V·16 B are in flight per lane; the adds still happen strictly in
+//     client order, which keeps the result bit-identical to the reference;
+//   * row pointers and weights are wave-uniform → scalar (SGPR) loads.
+#include <hip/hip_fp16.h>
+
+#include "common.h"
+
+namespace fsagg {
+namespace {
+
+constexpr int kBlock = 256;
+
+// clang ext-vector (the nontemporal builtin needs a native vector type)
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// Row pointers arrive through a table, so the compiler cannot prove they are
+// global memory and would emit flat loads; cast to the global address space
+// (addrspace 1) so the streaming loads are global_load_dwordx4 (nt).
+typedef __attribute__((address_space(1))) const f4 gf4;
+
+template <bool NT>
+__device__ __forceinline__ f4 ld4(const f4 *p) {
+  gf4 *g = (gf4 *)(p);
+  if constexpr (NT) {
+    return __builtin_nontemporal_load(g);
+  } else {
+    return *g;
+  }
+}
+
+__device__ __forceinline__ f4 mul4(f4 a, float s) {
+  return f4{mul_rn(a.x, s), mul_rn(a.y, s), mul_rn(a.z, s), mul_rn(a.w, s)};
+}
+__device__ __forceinline__ f4 add4(f4 a, f4 b) {
+  return f4{add_rn(a.x, b.x), add_rn(a.y, b.y), add_rn(a.z, b.z),
+            add_rn(a.w, b.w)};
+}
+
+// One tile of V f4 columns per thread.  GUARD handles the ragged last
+// tile; all other tiles run unguarded.
+template <int U, int V, bool PRE, bool BASE, bool NT, bool GUARD>
+__device__ __forceinline__ void wsum_tile(const float *const *__restrict__ rows,
+                                          const float *__restrict__ w,
+                                          const float *__restrict__ pre, int n,
+                                          int64_t nvec, int64_t t0,
+                                          const float *__restrict__ base,
+                                          float *__restrict__ out) {
+  int64_t idx[V];
+  bool ok[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    idx[v] = t0 + v * kBlock + threadIdx.x;
+    ok[v] = !GUARD || idx[v] < nvec;
+  }
+  f4 acc[V];
+  // client 0 initialises the accumulator (the reference's i == 0 branch)
+  {
+    const f4 *r = reinterpret_cast<const f4 *>(rows[0]);
+    const float w0 = w[0];
+    const float s0 = PRE ? pre[0] : 1.0f;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      f4 x = ok[v] ? ld4<NT>(r + idx[v]) : f4{0.0f, 0.0f, 0.0f, 0.0f};
+      if (PRE) x = mul4(x, s0);
+      acc[v] = mul4(x, w0);
+    }
+  }
+  int i = 1;
+  for (; i + U <= n; i += U) {
+    f4 x[U][V];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const f4 *r = reinterpret_cast<const f4 *>(rows[i + u]);
+#pragma unroll
+      for (int v = 0; v < V; ++v)
+        x[u][v] = ok[v] ? ld4<NT>(r + idx[v]) : f4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float wu = w[i + u];
+      const float su = PRE ? pre[i + u] : 1.0f;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        f4 t = x[u][v];
+        if (PRE) t = mul4(t, su);
+        acc[v] = add4(acc[v], mul4(t, wu));
+      }
+    }
+  }
+  for (; i < n; ++i) {
+    const f4 *r = reinterpret_cast<const f4 *>(rows[i]);
+    const float wi = w[i];
+    const float si = PRE ? pre[i] : 1.0f;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      f4 t = ok[v] ? ld4<NT>(r + idx[v]) : f4{0.0f, 0.0f, 0.0f, 0.0f};
+      if (PRE) t = mul4(t, si);
+      acc[v] = add4(acc[v], mul4(t, wi));
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    if (!ok[v]) continue;
+    f4 a = acc[v];
+    if (BASE) a = add4(reinterpret_cast<const f4 *>(base)[idx[v]], a);
+    reinterpret_cast<f4 *>(out)[idx[v]] = a;
+  }
+}
+
+template <int U, int V, bool PRE, bool BASE, bool NT>
+__global__ __launch_bounds__(kBlock) void wsum_f32_vec_kernel(
+    const float *const *__restrict__ rows, const float *__restrict__ w,
+    const float *__restrict__ pre, int n, int64_t nvec,
+    const float *__restrict__ base, float *__restrict__ out) {
+  constexpr int64_t tile = int64_t(kBlock) * V;
+  const int64_t full = nvec / tile * tile;
+  for (int64_t t0 = int64_t(blockIdx.x) * tile; t0 < nvec;
+       t0 += int64_t(gridDim.x) * tile) {
+    if (t0 < full)
+      wsum_tile<U, V, PRE, BASE, NT, false>(rows, w, pre, n, nvec, t0, base,
+                                            out);
+    else
+      wsum_tile<U, V, PRE, BASE, NT, true>(rows, w, pre, n, nvec, t0, base,
+                                           out);
+  }
+}
+
+// Scalar tail: elements [start, numel) (fewer than 4), one thread each.
+__global__ void wsum_f32_tail_kernel(const float *const *__restrict__ rows,
+                                     const float *__restrict__ w,
+                                     const float *__restrict__ pre, int n,
+                                     int64_t start, int64_t numel,
+                                     const float *__restrict__ base,
+                                     float *__restrict__ out) {
+  const int64_t p = start + threadIdx.x;
+  if (p >= numel) return;
+  float x = rows[0][p];
+  if (pre) x = mul_rn(x, pre[0]);
+  float acc = mul_rn(x, w[0]);
+  for (int i = 1; i < n; ++i) {
+    float t = rows[i][p];
+    if (pre) t = mul_rn(t, pre[i]);
+    acc = add_rn(acc, mul_rn(t, w[i]));
+  }
+  if (base) acc = add_rn(base[p], acc);
+  out[p] = acc;
+}
+
+// Tunables of the streaming kernel (measured on MI355X).
+constexpr int kU = 8;  // client rows in flight per batch
+constexpr int kV = 2;  // f4 columns per thread
+
+template <bool PRE, bool BASE>
+void launch_wsum(const float *const *rows, const float *w, const float *pre,
+                 int n, int64_t nvec, const float *base, float *out,
+                 hipStream_t s) {
+  const int64_t tiles = (nvec + int64_t(kBlock) * kV - 1) / (int64_t(kBlock) * kV);
+  const unsigned grid = stream_grid(tiles, 1, 256 * 16);
+  hipLaunchKernelGGL((wsum_f32_vec_kernel<kU, kV, PRE, BASE, true>),
+                     dim3(grid), dim3(kBlock), 0, s, rows, w, pre, n, nvec,
+                     base, out);
+}
+
+// ---------------------------------------------------------------------------
+// non-fp32 buckets
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint16_t f2bf_rne(float f) {
+  // c10::detail::round_to_nearest_even
+  if (__builtin_isnan(f)) return 0x7FC0;
+  uint32_t u = __float_as_uint(f);
+  u += ((u >> 16) & 1u) + 0x7FFFu;
+  return static_cast<uint16_t>(u >> 16);
+}
+__device__ __forceinline__ float bf2f(uint16_t b) {
+  return __uint_as_float(uint32_t(b) << 16);
+}
+
+template <int DT>
+__global__ __launch_bounds__(kBlock) void wsum_typed_kernel(
+    const void *const *__restrict__ rows, const double *__restrict__ w, int n,
+    int64_t numel, void *__restrict__ out) {
+  for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < numel;
+       p += int64_t(gridDim.x) * kBlock) {
+    if constexpr (DT == FSAGG_F64) {
+      double acc = __dmul_rn(static_cast<const double *>(rows[0])[p], w[0]);
+      for (int i = 1; i < n; ++i)
+        acc = __dadd_rn(acc,
+                        __dmul_rn(static_cast<const double *>(rows[i])[p], w[i]));
+      static_cast<double *>(out)[p] = acc;
+    } else if constexpr (DT == FSAGG_F16) {
+      auto ld = [&](int i) {
+        return __half2float(static_cast<const __half *>(rows[i])[p]);
+      };
+      __half acc = __float2half(mul_rn(ld(0), float(w[0])));
+      for (int i = 1; i < n; ++i) {
+        __half t = __float2half(mul_rn(ld(i), float(w[i])));
+        acc = __float2half(add_rn(__half2float(acc), __half2float(t)));
+      }
+      static_cast<__half *>(out)[p] = acc;
+    } else if constexpr (DT == FSAGG_BF16) {
+      auto ld = [&](int i) {
+        return bf2f(static_cast<const uint16_t *>(rows[i])[p]);
+      };
+      uint16_t acc = f2bf_rne(mul_rn(ld(0), float(w[0])));
+      for (int i = 1; i < n; ++i) {
+        uint16_t t = f2bf_rne(mul_rn(ld(i), float(w[i])));
+        acc = f2bf_rne(add_rn(bf2f(acc), bf2f(t)));
+      }
+      static_cast<uint16_t *>(out)[p] = acc;
+    } else {  // FSAGG_I64 -> f32
+      auto ld = [&](int i) {
+        return static_cast<float>(static_cast<const int64_t *>(rows[i])[p]);
+      };
+      float acc = mul_rn(ld(0), float(w[0]));
+      for (int i = 1; i < n; ++i) acc = add_rn(acc, mul_rn(ld(i), float(w[i])));
+      static_cast<float *>(out)[p] = acc;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// online running mean, init+update add, synthetic fill
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void online_inc_kernel(
+    float *__restrict__ m, const float *__restrict__ x, float c, float s,
+    float d, int64_t numel) {
+  for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < numel;
+       p += int64_t(gridDim.x) * kBlock) {
+    m[p] = __fdiv_rn(add_rn(mul_rn(c, m[p]), mul_rn(s, x[p])), d);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void add_kernel(
+    const float *__restrict__ a, const float *__restrict__ b,
+    float *__restrict__ out, int64_t nvec, int64_t numel) {
+  const int64_t stride = int64_t(gridDim.x) * kBlock;
+  for (int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x; q < nvec;
+       q += stride) {
+    f4 x = reinterpret_cast<const f4 *>(a)[q];
+    f4 y = reinterpret_cast<const f4 *>(b)[q];
+    reinterpret_cast<f4 *>(out)[q] = add4(x, y);
+  }
+  for (int64_t p = nvec * 4 + int64_t(blockIdx.x) * kBlock + threadIdx.x;
+       p < numel; p += stride)
+    out[p] = add_rn(a[p], b[p]);
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z ^= z >> 30;
+  z *= 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 27;
+  z *= 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return z;
+}
+
+__global__ __launch_bounds__(kBlock) void fill_uniform_kernel(
+    float *__restrict__ X, int n, int64_t numel, int64_t ld, uint64_t seed,
+    int64_t off) {
+  const uint64_t total = uint64_t(n) * uint64_t(ld);
+  for (uint64_t q = uint64_t(blockIdx.x) * kBlock + threadIdx.x; q < total;
+       q += uint64_t(gridDim.x) * kBlock) {
+    const uint64_t c = q / uint64_t(ld);
+    const uint64_t j = q - c * uint64_t(ld);
+    float v = 0.0f;
+    if (j < uint64_t(numel)) {
+      const uint64_t z = mix64(seed * 0x9E3779B97F4A7C15ull ^ (c << 40) ^
+                               (uint64_t(off) + j));
+      v = float(uint32_t(z >> 40)) * 0x1p-23f - 1.0f;  // exact, in [-1, 1)
+    }
+    X[q] = v;
+  }
+}
+
+}  // namespace
+}  // namespace fsagg
+
+using namespace fsagg;
+
+extern "C" int fsagg_weighted_sum_f32(const float *const *rows,
+                                      const float *weights,
+                                      const float *prescale, int n,
+                                      int64_t numel, const float *base,
+                                      float *out, fsagg_stream_t stream) {
+  if (!rows || !weights || !out || n < 1 || numel < 0) {
+    set_error("fsagg_weighted_sum_f32: invalid argument (n=%d numel=%lld)", n,
+              (long long)numel);
+    return FSAGG_EINVAL;
+  }
+  if (!aligned16(out) || (base && !aligned16(base))) {
+    set_error("fsagg_weighted_sum_f32: out/base must be 16-byte aligned");
+    return FSAGG_EINVAL;
+  }
+  if (numel == 0) return FSAGG_OK;
+  hipStream_t s = as_stream(stream);
+  const int64_t nvec = numel / 4;
+  if (nvec > 0) {
+    if (prescale) {
+      if (base) launch_wsum<true, true>(rows, weights, prescale, n, nvec, base, out, s);
+      else launch_wsum<true, false>(rows, weights, prescale, n, nvec, base, out, s);
+    } else {
+      if (base) launch_wsum<false, true>(rows, weights, prescale, n, nvec, base, out, s);
+      else launch_wsum<false, false>(rows, weights, prescale, n, nvec, base, out, s);
+    }
+  }
+  if (numel > nvec * 4) {
+    hipLaunchKernelGGL(wsum_f32_tail_kernel, dim3(1), dim3(kWave), 0, s, rows,
+                       weights, prescale, n, nvec * 4, numel, base, out);
+  }
+  return check_launch("fsagg_weighted_sum_f32");
+}
+
+extern "C" int fsagg_weighted_sum_typed(const void *const *rows, int in_dtype,
+                                        const double *weights, int n,
+                                        int64_t numel, void *out,
+                                        fsagg_stream_t stream) {
+  if (!rows || !weights || !out || n < 1 || numel < 0) {
+    set_error("fsagg_weighted_sum_typed: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  if (numel == 0) return FSAGG_OK;
+  hipStream_t s = as_stream(stream);
+  const unsigned grid = stream_grid(numel, kBlock, 256 * 8);
+  switch (in_dtype) {
+    case FSAGG_F16:
+      hipLaunchKernelGGL(wsum_typed_kernel<FSAGG_F16>, dim3(grid), dim3(kBlock), 0, s, rows, weights, n, numel, out);
+      break;
+    case FSAGG_BF16:
+      hipLaunchKernelGGL(wsum_typed_kernel<FSAGG_BF16>, dim3(grid), dim3(kBlock), 0, s, rows, weights, n, numel, out);
+      break;
+    case FSAGG_F64:
+      hipLaunchKernelGGL(wsum_typed_kernel<FSAGG_F64>, dim3(grid), dim3(kBlock), 0, s, rows, weights, n, numel, out);
+      break;
+    case FSAGG_I64:
+      hipLaunchKernelGGL(wsum_typed_kernel<FSAGG_I64>, dim3(grid), dim3(kBlock), 0, s, rows, weights, n, numel, out);
+      break;
+    default:
+      set_error("fsagg_weighted_sum_typed: unsupported dtype %d", in_dtype);
+      return FSAGG_EINVAL;
+  }
+  return check_launch("fsagg_weighted_sum_typed");
+}
+
+extern "C" int fsagg_online_inc_f32(float *m, const float *x, float cnt,
+                                    float s, float denom, int64_t numel,
+                                    fsagg_stream_t stream) {
+  if (!m || !x || numel < 0) {
+    set_error("fsagg_online_inc_f32: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  if (numel == 0) return FSAGG_OK;
+  hipLaunchKernelGGL(online_inc_kernel, dim3(stream_grid(numel, kBlock, 256 * 8)),
+                     dim3(kBlock), 0, as_stream(stream), m, x, cnt, s, denom,
+                     numel);
+  return check_launch("fsagg_online_inc_f32");
+}
+
+extern "C" int fsagg_add_f32(const float *a, const float *b, float *out,
+                             int64_t numel, fsagg_stream_t stream) {
+  if (!a || !b || !out || numel < 0) {
+    set_error("fsagg_add_f32: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  if (!aligned16(a) || !aligned16(b) || !aligned16(out)) {
+    set_error("fsagg_add_f32: pointers must be 16-byte aligned");
+    return FSAGG_EINVAL;
+  }
+  if (numel == 0) return FSAGG_OK;
+  const int64_t nvec = numel / 4;
+  hipLaunchKernelGGL(add_kernel, dim3(stream_grid(nvec + 1, kBlock, 256 * 8)),
+                     dim3(kBlock), 0, as_stream(stream), a, b, out, nvec, numel);
+  return check_launch("fsagg_add_f32");
+}
+
+extern "C" int fsagg_fill_uniform_f32(float *X, int n, int64_t numel,
+                                      int64_t ld, uint64_t seed,
+                                      int64_t index_offset,
+                                      fsagg_stream_t stream) {
+  if (!X || n < 1 || numel < 0 || ld < numel) {
+    set_error("fsagg_fill_uniform_f32: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  const int64_t total = int64_t(n) * ld;
+  if (total == 0) return FSAGG_OK;
+  hipLaunchKernelGGL(fill_uniform_kernel, dim3(stream_grid(total, kBlock, 256 * 16)),
+                     dim3(kBlock), 0, as_stream(stream), X, n, numel, ld, seed,
+                     index_offset);
+  return check_launch("fsagg_fill_uniform_f32");
+}

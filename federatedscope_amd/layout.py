@@ -1,0 +1,142 @@
+"""Client buckets: flattening per-client state_dicts into device rows.
+
+A :class:`BucketLayout` maps the fp32 keys of a model (client 0's key order —
+the order every reference aggregator iterates, e.g.
+clients_avg_aggregator.py:70) to ``(offset, numel, shape)`` inside one flat
+fp32 bucket.  Every key starts on a 16-element (64-byte) boundary so that any
+key is itself a 16-byte-aligned sub-bucket (per-key launches for keys some
+clients lack reuse the same rows).  Keys of other dtypes (fp16, bf16, fp64,
+int64 — SURVEY A5) are listed separately and reduced per key.
+
+A :class:`ClientStack` is the device-resident ``[capacity][numel]`` slab the
+server fills as client updates arrive (host dicts are staged through pinned
+buffers and copied asynchronously) and the aggregators stream over.
+"""
+from collections import OrderedDict
+
+import torch
+
+from .core.auxiliaries.utils import param2tensor
+
+KEY_ALIGN = 16  # elements
+
+
+class BucketLayout:
+    def __init__(self, template):
+        self.keys = []          # fp32 keys in template order
+        self.offsets = {}
+        self.numels = {}
+        self.shapes = {}
+        self.other = OrderedDict()  # key -> dtype (non-fp32 keys)
+        self.order = list(template.keys())
+        off = 0
+        for k, v in template.items():
+            t = param2tensor(v)
+            if not isinstance(t, torch.Tensor):
+                t = torch.as_tensor(t)
+            if t.dtype == torch.float32:
+                self.keys.append(k)
+                self.offsets[k] = off
+                self.numels[k] = t.numel()
+                self.shapes[k] = tuple(t.shape)
+                off += -(-t.numel() // KEY_ALIGN) * KEY_ALIGN
+            else:
+                self.other[k] = t.dtype
+                self.shapes[k] = tuple(t.shape)
+        self.numel = max(off, KEY_ALIGN)
+
+    def signature(self):
+        return (tuple(self.order), tuple(
+            (k, self.shapes[k]) for k in self.keys), tuple(self.other.items()))
+
+    def segments(self, keys=None):
+        """Element offsets [0, ..., numel] splitting the bucket per key
+        (padding folded into the preceding key; zeros add nothing to sums of
+        squares)."""
+        ks = self.keys if keys is None else keys
+        offs = [self.offsets[k] for k in ks] + [self.numel]
+        offs[0] = 0
+        return offs
+
+    def pack_host(self, model, out):
+        """Copy the fp32 keys of ``model`` into the flat CPU tensor ``out``
+        (padding and missing keys zero)."""
+        out.zero_()
+        for k in self.keys:
+            if k not in model:
+                continue
+            t = param2tensor(model[k])
+            o, m = self.offsets[k], self.numels[k]
+            out[o:o + m].copy_(t.reshape(-1))
+        return out
+
+    def pack_device(self, model, out_row):
+        """Pack into a device row (``out_row`` 1-D fp32 cuda tensor)."""
+        devs = {param2tensor(model[k]).device.type for k in self.keys
+                if k in model}
+        if devs <= {'cuda'}:
+            # device-resident update: per-key device copies (padding and
+            # absent keys keep whatever the row holds; stacks start zeroed)
+            for k in self.keys:
+                if k not in model:
+                    continue
+                t = param2tensor(model[k])
+                o, m = self.offsets[k], self.numels[k]
+                out_row[o:o + m].copy_(t.reshape(-1), non_blocking=True)
+            return out_row
+        host = _pinned(self.numel)
+        self.pack_host(model, host)
+        out_row.copy_(host, non_blocking=True)
+        # the pinned staging buffer is reused: wait for this copy to land
+        torch.cuda.current_stream(out_row.device).synchronize()
+        return out_row
+
+    def unpack(self, flat, keys=None):
+        """Views of the flat bucket, one per fp32 key, in the given order."""
+        out = OrderedDict()
+        for k in (self.keys if keys is None else keys):
+            o, m = self.offsets[k], self.numels[k]
+            out[k] = flat[o:o + m].view(self.shapes[k])
+        return out
+
+
+_PINNED = {}
+
+
+def _pinned(numel):
+    b = _PINNED.get('buf')
+    if b is None or b.numel() < numel:
+        b = torch.empty(numel, dtype=torch.float32, pin_memory=True)
+        _PINNED['buf'] = b
+    return b[:numel]
+
+
+class ClientStack:
+    """Device slab ``[capacity][layout.numel]`` of packed client updates."""
+
+    def __init__(self, layout, capacity, device):
+        self.layout = layout
+        self.device = torch.device(device)
+        self.slab = torch.empty((max(1, capacity), layout.numel),
+                                dtype=torch.float32, device=self.device)
+
+    @property
+    def capacity(self):
+        return self.slab.shape[0]
+
+    def ensure(self, capacity):
+        if capacity > self.capacity:
+            self.slab = torch.empty((capacity, self.layout.numel),
+                                    dtype=torch.float32, device=self.device)
+
+    def load(self, i, model):
+        self.layout.pack_device(model, self.slab[i])
+
+    def rows(self, idx=None, key=None):
+        from .ops import RowTable
+        if key is None:
+            return RowTable.from_slab(self.slab, rows=idx,
+                                      numel=self.layout.numel)
+        return RowTable.from_slab(self.slab, rows=idx,
+                                  col_offset=self.layout.offsets[key],
+                                  numel=self.layout.numels[key])

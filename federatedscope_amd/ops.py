@@ -1,0 +1,307 @@
+"""Tensor-level wrappers around libfsagg's C ABI.
+
+Every function validates shapes, dtypes, devices and alignment on the host
+BEFORE anything is launched (a malformed launch on a GPU box can fault the
+whole node), then calls the HIP kernel on the current torch stream of the
+tensors' device.  PyTorch is only the device-memory / stream container here.
+"""
+import math
+
+import torch
+
+from . import _lib as L
+
+ALIGN_BYTES = 16
+
+
+def _stream(device):
+    return ctypes_ptr(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ctypes_ptr(x):
+    return int(x) if x else None
+
+
+def _check_f32_cuda(t, what):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError('%s must be a torch.Tensor' % what)
+    if t.device.type != 'cuda':
+        raise ValueError('%s must live on a GPU (got %s)' % (what, t.device))
+    if t.dtype != torch.float32:
+        raise ValueError('%s must be float32 (got %s)' % (what, t.dtype))
+    if not t.is_contiguous():
+        raise ValueError('%s must be contiguous' % what)
+    if t.data_ptr() % ALIGN_BYTES:
+        raise ValueError('%s must be 16-byte aligned' % what)
+
+
+class RowTable:
+    """A device array of client row pointers (see include/fsagg.h).
+
+    Row i is a flat fp32 bucket of ``numel`` elements that starts at
+    ``ptrs[i]``; table order is the reduction order.  The table keeps the
+    tensors it points into alive.
+    """
+
+    def __init__(self, ptrs, numel, device, keepalive=()):
+        if len(ptrs) < 1:
+            raise ValueError('RowTable needs at least one row')
+        for p in ptrs:
+            if p % ALIGN_BYTES:
+                raise ValueError('client row pointer 0x%x is not 16-byte '
+                                 'aligned' % p)
+        self.ptrs = list(ptrs)
+        self.n = len(ptrs)
+        self.numel = int(numel)
+        self.device = torch.device(device)
+        self.table = torch.tensor(self.ptrs, dtype=torch.int64,
+                                  device=self.device)
+        self._keep = tuple(keepalive)
+
+    @classmethod
+    def from_slab(cls, slab, rows=None, col_offset=0, numel=None):
+        """Rows of a 2-D [n][ld] fp32 slab; ``rows`` selects/reorders."""
+        _check_f32_cuda(slab, 'slab')
+        if slab.dim() != 2:
+            raise ValueError('slab must be 2-D [clients, ld]')
+        n, ld = slab.shape
+        numel = ld - col_offset if numel is None else int(numel)
+        if col_offset < 0 or col_offset + numel > ld:
+            raise ValueError('column range [%d, %d) outside ld=%d' %
+                             (col_offset, col_offset + numel, ld))
+        idx = range(n) if rows is None else [int(r) for r in rows]
+        for r in idx:
+            if not 0 <= r < n:
+                raise IndexError('row %d outside slab of %d rows' % (r, n))
+        base = slab.data_ptr()
+        rowb = slab.stride(0) * 4
+        ptrs = [base + r * rowb + col_offset * 4 for r in idx]
+        return cls(ptrs, numel, slab.device, keepalive=(slab, ))
+
+    @classmethod
+    def from_tensors(cls, tensors, numel=None, offset=0):
+        """One flat fp32 device tensor per client."""
+        if not tensors:
+            raise ValueError('no client tensors')
+        dev = tensors[0].device
+        m = min(t.numel() for t in tensors)
+        numel = m - offset if numel is None else int(numel)
+        ptrs = []
+        for i, t in enumerate(tensors):
+            _check_f32_cuda(t, 'client tensor %d' % i)
+            if t.device != dev:
+                raise ValueError('client tensors on different devices')
+            if offset + numel > t.numel():
+                raise ValueError('client tensor %d shorter than numel' % i)
+            ptrs.append(t.data_ptr() + 4 * offset)
+        return cls(ptrs, numel, dev, keepalive=tuple(tensors))
+
+    def ptr(self):
+        return self.table.data_ptr()
+
+
+def _fp32_dev(values, device):
+    return torch.tensor([float(v) for v in values], dtype=torch.float32,
+                        device=device)
+
+
+def _check_out(out, numel, device, what='out'):
+    _check_f32_cuda(out, what)
+    if out.device != device:
+        raise ValueError('%s on %s, rows on %s' % (what, out.device, device))
+    if out.numel() < numel:
+        raise ValueError('%s has %d elements < numel %d' %
+                         (what, out.numel(), numel))
+
+
+def weighted_sum(rows, weights, out, prescale=None, base=None, stream=None):
+    """out = [base +] Σ_i fl32(fl32(x_i·s_i)·w_i) in row order (no FMA).
+
+    ``weights``/``prescale`` are Python floats (the reference's doubles); they
+    are rounded to fp32 here exactly as ATen reads a wrapped scalar."""
+    if len(weights) != rows.n:
+        raise ValueError('%d weights for %d rows' % (len(weights), rows.n))
+    _check_out(out, rows.numel, rows.device)
+    if base is not None:
+        _check_out(base, rows.numel, rows.device, 'base')
+    w = weights if isinstance(weights, torch.Tensor) else _fp32_dev(
+        weights, rows.device)
+    s = None
+    if prescale is not None:
+        if len(prescale) != rows.n:
+            raise ValueError('prescale length mismatch')
+        s = prescale if isinstance(prescale, torch.Tensor) else _fp32_dev(
+            prescale, rows.device)
+    st = stream if stream is not None else _stream(rows.device)
+    L.check(L.load().fsagg_weighted_sum_f32(
+        rows.ptr(), w.data_ptr(), s.data_ptr() if s is not None else None,
+        rows.n, rows.numel, base.data_ptr() if base is not None else None,
+        out.data_ptr(), st), 'fsagg_weighted_sum_f32')
+    return out
+
+
+_TYPED = {
+    torch.float16: (L.FSAGG_F16, torch.float16),
+    torch.bfloat16: (L.FSAGG_BF16, torch.bfloat16),
+    torch.float64: (L.FSAGG_F64, torch.float64),
+    torch.int64: (L.FSAGG_I64, torch.float32),
+}
+
+
+def typed_out_dtype(dtype):
+    return _TYPED[dtype][1]
+
+
+def weighted_sum_typed(tensors, weights, out):
+    """Non-fp32 keys (A5 dtype rules): tensors are per-client contiguous device
+    tensors of one dtype; weights are Python floats (kept as doubles)."""
+    dt = tensors[0].dtype
+    if dt not in _TYPED:
+        raise ValueError('unsupported dtype %s' % dt)
+    code, odt = _TYPED[dt]
+    numel = tensors[0].numel()
+    dev = tensors[0].device
+    for t in tensors:
+        if t.dtype != dt or t.numel() != numel or t.device != dev or \
+                not t.is_contiguous() or dev.type != 'cuda':
+            raise ValueError('typed rows must be contiguous %s tensors of %d '
+                             'elements on one GPU' % (dt, numel))
+    if out.dtype != odt or out.numel() != numel or out.device != dev or \
+            not out.is_contiguous():
+        raise ValueError('out must be a contiguous %s tensor of %d elements' %
+                         (odt, numel))
+    if len(weights) != len(tensors):
+        raise ValueError('weights length mismatch')
+    tab = torch.tensor([t.data_ptr() for t in tensors], dtype=torch.int64,
+                       device=dev)
+    w = torch.tensor([float(x) for x in weights], dtype=torch.float64,
+                     device=dev)
+    L.check(L.load().fsagg_weighted_sum_typed(tab.data_ptr(), code,
+                                              w.data_ptr(), len(tensors),
+                                              numel, out.data_ptr(),
+                                              _stream(dev)),
+            'fsagg_weighted_sum_typed')
+    return out
+
+
+def online_inc(m, x, cnt, sample_size):
+    """m = (cnt*m + s*x) / (cnt + s), every op rounded to fp32."""
+    _check_f32_cuda(m, 'maintained')
+    _check_f32_cuda(x, 'client update')
+    if x.numel() < m.numel() or x.device != m.device:
+        raise ValueError('client update does not cover the maintained bucket')
+    L.check(L.load().fsagg_online_inc_f32(
+        m.data_ptr(), x.data_ptr(), float(cnt), float(sample_size),
+        float(cnt + sample_size), m.numel(), _stream(m.device)),
+            'fsagg_online_inc_f32')
+    return m
+
+
+def add(a, b, out):
+    for t, nm in ((a, 'a'), (b, 'b'), (out, 'out')):
+        _check_f32_cuda(t, nm)
+    if not (a.numel() == b.numel() == out.numel()):
+        raise ValueError('add: size mismatch')
+    L.check(L.load().fsagg_add_f32(a.data_ptr(), b.data_ptr(), out.data_ptr(),
+                                   out.numel(), _stream(out.device)),
+            'fsagg_add_f32')
+    return out
+
+
+def coord_median(rows, out, base=None):
+    _check_out(out, rows.numel, rows.device)
+    if base is not None:
+        _check_out(base, rows.numel, rows.device, 'base')
+    L.check(L.load().fsagg_coord_median_f32(
+        rows.ptr(), rows.n, rows.numel,
+        base.data_ptr() if base is not None else None, out.data_ptr(),
+        _stream(rows.device)), 'fsagg_coord_median_f32')
+    return out
+
+
+def trimmed_mean(rows, k, out, divisor=None, base=None):
+    if k < 0 or 2 * k >= rows.n:
+        raise ValueError('trimmed mean needs 0 <= 2k < n (k=%d n=%d)' %
+                         (k, rows.n))
+    _check_out(out, rows.numel, rows.device)
+    if base is not None:
+        _check_out(base, rows.numel, rows.device, 'base')
+    div = float(rows.n - 2 * k if divisor is None else divisor)
+    L.check(L.load().fsagg_trimmed_mean_f32(
+        rows.ptr(), rows.n, rows.numel, int(k), div,
+        base.data_ptr() if base is not None else None, out.data_ptr(),
+        _stream(rows.device)), 'fsagg_trimmed_mean_f32')
+    return out
+
+
+class Workspace:
+    """Grow-only device scratch owned by the caller (the library allocates
+    nothing)."""
+
+    def __init__(self):
+        self.buf = {}
+
+    def get(self, device, nbytes):
+        key = str(device)
+        b = self.buf.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8,
+                            device=device)
+            self.buf[key] = b
+        return b
+
+
+_WS = Workspace()
+
+
+def pairdist(rows, seg_offsets, workspace=None):
+    """Krum distance matrix D[n][n] (fp32, device): sum over key segments of
+    per-key L2 distances; D[a][a] = +inf."""
+    if rows.n < 2:
+        raise ValueError('Krum needs at least two clients')
+    offs = [int(o) for o in seg_offsets]
+    if offs[0] != 0 or offs[-1] != rows.numel or \
+            any(b < a for a, b in zip(offs, offs[1:])):
+        raise ValueError('segment offsets must rise from 0 to numel')
+    nseg = len(offs) - 1
+    lib = L.load()
+    need = lib.fsagg_pairdist_workspace_bytes(rows.n, rows.numel, nseg)
+    ws = (workspace or _WS).get(rows.device, need)
+    seg = torch.tensor(offs, dtype=torch.int64, device=rows.device)
+    D = torch.empty((rows.n, rows.n), dtype=torch.float32, device=rows.device)
+    L.check(lib.fsagg_pairdist_f32(rows.ptr(), rows.n, rows.numel,
+                                   seg.data_ptr(), nseg, D.data_ptr(),
+                                   ws.data_ptr(), ws.numel(),
+                                   _stream(rows.device)), 'fsagg_pairdist_f32')
+    return D
+
+
+def row_sqnorm(rows, workspace=None):
+    """Per-row Σx² in float64 (device tensor [n])."""
+    lib = L.load()
+    need = lib.fsagg_rownorm_workspace_bytes(rows.n, rows.numel)
+    ws = (workspace or _WS).get(rows.device, need)
+    sq = torch.empty(rows.n, dtype=torch.float64, device=rows.device)
+    L.check(lib.fsagg_row_sqnorm_f32(rows.ptr(), rows.n, rows.numel,
+                                     sq.data_ptr(), ws.data_ptr(), ws.numel(),
+                                     _stream(rows.device)),
+            'fsagg_row_sqnorm_f32')
+    return sq
+
+
+def fill_uniform(slab, numel, seed, index_offset=0):
+    """Deterministic synthetic updates into a [n][ld] slab (benchmarks)."""
+    _check_f32_cuda(slab, 'slab')
+    n, ld = slab.shape
+    if numel > ld:
+        raise ValueError('numel > ld')
+    L.check(L.load().fsagg_fill_uniform_f32(slab.data_ptr(), n, int(numel),
+                                            ld, int(seed) & (2**64 - 1),
+                                            int(index_offset),
+                                            _stream(slab.device)),
+            'fsagg_fill_uniform_f32')
+    return slab
+
+
+def round_up(x, a):
+    return int(math.ceil(x / a) * a)

@@ -1,0 +1,166 @@
+/*
+ * fsagg.h — C ABI of libfsagg.so, the MI355X (gfx950) server-side aggregation
+ * engine that backs federatedscope_amd's Aggregator.aggregate() drop-ins.
+ *
+ * The reference has no native code: every entry point below
+ * replaces a Python/ATen loop inside federatedscope/core/aggregators.  The
+ * reference interface each one stands in for is cited per function.  The
+ * Python side binds these with ctypes (federatedscope_amd/_lib.py); the
+ * binding stub a FederatedScope maintainer would add is in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Every pointer argument marked (device) is HBM memory owned by the caller
+ *    (torch tensors' data_ptr()); the library never allocates or frees.
+ *  - A "row table" is a DEVICE array of n pointers, row i being client i's
+ *    flattened fp32 update of `numel` elements (the client's parameter
+ *    bucket).  Order in the table = reduction order = the reference's
+ *    client_feedback list order.  Rows and `out` must be 16-byte aligned.
+ *  - All calls are asynchronous on `stream` (a hipStream_t; NULL = the null
+ *    stream).  Return 0 on success, a negative code on failure; the message
+ *    is in fsagg_last_error() (thread-local).  No C++ exception crosses the
+ *    ABI.
+ *  - No FMA contraction anywhere on a bit-exact path: x*w and acc+t are each
+ *    rounded to fp32, exactly as ATen's CPU kernels do.
+ */
+#ifndef FSAGG_H_
+#define FSAGG_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *fsagg_stream_t; /* hipStream_t */
+
+#define FSAGG_VERSION 1
+
+enum fsagg_status {
+  FSAGG_OK = 0,
+  FSAGG_EINVAL = -1,   /* bad argument (null pointer, n < 1, misaligned) */
+  FSAGG_EHIP = -2,     /* a HIP runtime call failed */
+  FSAGG_ESPACE = -3,   /* workspace too small */
+};
+
+/* Element types of a client bucket (fsagg_weighted_sum_typed). */
+enum fsagg_dtype {
+  FSAGG_F32 = 0,
+  FSAGG_F16 = 1,
+  FSAGG_BF16 = 2,
+  FSAGG_F64 = 3,
+  FSAGG_I64 = 4, /* int64 input, fp32 output (ATen promotion of int*float) */
+};
+
+int fsagg_version(void);
+const char *fsagg_last_error(void);
+
+/*
+ * Weighted sum over clients, per element, in row-table order:
+ *     t_i  = fl32(x_i[p] * s_i)            (only if prescale != NULL)
+ *     acc  = fl32(t_0 * w_0)
+ *     acc  = fl32(acc + fl32(t_i * w_i))   for i = 1 .. n-1
+ *     out[p] = base ? fl32(base[p] + acc) : acc
+ * Replaces ClientsAvgAggregator._para_weighted_avg
+ *   (federatedscope/core/aggregators/clients_avg_aggregator.py:60-100),
+ * AsynClientsAvgAggregator._para_weighted_avg + init add
+ *   (asyn_clients_avg_aggregator.py:36-40,53-84),
+ * the multi-Krum average (krum_aggregator.py:35-39,79-90) and the scaled
+ * average of NormboundingAggregator (normbounding_aggregator.py:35-47).
+ *   rows     (device) n row pointers; weights (device) n fp32 (already
+ *            rounded from the reference's double weights);
+ *   prescale (device) n fp32 or NULL; base (device) numel fp32 or NULL.
+ */
+int fsagg_weighted_sum_f32(const float *const *rows, const float *weights,
+                           const float *prescale, int n, int64_t numel,
+                           const float *base, float *out,
+                           fsagg_stream_t stream);
+
+/*
+ * Same contract for non-fp32 buckets (A5's dtype rules): the product x*w is
+ * computed in float (f16/bf16/i64) or double (f64) and rounded to the output
+ * type, then accumulated with one rounding per add.  weights are DOUBLE on
+ * the device (the f64 path uses them unrounded).  out_dtype is in_dtype,
+ * except FSAGG_I64 whose output is FSAGG_F32.
+ */
+int fsagg_weighted_sum_typed(const void *const *rows, int in_dtype,
+                             const double *weights, int n, int64_t numel,
+                             void *out, fsagg_stream_t stream);
+
+/*
+ * Online running mean, one client:  m = fl(fl(fl(c*m) + fl(s*x)) / d)
+ * with c = cnt, s = sample_size, d = cnt + s given as fp32.
+ * Replaces OnlineClientsAvgAggregator.inc (clients_avg_aggregator.py:125-142).
+ */
+int fsagg_online_inc_f32(float *m, const float *x, float cnt, float s,
+                         float denom, int64_t numel, fsagg_stream_t stream);
+
+/* out = a + b elementwise (the robust rules' init + update; e.g.
+ * median_aggregator.py:37-41).  out may alias a or b. */
+int fsagg_add_f32(const float *a, const float *b, float *out, int64_t numel,
+                  fsagg_stream_t stream);
+
+/*
+ * Coordinate-wise median over the n rows:  (lo - (-hi)) / 2  with lo/hi the
+ * lower/upper middle order statistics (== (median(T) - median(-T))/2 of
+ * median_aggregator.py:43-52, bit-exact), NaN if the column holds a NaN;
+ * out = base ? base + med : med.
+ */
+int fsagg_coord_median_f32(const float *const *rows, int n, int64_t numel,
+                           const float *base, float *out,
+                           fsagg_stream_t stream);
+
+/*
+ * Coordinate-wise trimmed mean: drop the k largest and k smallest of each
+ * column, sum the rest, divide by `divisor` (n - 2k for trimmed mean,
+ * gamma for Bulyan); out = base ? base + r : r.
+ * Replaces TrimmedmeanAggregator._aggre_with_trimmedmean
+ * (trimmedmean_aggregator.py:44-57) and Bulyan's second stage
+ * (bulyan_aggregator.py:92-105).  Requires 2k < n.
+ */
+int fsagg_trimmed_mean_f32(const float *const *rows, int n, int64_t numel,
+                           int k, float divisor, const float *base,
+                           float *out, fsagg_stream_t stream);
+
+/*
+ * Krum pairwise distances, per key segment.  seg_off (device, int64,
+ * nseg+1 entries, seg_off[0] = 0, seg_off[nseg] = numel) splits each row into
+ * the state_dict keys.  Produces D (device, n*n fp32, row-major):
+ *     D[a][b] = Σ_seg fl32( sqrt( Σ_{p in seg} (x_a[p] - x_b[p])^2 ) ),
+ *     D[a][a] = +inf
+ * — the sum over keys of per-key L2 distances of
+ * KrumAggregator._calculate_distance (krum_aggregator.py:41-56) filled as in
+ * _calculate_score (:58-73).  Per-key sums accumulate in fp32 within a chunk
+ * and in fp64 across chunks (fixed order, deterministic).
+ * Workspace: fsagg_pairdist_workspace_bytes(n, numel, nseg) bytes (device).
+ */
+size_t fsagg_pairdist_workspace_bytes(int n, int64_t numel, int nseg);
+int fsagg_pairdist_f32(const float *const *rows, int n, int64_t numel,
+                       const int64_t *seg_off, int nseg, float *D,
+                       void *workspace, size_t workspace_bytes,
+                       fsagg_stream_t stream);
+
+/*
+ * Per-row squared L2 norm in fp64 (deterministic two-level reduction):
+ * sq[i] = Σ_p x_i[p]^2.  The norm of NormboundingAggregator's flattened update
+ * (normbounding_aggregator.py:39-41, torch.norm(param, p=2)).
+ * Workspace: fsagg_rownorm_workspace_bytes(n, numel).
+ */
+size_t fsagg_rownorm_workspace_bytes(int n, int64_t numel);
+int fsagg_row_sqnorm_f32(const float *const *rows, int n, int64_t numel,
+                         double *sq, void *workspace, size_t workspace_bytes,
+                         fsagg_stream_t stream);
+
+/*
+ * Deterministic synthetic client updates (benchmarks / tests): fills the
+ * [n][ld] slab X with u = hash(seed, client, index) mapped to [-1, 1),
+ * index < numel; the same generator is restated on the host by the tests.
+ */
+int fsagg_fill_uniform_f32(float *X, int n, int64_t numel, int64_t ld,
+                           uint64_t seed, int64_t index_offset,
+                           fsagg_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FSAGG_H_ */

@@ -1,0 +1,396 @@
+"""TEST INFRASTRUCTURE — numpy restatement of FederatedScope's server-side
+aggregation rules (reference v0.3.0, ``federatedscope/core/aggregators``).
+
+This module is the parity checker and the timed CPU baseline ("port") only.
+It is never imported by the product package.  Pinned against golden vectors
+generated from the real reference (tools/gen_golden.py, tests/golden/).
+
+A "model" is an ``OrderedDict[str, array]``; arrays are numpy arrays of
+float32 / float16 / float64 / int64, or :class:`BF16` for bfloat16 keys.
+Every rule mirrors the reference's arithmetic op for op:
+
+* elementwise fp32 ops are IEEE-rounded one at a time (numpy never fuses a
+  multiply-add), which makes FedAvg / async / online / median bit-exact;
+* ATen reductions whose order is ISA-dependent (``torch.dist``, the cascade
+  ``sum`` in trimmed mean, ``torch.norm``) are restated with float64
+  accumulation and compared under a stated tolerance.
+"""
+import math
+from collections import OrderedDict
+
+import numpy as np
+
+__all__ = [
+    'BF16', 'fedavg_weights', 'para_weighted_avg', 'asyn_weighted_avg',
+    'asyn_aggregate', 'online_aggregate', 'krum_distance', 'krum_distance_matrix',
+    'krum_scores', 'krum_select', 'krum_aggregate', 'median_update',
+    'median_aggregate', 'trimmed_mean_update', 'trimmedmean_aggregate',
+    'bulyan_aggregate', 'normbounding_aggregate', 'interpolate_aggregate',
+    'add_init', 'f32', 'trimmed_tolerance', 'bulyan_select', 'asyn_weights',
+]
+
+f32 = np.float32
+
+
+class BF16:
+    """bfloat16 array stored as its uint16 bit patterns."""
+    __slots__ = ('bits', )
+
+    def __init__(self, bits):
+        self.bits = np.asarray(bits, dtype=np.uint16)
+
+    @property
+    def shape(self):
+        return self.bits.shape
+
+    def to_f32(self):
+        return (self.bits.astype(np.uint32) << 16).view(np.float32)
+
+    @staticmethod
+    def from_f32(x):
+        """Round-to-nearest-even f32 → bf16 (NaN kept quiet)."""
+        x = np.asarray(x, dtype=np.float32)
+        u = x.view(np.uint32).astype(np.uint64)
+        rounded = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+        nan = np.isnan(x)
+        if nan.any():
+            rounded = np.where(nan, ((u >> 16) | 0x40).astype(np.uint16),
+                               rounded)
+        return BF16(rounded.astype(np.uint16))
+
+
+def _kind(a):
+    if isinstance(a, BF16):
+        return 'bf16'
+    return {np.dtype(np.float32): 'f32', np.dtype(np.float16): 'f16',
+            np.dtype(np.float64): 'f64'}.get(a.dtype, 'int')
+
+
+# ---------------------------------------------------------------------------
+# FedAvg  (clients_avg_aggregator.py:60-100)
+# ---------------------------------------------------------------------------
+def fedavg_weights(sizes, ignore_weight=False, use_ss=False):
+    """Per-client weights as the reference computes them: Python doubles.
+
+    ``training_set_size`` is a Python sum of the sample sizes (:64-67);
+    weight = 1/n if ignore_weight (:77-78), 1.0 under secret sharing (:79-82),
+    else size_i / total (:84)."""
+    total = 0
+    for s in sizes:
+        total += s
+    n = len(sizes)
+    out = []
+    for s in sizes:
+        if ignore_weight:
+            out.append(1.0 / n)
+        elif use_ss:
+            out.append(1.0)
+        else:
+            out.append(s / total)
+    return out
+
+
+def _scaled(x, w):
+    """``x * w`` with ``w`` a Python float (ATen mul with a wrapped scalar).
+
+    The scalar is read in the op's compute type: float for f32/f16/bf16
+    (result rounded to the storage type), double for f64; integer tensors
+    promote to the default dtype float32 (x cast first)."""
+    k = _kind(x)
+    if k == 'f32':
+        return x * f32(w)
+    if k == 'f16':
+        return (x.astype(f32) * f32(w)).astype(np.float16)
+    if k == 'bf16':
+        return BF16.from_f32(x.to_f32() * f32(w))
+    if k == 'f64':
+        return x * np.float64(w)
+    return x.astype(f32) * f32(w)
+
+
+def _accum(acc, t):
+    """``acc += t`` (in place add, result in acc's dtype)."""
+    k = _kind(acc)
+    if k == 'bf16':
+        tk = t.to_f32() if isinstance(t, BF16) else t.astype(f32)
+        return BF16.from_f32(acc.to_f32() + tk)
+    if k == 'f16':
+        return (acc.astype(f32) + t.astype(f32)).astype(np.float16)
+    return (acc + t).astype(acc.dtype)
+
+
+def para_weighted_avg(models, ignore_weight=False, use_ss=False,
+                      recover_fun=None, weights=None):
+    """``ClientsAvgAggregator._para_weighted_avg`` (clients_avg_aggregator.py:60-100).
+
+    ``models`` is a list of ``(sample_size, OrderedDict)``.  Keys come from
+    client 0; a client missing a key is skipped without renormalising
+    (:74-75).  Per element: acc = x0*w0, then acc = acc + xi*wi in list order.
+    ``weights`` overrides the per-client weights (used by the async rule)."""
+    sizes = [s for s, _ in models]
+    total = 0
+    for s in sizes:
+        total += s
+    if weights is None:
+        weights = fedavg_weights(sizes, ignore_weight, use_ss)
+    out = OrderedDict()
+    first = models[0][1]
+    for key in first:
+        acc = None
+        for i, (_, local) in enumerate(models):
+            if key not in local:
+                continue
+            t = _scaled(local[key], weights[i])
+            # the reference writes acc at i == 0 (client 0 always has key)
+            acc = t if acc is None else _accum(acc, t)
+        if use_ss and recover_fun is not None:
+            acc = recover_fun(acc)
+            acc = np.asarray(acc) / total
+            acc = np.asarray(acc, dtype=f32)
+        out[key] = acc
+    return out
+
+
+def add_init(init, update):
+    """``updated[key] = init[key] + update[key]`` over the update's keys
+    (e.g. median_aggregator.py:37-41)."""
+    out = OrderedDict()
+    for k in update:
+        a, b = init[k], update[k]
+        if isinstance(a, BF16) or isinstance(b, BF16):
+            raise NotImplementedError('bf16 init+update')
+        out[k] = (a + b)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Async  (asyn_clients_avg_aggregator.py:14-84)
+# ---------------------------------------------------------------------------
+def asyn_weights(sizes, staleness, factor, ignore_weight=False):
+    total = 0
+    for s in sizes:
+        total += s
+    n = len(sizes)
+    out = []
+    for i, s in enumerate(sizes):
+        w = 1.0 / n if ignore_weight else s / total
+        w *= 1.0 / ((1.0 + staleness[i])**factor)  # discount_func :42-51
+        out.append(w)
+    return out
+
+
+def asyn_weighted_avg(models, staleness, factor, ignore_weight=False):
+    """_para_weighted_avg of the async rule: every key cast with ``.float()``
+    (:74-77) and no missing-key check."""
+    sizes = [s for s, _ in models]
+    w = asyn_weights(sizes, staleness, factor, ignore_weight)
+    fl = [(s, OrderedDict((k, _to_float(v)) for k, v in d.items()))
+          for s, d in models]
+    return para_weighted_avg(fl, weights=w)
+
+
+def asyn_aggregate(models, staleness, factor, init, ignore_weight=False):
+    return add_init(init, asyn_weighted_avg(models, staleness, factor,
+                                            ignore_weight))
+
+
+def _to_float(v):
+    if isinstance(v, BF16):
+        return v.to_f32()
+    return np.asarray(v).astype(f32)
+
+
+# ---------------------------------------------------------------------------
+# Online running mean  (clients_avg_aggregator.py:115-148)
+# ---------------------------------------------------------------------------
+def online_aggregate(init, clients):
+    """reset(): zeros like the server model; inc((s, x)) per client:
+    m = (cnt*m + s*x) / (cnt + s); cnt += s."""
+    m = OrderedDict((k, np.zeros_like(v)) for k, v in init.items())
+    cnt = 0
+    for s, x in clients:
+        for k in m:
+            if k not in x:
+                continue
+            m[k] = ((f32(cnt) * m[k] + f32(s) * x[k]) / f32(cnt + s)).astype(
+                m[k].dtype)
+        cnt += s
+    return m
+
+
+# ---------------------------------------------------------------------------
+# Krum  (krum_aggregator.py:41-90)
+# ---------------------------------------------------------------------------
+def krum_distance(a, b):
+    """Sum over a's keys of the per-key L2 distance (:41-56).  Each per-key
+    ``torch.dist`` is restated in float64 and rounded to fp32; the running
+    total is an fp32 0-dim tensor started from Python 0.0."""
+    dist = f32(0.0)
+    for k in a:
+        x = _to_float(a[k]).astype(np.float64).ravel()
+        y = _to_float(b[k]).astype(np.float64).ravel()
+        d = f32(math.sqrt(float(np.dot(x - y, x - y))))
+        dist = f32(dist + d)
+    return dist
+
+
+def krum_distance_matrix(paras):
+    n = len(paras)
+    D = np.zeros((n, n), dtype=f32)
+    for a in range(n):
+        D[a, a] = np.inf
+        for b in range(a + 1, n):
+            D[a, b] = D[b, a] = krum_distance(paras[a], paras[b])
+    return D
+
+
+def krum_scores(D, f):
+    """Sort each row, sum the first n-f-2 columns with Python slice
+    semantics (a non-positive count slices from the end) (:58-77)."""
+    n = D.shape[0]
+    closest = n - f - 2
+    S = np.sort(D, axis=1)[:, :closest]
+    return S.astype(np.float64).sum(axis=1).astype(f32)
+
+
+def krum_select(scores, agg_num):
+    order = np.argsort(scores, kind='stable')
+    return [int(i) for i in order[:agg_num]]
+
+
+def krum_aggregate(models, f, agg_num, init, D=None):
+    """Multi-Krum: weighted average of the agg_num lowest-score clients in
+    ascending-score order, then init + avg (:21-39, :79-90)."""
+    if D is None:
+        D = krum_distance_matrix([d for _, d in models])
+    sel = krum_select(krum_scores(D, f), agg_num)
+    avg = para_weighted_avg([models[i] for i in sel])
+    return add_init(init, avg), sel
+
+
+# ---------------------------------------------------------------------------
+# Coordinate-wise median  (median_aggregator.py:43-52)
+# ---------------------------------------------------------------------------
+def median_update(models):
+    """(median(T) - median(-T)) / 2 with torch's lower median; NaN if any."""
+    first = models[0][1]
+    out = OrderedDict()
+    for k in first:
+        T = np.stack([_to_float(d[k]) for _, d in models], 0)
+        n = T.shape[0]
+        S = np.sort(T, axis=0)
+        lo = S[(n - 1) // 2]
+        hi = S[n // 2]
+        med_pos = lo                      # torch.median → lower median
+        med_neg = -hi                     # lower median of -T is -(upper)
+        r = (med_pos - med_neg) / f32(2)
+        nan = np.isnan(T).any(axis=0)
+        if nan.any():
+            r = np.where(nan, np.float32(np.nan), r)
+        out[k] = r.astype(f32)
+    return out
+
+
+def median_aggregate(models, init):
+    return add_init(init, median_update(models))
+
+
+# ---------------------------------------------------------------------------
+# Trimmed mean  (trimmedmean_aggregator.py:44-57)
+# ---------------------------------------------------------------------------
+def trimmed_mean_update(models, excluded_num, divisor=None):
+    """(Σ all − Σ top-k − Σ bottom-k) / (n − 2k) per coordinate.
+
+    The reference sums ``cat([T, -top, bottom])`` with ATen's cascade sum
+    (host-ISA dependent order); here the kept middle is summed in float64 and
+    rounded once, then divided in fp32 — compare under tolerance."""
+    first = models[0][1]
+    out = OrderedDict()
+    for k in first:
+        T = np.stack([_to_float(d[k]) for _, d in models], 0)
+        n = T.shape[0]
+        S = np.sort(T, axis=0)
+        mid = S[excluded_num:n - excluded_num].astype(np.float64).sum(0)
+        div = (n - 2 * excluded_num) if divisor is None else divisor
+        out[k] = (mid.astype(f32) / f32(div)).astype(f32)
+    return out
+
+
+def trimmedmean_aggregate(models, ratio, init):
+    k = int(len(models) * ratio)
+    return add_init(init, trimmed_mean_update(models, k))
+
+
+def trimmed_tolerance(models, excluded_num, divisor=None):
+    """Elementwise abs tolerance: the reference sums n + 2k fp32 values of
+    magnitude ≤ max|x| in fp32, so its error is ≤ ~(n+2k)·ε·Σ|x| loosely;
+    we use 4·ε·(Σ|x| + 2·Σ|top|)/div, per SURVEY §8c."""
+    first = models[0][1]
+    out = OrderedDict()
+    eps = float(np.finfo(np.float32).eps)
+    for k in first:
+        T = np.stack([_to_float(d[k]) for _, d in models], 0).astype(
+            np.float64)
+        n = T.shape[0]
+        div = (n - 2 * excluded_num) if divisor is None else divisor
+        out[k] = 8 * eps * (2 * np.abs(T).sum(0)) / div + 1e-30
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Bulyan  (bulyan_aggregator.py:75-106)
+# ---------------------------------------------------------------------------
+def bulyan_select(models, f, rate, D=None):
+    if D is None:
+        D = krum_distance_matrix([d for _, d in models])
+    scores = krum_scores(D, f)
+    order = np.argsort(scores, kind='stable')
+    keep = len(models) - int(2 * rate * f)
+    return [int(i) for i in order[:max(keep, 0)]], scores
+
+
+def bulyan_aggregate(models, f, rate, init, D=None):
+    sel, _ = bulyan_select(models, f, rate, D)
+    reliable = [models[i] for i in sel]
+    k = int(rate * f)
+    gamma = len(reliable) - 2 * k
+    upd = trimmed_mean_update(reliable, k, divisor=gamma)
+    # keys follow client 0 of the ORIGINAL list (global_update deepcopy, :81)
+    upd = OrderedDict((key, upd[key]) for key in models[0][1])
+    return add_init(init, upd), sel
+
+
+# ---------------------------------------------------------------------------
+# Norm bounding  (normbounding_aggregator.py:35-70)
+# ---------------------------------------------------------------------------
+def normbounding_aggregate(models, bound, init):
+    tmp = []
+    for s, d in models:
+        present = [k for k in init if k in d]
+        flat = np.concatenate([_to_float(d[k]).ravel() for k in present])
+        norm = f32(math.sqrt(float(np.dot(flat.astype(np.float64),
+                                          flat.astype(np.float64)))))
+        if norm > bound:
+            rate = f32(f32(bound) / norm)
+            scaled = rate * flat
+            rec = OrderedDict()
+            off = 0
+            for k in init:
+                if k in present:
+                    sz = int(np.prod(init[k].shape))
+                    rec[k] = scaled[off:off + sz].reshape(init[k].shape)
+                    off += sz
+                else:
+                    rec[k] = init[k].copy()
+            tmp.append((s, rec))
+        else:
+            tmp.append((s, d))
+    return add_init(init, para_weighted_avg(tmp))
+
+
+# ---------------------------------------------------------------------------
+# Server/clients interpolation  (server_clients_interpolate_aggregator.py:20-30)
+# ---------------------------------------------------------------------------
+def interpolate_aggregate(models, global_model, beta):
+    avg = para_weighted_avg(models)
+    return para_weighted_avg([((1 - beta), global_model), (beta, avg)])

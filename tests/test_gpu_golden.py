@@ -1,0 +1,199 @@
+"""GPU parity: the drop-in aggregators (HIP path through libfsagg's C ABI)
+against the reference's own outputs (tests/golden, generated from
+FederatedScope v0.3.0 by tools/gen_golden.py) and the CPU oracle.
+
+Bars: FedAvg / async / online / interpolation / median / Krum average
+bit-exact; Krum & Bulyan selected indices exact; trimmed mean, Bulyan and
+norm bounding within the tolerance stated per test.
+"""
+from collections import OrderedDict
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from golden_io import case_names, load_case
+
+pytestmark = pytest.mark.gpu
+
+
+def to_torch(a, device='cuda'):
+    if isinstance(a, O.BF16):
+        return torch.from_numpy(a.bits.view(np.int16).copy()).view(
+            torch.bfloat16).to(device)
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+
+
+def to_np(t):
+    t = t.detach().cpu()
+    if t.dtype == torch.bfloat16:
+        return O.BF16(t.view(torch.int16).numpy().view(np.uint16))
+    return t.numpy()
+
+
+def feedback(clients, device='cuda'):
+    return [(s, OrderedDict((k, to_torch(v, device)) for k, v in d.items()))
+            for s, d in clients]
+
+
+def cfg(**kw):
+    bft = SimpleNamespace(krum_agg_num=kw.get('agg_num', 1),
+                          trimmedmean_excluded_ratio=kw.get('ratio', 0.1),
+                          normbounding_norm_bound=kw.get('bound', 1.0))
+    return SimpleNamespace(
+        federate=SimpleNamespace(ignore_weight=kw.get('iw', False),
+                                 use_ss=False,
+                                 client_num=kw.get('client_num', 1000),
+                                 sample_client_rate=kw.get('rate', 1.0)),
+        aggregator=SimpleNamespace(byzantine_node_num=kw.get('f', 0),
+                                   BFT_args=bft),
+        asyn=SimpleNamespace(staleness_discount_factor=kw.get('factor', 1.0)))
+
+
+class DictModel(torch.nn.Module):
+    def __init__(self, sd):
+        super().__init__()
+        self._sd = OrderedDict((k, to_torch(v, 'cpu')) for k, v in sd.items())
+
+    def state_dict(self, *a, **kw):
+        return OrderedDict((k, v.clone()) for k, v in self._sd.items())
+
+
+def bits(a):
+    if isinstance(a, O.BF16):
+        return a.bits.tobytes()
+    return np.ascontiguousarray(a).tobytes()
+
+
+def assert_bit_exact(got, want, what):
+    assert list(got.keys()) == list(want.keys()), what
+    for k in want:
+        g = to_np(got[k])
+        w = want[k]
+        if not isinstance(w, O.BF16):
+            assert g.dtype == np.asarray(w).dtype, (what, k, g.dtype)
+            assert g.shape == np.asarray(w).shape, (what, k)
+        assert bits(g) == bits(w), (what, k)
+
+
+@pytest.mark.parametrize('name', case_names('fedavg_'))
+def test_fedavg(name):
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    meta, clients, out, _, _ = load_case(name)
+    for dev in ('cuda', 'cpu'):   # device-resident and host-dict inputs
+        agg = ClientsAvgAggregator(config=cfg(iw=meta['ignore_weight']))
+        got = agg.aggregate({'client_feedback': feedback(clients, dev),
+                             'recover_fun': None})
+        assert_bit_exact(got, out, name + '/' + dev)
+        assert all(v.device.type == dev for v in got.values())
+
+
+@pytest.mark.parametrize('name', case_names('interp_'))
+def test_interpolate(name):
+    from federatedscope_amd.core.aggregators import \
+        ServerClientsInterpolateAggregator
+    meta, clients, out, init, _ = load_case(name)
+    agg = ServerClientsInterpolateAggregator(model=DictModel(init),
+                                             config=cfg(), beta=meta['beta'])
+    got = agg.aggregate({'client_feedback': feedback(clients)})
+    assert_bit_exact(got, out, name)
+
+
+@pytest.mark.parametrize('name', case_names('asyn_'))
+def test_asyn(name):
+    from federatedscope_amd.core.aggregators import AsynClientsAvgAggregator
+    meta, clients, out, init, _ = load_case(name)
+    agg = AsynClientsAvgAggregator(model=DictModel(init), config=cfg(
+        iw=meta['ignore_weight'], factor=meta['factor']))
+    got = agg.aggregate({
+        'client_feedback': feedback(clients),
+        'recover_fun': None,
+        'staleness': [(i, s) for i, s in enumerate(meta['staleness'])]
+    })
+    assert_bit_exact(got, out, name)
+
+
+@pytest.mark.parametrize('name', case_names('online_'))
+def test_online(name):
+    from federatedscope_amd.core.aggregators import \
+        OnlineClientsAvgAggregator
+    meta, clients, out, init, _ = load_case(name)
+    agg = OnlineClientsAvgAggregator(model=DictModel(init), config=cfg())
+    agg.reset()
+    for s, d in feedback(clients):
+        agg.inc((s, d))
+    assert_bit_exact(agg.aggregate({}), out, name)
+
+
+@pytest.mark.parametrize('name', case_names('krum_'))
+def test_krum(name):
+    from federatedscope_amd.core.aggregators import KrumAggregator
+    meta, clients, out, init, extra = load_case(name)
+    agg = KrumAggregator(model=DictModel(init), config=cfg(
+        f=meta['f'], agg_num=meta['agg_num'],
+        client_num=max(2 * meta['f'] + 3, 50)))
+    fb = feedback(clients)
+    D, _, _ = agg.distance_matrix(fb)
+    n = len(clients)
+    off = ~np.eye(n, dtype=bool)
+    # per-key sums in fp32 chunks + fp64 across chunks vs ATen's fp32 dist
+    np.testing.assert_allclose(D.numpy()[off], extra['D'][off], rtol=1e-5)
+    assert np.isinf(np.diag(D.numpy())).all()
+    got = agg.aggregate({'client_feedback': fb})
+    assert agg.last_selection == [int(i) for i in
+                                  extra['order'][:meta['agg_num']]]
+    assert_bit_exact(got, out, name)
+
+
+@pytest.mark.parametrize('name', case_names('orderstat_'))
+def test_median_and_trimmed(name):
+    from federatedscope_amd.core.aggregators import (MedianAggregator,
+                                                     TrimmedmeanAggregator)
+    meta, clients, out, init, extra = load_case(name)
+    fb = feedback(clients)
+    got = MedianAggregator(model=DictModel(init), config=cfg(f=1)).aggregate(
+        {'client_feedback': fb})
+    assert_bit_exact(got, out, name)
+    eps = np.finfo(np.float32).eps
+    for ratio in meta['tm_ratios']:
+        got = TrimmedmeanAggregator(model=DictModel(init), config=cfg(
+            f=1, ratio=ratio)).aggregate({'client_feedback': fb})
+        k = int(len(clients) * ratio)
+        tol = O.trimmed_tolerance(clients, k)
+        ours = O.add_init(init, O.trimmed_mean_update(clients, k))
+        for key in got:
+            g = to_np(got[key]).astype(np.float64)
+            ref = extra['tm|%s|%s' % (ratio, key)]
+            # vs the reference (ATen cascade sum): its own rounding bound
+            assert (np.abs(g - ref) <= tol[key] + 4 * eps * np.abs(ref)).all()
+            # vs the oracle's fp64 middle sum: a few ulps
+            assert (np.abs(g - ours[key]) <=
+                    4 * eps * (np.abs(ours[key]) + np.abs(init[key]))).all()
+
+
+@pytest.mark.parametrize('name', case_names('bulyan_'))
+def test_bulyan(name):
+    from federatedscope_amd.core.aggregators import BulyanAggregator
+    meta, clients, out, init, extra = load_case(name)
+    agg = BulyanAggregator(model=DictModel(init), config=cfg(
+        f=meta['f'], rate=meta['rate'], client_num=4 * meta['f'] + 3))
+    got = agg.aggregate({'client_feedback': feedback(clients)})
+    keep = len(clients) - int(2 * meta['rate'] * meta['f'])
+    assert agg.last_selection == [int(i) for i in extra['order'][:keep]]
+    for key in out:
+        np.testing.assert_allclose(to_np(got[key]), out[key], rtol=1e-5,
+                                   atol=1e-6)
+
+
+@pytest.mark.parametrize('name', case_names('normbound_'))
+def test_normbounding(name):
+    from federatedscope_amd.core.aggregators import NormboundingAggregator
+    meta, clients, out, init, _ = load_case(name)
+    agg = NormboundingAggregator(model=DictModel(init),
+                                 config=cfg(bound=meta['bound']))
+    got = agg.aggregate({'client_feedback': feedback(clients)})
+    for key in out:
+        np.testing.assert_allclose(to_np(got[key]), out[key], rtol=1e-6,
+                                   atol=1e-7)
