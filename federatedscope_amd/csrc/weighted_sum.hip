@@ -161,9 +161,12 @@ __global__ void wsum_f32_tail_kernel(const float *const *__restrict__ rows,
   out[p] = acc;
 }
 
-// Tunables of the streaming kernel (measured on MI355X).
-constexpr int kU = 8;  // client rows in flight per batch
-constexpr int kV = 2;  // f4 columns per thread
+// Tunables of the streaming kernel, picked by interleaved timing on MI355X
+// (tools/tune_wsum.py, profiles/r01_tune_wsum.txt): 2 client rows × 8 float4
+// columns in flight per lane (256 B/lane), nt loads — 6.53 TB/s at
+// 100 × 25M, equal to the chip's nt read-only stream.
+constexpr int kU = 2;  // client rows in flight per batch
+constexpr int kV = 8;  // f4 columns per thread
 
 template <bool PRE, bool BASE>
 void launch_wsum(const float *const *rows, const float *w, const float *pre,
@@ -190,6 +193,16 @@ __device__ __forceinline__ float bf2f(uint16_t b) {
   return __uint_as_float(uint32_t(b) << 16);
 }
 
+// ATen rounds x*w to float first and then to half (two roundings).  Left
+// alone, the backend fuses fptrunc(fmul) into one v_fma_mixlo_f16 (a single
+// rounding of the exact product), which differs in the last bit; the empty
+// asm makes the fp32 product a materialised value.
+__device__ __forceinline__ float mul_f32_materialized(float a, float b) {
+  float p = mul_rn(a, b);
+  asm volatile("" : "+v"(p));
+  return p;
+}
+
 template <int DT>
 __global__ __launch_bounds__(kBlock) void wsum_typed_kernel(
     const void *const *__restrict__ rows, const double *__restrict__ w, int n,
@@ -206,9 +219,9 @@ __global__ __launch_bounds__(kBlock) void wsum_typed_kernel(
       auto ld = [&](int i) {
         return __half2float(static_cast<const __half *>(rows[i])[p]);
       };
-      __half acc = __float2half(mul_rn(ld(0), float(w[0])));
+      __half acc = __float2half(mul_f32_materialized(ld(0), float(w[0])));
       for (int i = 1; i < n; ++i) {
-        __half t = __float2half(mul_rn(ld(i), float(w[i])));
+        __half t = __float2half(mul_f32_materialized(ld(i), float(w[i])));
         acc = __float2half(add_rn(__half2float(acc), __half2float(t)));
       }
       static_cast<__half *>(out)[p] = acc;
@@ -401,4 +414,81 @@ extern "C" int fsagg_fill_uniform_f32(float *X, int n, int64_t numel,
                      dim3(kBlock), 0, as_stream(stream), X, n, numel, ld, seed,
                      index_offset);
   return check_launch("fsagg_fill_uniform_f32");
+}
+
+// ---------------------------------------------------------------------------
+// Internal tuning entry points (tools/tune_wsum.py); not part of the ABI.
+// ---------------------------------------------------------------------------
+namespace fsagg {
+namespace {
+
+template <int U, int V, bool NT>
+void launch_variant(const float *const *rows, const float *w, int n,
+                    int64_t nvec, float *out, unsigned grid, hipStream_t s) {
+  const int64_t tiles = (nvec + int64_t(kBlock) * V - 1) / (int64_t(kBlock) * V);
+  if (grid == 0) grid = stream_grid(tiles, 1, 256 * 16);
+  hipLaunchKernelGGL((wsum_f32_vec_kernel<U, V, false, false, NT>),
+                     dim3(grid), dim3(kBlock), 0, s, rows, w, nullptr, n, nvec,
+                     nullptr, out);
+}
+
+// read-only stream: Σ of a buffer per thread, one float written per thread
+template <bool NT>
+__global__ __launch_bounds__(kBlock) void readbw_kernel(const f4 *__restrict__ x,
+                                                        int64_t nvec,
+                                                        float *__restrict__ out) {
+  f4 acc = f4{0.0f, 0.0f, 0.0f, 0.0f};
+  const int64_t stride = int64_t(gridDim.x) * kBlock;
+  int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  for (; q + 3 * stride < nvec; q += 4 * stride) {
+    const f4 a = ld4<NT>(x + q), b = ld4<NT>(x + q + stride),
+             c = ld4<NT>(x + q + 2 * stride), d = ld4<NT>(x + q + 3 * stride);
+    acc += a + b + c + d;
+  }
+  for (; q < nvec; q += stride) acc += ld4<NT>(x + q);
+  out[int64_t(blockIdx.x) * kBlock + threadIdx.x] = acc.x + acc.y + acc.z + acc.w;
+}
+
+}  // namespace
+}  // namespace fsagg
+
+extern "C" int fsagg_tune_wsum(int variant, unsigned grid,
+                               const float *const *rows, const float *w, int n,
+                               int64_t numel, float *out,
+                               fsagg_stream_t stream) {
+  using namespace fsagg;
+  hipStream_t s = as_stream(stream);
+  const int64_t nvec = numel / 4;
+  switch (variant) {
+    case 0: launch_variant<8, 2, true>(rows, w, n, nvec, out, grid, s); break;
+    case 1: launch_variant<2, 8, true>(rows, w, n, nvec, out, grid, s); break;
+    case 2: launch_variant<4, 8, true>(rows, w, n, nvec, out, grid, s); break;
+    case 3: launch_variant<1, 8, true>(rows, w, n, nvec, out, grid, s); break;
+    case 4: launch_variant<2, 16, true>(rows, w, n, nvec, out, grid, s); break;
+    case 5: launch_variant<1, 16, true>(rows, w, n, nvec, out, grid, s); break;
+    case 6: launch_variant<4, 4, true>(rows, w, n, nvec, out, grid, s); break;
+    case 7: launch_variant<3, 8, true>(rows, w, n, nvec, out, grid, s); break;
+    case 8: launch_variant<2, 8, false>(rows, w, n, nvec, out, grid, s); break;
+    case 9: launch_variant<1, 32, true>(rows, w, n, nvec, out, grid, s); break;
+    case 10: launch_variant<2, 12, true>(rows, w, n, nvec, out, grid, s); break;
+    case 11: launch_variant<3, 4, true>(rows, w, n, nvec, out, grid, s); break;
+    default: set_error("variant"); return FSAGG_EINVAL;
+  }
+  return check_launch("fsagg_tune_wsum");
+}
+
+extern "C" int fsagg_tune_readbw(int nt, unsigned grid, const float *x,
+                                 int64_t numel, float *out,
+                                 fsagg_stream_t stream) {
+  using namespace fsagg;
+  const int64_t nvec = numel / 4;
+  if (nt)
+    hipLaunchKernelGGL(readbw_kernel<true>, dim3(grid), dim3(kBlock), 0,
+                       as_stream(stream), reinterpret_cast<const f4 *>(x),
+                       nvec, out);
+  else
+    hipLaunchKernelGGL(readbw_kernel<false>, dim3(grid), dim3(kBlock), 0,
+                       as_stream(stream), reinterpret_cast<const f4 *>(x),
+                       nvec, out);
+  return check_launch("fsagg_tune_readbw");
 }

@@ -23,7 +23,7 @@ def to_torch(a, device='cuda'):
     if isinstance(a, O.BF16):
         return torch.from_numpy(a.bits.view(np.int16).copy()).view(
             torch.bfloat16).to(device)
-    return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+    return torch.from_numpy(np.array(a, copy=True)).to(device)
 
 
 def to_np(t):

@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of weighted-sum variants (rows in flight U ×
+float4 columns per lane V × nt loads × grid) on 100 × 25M, plus the
+read-only stream ceiling.  Prints one line per variant: median/min ms and
+GB/s.  GPU only; run through tools/gpu_job.sh."""
+import ctypes
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+from federatedscope_amd import _lib, ops  # noqa: E402
+
+VARIANTS = {0: 'U8V2nt', 1: 'U2V8nt', 2: 'U4V8nt', 3: 'U1V8nt', 4: 'U2V16nt',
+            5: 'U1V16nt', 6: 'U4V4nt', 7: 'U3V8nt', 8: 'U2V8', 9: 'U1V32nt',
+            10: 'U2V12nt', 11: 'U3V4nt'}
+
+
+def main():
+    n = int(os.environ.get('N', 100))
+    P = int(os.environ.get('P', 25_000_000))
+    rounds = int(os.environ.get('ROUNDS', 7))
+    lib = _lib.load()
+    lib.fsagg_tune_wsum.argtypes = [ctypes.c_int, ctypes.c_uint,
+                                    ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_int, ctypes.c_int64,
+                                    ctypes.c_void_p, ctypes.c_void_p]
+    lib.fsagg_tune_readbw.argtypes = [ctypes.c_int, ctypes.c_uint,
+                                      ctypes.c_void_p, ctypes.c_int64,
+                                      ctypes.c_void_p, ctypes.c_void_p]
+    dev = torch.device('cuda', 0)
+    slab = torch.empty((n, P), dtype=torch.float32, device=dev)
+    ops.fill_uniform(slab, P, seed=1)
+    rows = ops.RowTable.from_slab(slab)
+    w = torch.full((n, ), 1.0 / n, dtype=torch.float32, device=dev)
+    out = torch.empty(P, dtype=torch.float32, device=dev)
+    ref = torch.empty_like(out)
+    ops.weighted_sum(rows, w, ref)
+    st = torch.cuda.current_stream().cuda_stream
+    red = torch.empty(256 * 16 * 256 * 4, dtype=torch.float32, device=dev)
+    grids = [int(g) for g in os.environ.get('GRIDS', '0,2048').split(',')]
+    cases = []
+    for v in VARIANTS:
+        for g in grids:
+            cases.append(('wsum', v, g))
+    for nt in (0, 1):
+        for g in (4096, 8192, 16384):
+            cases.append(('read', nt, g))
+    times = {c: [] for c in cases}
+    for r in range(rounds):
+        for c in cases:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            if c[0] == 'wsum':
+                _lib.check(lib.fsagg_tune_wsum(c[1], c[2], rows.ptr(),
+                                               w.data_ptr(), n, P,
+                                               out.data_ptr(), st), 'tune')
+            else:
+                _lib.check(lib.fsagg_tune_readbw(c[1], c[2], slab.data_ptr(),
+                                                 n * P, red.data_ptr(), st),
+                           'readbw')
+            e1.record()
+            e1.synchronize()
+            times[c].append(e0.elapsed_time(e1))
+            if r == 0 and c[0] == 'wsum':
+                assert torch.equal(out, ref), c
+        print('round', r, 'done', file=sys.stderr, flush=True)
+    for c in cases:
+        t = times[c][1:]
+        med, mn = statistics.median(t), min(t)
+        nbytes = 4.0 * n * P + (4.0 * P if c[0] == 'wsum' else 0)
+        name = VARIANTS[c[1]] if c[0] == 'wsum' else ('read nt=%d' % c[1])
+        print('%-5s %-10s grid=%-5d med %.3f ms min %.3f ms  %.0f GB/s (med)'
+              % (c[0], name, c[2], med, mn, nbytes / med / 1e6))
+
+
+if __name__ == '__main__':
+    main()
