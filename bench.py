@@ -70,6 +70,59 @@ def cpu_baseline_leg(slab, n, P_sample, weights, out_dev):
     return t, exact
 
 
+def e2e_leg(args, dev, weights, sizes):
+    """Host state_dicts in, host state_dict out, through the drop-in
+    ClientsAvgAggregator (pinned double-buffered staging, H2D, kernel, D2H).
+    Reported on its own JSON line; never the bench `value`."""
+    from collections import OrderedDict
+    from types import SimpleNamespace
+
+    import torch
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    n = args.clients
+    if args.layout == 'resnet50':
+        with open(os.path.join(ROOT, 'tools', 'resnet50_layout.json')) as f:
+            keys = [(k, tuple(s)) for k, s in json.load(f)['keys']]
+    else:
+        keys = [('w', (args.params, ))]
+    P = sum(int(torch.Size(s).numel()) for _, s in keys)
+    log('e2e: building %d host clients x %d params (%d keys)' %
+        (n, P, len(keys)))
+    g = torch.Generator().manual_seed(0)
+    clients = [(sizes[i], OrderedDict((k, torch.rand(s, generator=g))
+                                      for k, s in keys)) for i in range(n)]
+    cfg = SimpleNamespace(federate=SimpleNamespace(ignore_weight=False,
+                                                   use_ss=False))
+    agg = ClientsAvgAggregator(device=dev, config=cfg)
+    info = {'client_feedback': clients, 'recover_fun': None}
+    agg.aggregate(info)
+    ts = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = agg.aggregate(info)
+        ts.append(time.perf_counter() - t0)
+        log('e2e aggregate %.3f s' % ts[-1])
+    # PCIe reference: one pinned 1 GB H2D
+    host = torch.empty(2**28, dtype=torch.float32, pin_memory=True)
+    d = torch.empty_like(host, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    d.copy_(host, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d = host.numel() * 4 / (time.perf_counter() - t0) / 1e9
+    t = min(ts)
+    rec = {'e2e': {
+        'what': 'ClientsAvgAggregator.aggregate, host dicts in/out',
+        'layout': args.layout, 'clients': n, 'params': P,
+        'keys': len(keys), 'seconds': round(t, 4),
+        'GBps_algorithmic': round(4.0 * n * P / t / 1e9, 3),
+        'pinned_h2d_GBps': round(h2d, 2),
+        'host_threads': torch.get_num_threads(),
+        'out_device': str(next(iter(out.values())).device)}}
+    print(json.dumps(rec), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -81,6 +134,9 @@ def main():
     ap.add_argument('--cpu-sample', type=int, default=5_000_000,
                     help='columns of the workload timed on the CPU baseline')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--e2e', action='store_true',
+                    help='also time host dicts -> aggregate() -> host dicts')
+    ap.add_argument('--layout', default='flat', choices=['flat', 'resnet50'])
     ap.add_argument('--traffic', default=os.path.join(
         ROOT, 'profiles', 'traffic_fedavg_c3.json'))
     args = ap.parse_args()
@@ -214,6 +270,10 @@ def main():
             'cpu_baseline': cpu,
         }
         print(json.dumps(rec), flush=True)
+    if args.e2e and world == 1:
+        del slab, rows
+        torch.cuda.empty_cache()
+        e2e_leg(args, dev, weights, sizes)
     if world > 1:
         dist.destroy_process_group()
 

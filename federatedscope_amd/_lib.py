@@ -36,6 +36,9 @@ SIGNATURES = {
     'fsagg_pairdist_workspace_bytes': (_c_sz, [_c_i, _c_i64, _c_i]),
     'fsagg_pairdist_f32': (_c_i, [_c_p, _c_i, _c_i64, _c_p, _c_i, _c_p, _c_p,
                                   _c_sz, _c_p]),
+    'fsagg_pairdist_segsq_f32': (_c_i, [_c_p, _c_i, _c_i64, _c_p, _c_i, _c_p,
+                                        _c_p, _c_sz, _c_p]),
+    'fsagg_pairdist_finish_f64': (_c_i, [_c_p, _c_i, _c_i, _c_p, _c_p]),
     'fsagg_rownorm_workspace_bytes': (_c_sz, [_c_i, _c_i64]),
     'fsagg_row_sqnorm_f32': (_c_i, [_c_p, _c_i, _c_i64, _c_p, _c_p, _c_sz,
                                     _c_p]),

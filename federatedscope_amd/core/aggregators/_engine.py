@@ -93,11 +93,10 @@ class DeviceEngine:
             st = ClientStack(layout, max(len(models), 1), self.compute_device)
             st.slab.zero_()
             self._stacks[key] = st
-        for i, m in enumerate(models):
-            if as_float:
-                m = OrderedDict((k, param2tensor(v).float())
-                                for k, v in m.items())
-            st.load(i, m)
+        if as_float:
+            models = [OrderedDict((k, param2tensor(v).float())
+                                  for k, v in m.items()) for m in models]
+        st.load_many(models)
         return st
 
     def _bucket(self, layout, model, as_float=False):

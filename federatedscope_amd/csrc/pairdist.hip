@@ -172,27 +172,48 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   }
 }
 
-__global__ __launch_bounds__(kBlock) void pairdist_final_kernel(
+// Σ over a segment's chunks (fixed chunk order, fp64) for every pair of the
+// tile layout; thread = (segment, tile pair, element): consecutive threads
+// read consecutive partials of one chunk (coalesced).  Output: the full
+// symmetric [nseg][n][n] matrix of per-key squared distances (diag 0).
+__global__ __launch_bounds__(kBlock) void pairdist_segsq_kernel(
     const float *__restrict__ partial, int n, PairPlan pl, int nseg,
-    const int *__restrict__ prefix, float *__restrict__ D) {
+    const int *__restrict__ prefix, double *__restrict__ segsq) {
+  const int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  const int64_t per_seg = int64_t(pl.ntp) * kTS * kTS;
+  if (q >= per_seg * nseg) return;
+  const int s = int(q / per_seg);
+  const int r = int(q - int64_t(s) * per_seg);
+  const int tp = r / (kTS * kTS), e = r % (kTS * kTS);
+  int ti, tj;
+  tp_to_tiles(tp, pl.nt, ti, tj);
+  const int i = ti * kTS + e / kTS, j = tj * kTS + e % kTS;
+  if (i >= n || j >= n || i >= j) return;
+  double sq = 0.0;
+  for (int c = prefix[s]; c < prefix[s + 1]; ++c)
+    sq += double(partial[int64_t(c) * per_seg + r]);
+  double *m = segsq + int64_t(s) * n * n;
+  m[int64_t(i) * n + j] = sq;
+  m[int64_t(j) * n + i] = sq;
+  if (i == 0 && j == 1) {
+    // the diagonal of this segment (one writer per segment)
+    for (int d = 0; d < n; ++d) m[int64_t(d) * n + d] = 0.0;
+  }
+}
+
+// D[a][b] = Σ_seg fl32(sqrt(segsq[seg][a][b])) accumulated in fp32 in key
+// order (the reference's `distance += torch.dist(...)`), D[a][a] = +inf.
+__global__ __launch_bounds__(kBlock) void pairdist_finish_kernel(
+    const double *__restrict__ segsq, int n, int nseg, float *__restrict__ D) {
   const int q = blockIdx.x * kBlock + threadIdx.x;
   if (q >= n * n) return;
-  const int a = q / n, b = q - (q / n) * n;
-  if (a == b) {
+  if (q / n == q % n) {
     D[q] = __builtin_inff();
     return;
   }
-  const int i = a < b ? a : b, j = a < b ? b : a;
-  const int ti = i / kTS, tj = j / kTS, u = i % kTS, v = j % kTS;
-  const int tp = ti * pl.nt - ti * (ti - 1) / 2 + (tj - ti);
-  const int e = u * kTS + v;
   float dist = 0.0f;
-  for (int s = 0; s < nseg; ++s) {
-    double sq = 0.0;
-    for (int c = prefix[s]; c < prefix[s + 1]; ++c)
-      sq += double(partial[(int64_t(c) * pl.ntp + tp) * (kTS * kTS) + e]);
-    dist = add_rn(dist, float(sqrt(sq)));
-  }
+  for (int s = 0; s < nseg; ++s)
+    dist = add_rn(dist, float(sqrt(segsq[int64_t(s) * n * n + q])));
   D[q] = dist;
 }
 
@@ -256,7 +277,31 @@ extern "C" size_t fsagg_pairdist_workspace_bytes(int n, int64_t numel,
   const PairPlan pl = make_plan(n, numel, nseg);
   return align256(sizeof(int) * size_t(nseg + 1)) +
          align256(sizeof(float) * size_t(pl.max_chunks) * size_t(pl.ntp) *
-                  kTS * kTS);
+                  kTS * kTS) +
+         align256(sizeof(double) * size_t(nseg) * size_t(n) * size_t(n));
+}
+
+// Enqueue the chunk and per-segment kernels; segsq receives [nseg][n][n].
+static int pairdist_segsq_impl(const float *const *rows, int n, int64_t numel,
+                               const int64_t *seg_off, int nseg,
+                               double *segsq, void *workspace,
+                               hipStream_t s) {
+  const PairPlan pl = make_plan(n, numel, nseg);
+  int *prefix = static_cast<int *>(workspace);
+  float *partial = reinterpret_cast<float *>(
+      static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)));
+  hipLaunchKernelGGL(chunk_prefix_kernel, dim3(1), dim3(1), 0, s, seg_off,
+                     nseg, pl.chl, prefix);
+  if (numel > 0)
+    hipLaunchKernelGGL(pairdist_chunk_kernel,
+                       dim3(unsigned(pl.max_chunks), unsigned(pl.groups)),
+                       dim3(kBlock), 0, s, rows, n, pl, seg_off, nseg, prefix,
+                       partial);
+  const int64_t items = int64_t(pl.ntp) * kTS * kTS * nseg;
+  hipLaunchKernelGGL(pairdist_segsq_kernel,
+                     dim3(unsigned((items + kBlock - 1) / kBlock)),
+                     dim3(kBlock), 0, s, partial, n, pl, nseg, prefix, segsq);
+  return FSAGG_OK;
 }
 
 extern "C" int fsagg_pairdist_f32(const float *const *rows, int n,
@@ -274,22 +319,51 @@ extern "C" int fsagg_pairdist_f32(const float *const *rows, int n,
               need);
     return FSAGG_ESPACE;
   }
-  const PairPlan pl = make_plan(n, numel, nseg);
   hipStream_t s = as_stream(stream);
-  int *prefix = static_cast<int *>(workspace);
-  float *partial = reinterpret_cast<float *>(
-      static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)));
-  hipLaunchKernelGGL(chunk_prefix_kernel, dim3(1), dim3(1), 0, s, seg_off,
-                     nseg, pl.chl, prefix);
-  if (numel > 0)
-    hipLaunchKernelGGL(pairdist_chunk_kernel,
-                       dim3(unsigned(pl.max_chunks), unsigned(pl.groups)),
-                       dim3(kBlock), 0, s, rows, n, pl, seg_off, nseg, prefix,
-                       partial);
-  hipLaunchKernelGGL(pairdist_final_kernel,
+  const PairPlan pl = make_plan(n, numel, nseg);
+  double *segsq = reinterpret_cast<double *>(
+      static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)) +
+      align256(sizeof(float) * size_t(pl.max_chunks) * size_t(pl.ntp) * kTS *
+               kTS));
+  pairdist_segsq_impl(rows, n, numel, seg_off, nseg, segsq, workspace, s);
+  hipLaunchKernelGGL(pairdist_finish_kernel,
                      dim3(unsigned((n * n + kBlock - 1) / kBlock)),
-                     dim3(kBlock), 0, s, partial, n, pl, nseg, prefix, D);
+                     dim3(kBlock), 0, s, segsq, n, nseg, D);
   return check_launch("fsagg_pairdist_f32");
+}
+
+extern "C" int fsagg_pairdist_segsq_f32(const float *const *rows, int n,
+                                        int64_t numel, const int64_t *seg_off,
+                                        int nseg, double *segsq,
+                                        void *workspace,
+                                        size_t workspace_bytes,
+                                        fsagg_stream_t stream) {
+  if (!rows || !seg_off || !segsq || n < 2 || nseg < 1 || numel < 0) {
+    set_error("fsagg_pairdist_segsq_f32: invalid argument (n=%d nseg=%d)", n,
+              nseg);
+    return FSAGG_EINVAL;
+  }
+  const size_t need = fsagg_pairdist_workspace_bytes(n, numel, nseg);
+  if (!workspace || workspace_bytes < need) {
+    set_error("fsagg_pairdist_segsq_f32: workspace %zu < %zu bytes",
+              workspace_bytes, need);
+    return FSAGG_ESPACE;
+  }
+  pairdist_segsq_impl(rows, n, numel, seg_off, nseg, segsq, workspace,
+                      as_stream(stream));
+  return check_launch("fsagg_pairdist_segsq_f32");
+}
+
+extern "C" int fsagg_pairdist_finish_f64(const double *segsq, int n, int nseg,
+                                         float *D, fsagg_stream_t stream) {
+  if (!segsq || !D || n < 2 || nseg < 1) {
+    set_error("fsagg_pairdist_finish_f64: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  hipLaunchKernelGGL(pairdist_finish_kernel,
+                     dim3(unsigned((n * n + kBlock - 1) / kBlock)),
+                     dim3(kBlock), 0, as_stream(stream), segsq, n, nseg, D);
+  return check_launch("fsagg_pairdist_finish_f64");
 }
 
 extern "C" size_t fsagg_rownorm_workspace_bytes(int n, int64_t numel) {

@@ -10,11 +10,11 @@
 // selected subsets all stream without a gather copy.  Bytes per element:
 // 4·n read + 4 written (+4 read for the fused `base` add) — the whole kernel
 // is HBM-bound (0.5 FLOP/B), so the design goal is pure streaming:
-//   * each thread owns V f4 columns of the bucket (16 B/lane, 1 KiB per
-//     wave-instruction per row, fully coalesced);
-//   * the client loop issues U rows' loads before consuming any of them, so
-//     U·V·16 B are in flight per lane; the adds still happen strictly in
-//     client order, which keeps the result bit-identical to the reference;
+//   * each thread owns V float4 columns of the bucket (16 B/lane, 1 KiB per
+//     wave-instruction per row, fully coalesced), V up to 24: 384 B of one
+//     client row in flight per lane before any of it is consumed;
+//   * the adds happen strictly in client order, which keeps the result
+//     bit-identical to the reference;
 //   * row pointers and weights are wave-uniform → scalar (SGPR) loads.
 #include <hip/hip_fp16.h>
 
@@ -140,6 +140,29 @@ __global__ __launch_bounds__(kBlock) void wsum_f32_vec_kernel(
   }
 }
 
+// Block-contiguous partition: block b streams float4 columns
+// [b·chunk, (b+1)·chunk) in tiles of kBlock·V.  With grid = (resident blocks
+// per CU) × 256 every CU gets the same byte count, so no CU idles through a
+// tail wave while the others finish (the tile-granular grid-stride form
+// leaves up to one tile-round of imbalance).
+template <int U, int V, bool PRE, bool BASE, bool NT>
+__global__ __launch_bounds__(kBlock) void wsum_f32_part_kernel(
+    const float *const *__restrict__ rows, const float *__restrict__ w,
+    const float *__restrict__ pre, int n, int64_t nvec, int64_t chunk,
+    const float *__restrict__ base, float *__restrict__ out) {
+  constexpr int64_t tile = int64_t(kBlock) * V;
+  const int64_t lo = int64_t(blockIdx.x) * chunk;
+  const int64_t hi = lo + chunk < nvec ? lo + chunk : nvec;
+  for (int64_t t0 = lo; t0 < hi; t0 += tile) {
+    if (t0 + tile <= hi)
+      wsum_tile<U, V, PRE, BASE, NT, false>(rows, w, pre, n, hi, t0, base,
+                                            out);
+    else
+      wsum_tile<U, V, PRE, BASE, NT, true>(rows, w, pre, n, hi, t0, base,
+                                           out);
+  }
+}
+
 // Scalar tail: elements [start, numel) (fewer than 4), one thread each.
 __global__ void wsum_f32_tail_kernel(const float *const *__restrict__ rows,
                                      const float *__restrict__ w,
@@ -161,22 +184,42 @@ __global__ void wsum_f32_tail_kernel(const float *const *__restrict__ rows,
   out[p] = acc;
 }
 
-// Tunables of the streaming kernel, picked by interleaved timing on MI355X
-// (tools/tune_wsum.py, profiles/r01_tune_wsum.txt): 2 client rows × 8 float4
-// columns in flight per lane (256 B/lane), nt loads — 6.53 TB/s at
-// 100 × 25M, equal to the chip's nt read-only stream.
-constexpr int kU = 2;  // client rows in flight per batch
-constexpr int kV = 8;  // f4 columns per thread
+// Launch shape of the streaming kernel, from interleaved timing on MI355X
+// (tools/tune_wsum.py; profiles/r01_tune_wsum_box*.txt).  One client row in
+// flight (U = 1) and V float4 columns per lane; V is the largest that still
+// gives >= ~1000 one-tile workgroups (≈ 2 rounds of the 2 × 256 resident
+// workgroups at the ~200 VGPRs V = 24 needs).  At 100 × 25M that is V = 24,
+// 1018 workgroups: 1.43–1.45 ms = 6.95–7.08 TB/s on two boxes, above the
+// chip's plain nt read stream (6.5–6.7 TB/s); V = 20 (1221 workgroups,
+// a ragged third round) loses 25 %.
+constexpr int kU = 1;
+
+template <bool PRE, bool BASE, int V>
+void launch_wsum_v(const float *const *rows, const float *w, const float *pre,
+                   int n, int64_t nvec, const float *base, float *out,
+                   hipStream_t s) {
+  const int64_t tiles = (nvec + int64_t(kBlock) * V - 1) / (int64_t(kBlock) * V);
+  const unsigned grid = stream_grid(tiles, 1, 256 * 16);
+  hipLaunchKernelGGL((wsum_f32_vec_kernel<kU, V, PRE, BASE, true>),
+                     dim3(grid), dim3(kBlock), 0, s, rows, w, pre, n, nvec,
+                     base, out);
+}
 
 template <bool PRE, bool BASE>
 void launch_wsum(const float *const *rows, const float *w, const float *pre,
                  int n, int64_t nvec, const float *base, float *out,
                  hipStream_t s) {
-  const int64_t tiles = (nvec + int64_t(kBlock) * kV - 1) / (int64_t(kBlock) * kV);
-  const unsigned grid = stream_grid(tiles, 1, 256 * 16);
-  hipLaunchKernelGGL((wsum_f32_vec_kernel<kU, kV, PRE, BASE, true>),
-                     dim3(grid), dim3(kBlock), 0, s, rows, w, pre, n, nvec,
-                     base, out);
+  auto tiles = [&](int v) { return (nvec + 256 * v - 1) / (256 * v); };
+  if (tiles(24) >= 1000)
+    launch_wsum_v<PRE, BASE, 24>(rows, w, pre, n, nvec, base, out, s);
+  else if (tiles(16) >= 1000)
+    launch_wsum_v<PRE, BASE, 16>(rows, w, pre, n, nvec, base, out, s);
+  else if (tiles(8) >= 1000)
+    launch_wsum_v<PRE, BASE, 8>(rows, w, pre, n, nvec, base, out, s);
+  else if (tiles(4) >= 1000)
+    launch_wsum_v<PRE, BASE, 4>(rows, w, pre, n, nvec, base, out, s);
+  else
+    launch_wsum_v<PRE, BASE, 1>(rows, w, pre, n, nvec, base, out, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -469,12 +512,40 @@ extern "C" int fsagg_tune_wsum(int variant, unsigned grid,
     case 6: launch_variant<4, 4, true>(rows, w, n, nvec, out, grid, s); break;
     case 7: launch_variant<3, 8, true>(rows, w, n, nvec, out, grid, s); break;
     case 8: launch_variant<2, 8, false>(rows, w, n, nvec, out, grid, s); break;
-    case 9: launch_variant<1, 32, true>(rows, w, n, nvec, out, grid, s); break;
-    case 10: launch_variant<2, 12, true>(rows, w, n, nvec, out, grid, s); break;
-    case 11: launch_variant<3, 4, true>(rows, w, n, nvec, out, grid, s); break;
+    case 9: launch_variant<1, 12, true>(rows, w, n, nvec, out, grid, s); break;
+    case 10: launch_variant<1, 20, true>(rows, w, n, nvec, out, grid, s); break;
+    case 11: launch_variant<1, 24, true>(rows, w, n, nvec, out, grid, s); break;
     default: set_error("variant"); return FSAGG_EINVAL;
   }
   return check_launch("fsagg_tune_wsum");
+}
+
+extern "C" int fsagg_tune_wsum_part(int variant, unsigned grid,
+                                    const float *const *rows, const float *w,
+                                    int n, int64_t numel, float *out,
+                                    fsagg_stream_t stream) {
+  using namespace fsagg;
+  hipStream_t s = as_stream(stream);
+  const int64_t nvec = numel / 4;
+  int64_t chunk = (nvec + grid - 1) / grid;
+  chunk = (chunk + 63) / 64 * 64;
+#define FSAGG_TP(U, V)                                                        \
+  hipLaunchKernelGGL((wsum_f32_part_kernel<U, V, false, false, true>),       \
+                     dim3(grid), dim3(kBlock), 0, s, rows, w, nullptr, n,    \
+                     nvec, chunk, nullptr, out)
+  switch (variant) {
+    case 0: FSAGG_TP(1, 8); break;
+    case 1: FSAGG_TP(1, 12); break;
+    case 2: FSAGG_TP(1, 16); break;
+    case 3: FSAGG_TP(1, 24); break;
+    case 4: FSAGG_TP(2, 8); break;
+    case 5: FSAGG_TP(2, 12); break;
+    case 6: FSAGG_TP(1, 32); break;
+    case 7: FSAGG_TP(4, 4); break;
+    default: set_error("variant"); return FSAGG_EINVAL;
+  }
+#undef FSAGG_TP
+  return check_launch("fsagg_tune_wsum_part");
 }
 
 extern "C" int fsagg_tune_readbw(int nt, unsigned grid, const float *x,

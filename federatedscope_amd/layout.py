@@ -61,13 +61,15 @@ class BucketLayout:
     def pack_host(self, model, out):
         """Copy the fp32 keys of ``model`` into the flat CPU tensor ``out``
         (padding and missing keys zero)."""
-        out.zero_()
-        for k in self.keys:
-            if k not in model:
-                continue
-            t = param2tensor(model[k])
+        ends = [self.offsets[k] for k in self.keys[1:]] + [self.numel]
+        for k, end in zip(self.keys, ends):
             o, m = self.offsets[k], self.numels[k]
-            out[o:o + m].copy_(t.reshape(-1))
+            if k not in model:
+                out[o:end].zero_()
+                continue
+            out[o:o + m].copy_(param2tensor(model[k]).reshape(-1))
+            if end > o + m:
+                out[o + m:end].zero_()
         return out
 
     def pack_device(self, model, out_row):
@@ -84,11 +86,10 @@ class BucketLayout:
                 o, m = self.offsets[k], self.numels[k]
                 out_row[o:o + m].copy_(t.reshape(-1), non_blocking=True)
             return out_row
-        host = _pinned(self.numel)
-        self.pack_host(model, host)
-        out_row.copy_(host, non_blocking=True)
-        # the pinned staging buffer is reused: wait for this copy to land
-        torch.cuda.current_stream(out_row.device).synchronize()
+        st = HostStager(out_row.device, nbuf=1)
+        st.put(self, model, out_row)
+        st.finish()
+        st.events[0].synchronize()
         return out_row
 
     def unpack(self, flat, keys=None):
@@ -103,12 +104,47 @@ class BucketLayout:
 _PINNED = {}
 
 
-def _pinned(numel):
-    b = _PINNED.get('buf')
+def _pinned(numel, slot=0):
+    b = _PINNED.get(slot)
     if b is None or b.numel() < numel:
         b = torch.empty(numel, dtype=torch.float32, pin_memory=True)
-        _PINNED['buf'] = b
+        _PINNED[slot] = b
     return b[:numel]
+
+
+class HostStager:
+    """Double-buffered host→device staging of client buckets.
+
+    Packing client i+1 into one pinned buffer (a multi-threaded host copy)
+    overlaps the DMA of client i out of the other buffer; the copies run on
+    a side stream and the consumer stream waits on it once at the end."""
+
+    def __init__(self, device, nbuf=2):
+        self.device = torch.device(device)
+        self.stream = torch.cuda.Stream(self.device)
+        # the rows being overwritten may still be read by kernels queued on
+        # the consumer stream (the stack is reused across rounds)
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        self.nbuf = nbuf
+        self.events = [None] * nbuf
+        self.i = 0
+
+    def put(self, layout, model, dst_row):
+        slot = self.i % self.nbuf
+        self.i += 1
+        ev = self.events[slot]
+        if ev is not None:
+            ev.synchronize()          # the DMA that last read this buffer
+        host = _pinned(layout.numel, slot)
+        layout.pack_host(model, host)
+        with torch.cuda.stream(self.stream):
+            dst_row.copy_(host, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        self.events[slot] = ev
+
+    def finish(self):
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
 
 
 class ClientStack:
@@ -131,6 +167,22 @@ class ClientStack:
 
     def load(self, i, model):
         self.layout.pack_device(model, self.slab[i])
+
+    def load_many(self, models):
+        """Stage every client: device-resident dicts by device copies, host
+        dicts through the double-buffered pinned stager."""
+        stager = None
+        for i, m in enumerate(models):
+            on_host = any(param2tensor(m[k]).device.type != 'cuda'
+                          for k in self.layout.keys if k in m)
+            if on_host:
+                if stager is None:
+                    stager = HostStager(self.device)
+                stager.put(self.layout, m, self.slab[i])
+            else:
+                self.layout.pack_device(m, self.slab[i])
+        if stager is not None:
+            stager.finish()
 
     def rows(self, idx=None, key=None):
         from .ops import RowTable

@@ -276,6 +276,47 @@ def pairdist(rows, seg_offsets, workspace=None):
     return D
 
 
+def pairdist_segsq(rows, seg_offsets, workspace=None):
+    """Per-key squared pair distances [nseg][n][n] (fp64, device) — the
+    shard-local half of Krum's distance matrix (summed across ranks by the
+    caller, then :func:`pairdist_finish`)."""
+    if rows.n < 2:
+        raise ValueError('Krum needs at least two clients')
+    offs = [int(o) for o in seg_offsets]
+    if offs[0] != 0 or offs[-1] != rows.numel or \
+            any(b < a for a, b in zip(offs, offs[1:])):
+        raise ValueError('segment offsets must rise from 0 to numel')
+    nseg = len(offs) - 1
+    lib = L.load()
+    need = lib.fsagg_pairdist_workspace_bytes(rows.n, rows.numel, nseg)
+    ws = (workspace or _WS).get(rows.device, need)
+    seg = torch.tensor(offs, dtype=torch.int64, device=rows.device)
+    sq = torch.empty((nseg, rows.n, rows.n), dtype=torch.float64,
+                     device=rows.device)
+    L.check(lib.fsagg_pairdist_segsq_f32(rows.ptr(), rows.n, rows.numel,
+                                         seg.data_ptr(), nseg, sq.data_ptr(),
+                                         ws.data_ptr(), ws.numel(),
+                                         _stream(rows.device)),
+            'fsagg_pairdist_segsq_f32')
+    return sq
+
+
+def pairdist_finish(segsq):
+    """D[a][b] = Σ_seg fl32(sqrt(segsq[seg][a][b])), D[a][a] = +inf."""
+    if segsq.dtype != torch.float64 or segsq.dim() != 3 or \
+            segsq.shape[1] != segsq.shape[2] or segsq.device.type != 'cuda' \
+            or not segsq.is_contiguous():
+        raise ValueError('segsq must be a contiguous [nseg][n][n] float64 '
+                         'GPU tensor')
+    nseg, n, _ = segsq.shape
+    D = torch.empty((n, n), dtype=torch.float32, device=segsq.device)
+    L.check(L.load().fsagg_pairdist_finish_f64(segsq.data_ptr(), n, nseg,
+                                               D.data_ptr(),
+                                               _stream(segsq.device)),
+            'fsagg_pairdist_finish_f64')
+    return D
+
+
 def row_sqnorm(rows, workspace=None):
     """Per-row Σx² in float64 (device tensor [n])."""
     lib = L.load()

@@ -141,6 +141,22 @@ int fsagg_pairdist_f32(const float *const *rows, int n, int64_t numel,
                        fsagg_stream_t stream);
 
 /*
+ * The two halves of fsagg_pairdist_f32, for the multi-GPU (parameter-range
+ * sharded) Krum: every rank computes per-key squared distances over its own
+ * coordinate range, the [nseg][n][n] fp64 partials are summed across ranks
+ * (one RCCL all-reduce — the path's only exchange step), and every rank
+ * finishes D from the summed partials.
+ *   segsq (device) nseg*n*n doubles: Σ_{p in seg} (x_a[p]-x_b[p])^2, diag 0.
+ *   Workspace: fsagg_pairdist_workspace_bytes(n, numel, nseg).
+ */
+int fsagg_pairdist_segsq_f32(const float *const *rows, int n, int64_t numel,
+                             const int64_t *seg_off, int nseg, double *segsq,
+                             void *workspace, size_t workspace_bytes,
+                             fsagg_stream_t stream);
+int fsagg_pairdist_finish_f64(const double *segsq, int n, int nseg, float *D,
+                              fsagg_stream_t stream);
+
+/*
  * Per-row squared L2 norm in fp64 (deterministic two-level reduction):
  * sq[i] = Σ_p x_i[p]^2.  The norm of NormboundingAggregator's flattened update
  * (normbounding_aggregator.py:39-41, torch.norm(param, p=2)).

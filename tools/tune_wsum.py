@@ -13,8 +13,11 @@ import torch  # noqa: E402
 from federatedscope_amd import _lib, ops  # noqa: E402
 
 VARIANTS = {0: 'U8V2nt', 1: 'U2V8nt', 2: 'U4V8nt', 3: 'U1V8nt', 4: 'U2V16nt',
-            5: 'U1V16nt', 6: 'U4V4nt', 7: 'U3V8nt', 8: 'U2V8', 9: 'U1V32nt',
-            10: 'U2V12nt', 11: 'U3V4nt'}
+            5: 'U1V16nt', 6: 'U4V4nt', 7: 'U3V8nt', 8: 'U2V8', 9: 'U1V12nt',
+            10: 'U1V20nt', 11: 'U1V24nt'}
+
+PART = {0: 'U1V8', 1: 'U1V12', 2: 'U1V16', 3: 'U1V24', 4: 'U2V8', 5: 'U2V12',
+        6: 'U1V32', 7: 'U4V4'}
 
 
 def main():
@@ -26,6 +29,7 @@ def main():
                                     ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_int, ctypes.c_int64,
                                     ctypes.c_void_p, ctypes.c_void_p]
+    lib.fsagg_tune_wsum_part.argtypes = lib.fsagg_tune_wsum.argtypes
     lib.fsagg_tune_readbw.argtypes = [ctypes.c_int, ctypes.c_uint,
                                       ctypes.c_void_p, ctypes.c_int64,
                                       ctypes.c_void_p, ctypes.c_void_p]
@@ -41,9 +45,14 @@ def main():
     red = torch.empty(256 * 16 * 256 * 4, dtype=torch.float32, device=dev)
     grids = [int(g) for g in os.environ.get('GRIDS', '0,2048').split(',')]
     cases = []
-    for v in VARIANTS:
+    for v in [int(x) for x in os.environ.get('VARS', ','.join(
+            str(k) for k in VARIANTS)).split(',')]:
         for g in grids:
             cases.append(('wsum', v, g))
+    for v in PART:
+        for g in [int(x) for x in os.environ.get(
+                'PGRIDS', '256,512,768,1024,2048').split(',')]:
+            cases.append(('part', v, g))
     for nt in (0, 1):
         for g in (4096, 8192, 16384):
             cases.append(('read', nt, g))
@@ -53,7 +62,12 @@ def main():
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record()
-            if c[0] == 'wsum':
+            if c[0] == 'part':
+                _lib.check(lib.fsagg_tune_wsum_part(c[1], c[2], rows.ptr(),
+                                                    w.data_ptr(), n, P,
+                                                    out.data_ptr(), st),
+                           'tune_part')
+            elif c[0] == 'wsum':
                 _lib.check(lib.fsagg_tune_wsum(c[1], c[2], rows.ptr(),
                                                w.data_ptr(), n, P,
                                                out.data_ptr(), st), 'tune')
@@ -64,14 +78,15 @@ def main():
             e1.record()
             e1.synchronize()
             times[c].append(e0.elapsed_time(e1))
-            if r == 0 and c[0] == 'wsum':
+            if r == 0 and c[0] in ('wsum', 'part'):
                 assert torch.equal(out, ref), c
         print('round', r, 'done', file=sys.stderr, flush=True)
     for c in cases:
         t = times[c][1:]
         med, mn = statistics.median(t), min(t)
-        nbytes = 4.0 * n * P + (4.0 * P if c[0] == 'wsum' else 0)
-        name = VARIANTS[c[1]] if c[0] == 'wsum' else ('read nt=%d' % c[1])
+        nbytes = 4.0 * n * P + (4.0 * P if c[0] != 'read' else 0)
+        name = {'wsum': VARIANTS, 'part': PART}[c[0]][c[1]] \
+            if c[0] != 'read' else ('read nt=%d' % c[1])
         print('%-5s %-10s grid=%-5d med %.3f ms min %.3f ms  %.0f GB/s (med)'
               % (c[0], name, c[2], med, mn, nbytes / med / 1e6))
 
