@@ -22,7 +22,7 @@ def ctypes_ptr(x):
     return int(x) if x else None
 
 
-def _check_f32_cuda(t, what):
+def _check_f32_cuda(t, what, align=ALIGN_BYTES):
     if not isinstance(t, torch.Tensor):
         raise TypeError('%s must be a torch.Tensor' % what)
     if t.device.type != 'cuda':
@@ -31,8 +31,8 @@ def _check_f32_cuda(t, what):
         raise ValueError('%s must be float32 (got %s)' % (what, t.dtype))
     if not t.is_contiguous():
         raise ValueError('%s must be contiguous' % what)
-    if t.data_ptr() % ALIGN_BYTES:
-        raise ValueError('%s must be 16-byte aligned' % what)
+    if t.data_ptr() % align:
+        raise ValueError('%s must be %d-byte aligned' % (what, align))
 
 
 class RowTable:
@@ -47,9 +47,12 @@ class RowTable:
         if len(ptrs) < 1:
             raise ValueError('RowTable needs at least one row')
         for p in ptrs:
-            if p % ALIGN_BYTES:
-                raise ValueError('client row pointer 0x%x is not 16-byte '
+            if p % 4:
+                raise ValueError('client row pointer 0x%x is not 4-byte '
                                  'aligned' % p)
+        # the streaming weighted sum reads 16 B per lane; the order-statistic
+        # and distance kernels read 4 B per lane and take any fp32 row
+        self.aligned16 = all(p % ALIGN_BYTES == 0 for p in ptrs)
         self.ptrs = list(ptrs)
         self.n = len(ptrs)
         self.numel = int(numel)
@@ -61,7 +64,7 @@ class RowTable:
     @classmethod
     def from_slab(cls, slab, rows=None, col_offset=0, numel=None):
         """Rows of a 2-D [n][ld] fp32 slab; ``rows`` selects/reorders."""
-        _check_f32_cuda(slab, 'slab')
+        _check_f32_cuda(slab, 'slab', align=4)
         if slab.dim() != 2:
             raise ValueError('slab must be 2-D [clients, ld]')
         n, ld = slab.shape
@@ -88,7 +91,7 @@ class RowTable:
         numel = m - offset if numel is None else int(numel)
         ptrs = []
         for i, t in enumerate(tensors):
-            _check_f32_cuda(t, 'client tensor %d' % i)
+            _check_f32_cuda(t, 'client tensor %d' % i, align=4)
             if t.device != dev:
                 raise ValueError('client tensors on different devices')
             if offset + numel > t.numel():
@@ -105,8 +108,8 @@ def _fp32_dev(values, device):
                         device=device)
 
 
-def _check_out(out, numel, device, what='out'):
-    _check_f32_cuda(out, what)
+def _check_out(out, numel, device, what='out', align=ALIGN_BYTES):
+    _check_f32_cuda(out, what, align=align)
     if out.device != device:
         raise ValueError('%s on %s, rows on %s' % (what, out.device, device))
     if out.numel() < numel:
@@ -121,6 +124,9 @@ def weighted_sum(rows, weights, out, prescale=None, base=None, stream=None):
     are rounded to fp32 here exactly as ATen reads a wrapped scalar."""
     if len(weights) != rows.n:
         raise ValueError('%d weights for %d rows' % (len(weights), rows.n))
+    if not rows.aligned16:
+        raise ValueError('weighted_sum needs 16-byte aligned client rows '
+                         '(pack them with BucketLayout / ClientStack)')
     _check_out(out, rows.numel, rows.device)
     if base is not None:
         _check_out(base, rows.numel, rows.device, 'base')
@@ -209,9 +215,9 @@ def add(a, b, out):
 
 
 def coord_median(rows, out, base=None):
-    _check_out(out, rows.numel, rows.device)
+    _check_out(out, rows.numel, rows.device, align=4)
     if base is not None:
-        _check_out(base, rows.numel, rows.device, 'base')
+        _check_out(base, rows.numel, rows.device, 'base', align=4)
     L.check(L.load().fsagg_coord_median_f32(
         rows.ptr(), rows.n, rows.numel,
         base.data_ptr() if base is not None else None, out.data_ptr(),
@@ -223,9 +229,9 @@ def trimmed_mean(rows, k, out, divisor=None, base=None):
     if k < 0 or 2 * k >= rows.n:
         raise ValueError('trimmed mean needs 0 <= 2k < n (k=%d n=%d)' %
                          (k, rows.n))
-    _check_out(out, rows.numel, rows.device)
+    _check_out(out, rows.numel, rows.device, align=4)
     if base is not None:
-        _check_out(base, rows.numel, rows.device, 'base')
+        _check_out(base, rows.numel, rows.device, 'base', align=4)
     div = float(rows.n - 2 * k if divisor is None else divisor)
     L.check(L.load().fsagg_trimmed_mean_f32(
         rows.ptr(), rows.n, rows.numel, int(k), div,
