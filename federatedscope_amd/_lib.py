@@ -46,6 +46,22 @@ SIGNATURES = {
                                       ctypes.c_uint64, _c_i64, _c_p]),
 }
 
+
+
+class OptParams(ctypes.Structure):
+    """struct fsagg_opt_params (include/fsagg.h)."""
+    _fields_ = [('kind', _c_i), ('flags', _c_i), ('lr', _c_f),
+                ('momentum', _c_f), ('dampening', _c_f),
+                ('weight_decay', _c_f), ('beta1', _c_f), ('beta2', _c_f),
+                ('eps', _c_f), ('step_size', _c_f),
+                ('bias_correction2_sqrt', _c_f)]
+
+
+FSAGG_OPT_SGD, FSAGG_OPT_ADAM = 0, 1
+FSAGG_OPT_NESTEROV, FSAGG_OPT_FIRST_STEP = 1, 2
+SIGNATURES['fsagg_server_opt_step_f32'] = (
+    _c_i, [_c_p, _c_p, _c_p, _c_p, _c_i64, ctypes.POINTER(OptParams), _c_p])
+
 _lib = None
 
 

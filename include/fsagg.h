@@ -168,6 +168,29 @@ int fsagg_row_sqnorm_f32(const float *const *rows, int n, int64_t numel,
                          fsagg_stream_t stream);
 
 /*
+ * FedOpt server step on the aggregated bucket (fedopt_aggregator.py:26-44):
+ * per element g = param - avg, then one torch.optim step in place on param
+ * and the optimizer state buckets (SGD: state0 = momentum buffer; Adam:
+ * state0 = exp_avg, state1 = exp_avg_sq).  Scalars are the host's doubles
+ * rounded to fp32 (Adam's step_size = lr / (1 - beta1^t) and
+ * bias_correction2_sqrt = sqrt(1 - beta2^t) are computed on the host, as
+ * torch does).  Tolerance-pinned: ATen's CPU optimizer arithmetic (fmadd in
+ * the vectorised body) is ISA-dependent.
+ */
+enum fsagg_opt_kind { FSAGG_OPT_SGD = 0, FSAGG_OPT_ADAM = 1 };
+enum fsagg_opt_flags { FSAGG_OPT_NESTEROV = 1, FSAGG_OPT_FIRST_STEP = 2 };
+typedef struct fsagg_opt_params {
+  int kind;
+  int flags;
+  float lr, momentum, dampening, weight_decay;
+  float beta1, beta2, eps, step_size, bias_correction2_sqrt;
+} fsagg_opt_params;
+int fsagg_server_opt_step_f32(float *param, const float *avg, float *state0,
+                              float *state1, int64_t numel,
+                              const fsagg_opt_params *hp,
+                              fsagg_stream_t stream);
+
+/*
  * Deterministic synthetic client updates (benchmarks / tests): fills the
  * [n][ld] slab X with u = hash(seed, client, index) mapped to [-1, 1),
  * index < numel; the same generator is restated on the host by the tests.

@@ -197,3 +197,32 @@ def test_normbounding(name):
     for key in out:
         np.testing.assert_allclose(to_np(got[key]), out[key], rtol=1e-6,
                                    atol=1e-7)
+
+
+class ParamModel(torch.nn.Module):
+    """Module whose parameters are the fixture's init tensors."""
+    def __init__(self, sd):
+        super().__init__()
+        for k, v in sd.items():
+            self.register_parameter(k, torch.nn.Parameter(to_torch(v, 'cpu')))
+
+
+@pytest.mark.parametrize('opt', ['SGD', 'SGDm', 'Adam'])
+def test_fedopt_chain(opt):
+    """Three chained FedOpt rounds (optimizer state carried across rounds)
+    against the reference (torch.optim on CPU): tolerance-pinned, the
+    reference's vectorised fmadd arithmetic being ISA-dependent."""
+    from federatedscope_amd.core.aggregators import FedOptAggregator
+    metas = [load_case('fedopt_%s_%d' % (opt, r)) for r in range(3)]
+    meta0, _, _, init, _ = metas[0]
+    c = cfg()
+    c.fedopt = SimpleNamespace(optimizer=dict(meta0['opt']), annealing=False)
+    agg = FedOptAggregator(config=c, model=ParamModel(init))
+    for r, (meta, clients, out, _, _) in enumerate(metas):
+        got = agg.aggregate({'client_feedback': feedback(clients),
+                             'recover_fun': None})
+        assert list(got.keys()) == list(out.keys())
+        for k in out:
+            np.testing.assert_allclose(to_np(got[k]), out[k], rtol=2e-6,
+                                       atol=1e-7, err_msg='%s r%d %s' %
+                                       (opt, r, k))
