@@ -27,6 +27,7 @@ __all__ = [
     'median_aggregate', 'trimmed_mean_update', 'trimmedmean_aggregate',
     'bulyan_aggregate', 'normbounding_aggregate', 'interpolate_aggregate',
     'add_init', 'f32', 'trimmed_tolerance', 'bulyan_select', 'asyn_weights',
+    'FedOptState',
 ]
 
 f32 = np.float32
@@ -394,3 +395,64 @@ def normbounding_aggregate(models, bound, init):
 def interpolate_aggregate(models, global_model, beta):
     avg = para_weighted_avg(models)
     return para_weighted_avg([((1 - beta), global_model), (beta, avg)])
+
+
+# ---------------------------------------------------------------------------
+# FedOpt  (fedopt_aggregator.py:26-44 + torch.optim single-tensor SGD/Adam)
+# ---------------------------------------------------------------------------
+def _fma32(a, b, c):
+    """fp32 fused multiply-add, emulated in float64 (a·b is exact there)."""
+    return (np.float64(a) * np.float64(b) + np.asarray(c, np.float64)).astype(
+        f32)
+
+
+class FedOptState:
+    """Server optimizer state carried across rounds (torch.optim semantics,
+    ATen's vectorised fmadd for add(alpha); tolerance-pinned)."""
+
+    def __init__(self, params, opt):
+        self.params = OrderedDict((k, np.asarray(v, f32).copy())
+                                  for k, v in params.items())
+        self.opt = dict(opt)
+        self.buf = {}
+        self.m = {}
+        self.v = {}
+        self.t = 0
+
+    def step(self, models):
+        avg = para_weighted_avg(models)
+        o = self.opt
+
+        self.t += 1
+        for k, x in self.params.items():
+            if k not in avg:
+                continue
+            g = x - avg[k]
+            wd = o.get('weight_decay', 0.0)
+            if wd:
+                g = _fma32(x, wd, g)
+            if o['type'] == 'SGD':
+                mom = o.get('momentum', 0.0)
+                if mom:
+                    if k not in self.buf:
+                        self.buf[k] = g.copy()
+                    else:
+                        self.buf[k] = _fma32(
+                            g, 1 - o.get('dampening', 0.0),
+                            self.buf[k] * f32(mom))
+                    g = _fma32(self.buf[k], mom, g) if o.get(
+                        'nesterov', False) else self.buf[k]
+                self.params[k] = _fma32(g, -o['lr'], x)
+            else:
+                b1, b2 = o.get('betas', (0.9, 0.999))
+                eps = o.get('eps', 1e-8)
+                m = self.m.get(k, np.zeros_like(x))
+                v = self.v.get(k, np.zeros_like(x))
+                m = _fma32(f32(1 - b1), g - m, m)
+                v = v * f32(b2) + (f32(1 - b2) * g) * g
+                bc1 = 1 - b1**self.t
+                bc2 = 1 - b2**self.t
+                denom = np.sqrt(v) / f32(bc2**0.5) + f32(eps)
+                self.params[k] = x + (f32(-(o['lr'] / bc1)) * m) / denom
+                self.m[k], self.v[k] = m, v
+        return OrderedDict((k, v.copy()) for k, v in self.params.items())

@@ -358,7 +358,10 @@ def fedopt_cases(rng):
         for r in range(3):
             clients = rand_clients(rng, 4, shapes)
             rounds.append(clients)
-            outs.append(run(agg, clients))
+            # state_dict() shares storage with the parameters the next
+            # rounds update in place: snapshot it
+            outs.append(OrderedDict((k, v.detach().clone())
+                                    for k, v in run(agg, clients).items()))
         # save each round as its own case sharing the optimizer state chain
         for r in range(3):
             save_case('fedopt_%s_%d' % (opt['type'] + ('m' if 'momentum' in
