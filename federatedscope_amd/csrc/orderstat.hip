@@ -214,6 +214,177 @@ __global__ __launch_bounds__(kBlock) void orderstat_radix_kernel(
   out[p] = r;
 }
 
+// ---- 64 < n <= 255: LDS byte-histogram radix select ----------------------
+// Keys stay in registers (one lane = one coordinate).  A rank is found in 4
+// passes of 8 bits: each pass adds the lane's matching keys into a private
+// 256-bin histogram of byte counters in LDS (ds_add_u32 of 1 << 8·(d & 3)
+// into word d / 4; n <= 255 keeps every byte from overflowing), then the lane
+// scans its 64 words (v_sad_u8 sums four bins per word) for the bin that
+// holds the rank.  ≈ 4·(3n + 400) VALU per rank instead of the 2·32·n of the
+// bit-by-bit select.  Histogram words are laid out [word][lane], so the 64
+// lanes of a wave always hit 64 distinct banks.
+constexpr int kHistWords = 64;                   // 256 byte bins per lane
+constexpr int kHistLds = 4 * kHistWords * kWave; // 4 waves: 64 KiB
+
+__device__ __forceinline__ void hist_clear(uint32_t *H) {
+#pragma unroll
+  for (int w = 0; w < kHistWords; ++w) H[w * kWave] = 0u;
+}
+
+template <int N>
+__device__ __forceinline__ void hist_add(uint32_t *H, const uint32_t (&k)[N],
+                                         int n, uint32_t mask, uint32_t prefix,
+                                         int shift) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    if (j < n) {  // wave-uniform
+      const uint32_t key = k[j];
+      if ((key & mask) == prefix) {
+        const uint32_t d = (key >> shift) & 255u;
+        atomicAdd(&H[(d >> 2) * kWave], 1u << ((d & 3u) * 8u));
+      }
+    }
+  }
+}
+
+// Bin (0..255) holding rank r of the histogram, and the count below it.
+__device__ __forceinline__ uint32_t hist_scan(const uint32_t *H, int r,
+                                             int &below) {
+  int cum = 0, fcum = 0;
+  uint32_t fw = 0, fx = 0;
+  bool found = false;
+#pragma unroll 8
+  for (int w = 0; w < kHistWords; ++w) {
+    const uint32_t x = H[w * kWave];
+    const int s = int(__builtin_amdgcn_sad_u8(x, 0u, 0u));
+    const bool here = !found && cum + s > r;
+    fw = here ? uint32_t(w) : fw;
+    fx = here ? x : fx;
+    fcum = here ? cum : fcum;
+    found |= here;
+    cum += s;
+  }
+  uint32_t byte = 3;
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const int c = int((fx >> (8 * b)) & 255u);
+    const bool stop = byte == 3 && fcum + c > r;
+    byte = stop ? uint32_t(b) : byte;
+    fcum += (byte == 3) ? c : 0;
+  }
+  below = fcum;
+  return fw * 4 + byte;
+}
+
+// Refine rank r below a first-pass bin d0 (passes 2..4).
+template <int N>
+__device__ __forceinline__ uint32_t hist_refine(uint32_t *H,
+                                               const uint32_t (&k)[N], int n,
+                                               uint32_t d0, int r) {
+  uint32_t prefix = d0 << 24;
+#pragma unroll 1
+  for (int pass = 1; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    const uint32_t mask = 0xFFFFFFFFu << (shift + 8);
+    hist_clear(H);
+    hist_add<N>(H, k, n, mask, prefix, shift);
+    int below;
+    const uint32_t d = hist_scan(H, r, below);
+    r -= below;
+    prefix |= d << shift;
+  }
+  return prefix;
+}
+
+template <int N, int MODE>
+__global__ __launch_bounds__(kBlock) void orderstat_hist_kernel(
+    const float *const *__restrict__ rows, int n, int64_t numel, int kk,
+    float divisor, const float *__restrict__ base, float *__restrict__ out) {
+  __shared__ uint32_t hist[kHistLds];
+  uint32_t *H = hist + (threadIdx.x / kWave) * kHistWords * kWave +
+                (threadIdx.x & (kWave - 1));
+  const int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  const bool live = p < numel;
+  uint32_t k[N];
+  bool nan = false, nonfinite = false;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    if (j < n) {
+      const float x = live ? rows[j][p] : 0.0f;
+      nan |= __builtin_isnan(x);
+      nonfinite |= !__builtin_isfinite(x);
+      k[j] = f2key(x);
+    } else {
+      k[j] = kPad;
+    }
+  }
+  // pass 1 is shared by both ranks
+  hist_clear(H);
+  hist_add<N>(H, k, n, 0u, 0u, 24);
+  const int r1 = MODE == kMedian ? (n - 1) / 2 : kk;
+  const int r2 = MODE == kMedian ? n / 2 : n - kk - 1;
+  int b1, b2;
+  const uint32_t d1 = hist_scan(H, r1, b1);
+  const uint32_t d2 = hist_scan(H, r2, b2);
+  const uint32_t k1 = hist_refine<N>(H, k, n, d1, r1 - b1);
+  uint32_t k2;
+  if (MODE == kMedian) {
+    // the upper middle is k1 itself or the smallest key above it
+    int le = 0;
+    uint32_t above = kPad;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      if (j < n) {
+        le += k[j] <= k1;
+        above = k[j] > k1 && k[j] < above ? k[j] : above;
+      }
+    }
+    k2 = le > r2 ? k1 : above;
+  } else {
+    k2 = hist_refine<N>(H, k, n, d2, r2 - b2);
+  }
+  if (!live) return;
+  float r;
+  if constexpr (MODE == kMedian) {
+    r = __fdiv_rn(key2f(k1) - (-key2f(k2)), 2.0f);
+    if (nan) r = __builtin_nanf("");
+  } else {
+    float s;
+    if (!nonfinite) {
+      int below = 0, eq_lo = 0, inside = 0;
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        if (j < n) {
+          below += k[j] < k1;
+          eq_lo += k[j] == k1;
+          const bool in = k[j] > k1 && k[j] < k2;
+          inside += in;
+          acc += in ? double(key2f(k[j])) : 0.0;
+        }
+      }
+      const int keep = n - 2 * kk;
+      if (k1 == k2) {
+        acc = double(key2f(k1)) * keep;
+      } else {
+        const int lo_kept = min(below + eq_lo, n - kk) - kk;
+        const int hi_kept = keep - lo_kept - inside;
+        acc += double(key2f(k1)) * lo_kept + double(key2f(k2)) * hi_kept;
+      }
+      s = float(acc);
+    } else if (kk > 0 || nan) {
+      s = __builtin_nanf("");
+    } else {
+      s = 0.0f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) s = j < n ? add_rn(s, key2f(k[j])) : s;
+    }
+    r = __fdiv_rn(s, divisor);
+  }
+  if (base) r = add_rn(base[p], r);
+  out[p] = r;
+}
+
 // ---- generic n: radix select (binary search on the key bits) -----------
 __device__ __forceinline__ uint32_t select_rank(const float *const *rows,
                                                 int n, int64_t p, int rank) {
@@ -300,7 +471,7 @@ int launch(const float *const *rows, int n, int64_t numel, int kk,
   else if (n <= 32) FSAGG_OS(32);
   else if (n <= 64) FSAGG_OS(64);
 #define FSAGG_RX(NN)                                                        \
-  hipLaunchKernelGGL((orderstat_radix_kernel<NN, MODE>), dim3(grid),       \
+  hipLaunchKernelGGL((orderstat_hist_kernel<NN, MODE>), dim3(grid),        \
                      dim3(kBlock), 0, s, rows, n, numel, kk, divisor, base, \
                      out)
   else if (n <= 96) FSAGG_RX(96);
@@ -308,7 +479,7 @@ int launch(const float *const *rows, int n, int64_t numel, int kk,
   else if (n <= 160) FSAGG_RX(160);
   else if (n <= 192) FSAGG_RX(192);
   else if (n <= 224) FSAGG_RX(224);
-  else if (n <= 256) FSAGG_RX(256);
+  else if (n <= 255) FSAGG_RX(256);
   else
     hipLaunchKernelGGL((orderstat_generic_kernel<MODE>), dim3(grid),
                        dim3(kBlock), 0, s, rows, n, numel, kk, divisor, base,

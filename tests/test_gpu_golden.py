@@ -223,6 +223,8 @@ def test_fedopt_chain(opt):
                              'recover_fun': None})
         assert list(got.keys()) == list(out.keys())
         for k in out:
+            # a few fp32 ulps of the O(1) parameters: ATen's CPU Adam
+            # (lerp/addcmul/addcdiv, vectorised fmadd) rounds differently
             np.testing.assert_allclose(to_np(got[k]), out[k], rtol=2e-6,
-                                       atol=1e-7, err_msg='%s r%d %s' %
+                                       atol=4e-7, err_msg='%s r%d %s' %
                                        (opt, r, k))
