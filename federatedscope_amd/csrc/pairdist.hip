@@ -51,8 +51,11 @@ PairPlan make_plan(int n, int64_t numel, int nseg) {
   pl.groups = (pl.ntp + kBlock - 1) / kBlock;
   pl.tpg = (pl.ntp + pl.groups - 1) / pl.groups;
   pl.ks = kBlock / pl.tpg;
+  // pitch ≡ 28 (mod 32) words: conflict-free b128 staging writes and reads
   pl.ldsp = pl.nt * kTS + 4;
-  pl.sub = kLdsFloats / pl.ldsp;
+  while (pl.ldsp % 32 != 28) pl.ldsp += 4;
+  pl.sub = kLdsFloats / pl.ldsp / kWave * kWave;  // a multiple of 64
+  if (pl.sub < kWave) pl.sub = kLdsFloats / pl.ldsp;
   int64_t chl = (numel + 1023) / 1024;
   if (chl < 2048) chl = 2048;
   pl.chl = chl;
@@ -124,12 +127,29 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
 
   for (int64_t cs = start; cs < end; cs += pl.sub) {
     const int len = int(end - cs < pl.sub ? end - cs : pl.sub);
-    // stage [n][len] → lds[coord][client]
-    const int items = n * len;
-    for (int q = tid; q < items; q += kBlock) {
-      const int r = q / len;
-      const int cc = q - r * len;
-      lds[cc * pl.ldsp + r] = rows[r][cs + cc];
+    // stage [n][len] → lds[coord][client]: each wave takes quads of client
+    // rows (wave-uniform row pointers, scalar loads), each lane 4 rows of one
+    // coordinate → one ds_write_b128 at lds[cc·ldsp + r0]; with ldsp ≡ 28
+    // (mod 32) words, 8 consecutive coordinates cover 32 distinct banks
+    {
+      const int wave = tid / kWave, lane = tid & (kWave - 1);
+      const int quads = (n + 3) / 4;
+      for (int qd = wave; qd < quads; qd += kBlock / kWave) {
+        const int r0 = qd * 4;
+        const float *p0 = rows[r0] + cs;
+        const float *p1 = r0 + 1 < n ? rows[r0 + 1] + cs : nullptr;
+        const float *p2 = r0 + 2 < n ? rows[r0 + 2] + cs : nullptr;
+        const float *p3 = r0 + 3 < n ? rows[r0 + 3] + cs : nullptr;
+#pragma unroll 4
+        for (int cc = lane; cc < len; cc += kWave) {
+          float4 v;
+          v.x = p0[cc];
+          v.y = p1 ? p1[cc] : 0.0f;
+          v.z = p2 ? p2[cc] : 0.0f;
+          v.w = p3 ? p3[cc] : 0.0f;
+          *reinterpret_cast<float4 *>(lds + cc * pl.ldsp + r0) = v;
+        }
+      }
     }
     __syncthreads();
     if (active) {
