@@ -57,6 +57,23 @@ def _first_device(model):
     return torch.device('cpu')
 
 
+class StagedSet:
+    """The client list of one aggregate() call, resident in a ClientStack:
+    client i lives in stack row ``slots[i]``."""
+
+    def __init__(self, layout, stack, slots):
+        self.layout = layout
+        self.stack = stack
+        self.slots = list(slots)
+        self.n = len(self.slots)
+
+    def rows(self, sel=None, key=None):
+        """RowTable over clients ``sel`` (indices into the client list, in
+        reduction order; default all), optionally one key's sub-range."""
+        idx = self.slots if sel is None else [self.slots[i] for i in sel]
+        return self.stack.rows(idx, key=key)
+
+
 class DeviceEngine:
     """Mixin: call ``_engine_init(device)`` from the constructor."""
 
@@ -139,18 +156,16 @@ class DeviceEngine:
         dicts = [m for _, m in models]
         template = dicts[0]
         n = len(dicts)
-        if staged is not None:
-            layout, stack = staged
-        else:
-            layout = self._layout(template, as_float=as_float)
-            stack = self._stack(layout, dicts, as_float=as_float)
+        st = staged if staged is not None else self._staged(
+            models, as_float=as_float)
+        layout = st.layout
         out = torch.empty(layout.numel, dtype=torch.float32,
                           device=self.compute_device)
         base = None
         if base_model is not None:
             base = self._bucket(layout, base_model, as_float=as_float)
-        ops.weighted_sum(stack.rows(list(range(n))), weights, out,
-                         prescale=prescale, base=base)
+        ops.weighted_sum(st.rows(), weights, out, prescale=prescale,
+                         base=base)
         # keys some clients lack: reduce over the clients that have them,
         # weights NOT renormalised (clients_avg_aggregator.py:74-75)
         for k in layout.keys:
@@ -159,7 +174,7 @@ class DeviceEngine:
                 continue
             o, m = layout.offsets[k], layout.numels[k]
             ops.weighted_sum(
-                stack.rows(have, key=k), [weights[i] for i in have],
+                st.rows(have, key=k), [weights[i] for i in have],
                 out[o:o + m],
                 prescale=None if prescale is None else
                 [prescale[i] for i in have],
@@ -178,16 +193,34 @@ class DeviceEngine:
             extra[k] = o
         return layout, out, extra, list(template.keys())
 
+    def _staged(self, models, as_float=False, require_all=False):
+        """Stage the client list (or reuse what DeviceIngress staged on
+        arrival) → StagedSet."""
+        from ..workers.ingress import StagedUpdate
+        dicts = [m for _, m in models]
+        if all(isinstance(d, StagedUpdate) for d in dicts):
+            ing = dicts[0].ingress
+            if all(d.ingress is ing for d in dicts) and \
+                    not ing.layout.other:
+                if require_all:
+                    for i, d in enumerate(dicts):
+                        if len(d) != len(ing.layout.keys):
+                            raise KeyError('client %d lacks keys' % i)
+                ing.sync()
+                return StagedSet(ing.layout, ing.stack,
+                                 [d.slot for d in dicts])
+        layout = self._layout(dicts[0], as_float=as_float)
+        if require_all:
+            for i, d in enumerate(dicts):
+                for k in layout.keys:
+                    if k not in d:
+                        raise KeyError('client %d lacks key %r' % (i, k))
+        stack = self._stack(layout, dicts, as_float=as_float)
+        return StagedSet(layout, stack, range(len(dicts)))
+
     def _stage_all(self, models, as_float=True):
         """Pack every client (robust rules need all keys in all clients)."""
-        dicts = [m for _, m in models]
-        layout = self._layout(dicts[0], as_float=as_float)
-        for i, d in enumerate(dicts):
-            for k in layout.keys:
-                if k not in d:
-                    raise KeyError('client %d lacks key %r' % (i, k))
-        stack = self._stack(layout, dicts, as_float=as_float)
-        return layout, stack
+        return self._staged(models, as_float=as_float, require_all=True)
 
 
 def _as_float_proto(v):

@@ -21,9 +21,10 @@ class BulyanAggregator(ClientsAvgAggregator):
     def aggregate(self, agg_info):
         models = agg_info["client_feedback"]
         out_dev = _first_device(models[0][1])
-        layout, stack = self._stage_all(models)
+        st = self._stage_all(models)
+        layout = st.layout
         n = len(models)
-        D = ops.pairdist(stack.rows(list(range(n))), layout.segments()).cpu()
+        D = ops.pairdist(st.rows(), layout.segments()).cpu()
         scores = krum_scores(D, self.byzantine_node_num)
         index_order = torch.sort(scores)[1].numpy()
         keep = n - int(2 * self.sample_client_rate * self.byzantine_node_num)
@@ -34,5 +35,5 @@ class BulyanAggregator(ClientsAvgAggregator):
         base = self._bucket(layout, self.model.state_dict(), as_float=True)
         out = torch.empty(layout.numel, dtype=torch.float32,
                           device=self.compute_device)
-        ops.trimmed_mean(stack.rows(sel), k, out, divisor=gamma, base=base)
+        ops.trimmed_mean(st.rows(sel), k, out, divisor=gamma, base=base)
         return self._emit(layout, out, list(models[0][1].keys()), out_dev)

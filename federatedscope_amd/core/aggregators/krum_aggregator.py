@@ -38,16 +38,16 @@ class KrumAggregator(ClientsAvgAggregator):
 
     def distance_matrix(self, models):
         """D (host fp32 [n, n]) as _calculate_score fills it (:58-73)."""
-        layout, stack = self._stage_all(models)
-        rows = stack.rows(list(range(len(models))))
-        return ops.pairdist(rows, layout.segments()).cpu(), layout, stack
+        st = self._stage_all(models)
+        return ops.pairdist(st.rows(), st.layout.segments()).cpu(), st
 
     def _calculate_score(self, models):
-        D, _, _ = self.distance_matrix([(0, m) for m in models])
+        D, _ = self.distance_matrix([(0, m) for m in models])
         return krum_scores(D, self.byzantine_node_num)
 
     def _krum_device(self, models, agg_num):
-        D, layout, stack = self.distance_matrix(models)
+        D, st = self.distance_matrix(models)
+        layout = st.layout
         scores = krum_scores(D, self.byzantine_node_num)
         index_order = torch.sort(scores)[1].numpy()
         sel = [int(i) for i in index_order[:agg_num]]
@@ -57,5 +57,5 @@ class KrumAggregator(ClientsAvgAggregator):
         base = self._bucket(layout, self.model.state_dict(), as_float=True)
         out = torch.empty(layout.numel, dtype=torch.float32,
                           device=self.compute_device)
-        ops.weighted_sum(stack.rows(sel), weights, out, base=base)
+        ops.weighted_sum(st.rows(sel), weights, out, base=base)
         return layout, out, list(models[0][1].keys())

@@ -19,9 +19,10 @@ class MedianAggregator(ClientsAvgAggregator):
     def aggregate(self, agg_info):
         models = agg_info["client_feedback"]
         out_dev = _first_device(models[0][1])
-        layout, stack = self._stage_all(models)
+        st = self._stage_all(models)
+        layout = st.layout
         base = self._bucket(layout, self.model.state_dict(), as_float=True)
         out = torch.empty(layout.numel, dtype=torch.float32,
                           device=self.compute_device)
-        ops.coord_median(stack.rows(list(range(len(models)))), out, base=base)
+        ops.coord_median(st.rows(), out, base=base)
         return self._emit(layout, out, list(models[0][1].keys()), out_dev)

@@ -24,14 +24,14 @@ class NormboundingAggregator(ClientsAvgAggregator):
         models = agg_info["client_feedback"]
         out_dev = _first_device(models[0][1])
         init = self.model.state_dict()
-        layout, stack = self._stage_all(models)
+        st = self._stage_all(models)
+        layout = st.layout
         if [k for k in init if k in models[0][1]] != layout.keys:
             raise NotImplementedError(
                 'norm bounding with client keys that differ from the server '
                 'model keys')
         n = len(models)
-        rows = stack.rows(list(range(n)))
-        sq = ops.row_sqnorm(rows).cpu().numpy()
+        sq = ops.row_sqnorm(st.rows()).cpu().numpy()
         pre = []
         bound32 = np.float32(self.norm_bound)
         for i in range(n):
@@ -43,5 +43,5 @@ class NormboundingAggregator(ClientsAvgAggregator):
         weights = self._weights(models)
         layout, flat, extra, keys = self._weighted_avg_device(
             models, weights, as_float=True, base_model=init, prescale=pre,
-            staged=(layout, stack))
+            staged=st)
         return self._emit(layout, flat, keys, out_dev, extra)

@@ -22,11 +22,12 @@ class TrimmedmeanAggregator(ClientsAvgAggregator):
     def aggregate(self, agg_info):
         models = agg_info["client_feedback"]
         out_dev = _first_device(models[0][1])
-        layout, stack = self._stage_all(models)
+        st = self._stage_all(models)
+        layout = st.layout
         n = len(models)
         k = int(n * self.excluded_ratio)
         base = self._bucket(layout, self.model.state_dict(), as_float=True)
         out = torch.empty(layout.numel, dtype=torch.float32,
                           device=self.compute_device)
-        ops.trimmed_mean(stack.rows(list(range(n))), k, out, base=base)
+        ops.trimmed_mean(st.rows(), k, out, base=base)
         return self._emit(layout, out, list(models[0][1].keys()), out_dev)

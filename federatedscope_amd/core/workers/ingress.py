@@ -1,0 +1,93 @@
+"""Server-side ingress: stage each client's upload into HBM on arrival.
+
+The reference buffers uploads as host dicts (Server.callback_funcs_model_para,
+federatedscope/core/workers/server.py:929-988) and only touches them when
+the round closes; a device engine would then pay the whole n×P host→device
+copy inside aggregate().  DeviceIngress instead copies each upload into its
+slot of a device ClientStack as it arrives (pinned double-buffered H2D on a
+side stream), so the copy overlaps waiting for the remaining clients, and
+hands the server a StagedUpdate to buffer in place of the dict.  The
+aggregators recognise StagedUpdates and read the slots directly
+(SURVEY §8(f) rank 1).
+"""
+from collections.abc import Mapping
+
+import torch
+
+from ...layout import BucketLayout, ClientStack, HostStager
+from ..auxiliaries.utils import param2tensor
+
+
+class StagedUpdate(Mapping):
+    """A client update resident in a ClientStack slot.  Behaves like the
+    read-only state_dict it came from (device views per key)."""
+
+    def __init__(self, ingress, slot, keys):
+        self.ingress = ingress
+        self.stack = ingress.stack
+        self.slot = slot
+        self._keys = list(keys)
+
+    def __getitem__(self, k):
+        lay = self.stack.layout
+        if k not in lay.offsets or k not in self._keys:
+            raise KeyError(k)
+        o, m = lay.offsets[k], lay.numels[k]
+        return self.stack.slab[self.slot, o:o + m].view(lay.shapes[k])
+
+    def __iter__(self):
+        return iter(self._keys)
+
+    def __len__(self):
+        return len(self._keys)
+
+
+class DeviceIngress:
+    """Stage uploads of one model layout into a device client stack."""
+
+    def __init__(self, template, capacity, device=None, as_float=False):
+        from ..aggregators._engine import compute_device
+        self.device = compute_device(device)
+        if as_float:
+            template = {k: torch.empty(param2tensor(v).shape)
+                        for k, v in template.items()}
+        self.layout = BucketLayout(template)
+        if self.layout.other:
+            raise NotImplementedError(
+                'ingress staging of non-fp32 keys %s' % list(self.layout.other))
+        self.stack = ClientStack(self.layout, capacity, self.device)
+        self.stack.slab.zero_()
+        self.as_float = as_float
+        self._stager = None
+        self.next_slot = 0
+
+    def reset(self):
+        """Start a new round: slots are reused (kernels of the previous round
+        are ordered before the next copies by HostStager)."""
+        self.next_slot = 0
+        self._stager = None
+
+    def receive(self, sample_size, model_para):
+        """Stage one upload; returns (sample_size, StagedUpdate)."""
+        if self.next_slot >= self.stack.capacity:
+            self.stack.ensure(self.stack.capacity * 2)
+        slot = self.next_slot
+        self.next_slot += 1
+        missing = [k for k in self.layout.keys if k not in model_para]
+        if missing:
+            raise KeyError('staged upload lacks keys %s' % missing)
+        src = {k: (param2tensor(model_para[k]).float() if self.as_float else
+                   param2tensor(model_para[k])) for k in self.layout.keys}
+        on_host = any(v.device.type != 'cuda' for v in src.values())
+        if on_host:
+            if self._stager is None:
+                self._stager = HostStager(self.device)
+            self._stager.put(self.layout, src, self.stack.slab[slot])
+        else:
+            self.layout.pack_device(src, self.stack.slab[slot])
+        return sample_size, StagedUpdate(self, slot, model_para.keys())
+
+    def sync(self):
+        """Make the current stream wait for every staged copy."""
+        if self._stager is not None:
+            self._stager.finish()

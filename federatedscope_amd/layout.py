@@ -161,9 +161,12 @@ class ClientStack:
         return self.slab.shape[0]
 
     def ensure(self, capacity):
+        """Grow to ``capacity`` rows, keeping the rows already staged."""
         if capacity > self.capacity:
-            self.slab = torch.empty((capacity, self.layout.numel),
-                                    dtype=torch.float32, device=self.device)
+            slab = torch.zeros((capacity, self.layout.numel),
+                               dtype=torch.float32, device=self.device)
+            slab[:self.capacity].copy_(self.slab)
+            self.slab = slab
 
     def load(self, i, model):
         self.layout.pack_device(model, self.slab[i])

@@ -135,7 +135,7 @@ def test_krum(name):
         f=meta['f'], agg_num=meta['agg_num'],
         client_num=max(2 * meta['f'] + 3, 50)))
     fb = feedback(clients)
-    D, _, _ = agg.distance_matrix(fb)
+    D, _ = agg.distance_matrix(fb)
     n = len(clients)
     off = ~np.eye(n, dtype=bool)
     # per-key sums in fp32 chunks + fp64 across chunks vs ATen's fp32 dist
