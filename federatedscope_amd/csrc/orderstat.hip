@@ -96,6 +96,27 @@ __device__ __forceinline__ float nonfinite_sum(const uint32_t (&k)[N], int n,
 
 enum Mode { kMedian = 0, kTrimmed = 1 };
 
+// Load a lane's column of n values into N key registers (pads = kPad).
+// Branch-free on purpose: rows past n re-read row n-1 (an L1/L2 hit) and are
+// masked to kPad, so all N loads issue back to back and the wave waits once
+// — a per-row `if (j < n)` splits the loop into N basic blocks and every
+// load then waits out its own HBM round trip.
+template <int N>
+__device__ __forceinline__ void load_column(const float *const *rows, int n,
+                                            int64_t p, uint32_t (&k)[N],
+                                            bool &nan, bool &nonfinite) {
+  float x[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) x[j] = rows[j < n ? j : n - 1][p];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const bool real = j < n;
+    nan |= real && __builtin_isnan(x[j]);
+    nonfinite |= real && !__builtin_isfinite(x[j]);
+    k[j] = real ? f2key(x[j]) : kPad;
+  }
+}
+
 template <int N, int MODE>
 __global__ __launch_bounds__(kBlock) void orderstat_reg_kernel(
     const float *const *__restrict__ rows, int n, int64_t numel, int kk,
@@ -104,17 +125,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_reg_kernel(
   if (p >= numel) return;
   uint32_t k[N];
   bool nan = false, nonfinite = false;
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-    if (j < n) {
-      const float x = rows[j][p];
-      nan |= __builtin_isnan(x);
-      nonfinite |= !__builtin_isfinite(x);
-      k[j] = f2key(x);
-    } else {
-      k[j] = kPad;
-    }
-  }
+  load_column<N>(rows, n, p, k, nan, nonfinite);
   bitonic_sort<N>(k);
   using Seq = std::make_integer_sequence<int, N>;
   float r;
@@ -146,17 +157,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_radix_kernel(
   if (p >= numel) return;
   uint32_t k[N];
   bool nan = false, nonfinite = false;
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-    if (j < n) {
-      const float x = rows[j][p];
-      nan |= __builtin_isnan(x);
-      nonfinite |= !__builtin_isfinite(x);
-      k[j] = f2key(x);
-    } else {
-      k[j] = kPad;
-    }
-  }
+  load_column<N>(rows, n, p, k, nan, nonfinite);
   const int r1 = MODE == kMedian ? (n - 1) / 2 : kk;
   const int r2 = MODE == kMedian ? n / 2 : n - kk - 1;
   // p = the key of rank r: the largest prefix with #(key <= prefix|lowbits) <= r
@@ -235,14 +236,16 @@ template <int N>
 __device__ __forceinline__ void hist_add(uint32_t *H, const uint32_t (&k)[N],
                                          int n, uint32_t mask, uint32_t prefix,
                                          int shift) {
+  // Pads (kPad, the largest key) may be counted: they sort after every
+  // real key and ranks are < n.  Only N = 256 must skip them — a bin could
+  // then reach 256 and overflow its byte.
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    if (j < n) {  // wave-uniform
-      const uint32_t key = k[j];
-      if ((key & mask) == prefix) {
-        const uint32_t d = (key >> shift) & 255u;
-        atomicAdd(&H[(d >> 2) * kWave], 1u << ((d & 3u) * 8u));
-      }
+    if (N == 256 && j >= n) continue;
+    const uint32_t key = k[j];
+    if ((key & mask) == prefix) {
+      const uint32_t d = (key >> shift) & 255u;
+      atomicAdd(&H[(d >> 2) * kWave], 1u << ((d & 3u) * 8u));
     }
   }
 }
@@ -307,17 +310,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_hist_kernel(
   const bool live = p < numel;
   uint32_t k[N];
   bool nan = false, nonfinite = false;
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-    if (j < n) {
-      const float x = live ? rows[j][p] : 0.0f;
-      nan |= __builtin_isnan(x);
-      nonfinite |= !__builtin_isfinite(x);
-      k[j] = f2key(x);
-    } else {
-      k[j] = kPad;
-    }
-  }
+  load_column<N>(rows, n, live ? p : 0, k, nan, nonfinite);
   // pass 1 is shared by both ranks
   hist_clear(H);
   hist_add<N>(H, k, n, 0u, 0u, 24);
