@@ -1,0 +1,111 @@
+"""End to end through the server counterpart (A2/A3) with uploads staged
+into HBM on arrival: the reference's own toy-LR course (configs[0] C1,
+tests/test_toy_lr.py) captured round by round (tools/capture_toy_lr.py) must
+be reproduced bit for bit, and robust rules must accept staged slots."""
+from collections import OrderedDict
+from types import SimpleNamespace
+
+import json
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from golden_io import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(**kw):
+    bft = SimpleNamespace(krum_agg_num=kw.get('agg_num', 1),
+                          trimmedmean_excluded_ratio=0.2,
+                          normbounding_norm_bound=1.0)
+    return SimpleNamespace(
+        federate=SimpleNamespace(ignore_weight=False, use_ss=False,
+                                 client_num=kw.get('client_num', 1000),
+                                 sample_client_rate=1.0),
+        aggregator=SimpleNamespace(byzantine_node_num=kw.get('f', 0),
+                                   BFT_args=bft),
+        asyn=SimpleNamespace(staleness_discount_factor=1.0))
+
+
+def _rounds():
+    with np.load(GOLDEN + '/toy_lr_rounds.npz', allow_pickle=False) as z:
+        meta = json.loads(str(z['meta']))
+        rounds = []
+        for r, rm in enumerate(meta['rounds_meta']):
+            ins = [(s, OrderedDict((k, z['r%d|x|%d|%s' % (r, i, k)])
+                                   for k in rm['keys']))
+                   for i, s in enumerate(rm['sizes'])]
+            out = OrderedDict((k, z['r%d|out|%s' % (r, k)])
+                              for k in rm['keys'])
+            rounds.append((ins, out))
+    return meta, rounds
+
+
+@pytest.mark.parametrize('stage', [True, False])
+def test_toy_lr_course_bit_exact(stage):
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    from federatedscope_amd.core.workers.server import AggregationServer
+    meta, rounds = _rounds()
+    assert meta['rounds'] == 20 and meta['test_loss'] < 0.3
+    class LR(torch.nn.Module):      # core/lr.py:4-10, toy data 5 features
+        def __init__(self):
+            super().__init__()
+            self.fc = torch.nn.Linear(5, 1)
+
+    model = LR()
+    srv = AggregationServer(model, ClientsAvgAggregator(config=_cfg()),
+                            sample_client_num=5, stage_on_arrival=stage)
+    for r, (ins, out) in enumerate(rounds):
+        for i, (s, d) in enumerate(ins):
+            moved = srv.callback_funcs_model_para(
+                r, i + 1, (s, OrderedDict((k, torch.from_numpy(v.copy()))
+                                          for k, v in d.items())))
+            assert moved == (i == len(ins) - 1)
+        got = srv.history[-1]
+        for k in out:
+            assert got[k].cpu().numpy().tobytes() == out[k].tobytes(), (r, k)
+        # and the server model now holds the aggregate
+        sd = model.state_dict()
+        for k in out:
+            assert sd[k].numpy().tobytes() == out[k].tobytes(), (r, k)
+    assert srv.state == 20
+
+
+def test_staged_robust_rules_match_unstaged():
+    from federatedscope_amd.core.aggregators import (KrumAggregator,
+                                                     MedianAggregator)
+    from federatedscope_amd.core.workers.ingress import DeviceIngress
+    rng = np.random.default_rng(3)
+    n = 12
+    clients = [(int(rng.integers(1, 50)), OrderedDict(
+        [('a', rng.standard_normal((7, 9)).astype(np.float32)),
+         ('b', rng.standard_normal(5).astype(np.float32))]))
+        for _ in range(n)]
+    init = OrderedDict((k, np.zeros_like(v)) for k, v in clients[0][1].items())
+
+    class M(torch.nn.Module):
+        def state_dict(self, *a, **kw):
+            return OrderedDict((k, torch.from_numpy(v)) for k, v in
+                               init.items())
+
+    ing = DeviceIngress(clients[0][1], n)
+    staged = [ing.receive(s, OrderedDict((k, torch.from_numpy(v.copy()))
+                                         for k, v in d.items()))
+              for s, d in clients]
+    host = [(s, OrderedDict((k, torch.from_numpy(v.copy()))
+                            for k, v in d.items())) for s, d in clients]
+    for cls, kw in ((MedianAggregator, {}), (KrumAggregator, {'agg_num': 3})):
+        a = cls(model=M(), config=_cfg(f=2, client_num=50, **kw))
+        b = cls(model=M(), config=_cfg(f=2, client_num=50, **kw))
+        g1 = a.aggregate({'client_feedback': staged})
+        g2 = b.aggregate({'client_feedback': host})
+        for k in g1:
+            assert torch.equal(g1[k].cpu(), g2[k].cpu()), (cls, k)
+    want = O.median_aggregate(clients, init)
+    g = MedianAggregator(model=M(), config=_cfg(f=2, client_num=50)
+                         ).aggregate({'client_feedback': staged})
+    for k in want:
+        assert g[k].cpu().numpy().tobytes() == want[k].tobytes()
