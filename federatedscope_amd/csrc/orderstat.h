@@ -1,0 +1,107 @@
+// Internal to libfsagg: device helpers shared by the order-statistics
+// translation units (orderstat.hip and the per-N orderstat_select.hip
+// instantiations).  Not part of the public ABI.
+#pragma once
+
+#include <utility>
+
+#include "common.h"
+
+namespace fsagg {
+namespace os {
+
+// Non-temporal global load at a 32-bit element offset from a row base (each
+// column value is read once).
+typedef __attribute__((address_space(1))) const float gfloat;
+__device__ __forceinline__ float ld_nt(const float *row, uint32_t off) {
+  return __builtin_nontemporal_load((gfloat *)(row) + off);
+}
+
+
+constexpr int kBlock = 256;
+constexpr uint32_t kPad = 0xFFFFFFFFu;
+
+// ---- compile-time bitonic network --------------------------------------
+template <int N, int SIZE, int STRIDE, int I>
+__device__ __forceinline__ void cmpx(uint32_t (&k)[N]) {
+  constexpr int J = I ^ STRIDE;
+  if constexpr (J > I) {
+    constexpr bool up = (I & SIZE) == 0;
+    const uint32_t a = k[I], b = k[J];
+    const uint32_t lo = a < b ? a : b;
+    const uint32_t hi = a < b ? b : a;
+    k[I] = up ? lo : hi;
+    k[J] = up ? hi : lo;
+  }
+}
+
+template <int N, int SIZE, int STRIDE, int... I>
+__device__ __forceinline__ void stage(uint32_t (&k)[N],
+                                      std::integer_sequence<int, I...>) {
+  (cmpx<N, SIZE, STRIDE, I>(k), ...);
+}
+
+template <int N, int SIZE, int STRIDE>
+__device__ __forceinline__ void merge_level(uint32_t (&k)[N]) {
+  stage<N, SIZE, STRIDE>(k, std::make_integer_sequence<int, N>{});
+  if constexpr (STRIDE > 1) merge_level<N, SIZE, STRIDE / 2>(k);
+}
+
+template <int N, int SIZE>
+__device__ __forceinline__ void sort_from(uint32_t (&k)[N]) {
+  merge_level<N, SIZE, SIZE / 2>(k);
+  if constexpr (SIZE < N) sort_from<N, SIZE * 2>(k);
+}
+
+template <int N>
+__device__ __forceinline__ void bitonic_sort(uint32_t (&k)[N]) {
+  sort_from<N, 2>(k);
+}
+
+// read k[idx] for a runtime idx without dynamic register indexing
+template <int N, int... I>
+__device__ __forceinline__ uint32_t pick(const uint32_t (&k)[N], int idx,
+                                         std::integer_sequence<int, I...>) {
+  uint32_t r = 0;
+  ((r = (I == idx) ? k[I] : r), ...);
+  return r;
+}
+
+// Σ key2f(k[j]) for lo <= j < hi, in float64, ascending order
+template <int N, int... I>
+__device__ __forceinline__ double mid_sum(const uint32_t (&k)[N], int lo,
+                                          int hi,
+                                          std::integer_sequence<int, I...>) {
+  double s = 0.0;
+  ((s += (I >= lo && I < hi) ? double(key2f(k[I])) : 0.0), ...);
+  return s;
+}
+
+// The reference computes cat([T, -top_k, -bottom_k]).sum(): for a column that
+// holds ±inf/NaN with k >= 1 an infinity is always among the excluded values,
+// so the fp32 sum is inf - inf = NaN; with k == 0 it is Σall (inf or NaN).
+template <int N, int... I>
+__device__ __forceinline__ float nonfinite_sum(const uint32_t (&k)[N], int n,
+                                               int kk, bool nan,
+                                               std::integer_sequence<int, I...>) {
+  if (kk > 0 || nan) return __builtin_nanf("");
+  float s = 0.0f;
+  ((s = (I < n) ? add_rn(s, key2f(k[I])) : s), ...);
+  return s;
+}
+
+enum Mode { kMedian = 0, kTrimmed = 1 };
+
+
+// The select kernel for register-array size N serves N - kSelStep < n <= N.
+constexpr int kSelStep = 8;
+
+// Launch the range-adaptive select kernel for 64 < n <= N (orderstat_select.hip,
+// one translation unit per N).
+template <int N, int MODE>
+void launch_select(const float *const *rows, int n, int64_t numel, int kk,
+                   float divisor, const float *base, float *out,
+                   hipStream_t s);
+
+}  // namespace os
+}  // namespace fsagg

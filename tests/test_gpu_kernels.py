@@ -98,8 +98,8 @@ def test_weighted_sum_row_order_is_reduction_order():
     assert b.cpu().numpy().tobytes() == wb.tobytes()
 
 
-@pytest.mark.parametrize('n', [1, 2, 3, 4, 7, 8, 31, 64, 65, 100, 127, 200,
-                               256, 300])
+@pytest.mark.parametrize('n', [1, 2, 3, 4, 7, 8, 31, 64, 65, 72, 73, 100,
+                               127, 200, 233, 250, 255, 256, 300])
 def test_median_trimmed_all_kernels(n):
     from federatedscope_amd import ops
     P = 3001
