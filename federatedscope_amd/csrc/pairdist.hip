@@ -31,6 +31,10 @@ constexpr int kBlock = 256;
 constexpr int kTS = 8;                       // pair tile side
 constexpr int kRedPitch = kTS * kTS + 1;     // 65: LDS pitch of a reduction slot
 constexpr int kLdsFloats = kBlock * kRedPitch;  // 16640 floats = 65 KiB
+// register-prefetched staging items per thread (each 4 rows × 4 coordinates):
+// a stage holds < kLdsFloats floats: ≤ 1040 items, ≤ 4 × 256 for most n
+constexpr int kStageItems = 4;
+typedef float f4v __attribute__((ext_vector_type(4)));
 
 struct PairPlan {
   int nt;       // tiles per side
@@ -56,9 +60,12 @@ PairPlan make_plan(int n, int64_t numel, int nseg) {
   while (pl.ldsp % 32 != 28) pl.ldsp += 4;
   pl.sub = kLdsFloats / pl.ldsp / kWave * kWave;  // a multiple of 64
   if (pl.sub < kWave) pl.sub = kLdsFloats / pl.ldsp;
-  int64_t chl = (numel + 1023) / 1024;
+  // ≈ 1000 chunks (two rounds of the 2 × 256 resident workgroups), a
+  // multiple of 64 coordinates so full stages stay 16-B aligned
+  const int64_t target = 1024 - nseg > 256 ? 1024 - nseg : 256;
+  int64_t chl = (numel + target - 1) / target;
   if (chl < 2048) chl = 2048;
-  pl.chl = chl;
+  pl.chl = (chl + 63) / 64 * 64;
   pl.max_chunks = numel / chl + nseg + 1;
   return pl;
 }
@@ -115,9 +122,16 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   int ti = 0, tj = 0;
   if (active) tp_to_tiles(tp, pl.nt, ti, tj);
 
-  // zero the staging area once: padded client rows stay zero
-  for (int q = tid; q < kLdsFloats; q += kBlock) lds[q] = 0.0f;
-  __syncthreads();
+  const int npad = pl.nt * kTS;  // client slots (rows >= n repeat row n-1)
+  const int quads = npad / 4;
+  // A full stage is staged from registers: item = (client quad, 4
+  // consecutive coordinates) = four 16-B row loads, issued for stage s + 1
+  // before stage s is computed, so the HBM latency hides behind the FMAs.
+  const int groups = pl.sub / 4;
+  const int items = quads * groups;
+  bool vec = (start & 3) == 0;
+  for (int r = 0; r < n; ++r)
+    vec = vec && (reinterpret_cast<uintptr_t>(rows[r]) & 15u) == 0;
 
   float acc[kTS][kTS];
 #pragma unroll
@@ -125,34 +139,67 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
 #pragma unroll
     for (int v = 0; v < kTS; ++v) acc[u][v] = 0.0f;
 
-  for (int64_t cs = start; cs < end; cs += pl.sub) {
-    const int len = int(end - cs < pl.sub ? end - cs : pl.sub);
-    // stage [n][len] → lds[coord][client]: each wave takes quads of client
-    // rows (wave-uniform row pointers, scalar loads), each lane 4 rows of one
-    // coordinate → one ds_write_b128 at lds[cc·ldsp + r0]; with ldsp ≡ 28
-    // (mod 32) words, 8 consecutive coordinates cover 32 distinct banks
-    {
-      const int wave = tid / kWave, lane = tid & (kWave - 1);
-      const int quads = (n + 3) / 4;
-      for (int qd = wave; qd < quads; qd += kBlock / kWave) {
-        const int r0 = qd * 4;
-        const float *p0 = rows[r0] + cs;
-        const float *p1 = r0 + 1 < n ? rows[r0 + 1] + cs : nullptr;
-        const float *p2 = r0 + 2 < n ? rows[r0 + 2] + cs : nullptr;
-        const float *p3 = r0 + 3 < n ? rows[r0 + 3] + cs : nullptr;
-#pragma unroll 4
-        for (int cc = lane; cc < len; cc += kWave) {
-          float4 v;
-          v.x = p0[cc];
-          v.y = p1 ? p1[cc] : 0.0f;
-          v.z = p2 ? p2[cc] : 0.0f;
-          v.w = p3 ? p3[cc] : 0.0f;
-          *reinterpret_cast<float4 *>(lds + cc * pl.ldsp + r0) = v;
+  f4v pre[kStageItems][4];
+  auto fetch = [&](int64_t cs) {
+#pragma unroll
+    for (int k = 0; k < kStageItems; ++k) {
+      const int it = tid + k * kBlock;
+      if (it < items) {
+        const int qd = it / groups, g = it - qd * groups;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = min(qd * 4 + e, n - 1);
+          pre[k][e] = __builtin_nontemporal_load(
+              reinterpret_cast<const f4v *>(rows[r] + cs) + g);
         }
       }
     }
+  };
+  auto stage_from_regs = [&]() {
+#pragma unroll
+    for (int k = 0; k < kStageItems; ++k) {
+      const int it = tid + k * kBlock;
+      if (it < items) {
+        const int qd = it / groups, g = it - qd * groups;
+        float *dst = lds + (4 * g) * pl.ldsp + qd * 4;
+        *reinterpret_cast<float4 *>(dst) =
+            make_float4(pre[k][0].x, pre[k][1].x, pre[k][2].x, pre[k][3].x);
+        *reinterpret_cast<float4 *>(dst + pl.ldsp) =
+            make_float4(pre[k][0].y, pre[k][1].y, pre[k][2].y, pre[k][3].y);
+        *reinterpret_cast<float4 *>(dst + 2 * pl.ldsp) =
+            make_float4(pre[k][0].z, pre[k][1].z, pre[k][2].z, pre[k][3].z);
+        *reinterpret_cast<float4 *>(dst + 3 * pl.ldsp) =
+            make_float4(pre[k][0].w, pre[k][1].w, pre[k][2].w, pre[k][3].w);
+      }
+    }
+  };
+  // partial or unaligned stage: guarded 4-B loads straight to LDS
+  auto stage_scalar = [&](int64_t cs, int len) {
+    const int wave = tid / kWave, lane = tid & (kWave - 1);
+    for (int qd = wave; qd < quads; qd += kBlock / kWave) {
+      const int r0 = qd * 4;
+      const float *p0 = rows[min(r0, n - 1)] + cs;
+      const float *p1 = rows[min(r0 + 1, n - 1)] + cs;
+      const float *p2 = rows[min(r0 + 2, n - 1)] + cs;
+      const float *p3 = rows[min(r0 + 3, n - 1)] + cs;
+      for (int cc = lane; cc < len; cc += kWave)
+        *reinterpret_cast<float4 *>(lds + cc * pl.ldsp + r0) =
+            make_float4(p0[cc], p1[cc], p2[cc], p3[cc]);
+    }
+  };
+
+  const bool prefetch = vec && items <= kStageItems * kBlock;
+  if (prefetch && end - start >= pl.sub) fetch(start);
+  for (int64_t cs = start; cs < end; cs += pl.sub) {
+    const int len = int(end - cs < pl.sub ? end - cs : pl.sub);
+    const bool full = prefetch && len == pl.sub;
+    if (full) stage_from_regs();
+    else stage_scalar(cs, len);
     __syncthreads();
+    // next full stage's loads fly while this one is computed
+    if (prefetch && end - (cs + pl.sub) >= pl.sub) fetch(cs + pl.sub);
     if (active) {
+#pragma unroll 2
       for (int cc = ksl; cc < len; cc += pl.ks) {
         const float4 *col = reinterpret_cast<const float4 *>(lds + cc * pl.ldsp);
         const float4 a0 = col[ti * 2], a1 = col[ti * 2 + 1];
@@ -192,33 +239,47 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   }
 }
 
-// Σ over a segment's chunks (fixed chunk order, fp64) for every pair of the
-// tile layout; thread = (segment, tile pair, element): consecutive threads
-// read consecutive partials of one chunk (coalesced).  Output: the full
-// symmetric [nseg][n][n] matrix of per-key squared distances (diag 0).
-__global__ __launch_bounds__(kBlock) void pairdist_segsq_kernel(
+// Σ over a segment's chunks in fp64 for every pair of the tile layout, in a
+// fixed order (deterministic, no atomics).  Block = (segment, 64 partial
+// columns); its 16 waves take every 16th chunk each (consecutive lanes read
+// consecutive partials of one chunk: coalesced), then the 16 slice sums are
+// added in slice order.  Output: the full symmetric [nseg][n][n] matrix of
+// per-key squared distances (diagonal 0).
+constexpr int kSegBlock = 1024;
+constexpr int kSegSlices = kSegBlock / kWave;
+
+__global__ __launch_bounds__(kSegBlock) void pairdist_segsq_kernel(
     const float *__restrict__ partial, int n, PairPlan pl, int nseg,
     const int *__restrict__ prefix, double *__restrict__ segsq) {
-  const int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-  const int64_t per_seg = int64_t(pl.ntp) * kTS * kTS;
-  if (q >= per_seg * nseg) return;
-  const int s = int(q / per_seg);
-  const int r = int(q - int64_t(s) * per_seg);
+  __shared__ double red[kSegSlices][kWave];
+  const int s = blockIdx.x;
+  const int per_seg = pl.ntp * kTS * kTS;
+  const int lane = threadIdx.x & (kWave - 1), slice = threadIdx.x / kWave;
+  const int r = blockIdx.y * kWave + lane;
+  double sq = 0.0;
+  if (r < per_seg) {
+#pragma unroll 4
+    for (int c = prefix[s] + slice; c < prefix[s + 1]; c += kSegSlices)
+      sq += double(partial[int64_t(c) * per_seg + r]);
+  }
+  red[slice][lane] = sq;
+  __syncthreads();
+  if (slice != 0 || r >= per_seg) return;
+  double t = 0.0;
+#pragma unroll
+  for (int k = 0; k < kSegSlices; ++k) t += red[k][lane];
   const int tp = r / (kTS * kTS), e = r % (kTS * kTS);
   int ti, tj;
   tp_to_tiles(tp, pl.nt, ti, tj);
   const int i = ti * kTS + e / kTS, j = tj * kTS + e % kTS;
-  if (i >= n || j >= n || i >= j) return;
-  double sq = 0.0;
-  for (int c = prefix[s]; c < prefix[s + 1]; ++c)
-    sq += double(partial[int64_t(c) * per_seg + r]);
   double *m = segsq + int64_t(s) * n * n;
-  m[int64_t(i) * n + j] = sq;
-  m[int64_t(j) * n + i] = sq;
   if (i == 0 && j == 1) {
     // the diagonal of this segment (one writer per segment)
     for (int d = 0; d < n; ++d) m[int64_t(d) * n + d] = 0.0;
   }
+  if (i >= n || j >= n || i >= j) return;
+  m[int64_t(i) * n + j] = t;
+  m[int64_t(j) * n + i] = t;
 }
 
 // D[a][b] = Σ_seg fl32(sqrt(segsq[seg][a][b])) accumulated in fp32 in key
@@ -317,10 +378,10 @@ static int pairdist_segsq_impl(const float *const *rows, int n, int64_t numel,
                        dim3(unsigned(pl.max_chunks), unsigned(pl.groups)),
                        dim3(kBlock), 0, s, rows, n, pl, seg_off, nseg, prefix,
                        partial);
-  const int64_t items = int64_t(pl.ntp) * kTS * kTS * nseg;
+  const int per_seg = pl.ntp * kTS * kTS;
   hipLaunchKernelGGL(pairdist_segsq_kernel,
-                     dim3(unsigned((items + kBlock - 1) / kBlock)),
-                     dim3(kBlock), 0, s, partial, n, pl, nseg, prefix, segsq);
+                     dim3(unsigned(nseg), unsigned((per_seg + kWave - 1) / kWave)),
+                     dim3(kSegBlock), 0, s, partial, n, pl, nseg, prefix, segsq);
   return FSAGG_OK;
 }
 
