@@ -62,6 +62,20 @@ FSAGG_OPT_NESTEROV, FSAGG_OPT_FIRST_STEP = 1, 2
 SIGNATURES['fsagg_server_opt_step_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_p, _c_i64, ctypes.POINTER(OptParams), _c_p])
 
+_c_d = ctypes.c_double
+FSAGG_WIRE_F32, FSAGG_WIRE_I8, FSAGG_WIRE_I16 = 0, 1, 2
+SIGNATURES['fsagg_wire_unpack_f32'] = (
+    _c_i, [_c_p, _c_p, _c_p, _c_i, _c_i64, _c_p, _c_p])
+SIGNATURES['fsagg_ss_recover_f32'] = (
+    _c_i, [_c_p, _c_p, _c_i, _c_i64, _c_d, _c_d, _c_d, _c_d, _c_i, _c_p, _c_p,
+           _c_p])
+SIGNATURES['fsagg_delta_sqnorm_workspace_bytes'] = (_c_sz, [_c_i, _c_i64,
+                                                            _c_i])
+SIGNATURES['fsagg_delta_wsum_f32'] = (
+    _c_i, [_c_p, _c_p, _c_i, _c_i64, _c_p, _c_p, _c_p])
+SIGNATURES['fsagg_delta_sqnorm_f32'] = (
+    _c_i, [_c_p, _c_i, _c_i64, _c_p, _c_p, _c_i, _c_p, _c_p, _c_sz, _c_p])
+
 _lib = None
 
 

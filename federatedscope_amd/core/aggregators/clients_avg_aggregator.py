@@ -33,10 +33,6 @@ class ClientsAvgAggregator(DeviceEngine, _ModelIO, Aggregator):
 
     def _weights(self, models):
         fed = self.cfg.federate
-        if fed.use_ss:
-            raise NotImplementedError(
-                'secret-sharing recovery (federate.use_ss) is not on the '
-                'device path yet')
         return fedavg_weights([s for s, _ in models],
                               ignore_weight=fed.ignore_weight)
 
@@ -44,10 +40,61 @@ class ClientsAvgAggregator(DeviceEngine, _ModelIO, Aggregator):
         """Weighted average of the client dicts (clients_avg_aggregator.py:60-100).
 
         Returns a state_dict in client 0's key order on client 0's device."""
+        if self.cfg.federate.use_ss:
+            if self.cfg.federate.ignore_weight:
+                raise NotImplementedError(
+                    'use_ss with ignore_weight (1/n-weighted fixed-point '
+                    'shares) has no device path')
+            return self._ss_avg(models, recover_fun)
         weights = self._weights(models)
         out_dev = _first_device(models[0][1])
         layout, flat, extra, keys = self._weighted_avg_device(models, weights)
         return self._emit(layout, flat, keys, out_dev, extra)
+
+    def _ss_avg(self, models, recover_fun):
+        """The use_ss branch (clients_avg_aggregator.py:79-98): every upload
+        is the client's share sum of sample_size·params in fixed point;
+        weight 1.0, Σ in float64 (numpy), then fixedpoint2float, ÷ total,
+        fp32 — fused in fsagg_ss_recover_f32.  Without a recover function
+        the float64 sums are returned (the reference leaves them numpy)."""
+        from ..secret_sharing import ss_params
+        dev = self.compute_device
+        total = 0
+        for size, _ in models:
+            total += size
+        params = ss_params(recover_fun) if recover_fun else None
+        avg = OrderedDict()
+        keys = list(models[0][1].keys())
+        out_dev = torch.device('cpu')
+        for key in keys:
+            shares = [_share_to_device(m[key], dev) for _, m in models
+                      if key in m]
+            if params is None:
+                avg[key] = ops.ss_recover(shares, 1.0, 0.0, 1.0, 1.0,
+                                          recover=False).to(out_dev)
+            else:
+                mod, maximum, eps = params
+                avg[key] = ops.ss_recover(shares, mod, maximum, eps,
+                                          float(total)).to(out_dev)
+        return avg
+
+
+def _share_to_device(x, dev):
+    """A client's share sum (numpy int64/float64 array, or a tensor of those
+    dtypes) as a contiguous device tensor."""
+    import numpy as np
+    if isinstance(x, torch.Tensor):
+        t = x.detach()
+    else:
+        a = np.asarray(x)
+        if a.dtype not in (np.int64, np.float64):
+            raise NotImplementedError('secret-sharing share of dtype %s' %
+                                      a.dtype)
+        t = torch.from_numpy(np.ascontiguousarray(a))
+    if t.dtype not in (torch.int64, torch.float64):
+        raise NotImplementedError('secret-sharing share of dtype %s' %
+                                  t.dtype)
+    return t.to(dev).contiguous()
 
 
 class OnlineClientsAvgAggregator(ClientsAvgAggregator):

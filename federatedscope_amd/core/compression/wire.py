@@ -1,0 +1,178 @@
+"""Quantised uploads decoded straight into the device client stack.
+
+The reference server dequantises every upload on the host
+(Server.callback_funcs_model_para → symmetric_uniform_dequantization,
+server.py:946-960; compression/utils.py:64-90) and aggregates fp32 dicts.
+Here an upload's wire form — int8/int16 codes of the ``*.weight_quant`` keys,
+their fp32 ``*.weight_scale`` scalars, and the unquantised fp32 keys — is
+packed into one pinned byte buffer, copied to the GPU in ONE DMA (about
+1 B per quantised parameter instead of 4), and expanded by one
+fsagg_wire_unpack_f32 launch into the client's fp32 row of the stack:
+``fl32(float(q) * scale)``, exactly the reference's ``value * alpha``.
+
+Packed buffer: [scales: nscale × f32][f32 keys][int16 codes][int8 codes],
+each region 16-byte aligned.
+"""
+from collections import OrderedDict
+
+import torch
+
+from ... import _lib as L
+from ... import ops
+from ...layout import BucketLayout
+from .utils import scale_to_f32
+
+_QUANT_KINDS = {torch.int8: L.FSAGG_WIRE_I8, torch.int16: L.FSAGG_WIRE_I16}
+
+
+def _align(x, a=16):
+    return -(-x // a) * a
+
+
+class QuantPlan:
+    """Static decode plan of one quantised model layout.
+
+    ``template`` is a wire dict (the output of
+    symmetric_uniform_quantization); the dequantised layout keeps the
+    wire order with ``x.weight_quant`` renamed ``x.weight`` and the
+    ``x.weight_scale`` entries dropped (utils.py:80-89)."""
+
+    def __init__(self, template):
+        deq = OrderedDict()
+        self.quant = OrderedDict()   # dequantised key -> (wire key, dtype)
+        self.plain = []              # fp32 keys sent as is
+        for key, value in template.items():
+            if 'weight_quant' in key:
+                t = value if isinstance(value, torch.Tensor) else \
+                    torch.as_tensor(value)
+                if t.dtype not in _QUANT_KINDS:
+                    raise TypeError('%s: codes must be int8/int16, got %s' %
+                                    (key, t.dtype))
+                k = key.replace('weight_quant', 'weight')
+                deq[k] = torch.empty(t.shape, dtype=torch.float32)
+                self.quant[k] = (key, t.dtype)
+            elif 'weight_scale' in key:
+                continue
+            else:
+                t = value if isinstance(value, torch.Tensor) else \
+                    torch.as_tensor(value)
+                if t.dtype != torch.float32:
+                    raise NotImplementedError(
+                        'wire staging of non-fp32 key %r (%s)' % (key,
+                                                                  t.dtype))
+                deq[key] = torch.empty(t.shape, dtype=torch.float32)
+                self.plain.append(key)
+        self.layout = BucketLayout(deq)
+        lay = self.layout
+        self.scale_keys = [self.quant[k][0].replace('weight_quant',
+                                                     'weight_scale')
+                           for k in lay.keys if k in self.quant]
+        nscale = len(self.scale_keys)
+        off = _align(4 * max(nscale, 1))
+        recs = []
+        self.regions = []            # (key, wire key, byte offset, dtype)
+        for want in (torch.float32, torch.int16, torch.int8):
+            width = torch.empty((), dtype=want).element_size()
+            for k in lay.keys:
+                if k in self.quant:
+                    wk, dt = self.quant[k]
+                    if dt == want:
+                        recs.append((off, lay.offsets[k], lay.numels[k],
+                                     _QUANT_KINDS[dt],
+                                     self.scale_keys.index(
+                                         wk.replace('weight_quant',
+                                                    'weight_scale'))))
+                        self.regions.append((k, wk, off, dt))
+                        off += lay.numels[k] * width
+                elif want == torch.float32:
+                    recs.append((off, lay.offsets[k], lay.numels[k],
+                                 L.FSAGG_WIRE_F32, -1))
+                    self.regions.append((k, k, off, torch.float32))
+                    off += lay.numels[k] * 4
+            off = _align(off)
+        self.records = recs
+        self.nbytes = max(off, 16)
+        self.nscale = nscale
+        self.max_len = max([r[2] for r in recs] + [0])
+        self.wire_keys = list(template.keys())
+        self._segs = {}
+
+    def segs(self, device):
+        d = str(device)
+        if d not in self._segs:
+            self._segs[d] = ops.wire_segments(self.records, device)
+        return self._segs[d]
+
+    def check(self, wire):
+        """The upload must carry exactly the plan's wire keys and dtypes."""
+        for k, (wk, dt) in self.quant.items():
+            v = wire.get(wk)
+            if not isinstance(v, torch.Tensor) or v.dtype != dt or \
+                    v.numel() != self.layout.numels[k]:
+                raise ValueError('upload key %r does not match the wire '
+                                 'layout (%s, %d elements)' %
+                                 (wk, dt, self.layout.numels[k]))
+        for k in self.plain:
+            v = wire.get(k)
+            if not isinstance(v, torch.Tensor) or \
+                    v.dtype != torch.float32 or \
+                    v.numel() != self.layout.numels[k]:
+                raise ValueError('upload key %r does not match the wire '
+                                 'layout' % k)
+        for sk in self.scale_keys:
+            if sk not in wire:
+                raise KeyError(sk)
+
+    def pack_host(self, wire, buf):
+        """Pack one upload into the pinned uint8 buffer ``buf``."""
+        scales = buf[:4 * max(self.nscale, 1)].view(torch.float32)
+        for j, sk in enumerate(self.scale_keys):
+            scales[j] = scale_to_f32(wire[sk])
+        for k, wk, off, dt in self.regions:
+            src = wire[wk].detach().reshape(-1)
+            width = src.element_size()
+            buf[off:off + src.numel() * width].view(dt).copy_(src)
+        return buf
+
+
+class WireStager:
+    """Double-buffered pinned → device staging of quantised uploads; the
+    DMA and the decode kernel run on a side stream, ordered after the
+    consumer stream's earlier work (stack rows are reused across rounds)."""
+
+    def __init__(self, plan, device, nbuf=2):
+        self.plan = plan
+        self.device = torch.device(device)
+        self.stream = torch.cuda.Stream(self.device)
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        self.nbuf = nbuf
+        self.host = [torch.empty(plan.nbytes, dtype=torch.uint8,
+                                 pin_memory=True) for _ in range(nbuf)]
+        self.dev = [torch.empty(plan.nbytes, dtype=torch.uint8,
+                                device=self.device) for _ in range(nbuf)]
+        self.events = [None] * nbuf
+        self.i = 0
+
+    def put(self, wire, dst_row):
+        """Stage one upload (a wire dict of host or device tensors) into the
+        fp32 row ``dst_row``."""
+        plan = self.plan
+        plan.check(wire)
+        b = self.i % self.nbuf
+        self.i += 1
+        if self.events[b] is not None:
+            self.events[b].synchronize()   # the DMA that last read host[b]
+        plan.pack_host(wire, self.host[b])
+        with torch.cuda.stream(self.stream):
+            self.dev[b].copy_(self.host[b], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+            scales = self.dev[b][:4 * max(plan.nscale, 1)].view(torch.float32)
+            ops.wire_unpack(self.dev[b], plan.segs(self.device),
+                            len(plan.records), plan.max_len, scales, dst_row,
+                            src_bytes=plan.nbytes,
+                            max_dst=plan.layout.numel)
+        self.events[b] = ev
+
+    def finish(self):
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)

@@ -45,13 +45,21 @@ class StagedUpdate(Mapping):
 class DeviceIngress:
     """Stage uploads of one model layout into a device client stack."""
 
-    def __init__(self, template, capacity, device=None, as_float=False):
+    def __init__(self, template, capacity, device=None, as_float=False,
+                 quantized=False):
         from ..aggregators._engine import compute_device
         self.device = compute_device(device)
-        if as_float:
-            template = {k: torch.empty(param2tensor(v).shape)
-                        for k, v in template.items()}
-        self.layout = BucketLayout(template)
+        self.plan = None
+        if quantized:
+            # template is a wire dict (symmetric_uniform_quantization)
+            from ..compression.wire import QuantPlan
+            self.plan = QuantPlan(template)
+            self.layout = self.plan.layout
+        else:
+            if as_float:
+                template = {k: torch.empty(param2tensor(v).shape)
+                            for k, v in template.items()}
+            self.layout = BucketLayout(template)
         if self.layout.other:
             raise NotImplementedError(
                 'ingress staging of non-fp32 keys %s' % list(self.layout.other))
@@ -86,6 +94,24 @@ class DeviceIngress:
         else:
             self.layout.pack_device(src, self.stack.slab[slot])
         return sample_size, StagedUpdate(self, slot, model_para.keys())
+
+    def receive_quantized(self, sample_size, wire):
+        """Stage one quantised upload (the wire dict of
+        symmetric_uniform_quantization): the codes cross PCIe as int8/int16
+        and are dequantised into the slot by fsagg_wire_unpack_f32 — the
+        reference's dequantise-on-receipt (server.py:946-960) fused with the
+        H2D copy.  Returns (sample_size, StagedUpdate of the fp32 keys)."""
+        if self.plan is None:
+            raise RuntimeError('ingress was not built for quantised uploads')
+        from ..compression.wire import WireStager
+        if self.next_slot >= self.stack.capacity:
+            self.stack.ensure(self.stack.capacity * 2)
+        slot = self.next_slot
+        self.next_slot += 1
+        if self._stager is None:
+            self._stager = WireStager(self.plan, self.device)
+        self._stager.put(wire, self.stack.slab[slot])
+        return sample_size, StagedUpdate(self, slot, self.layout.keys)
 
     def sync(self):
         """Make the current stream wait for every staged copy."""

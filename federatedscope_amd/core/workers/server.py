@@ -5,7 +5,8 @@ hot path:
 
 * callback_funcs_model_para (server.py:929-988): buffer an upload under
   msg_buffer['train'][round][sender] (stale ones in staled_msg_buffer, too old
-  ones dropped), optionally dequantise it, feed online aggregation;
+  ones dropped), optionally dequantise it (on the device, fused with the
+  staging copy — core/compression/wire.py), feed online aggregation;
 * check_and_move_on (:315-383, count-based part): aggregate once
   sample_client_num uploads of the current round are in;
 * _perform_federated_aggregation (:437-490): msg_list in arrival order plus
@@ -43,7 +44,9 @@ class AggregationServer:
 
     # -- server.py:929-988 ---------------------------------------------------
     def callback_funcs_model_para(self, round, sender, content):
-        if self.dequantize:
+        staged_quant = self.dequantize and self.stage_on_arrival and \
+            round == self.state
+        if self.dequantize and not staged_quant:
             from ..compression import symmetric_uniform_dequantization
             sample_size, quant_model = content
             content = (sample_size,
@@ -53,8 +56,13 @@ class AggregationServer:
                 if self.ingress is None:
                     self.ingress = DeviceIngress(content[1],
                                                  self.sample_client_num,
-                                                 device=self.device)
-                content = self.ingress.receive(*content)
+                                                 device=self.device,
+                                                 quantized=staged_quant)
+                if staged_quant:
+                    # dequantised on the device as the upload is staged
+                    content = self.ingress.receive_quantized(*content)
+                else:
+                    content = self.ingress.receive(*content)
             self.msg_buffer['train'].setdefault(round, dict())[sender] = \
                 content
         elif round >= self.state - self.staleness_toleration:

@@ -1,0 +1,145 @@
+// Wire formats of client uploads, decoded on the device (gfx950):
+//
+//  * symmetric uniform quantisation (core/compression/utils.py:70-90):
+//    the server's dequantisation `value * alpha` (int8/int16 codes times the
+//    fp32 0-dim scale, promoted to fp32: one rounding) fused with the scatter
+//    of an upload's packed wire bytes into its fp32 client-stack row, so
+//    only ~1 B per quantised parameter crosses PCIe;
+//  * additive secret sharing (core/secret_sharing/secret_sharing.py:88-98
+//    and clients_avg_aggregator.py:79-98): the server sums the clients'
+//    fixed-point shares (weight 1.0, numpy float64 semantics), maps the sum
+//    back with fixedpoint2float, divides by the total sample size and casts
+//    to fp32 — one fused pass instead of np.vectorize per element.
+//
+// Both are HBM-bound elementwise passes; every arithmetic step is one IEEE
+// operation in the reference's order, so the results are bit-exact.
+#include <cmath>
+
+#include "common.h"
+
+namespace fsagg {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kPerThread = 4;
+
+struct WireSeg {
+  int64_t src;  // byte offset of the segment in the packed upload
+  int64_t dst;  // element offset in the fp32 row
+  int64_t len;  // elements
+  int32_t kind; // FSAGG_WIRE_*
+  int32_t scale_idx;  // index into the upload's scale table (-1: none)
+};
+static_assert(sizeof(WireSeg) == 32, "WireSeg is part of the ABI");
+
+// grid = (ceil(max_len / (kBlock * kPerThread)), nseg): one y-row per
+// segment, consecutive threads take consecutive elements.
+__global__ __launch_bounds__(kBlock) void wire_unpack_kernel(
+    const unsigned char *__restrict__ src, const WireSeg *__restrict__ segs,
+    const float *__restrict__ scales, float *__restrict__ out) {
+  const WireSeg sg = segs[blockIdx.y];
+  const int64_t base = int64_t(blockIdx.x) * kBlock * kPerThread;
+  if (base >= sg.len) return;
+  const float s = sg.scale_idx >= 0 ? scales[sg.scale_idx] : 1.0f;
+#pragma unroll
+  for (int e = 0; e < kPerThread; ++e) {
+    const int64_t i = base + int64_t(e) * kBlock + threadIdx.x;
+    if (i >= sg.len) break;
+    float v;
+    if (sg.kind == FSAGG_WIRE_I8) {
+      v = mul_rn(float(reinterpret_cast<const int8_t *>(src + sg.src)[i]), s);
+    } else if (sg.kind == FSAGG_WIRE_I16) {
+      v = mul_rn(float(reinterpret_cast<const int16_t *>(src + sg.src)[i]),
+                 s);
+    } else {  // FSAGG_WIRE_F32: copied as is
+      v = reinterpret_cast<const float *>(src + sg.src)[i];
+    }
+    out[sg.dst + i] = v;
+  }
+}
+
+// numpy's float64 remainder (npy_divmod): the result takes the divisor's
+// sign; an exact zero becomes +0.0 for a positive divisor.
+__device__ __forceinline__ double py_mod(double a, double b) {
+  double m = fmod(a, b);
+  if (m != 0.0) {
+    if ((b < 0.0) != (m < 0.0)) m = __dadd_rn(m, b);
+  } else {
+    m = copysign(0.0, b);
+  }
+  return m;
+}
+
+__global__ __launch_bounds__(kBlock) void ss_recover_kernel(
+    const void *const *__restrict__ rows, const uint8_t *__restrict__ is_int,
+    int n, int64_t numel, double mod, double maximum, double epsilon,
+    double total, int recover, float *__restrict__ out,
+    double *__restrict__ out_sum) {
+  const int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (p >= numel) return;
+  // avg = x_0 * 1.0, then avg += x_i * 1.0 in list order (float64)
+  double acc = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double x =
+        is_int[i] ? __ll2double_rn(static_cast<const int64_t *>(rows[i])[p])
+                  : static_cast<const double *>(rows[i])[p];
+    acc = i == 0 ? x : __dadd_rn(acc, x);
+  }
+  if (!recover) {
+    out_sum[p] = acc;
+    return;
+  }
+  // _fixedpoint2float: x %= mod; x > maximum ? -(mod - x)/eps : x/eps
+  const double x = py_mod(acc, mod);
+  const double r = x > maximum ? -__ddiv_rn(__dsub_rn(mod, x), epsilon)
+                               : __ddiv_rn(x, epsilon);
+  // avg /= training_set_size; torch.FloatTensor(avg)
+  out[p] = __double2float_rn(__ddiv_rn(r, total));
+}
+
+}  // namespace
+}  // namespace fsagg
+
+using namespace fsagg;
+
+extern "C" int fsagg_wire_unpack_f32(const void *src, const void *segs,
+                                     const float *scales, int nseg,
+                                     int64_t max_len, float *out,
+                                     fsagg_stream_t stream) {
+  if (!src || !segs || !out || nseg < 0 || max_len < 0) {
+    set_error("fsagg_wire_unpack_f32: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  if (nseg == 0 || max_len == 0) return FSAGG_OK;
+  if (nseg > 65535) {
+    set_error("fsagg_wire_unpack_f32: %d segments > 65535", nseg);
+    return FSAGG_EINVAL;
+  }
+  const int64_t per = int64_t(kBlock) * kPerThread;
+  hipLaunchKernelGGL(wire_unpack_kernel,
+                     dim3(unsigned((max_len + per - 1) / per), unsigned(nseg)),
+                     dim3(kBlock), 0, as_stream(stream),
+                     static_cast<const unsigned char *>(src),
+                     static_cast<const WireSeg *>(segs), scales, out);
+  return check_launch("fsagg_wire_unpack_f32");
+}
+
+extern "C" int fsagg_ss_recover_f32(const void *const *rows,
+                                    const uint8_t *row_is_int, int n,
+                                    int64_t numel, double mod, double maximum,
+                                    double epsilon, double total, int recover,
+                                    float *out, double *out_sum,
+                                    fsagg_stream_t stream) {
+  if (!rows || !row_is_int || n < 1 || numel < 0 ||
+      (recover && !out) || (!recover && !out_sum)) {
+    set_error("fsagg_ss_recover_f32: invalid argument (n=%d)", n);
+    return FSAGG_EINVAL;
+  }
+  if (numel == 0) return FSAGG_OK;
+  hipLaunchKernelGGL(ss_recover_kernel,
+                     dim3(unsigned((numel + kBlock - 1) / kBlock)),
+                     dim3(kBlock), 0, as_stream(stream), rows, row_is_int, n,
+                     numel, mod, maximum, epsilon, total, recover, out,
+                     out_sum);
+  return check_launch("fsagg_ss_recover_f32");
+}

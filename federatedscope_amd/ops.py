@@ -352,3 +352,120 @@ def fill_uniform(slab, numel, seed, index_offset=0):
 
 def round_up(x, a):
     return int(math.ceil(x / a) * a)
+
+
+# -- wire formats and secret sharing ----------------
+WIRE_SEG_DTYPE = [('src', '<i8'), ('dst', '<i8'), ('len', '<i8'),
+                  ('kind', '<i4'), ('scale_idx', '<i4')]
+
+
+def wire_segments(records, device):
+    """Device table of (src_byte_off, dst_elem_off, len, kind, scale_idx)
+    records (32 B each, the layout fsagg_wire_unpack_f32 reads)."""
+    import numpy as np
+    arr = np.zeros(len(records), dtype=WIRE_SEG_DTYPE)
+    for i, (src, dst, ln, kind, sidx) in enumerate(records):
+        if kind not in (L.FSAGG_WIRE_F32, L.FSAGG_WIRE_I8, L.FSAGG_WIRE_I16):
+            raise ValueError('unknown wire kind %r' % kind)
+        width = {L.FSAGG_WIRE_F32: 4, L.FSAGG_WIRE_I8: 1,
+                 L.FSAGG_WIRE_I16: 2}[kind]
+        if src % width:
+            raise ValueError('segment %d source offset %d is not %d-byte '
+                             'aligned' % (i, src, width))
+        arr[i] = (src, dst, ln, kind, sidx)
+    return torch.from_numpy(arr.view(np.uint8).copy()).to(device)
+
+
+def wire_unpack(src, segs, nseg, max_len, scales, out, src_bytes=None,
+                max_dst=None):
+    """Decode one client's packed upload (``src``: device uint8 buffer) into
+    its fp32 row ``out`` per the device segment table ``segs``.  The caller
+    (which built ``segs`` with :func:`wire_segments`) states the extents it
+    checked: ``src_bytes`` ≤ src.numel(), every dst + len ≤ ``max_dst``."""
+    _check_f32_cuda(out, 'out', align=4)
+    if src.device != out.device or segs.device != out.device or \
+            scales.device != out.device:
+        raise ValueError('wire buffers on different devices')
+    if src.dtype != torch.uint8 or segs.dtype != torch.uint8 or \
+            scales.dtype != torch.float32:
+        raise ValueError('src/segs must be uint8, scales float32')
+    if segs.numel() != 32 * nseg:
+        raise ValueError('segment table holds %d bytes, expected %d' %
+                         (segs.numel(), 32 * nseg))
+    if src_bytes is not None and src_bytes > src.numel():
+        raise ValueError('packed upload larger than the staging buffer')
+    if max_dst is not None and max_dst > out.numel():
+        raise ValueError('segments write past the end of the row')
+    L.check(L.load().fsagg_wire_unpack_f32(
+        src.data_ptr(), segs.data_ptr(), scales.data_ptr(), int(nseg),
+        int(max_len), out.data_ptr(), _stream(out.device)),
+        'fsagg_wire_unpack_f32')
+    return out
+
+
+def ss_recover(shares, mod, maximum, epsilon, total, recover=True):
+    """Secret-sharing FedAvg of one key: ``shares`` are per-client device
+    tensors (float64 or int64, same shape).  Returns fp32 (recovered, divided
+    by ``total``) or, with ``recover=False``, the float64 share sums."""
+    if not shares:
+        raise ValueError('no shares')
+    dev = shares[0].device
+    shape = shares[0].shape
+    numel = shares[0].numel()
+    for i, t in enumerate(shares):
+        if t.device != dev or dev.type != 'cuda' or t.shape != shape or \
+                not t.is_contiguous() or t.dtype not in (torch.float64,
+                                                         torch.int64):
+            raise ValueError('share %d must be a contiguous float64/int64 '
+                             'tensor of shape %s on one GPU' % (i, shape))
+    tab = torch.tensor([t.data_ptr() for t in shares], dtype=torch.int64,
+                       device=dev)
+    is_int = torch.tensor([t.dtype == torch.int64 for t in shares],
+                          dtype=torch.uint8, device=dev)
+    out = torch.empty(shape, dtype=torch.float32 if recover else
+                      torch.float64, device=dev)
+    L.check(L.load().fsagg_ss_recover_f32(
+        tab.data_ptr(), is_int.data_ptr(), len(shares), numel, float(mod),
+        float(maximum), float(epsilon), float(total), 1 if recover else 0,
+        out.data_ptr() if recover else None,
+        None if recover else out.data_ptr(), _stream(dev)),
+        'fsagg_ss_recover_f32')
+    return out
+
+
+def delta_sqnorm(rows, seg_offsets, base=None, workspace=None):
+    """sq[i][s] = Σ_{p in key s} fl32(x_i[p] - base[p])² in float64 (device
+    tensor [n][nseg])."""
+    offs = [int(o) for o in seg_offsets]
+    if offs[0] != 0 or offs[-1] != rows.numel or \
+            any(b < a for a, b in zip(offs, offs[1:])):
+        raise ValueError('segment offsets must rise from 0 to numel')
+    if base is not None:
+        _check_out(base, rows.numel, rows.device, what='base', align=4)
+    nseg = len(offs) - 1
+    lib = L.load()
+    need = lib.fsagg_delta_sqnorm_workspace_bytes(rows.n, rows.numel, nseg)
+    ws = (workspace or _WS).get(rows.device, need)
+    seg = torch.tensor(offs, dtype=torch.int64, device=rows.device)
+    sq = torch.empty((rows.n, nseg), dtype=torch.float64, device=rows.device)
+    L.check(lib.fsagg_delta_sqnorm_f32(
+        rows.ptr(), rows.n, rows.numel,
+        None if base is None else base.data_ptr(), seg.data_ptr(), nseg,
+        sq.data_ptr(), ws.data_ptr(), ws.numel(), _stream(rows.device)),
+        'fsagg_delta_sqnorm_f32')
+    return sq
+
+
+def delta_wsum(rows, weights, base, out):
+    """out = Σ_i fl32(w_i · fl32(x_i − base)) (fp32, list order)."""
+    _check_out(base, rows.numel, rows.device, what='base', align=4)
+    _check_out(out, rows.numel, rows.device, align=4)
+    if len(weights) != rows.n:
+        raise ValueError('%d weights for %d rows' % (len(weights), rows.n))
+    w = _fp32_dev(weights, rows.device)
+    L.check(L.load().fsagg_delta_wsum_f32(rows.ptr(), w.data_ptr(), rows.n,
+                                          rows.numel, base.data_ptr(),
+                                          out.data_ptr(),
+                                          _stream(rows.device)),
+            'fsagg_delta_wsum_f32')
+    return out

@@ -191,6 +191,73 @@ int fsagg_server_opt_step_f32(float *param, const float *avg, float *state0,
                               fsagg_stream_t stream);
 
 /*
+ * Quantised / packed upload → fp32 client-stack row, in one launch.
+ * `src` (device) holds one client's packed wire bytes; `segs` (device) is an
+ * array of nseg records (32 B each, naturally aligned):
+ *     struct { int64_t src_byte_off, dst_elem_off, len;
+ *              int32_t kind, scale_idx; }
+ * kind FSAGG_WIRE_I8 / _I16: out[dst + i] = fl32(float(q[i]) * scales[idx])
+ *   — the server's symmetric_uniform_dequantization `value * alpha`
+ *   (federatedscope/core/compression/utils.py:70-90; int8/int16 codes times
+ *   the fp32 scale tensor, one fp32 rounding), fused with the H2D scatter;
+ * kind FSAGG_WIRE_F32: out[dst + i] = src_f32[i] (unquantised keys).
+ * scales (device) holds the upload's per-key fp32 scales; max_len is the
+ * longest segment.  Replaces Server.callback_funcs_model_para's
+ * dequantisation step (federatedscope/core/workers/server.py:946-960).
+ */
+enum fsagg_wire_kind { FSAGG_WIRE_F32 = 0, FSAGG_WIRE_I8 = 1,
+                       FSAGG_WIRE_I16 = 2 };
+int fsagg_wire_unpack_f32(const void *src, const void *segs,
+                          const float *scales, int nseg, int64_t max_len,
+                          float *out, fsagg_stream_t stream);
+
+/*
+ * Secret-sharing FedAvg (cfg.federate.use_ss) in one pass:
+ *     acc = Σ_i double(x_i[p])      (list order, weight 1.0; int64 shares
+ *                                    converted round-to-nearest, as numpy)
+ *     if recover:  x = acc mod `mod` (numpy float remainder)
+ *                  r = x > maximum ? -(mod - x) / epsilon : x / epsilon
+ *                  out[p] = fl32(r / total)
+ *     else:        out_sum[p] = acc
+ * Replaces the use_ss branch of ClientsAvgAggregator._para_weighted_avg
+ * (clients_avg_aggregator.py:79-98) with AdditiveSecretSharing.
+ * fixedpoint2float (federatedscope/core/secret_sharing/secret_sharing.py:
+ * 88-98) as recover_fun.  rows (device) n pointers to float64 or int64
+ * shares (row_is_int, device, n bytes); mod/maximum/epsilon are the
+ * AdditiveSecretSharing constants as doubles (mod = float(2*2^size + 1)).
+ */
+int fsagg_ss_recover_f32(const void *const *rows, const uint8_t *row_is_int,
+                         int n, int64_t numel, double mod, double maximum,
+                         double epsilon, double total, int recover,
+                         float *out, double *out_sum, fsagg_stream_t stream);
+
+/*
+ * Per-row, per-key squared L2 distance to a base row, in fp64:
+ *     sq[i][s] = Σ_{p in seg s} fl32(x_i[p] - base[p])^2   (base may be NULL)
+ * The ‖local − last‖² terms of calc_l2_dissim / calc_blocal_dissim
+ * (federatedscope/core/monitors/metric_calculator.py:309-372).
+ * seg_off (device) nseg+1 int64 offsets as for fsagg_pairdist_f32.
+ * Workspace: fsagg_delta_sqnorm_workspace_bytes(n, numel, nseg).
+ */
+size_t fsagg_delta_sqnorm_workspace_bytes(int n, int64_t numel, int nseg);
+int fsagg_delta_sqnorm_f32(const float *const *rows, int n, int64_t numel,
+                           const float *base, const int64_t *seg_off,
+                           int nseg, double *sq, void *workspace,
+                           size_t workspace_bytes, fsagg_stream_t stream);
+
+/*
+ * Weighted sum of client deltas, per element in row-table order from +0:
+ *     out[p] = Σ_i fl32(w_i * fl32(x_i[p] - base[p]))
+ * The global update Σ_i w_i (local_i − last) of calc_blocal_dissim
+ * (federatedscope/core/monitors/metric_calculator.py:342-349;
+ * `global_grads[k] += weights[i] * v` with fp32 tensors).  weights (device)
+ * n fp32 (the host's doubles rounded, as ATen casts the scalar).
+ */
+int fsagg_delta_wsum_f32(const float *const *rows, const float *weights,
+                         int n, int64_t numel, const float *base, float *out,
+                         fsagg_stream_t stream);
+
+/*
  * Deterministic synthetic client updates (benchmarks / tests): fills the
  * [n][ld] slab X with u = hash(seed, client, index) mapped to [-1, 1),
  * index < numel; the same generator is restated on the host by the tests.

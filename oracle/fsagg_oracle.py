@@ -27,7 +27,8 @@ __all__ = [
     'median_aggregate', 'trimmed_mean_update', 'trimmedmean_aggregate',
     'bulyan_aggregate', 'normbounding_aggregate', 'interpolate_aggregate',
     'add_init', 'f32', 'trimmed_tolerance', 'bulyan_select', 'asyn_weights',
-    'FedOptState',
+    'FedOptState', 'dequantize', 'ss_fedavg', 'calc_l2_dissim',
+    'calc_blocal_dissim',
 ]
 
 f32 = np.float32
@@ -456,3 +457,87 @@ class FedOptState:
                 self.params[k] = x + (f32(-(o['lr'] / bc1)) * m) / denom
                 self.m[k], self.v[k] = m, v
         return OrderedDict((k, v.copy()) for k, v in self.params.items())
+
+
+# ---------------------------------------------------------------------------
+# §8(f) rows: wire formats, secret sharing, update-dissimilarity metrics
+# ---------------------------------------------------------------------------
+def dequantize(wire):
+    """compression/utils.py:64-90: ``x.weight_quant * x.weight_scale`` in
+    fp32 (int codes promoted to float32, times the fp32 scale, one rounding),
+    other keys passed through, ``*.weight_scale`` dropped."""
+    out = OrderedDict()
+    for key, value in wire.items():
+        if 'weight_quant' in key:
+            alpha = np.float32(np.asarray(
+                wire[key.replace('weight_quant', 'weight_scale')]))
+            out[key.replace('weight_quant', 'weight')] = \
+                np.asarray(value).astype(np.float32) * alpha
+        elif 'weight_scale' in key:
+            continue
+        else:
+            out[key] = value
+    return out
+
+
+def _py_mod(a, b):
+    """numpy's float64 remainder (the sign of the divisor)."""
+    m = np.fmod(a, b)
+    fix = (m != 0) & ((b < 0) != (m < 0))
+    m = np.where(fix, m + b, m)
+    return np.where(m == 0, np.copysign(0.0, b), m)
+
+
+def ss_fedavg(models, mod_number, maximum, epsilon):
+    """clients_avg_aggregator.py:79-98 with AdditiveSecretSharing
+    .fixedpoint2float (secret_sharing.py:93-98): Σ shares (float64, weight
+    1.0, list order), x %= mod, x > maximum ? -(mod - x)/eps : x/eps,
+    ÷ total sample size, → fp32."""
+    total = 0
+    for s, _ in models:
+        total += s
+    mod = np.float64(float(mod_number))
+    mx = np.float64(float(maximum))
+    eps = np.float64(epsilon)
+    out = OrderedDict()
+    for key in models[0][1]:
+        acc = None
+        for _, m in models:
+            if key not in m:
+                continue
+            x = np.asarray(m[key]).astype(np.float64) * 1.0
+            acc = x if acc is None else acc + x
+        x = _py_mod(acc, mod)
+        r = np.where(x > mx, -1 * (mod - x) / eps, x / eps)
+        out[key] = (r / np.float64(total)).astype(np.float32)
+    return out
+
+
+def calc_l2_dissim(last, models):
+    """metric_calculator.py:360-372, fp64 accumulation (the reference's fp32
+    torch.norm is ISA-dependent; compared under a tolerance)."""
+    raw = []
+    for _, m in models:
+        sq = 0.0
+        for k, w in m.items():
+            g = (np.asarray(w, np.float32) - np.asarray(last[k], np.float32))
+            sq += float(np.sum(g.astype(np.float64) ** 2))
+        raw.append(math.sqrt(sq))
+    return {'raw': raw, 'mean': float(np.mean(raw))}
+
+
+def calc_blocal_dissim(last, models):
+    """metric_calculator.py:309-357 with fp64 sums of squares; the global
+    update Σ_i fl32(w_i · g_i) keeps the reference's fp32 op order."""
+    w = np.asarray([s for s, _ in models], dtype=np.float64)
+    w = w / np.sum(w)
+    out = OrderedDict()
+    for k in models[0][1]:
+        avg = 0.0
+        glob = np.zeros(np.asarray(last[k]).shape, np.float32)
+        for i, (_, m) in enumerate(models):
+            g = np.asarray(m[k], np.float32) - np.asarray(last[k], np.float32)
+            avg += w[i] * float(np.sum(g.astype(np.float64) ** 2))
+            glob = glob + np.float32(w[i]) * g
+        out[k] = math.sqrt(avg / float(np.sum(glob.astype(np.float64) ** 2)))
+    return out

@@ -1,0 +1,191 @@
+"""§8(f) rows on the GPU: quantised uploads decoded into the device stack,
+secret-sharing FedAvg, and the update-dissimilarity metrics — against the
+reference's own outputs (tests/golden/{quant,ss,dissim}_*.npz, written by
+tools/gen_golden_wire.py) and the CPU oracle.
+
+Bit-exact: dequantisation, quantised FedAvg, secret-sharing recovery.
+Tolerance: the dissimilarity metrics (the reference sums squares in fp32
+with ATen's ISA-dependent reduction order; rtol 1e-5 / 1e-4 as in
+tests/test_oracle_golden.py)."""
+from collections import OrderedDict
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from golden_io import case_names, load_case
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(use_ss=False):
+    return SimpleNamespace(federate=SimpleNamespace(
+        ignore_weight=False, use_ss=use_ss, client_num=1000,
+        sample_client_rate=1.0))
+
+
+def _torch_wire(d, device='cpu'):
+    return OrderedDict((k, torch.from_numpy(np.array(v)).to(device))
+                       for k, v in d.items())
+
+
+def _same_bits(got, want):
+    g = got.detach().cpu().numpy()
+    w = np.asarray(want)
+    assert g.dtype == w.dtype and g.shape == w.shape
+    assert g.tobytes() == w.tobytes()
+
+
+@pytest.mark.parametrize('name', case_names('quant_'))
+@pytest.mark.parametrize('device', ['cpu', 'cuda'])
+def test_dequantization_drop_in(name, device):
+    from federatedscope_amd.core.compression import \
+        symmetric_uniform_dequantization
+    _, clients, _, _, extra = load_case(name)
+    for i, (_, wire) in enumerate(clients):
+        got = symmetric_uniform_dequantization(_torch_wire(wire, device))
+        pre = 'deq|%d|' % i
+        want = OrderedDict((k[len(pre):], v) for k, v in extra.items()
+                           if k.startswith(pre))
+        assert list(got.keys()) == [k.replace('weight_quant', 'weight')
+                                    for k in wire if 'weight_scale' not in k]
+        for k, v in want.items():
+            assert got[k].device.type == device
+            _same_bits(got[k], v)
+
+
+@pytest.mark.parametrize('name', case_names('quant_'))
+@pytest.mark.parametrize('stage', [True, False])
+def test_quantized_uploads_through_server(name, stage):
+    """Server.callback_funcs_model_para with quantization.method='uniform':
+    staged uploads cross PCIe as int codes and are dequantised into the
+    stack by fsagg_wire_unpack_f32; the round's FedAvg is bit-exact."""
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    from federatedscope_amd.core.workers.server import AggregationServer
+    _, clients, out, _, _ = load_case(name)
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.p = torch.nn.ParameterDict()
+
+        def state_dict(self, *a, **kw):
+            return OrderedDict()
+
+        def load_state_dict(self, sd, strict=True):
+            self.loaded = sd
+
+    srv = AggregationServer(M(), ClientsAvgAggregator(config=_cfg()),
+                            sample_client_num=len(clients),
+                            stage_on_arrival=stage, dequantize=True)
+    for sender, (s, wire) in enumerate(clients):
+        srv.callback_funcs_model_para(0, sender, (s, _torch_wire(wire)))
+    got = srv.history[-1]
+    assert list(got.keys()) == list(out.keys())
+    for k in out:
+        _same_bits(got[k], out[k])
+
+
+def test_wire_unpack_large_int8_int16_mix():
+    from federatedscope_amd import _lib as L
+    from federatedscope_amd import ops
+    rng = np.random.default_rng(3)
+    q8 = rng.integers(-127, 128, 1_000_003).astype(np.int8)
+    q16 = rng.integers(-32767, 32768, 70_001).astype(np.int16)
+    f = rng.standard_normal(4099).astype(np.float32)
+    s8, s16 = np.float32(0.0123), np.float32(3.1e-5)
+    off_f, off16 = 16, 16 + f.nbytes
+    off8 = off16 + q16.nbytes
+    buf = np.zeros(off8 + q8.nbytes, np.uint8)
+    buf[:8].view(np.float32)[:] = [s8, s16]
+    buf[off_f:off16].view(np.float32)[:] = f
+    buf[off16:off8].view(np.int16)[:] = q16
+    buf[off8:].view(np.int8)[:] = q8
+    dev = torch.device('cuda')
+    src = torch.from_numpy(buf).to(dev)
+    out_n = 16 + 4099 + 70_001 + 1_000_003 + 64
+    out = torch.full((out_n, ), -7.0, device=dev)
+    d_f, d16, d8 = 16, 16 + 4099 + 3, 16 + 4099 + 3 + 70_001 + 5
+    recs = [(off_f, d_f, 4099, L.FSAGG_WIRE_F32, -1),
+            (off16, d16, 70_001, L.FSAGG_WIRE_I16, 1),
+            (off8, d8, 1_000_003, L.FSAGG_WIRE_I8, 0)]
+    segs = ops.wire_segments(recs, dev)
+    scales = src[:8].view(torch.float32)
+    ops.wire_unpack(src, segs, 3, 1_000_003, scales, out,
+                    src_bytes=src.numel(), max_dst=out_n)
+    o = out.cpu().numpy()
+    assert o[d_f:d_f + 4099].tobytes() == f.tobytes()
+    assert o[d16:d16 + 70_001].tobytes() == \
+        (q16.astype(np.float32) * s16).tobytes()
+    assert o[d8:d8 + 1_000_003].tobytes() == \
+        (q8.astype(np.float32) * s8).tobytes()
+    # untouched gaps keep their contents
+    assert (o[:16] == -7.0).all() and (o[d_f + 4099:d16] == -7.0).all()
+
+
+@pytest.mark.parametrize('name', case_names('ss_'))
+def test_secret_sharing_fedavg_bit_exact(name):
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    from federatedscope_amd.core.secret_sharing import AdditiveSecretSharing
+    meta, clients, out, _, _ = load_case(name)
+    ss = AdditiveSecretSharing(shared_party_num=len(clients))
+    assert str(ss.mod_number) == meta['mod_number']
+    agg = ClientsAvgAggregator(device='cuda', config=_cfg(use_ss=True))
+    got = agg.aggregate({'client_feedback': clients,
+                         'recover_fun': ss.fixedpoint2float})
+    assert list(got.keys()) == list(out.keys())
+    for k in out:
+        _same_bits(got[k], out[k])
+    # no recover function: the float64 share sums (numpy's x*1.0 + ...)
+    sums = agg.aggregate({'client_feedback': clients, 'recover_fun': None})
+    for k in out:
+        acc = None
+        for _, m in clients:
+            x = np.asarray(m[k]).astype(np.float64) * 1.0
+            acc = x if acc is None else acc + x
+        _same_bits(sums[k], acc)
+
+
+def test_secret_sharing_large_vs_oracle():
+    """100 parties' share sums over 1M coordinates (int64 and float64 rows,
+    wrapped int64 sums included) against the oracle restatement."""
+    from federatedscope_amd import ops
+    rng = np.random.default_rng(11)
+    mod = 2 * 2**60 + 1
+    n, P = 100, 1_000_000
+    shares = []
+    for i in range(n):
+        if i % 3:
+            shares.append(rng.integers(-2**62, 2**62, P, dtype=np.int64))
+        else:
+            shares.append(rng.integers(0, mod, P).astype(np.float64))
+    sizes = [int(s) for s in rng.integers(1, 500, n)]
+    want = O.ss_fedavg([(s, {'w': x}) for s, x in zip(sizes, shares)], mod,
+                       2**60, 1e8)['w']
+    dev = torch.device('cuda')
+    got = ops.ss_recover([torch.from_numpy(x).to(dev) for x in shares],
+                         float(mod), float(2**60), 1e8, float(sum(sizes)))
+    assert got.cpu().numpy().tobytes() == want.tobytes()
+
+
+@pytest.mark.parametrize('name', case_names('dissim_'))
+def test_dissimilarity_metrics(name):
+    from federatedscope_amd.core.monitors import (calc_blocal_dissim,
+                                                  calc_l2_dissim)
+    _, clients, _, last, extra = load_case(name)
+    tl = OrderedDict((k, torch.from_numpy(v)) for k, v in last.items())
+    tc = [(s, OrderedDict((k, torch.from_numpy(v)) for k, v in m.items()))
+          for s, m in clients]
+    l2 = calc_l2_dissim(tl, tc)
+    np.testing.assert_allclose(l2['raw'], extra['l2_raw'], rtol=1e-5)
+    np.testing.assert_allclose(l2['mean'], extra['l2_mean'], rtol=1e-5)
+    ol2 = O.calc_l2_dissim(last, clients)
+    np.testing.assert_allclose(l2['raw'], ol2['raw'], rtol=1e-12)
+    bl = calc_blocal_dissim(tl, tc)
+    assert list(bl.keys()) == [str(k) for k in extra['blocal_keys']]
+    np.testing.assert_allclose(list(bl.values()), extra['blocal'], rtol=1e-4)
+    obl = O.calc_blocal_dissim(last, clients)
+    np.testing.assert_allclose(list(bl.values()), list(obl.values()),
+                               rtol=1e-9)
