@@ -91,6 +91,14 @@ class QuantPlan:
                     off += lay.numels[k] * 4
             off = _align(off)
         self.records = recs
+        # regions of one dtype are back to back: one torch.cat per dtype
+        self.spans = []              # (dtype, byte start, byte end, wire keys)
+        for want in (torch.float32, torch.int16, torch.int8):
+            rs = [r for r in self.regions if r[3] == want]
+            if rs:
+                w = torch.empty((), dtype=want).element_size()
+                end = rs[-1][2] + self.layout.numels[rs[-1][0]] * w
+                self.spans.append((want, rs[0][2], end, [r[1] for r in rs]))
         self.nbytes = max(off, 16)
         self.nscale = nscale
         self.max_len = max([r[2] for r in recs] + [0])
@@ -126,12 +134,17 @@ class QuantPlan:
     def pack_host(self, wire, buf):
         """Pack one upload into the pinned uint8 buffer ``buf``."""
         scales = buf[:4 * max(self.nscale, 1)].view(torch.float32)
-        for j, sk in enumerate(self.scale_keys):
-            scales[j] = scale_to_f32(wire[sk])
-        for k, wk, off, dt in self.regions:
-            src = wire[wk].detach().reshape(-1)
-            width = src.element_size()
-            buf[off:off + src.numel() * width].view(dt).copy_(src)
+        sv = [wire[sk] for sk in self.scale_keys]
+        if sv and all(isinstance(v, torch.Tensor) and v.numel() == 1 and
+                      v.dtype == torch.float32 and v.device.type == 'cpu'
+                      for v in sv):
+            torch.cat([v.reshape(1) for v in sv], out=scales[:len(sv)])
+        else:
+            for j, v in enumerate(sv):
+                scales[j] = scale_to_f32(v)
+        for dt, a, b, wkeys in self.spans:
+            torch.cat([wire[wk].detach().reshape(-1).to('cpu')
+                       for wk in wkeys], out=buf[a:b].view(dt))
         return buf
 
 

@@ -27,6 +27,12 @@ class StagedUpdate(Mapping):
         self.stack = ingress.stack
         self.slot = slot
         self._keys = list(keys)
+        self._keyset = frozenset(self._keys)
+
+    def __contains__(self, k):
+        # the aggregators test key membership n·K times per round; Mapping's
+        # default would build a device view per test
+        return k in self._keyset
 
     def __getitem__(self, k):
         lay = self.stack.layout
