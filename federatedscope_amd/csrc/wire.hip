@@ -70,31 +70,81 @@ __device__ __forceinline__ double py_mod(double a, double b) {
   return m;
 }
 
-__global__ __launch_bounds__(kBlock) void ss_recover_kernel(
-    const void *const *__restrict__ rows, const uint8_t *__restrict__ is_int,
-    int n, int64_t numel, double mod, double maximum, double epsilon,
-    double total, int recover, float *__restrict__ out,
-    double *__restrict__ out_sum) {
-  const int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (p >= numel) return;
-  // avg = x_0 * 1.0, then avg += x_i * 1.0 in list order (float64)
-  double acc = 0.0;
-  for (int i = 0; i < n; ++i) {
-    const double x =
-        is_int[i] ? __ll2double_rn(static_cast<const int64_t *>(rows[i])[p])
-                  : static_cast<const double *>(rows[i])[p];
-    acc = i == 0 ? x : __dadd_rn(acc, x);
+// Two consecutive elements per lane (16-B loads of every share row), rows
+// taken four at a time so their loads are in flight together; the adds
+// stay in list order.
+__device__ __forceinline__ void ss_load2(const void *row, bool is_int,
+                                         int64_t p, bool two, double &x0,
+                                         double &x1) {
+  if (is_int) {
+    const int64_t *r = static_cast<const int64_t *>(row) + p;
+    if (two) {
+      const longlong2 v = *reinterpret_cast<const longlong2 *>(r);
+      x0 = __ll2double_rn(v.x);
+      x1 = __ll2double_rn(v.y);
+    } else {
+      x0 = __ll2double_rn(r[0]);
+      x1 = 0.0;
+    }
+  } else {
+    const double *r = static_cast<const double *>(row) + p;
+    if (two) {
+      const double2 v = *reinterpret_cast<const double2 *>(r);
+      x0 = v.x;
+      x1 = v.y;
+    } else {
+      x0 = r[0];
+      x1 = 0.0;
+    }
   }
-  if (!recover) {
-    out_sum[p] = acc;
-    return;
-  }
+}
+
+__device__ __forceinline__ float ss_recover_one(double acc, double mod,
+                                                double maximum, double epsilon,
+                                                double total) {
   // _fixedpoint2float: x %= mod; x > maximum ? -(mod - x)/eps : x/eps
   const double x = py_mod(acc, mod);
   const double r = x > maximum ? -__ddiv_rn(__dsub_rn(mod, x), epsilon)
                                : __ddiv_rn(x, epsilon);
   // avg /= training_set_size; torch.FloatTensor(avg)
-  out[p] = __double2float_rn(__ddiv_rn(r, total));
+  return __double2float_rn(__ddiv_rn(r, total));
+}
+
+__global__ __launch_bounds__(kBlock) void ss_recover_kernel(
+    const void *const *__restrict__ rows, const uint8_t *__restrict__ is_int,
+    int n, int64_t numel, double mod, double maximum, double epsilon,
+    double total, int recover, float *__restrict__ out,
+    double *__restrict__ out_sum) {
+  const int64_t p = 2 * (int64_t(blockIdx.x) * kBlock + threadIdx.x);
+  if (p >= numel) return;
+  const bool two = p + 1 < numel;
+  // avg = x_0 * 1.0, then avg += x_i * 1.0 in list order (float64)
+  double a0 = 0.0, a1 = 0.0;
+  int i = 0;
+  for (; i + 4 <= n; i += 4) {
+    double x[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      ss_load2(rows[i + u], is_int[i + u], p, two, x[u][0], x[u][1]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a0 = (i + u == 0) ? x[u][0] : __dadd_rn(a0, x[u][0]);
+      a1 = (i + u == 0) ? x[u][1] : __dadd_rn(a1, x[u][1]);
+    }
+  }
+  for (; i < n; ++i) {
+    double x0, x1;
+    ss_load2(rows[i], is_int[i], p, two, x0, x1);
+    a0 = i == 0 ? x0 : __dadd_rn(a0, x0);
+    a1 = i == 0 ? x1 : __dadd_rn(a1, x1);
+  }
+  if (!recover) {
+    out_sum[p] = a0;
+    if (two) out_sum[p + 1] = a1;
+    return;
+  }
+  out[p] = ss_recover_one(a0, mod, maximum, epsilon, total);
+  if (two) out[p + 1] = ss_recover_one(a1, mod, maximum, epsilon, total);
 }
 
 }  // namespace
@@ -136,8 +186,9 @@ extern "C" int fsagg_ss_recover_f32(const void *const *rows,
     return FSAGG_EINVAL;
   }
   if (numel == 0) return FSAGG_OK;
+  const int64_t pairs = (numel + 1) / 2;
   hipLaunchKernelGGL(ss_recover_kernel,
-                     dim3(unsigned((numel + kBlock - 1) / kBlock)),
+                     dim3(unsigned((pairs + kBlock - 1) / kBlock)),
                      dim3(kBlock), 0, as_stream(stream), rows, row_is_int, n,
                      numel, mod, maximum, epsilon, total, recover, out,
                      out_sum);

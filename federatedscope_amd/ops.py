@@ -418,6 +418,9 @@ def ss_recover(shares, mod, maximum, epsilon, total, recover=True):
                                                          torch.int64):
             raise ValueError('share %d must be a contiguous float64/int64 '
                              'tensor of shape %s on one GPU' % (i, shape))
+    # the kernel reads two elements per lane (16-B loads)
+    shares = [t if t.data_ptr() % ALIGN_BYTES == 0 else t.clone()
+              for t in shares]
     tab = torch.tensor([t.data_ptr() for t in shares], dtype=torch.int64,
                        device=dev)
     is_int = torch.tensor([t.dtype == torch.int64 for t in shares],

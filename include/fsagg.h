@@ -225,6 +225,7 @@ int fsagg_wire_unpack_f32(const void *src, const void *segs,
  * 88-98) as recover_fun.  rows (device) n pointers to float64 or int64
  * shares (row_is_int, device, n bytes); mod/maximum/epsilon are the
  * AdditiveSecretSharing constants as doubles (mod = float(2*2^size + 1)).
+ * Every share row must be 16-byte aligned.
  */
 int fsagg_ss_recover_f32(const void *const *rows, const uint8_t *row_is_int,
                          int n, int64_t numel, double mod, double maximum,

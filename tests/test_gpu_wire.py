@@ -148,13 +148,14 @@ def test_secret_sharing_fedavg_bit_exact(name):
         _same_bits(sums[k], acc)
 
 
-def test_secret_sharing_large_vs_oracle():
-    """100 parties' share sums over 1M coordinates (int64 and float64 rows,
-    wrapped int64 sums included) against the oracle restatement."""
+@pytest.mark.parametrize('n,P', [(100, 1_000_000), (7, 1001), (3, 1)])
+def test_secret_sharing_large_vs_oracle(n, P):
+    """Parties' share sums (int64 and float64 rows, wrapped int64 sums
+    included; odd lengths hit the kernel's single-element tail) against the
+    oracle restatement."""
     from federatedscope_amd import ops
-    rng = np.random.default_rng(11)
+    rng = np.random.default_rng(11 + P)
     mod = 2 * 2**60 + 1
-    n, P = 100, 1_000_000
     shares = []
     for i in range(n):
         if i % 3:
