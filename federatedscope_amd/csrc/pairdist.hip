@@ -9,18 +9,22 @@
 // honest clients, which is exactly the regime Krum must rank).
 //
 // Work decomposition
-//   * the flat bucket is cut into chunks of ≤ chl coordinates that never
-//     straddle a key (a per-key chunk prefix is built on the device);
-//     one workgroup per chunk (× tile-pair groups when n > 184);
+//   * the flat bucket is cut into ~1000 chunks that never straddle a key (a
+//     per-key chunk prefix is built on the device); one workgroup per chunk
+//     (× role groups when there are more tile pairs than threads);
 //   * the chunk streams through LDS in stages of `sub` coordinates, stored
-//     coordinate-major ([coord][client], row pitch ldsp) so one lane reads
-//     its 8 + 8 client values with four ds_read_b128;
-//   * each lane owns an 8×8 client-pair tile (64 fp32 accumulators) and a
-//     k-slice of the stage's coordinates; at the end of the chunk the
+//     coordinate-major ([coord][client], row pitch ldsp); a full stage is
+//     loaded with 16-B non-temporal loads into registers one stage ahead, so
+//     the HBM latency hides behind the current stage's FMAs;
+//   * the clients are cut into tiles of TS = 8 or 10 (whichever gives fewer
+//     pair slots: at n = 50, 15 × 100 = 1500 vs 28 × 64 = 1792); each lane
+//     owns one TS×TS tile pair of the upper triangle (TS² fp32 accumulators)
+//     and a k-slice of the stage's coordinates; at the end of the chunk the
 //     k-slices are summed through LDS in a fixed order → partial[chunk][pair];
-//   * a final kernel sums each key's chunks in fp64 (fixed order), takes the
-//     per-key sqrt, rounds to fp32 and accumulates the keys in fp32 in key
-//     order (the reference's `distance += torch.dist(...)`).
+//   * a 1024-thread kernel sums each key's chunks in fp64 (fixed order), and
+//     a final kernel takes the per-key sqrt, rounds to fp32 and accumulates
+//     the keys in fp32 in key order (the reference's
+//     `distance += torch.dist(...)`).
 // Deterministic: no atomics anywhere.
 #include "common.h"
 
@@ -28,15 +32,20 @@ namespace fsagg {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kTS = 8;                       // pair tile side
-constexpr int kRedPitch = kTS * kTS + 1;     // 65: LDS pitch of a reduction slot
+constexpr int kRedPitch = 65;                  // LDS pitch of a reduction slot
 constexpr int kLdsFloats = kBlock * kRedPitch;  // 16640 floats = 65 KiB
-// register-prefetched staging items per thread (each 4 rows × 4 coordinates):
-// a stage holds < kLdsFloats floats: ≤ 1040 items, ≤ 4 × 256 for most n
-constexpr int kStageItems = 4;
+// register-prefetched staging items per thread (each 4 rows × 4
+// coordinates); 10×10 tiles keep one fewer (their accumulators need the
+// registers) and stage fewer coordinates per pass
+constexpr int stage_items(int ts) { return ts == 10 ? 3 : 4; }
 typedef float f4v __attribute__((ext_vector_type(4)));
 
+// Client tiles of side ts (8 or 10: the one with fewer pair slots
+// ntp·ts²; at n = 50, 15 × 100 = 1500 against 28 × 64 = 1792); each lane
+// accumulates one ts × ts tile pair of the upper triangle (diagonal tiles
+// whole, so every lane runs the same code).
 struct PairPlan {
+  int ts;       // tile side
   int nt;       // tiles per side
   int ntp;      // upper-triangular tile pairs
   int groups;   // grid.y
@@ -50,15 +59,22 @@ struct PairPlan {
 
 PairPlan make_plan(int n, int64_t numel, int nseg) {
   PairPlan pl;
-  pl.nt = (n + kTS - 1) / kTS;
+  const int nt8 = (n + 7) / 8, nt10 = (n + 9) / 10;
+  pl.ts = int64_t(nt10) * (nt10 + 1) / 2 * 100 < int64_t(nt8) * (nt8 + 1) / 2 * 64
+              ? 10 : 8;
+  pl.nt = (n + pl.ts - 1) / pl.ts;
   pl.ntp = pl.nt * (pl.nt + 1) / 2;
   pl.groups = (pl.ntp + kBlock - 1) / kBlock;
   pl.tpg = (pl.ntp + pl.groups - 1) / pl.groups;
   pl.ks = kBlock / pl.tpg;
   // pitch ≡ 28 (mod 32) words: conflict-free b128 staging writes and reads
-  pl.ldsp = pl.nt * kTS + 4;
+  pl.ldsp = (pl.nt * pl.ts + 3) / 4 * 4 + 4;
   while (pl.ldsp % 32 != 28) pl.ldsp += 4;
   pl.sub = kLdsFloats / pl.ldsp / kWave * kWave;  // a multiple of 64
+  // full stages are prefetched into stage_items(ts) float4 quads per thread
+  const int quads = (pl.nt * pl.ts + 3) / 4;
+  const int cap = stage_items(pl.ts) * kBlock / quads * 4 / kWave * kWave;
+  if (cap >= kWave && pl.sub > cap) pl.sub = cap;
   if (pl.sub < kWave) pl.sub = kLdsFloats / pl.ldsp;
   // ≈ 1000 chunks (two rounds of the 2 × 256 resident workgroups), a
   // multiple of 64 coordinates so full stages stay 16-B aligned
@@ -94,6 +110,32 @@ __device__ __forceinline__ void tp_to_tiles(int tp, int nt, int &ti, int &tj) {
   tj = r + (tp - base);
 }
 
+// TS values of tile t at one staged coordinate row
+template <int TS>
+__device__ __forceinline__ void read_tile(const float *col, int t,
+                                          float (&x)[TS]) {
+  if constexpr (TS % 4 == 0) {  // ds_read_b128
+    const float4 *p = reinterpret_cast<const float4 *>(col + t * TS);
+#pragma unroll
+    for (int q = 0; q < TS / 4; ++q) {
+      const float4 v = p[q];
+      x[4 * q] = v.x;
+      x[4 * q + 1] = v.y;
+      x[4 * q + 2] = v.z;
+      x[4 * q + 3] = v.w;
+    }
+  } else {  // ds_read_b64 (t·TS floats is 8-B aligned for even TS)
+    const float2 *p = reinterpret_cast<const float2 *>(col + t * TS);
+#pragma unroll
+    for (int q = 0; q < TS / 2; ++q) {
+      const float2 v = p[q];
+      x[2 * q] = v.x;
+      x[2 * q + 1] = v.y;
+    }
+  }
+}
+
+template <int TS>
 __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     const float *const *__restrict__ rows, int n, PairPlan pl,
     const int64_t *__restrict__ seg_off, int nseg,
@@ -122,8 +164,8 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   int ti = 0, tj = 0;
   if (active) tp_to_tiles(tp, pl.nt, ti, tj);
 
-  const int npad = pl.nt * kTS;  // client slots (rows >= n repeat row n-1)
-  const int quads = npad / 4;
+  // client slots (rows >= n repeat row n-1), rounded to whole quads
+  const int quads = (pl.nt * TS + 3) / 4;
   // A full stage is staged from registers: item = (client quad, 4
   // consecutive coordinates) = four 16-B row loads, issued for stage s + 1
   // before stage s is computed, so the HBM latency hides behind the FMAs.
@@ -133,12 +175,16 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   for (int r = 0; r < n; ++r)
     vec = vec && (reinterpret_cast<uintptr_t>(rows[r]) & 15u) == 0;
 
-  float acc[kTS][kTS];
+  float acc[TS][TS];
 #pragma unroll
-  for (int u = 0; u < kTS; ++u)
+  for (int u = 0; u < TS; ++u)
 #pragma unroll
-    for (int v = 0; v < kTS; ++v) acc[u][v] = 0.0f;
+    for (int v = 0; v < TS; ++v) acc[u][v] = 0.0f;
 
+  constexpr int kStageItems = stage_items(TS);
+  // 8×8 tiles have the registers to unroll two coordinates (the LDS
+  // latency of one hides behind the FMAs of the other); 10×10 do not
+  constexpr int kUnroll = TS == 8 ? 2 : 1;
   f4v pre[kStageItems][4];
   auto fetch = [&](int64_t cs) {
 #pragma unroll
@@ -199,17 +245,16 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     // next full stage's loads fly while this one is computed
     if (prefetch && end - (cs + pl.sub) >= pl.sub) fetch(cs + pl.sub);
     if (active) {
-#pragma unroll 2
+#pragma unroll kUnroll
       for (int cc = ksl; cc < len; cc += pl.ks) {
-        const float4 *col = reinterpret_cast<const float4 *>(lds + cc * pl.ldsp);
-        const float4 a0 = col[ti * 2], a1 = col[ti * 2 + 1];
-        const float4 b0 = col[tj * 2], b1 = col[tj * 2 + 1];
-        const float a[kTS] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-        const float b[kTS] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        const float *col = lds + cc * pl.ldsp;
+        float a[TS], b[TS];
+        read_tile<TS>(col, ti, a);
+        read_tile<TS>(col, tj, b);
 #pragma unroll
-        for (int u = 0; u < kTS; ++u)
+        for (int u = 0; u < TS; ++u)
 #pragma unroll
-          for (int v = 0; v < kTS; ++v) {
+          for (int v = 0; v < TS; ++v) {
             const float d = a[u] - b[v];
             acc[u][v] = __builtin_fmaf(d, d, acc[u][v]);
           }
@@ -218,24 +263,31 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     __syncthreads();
   }
 
-  // sum the k-slices of each tile pair in slice order
-  if (ksl < pl.ks) {
-    float *slot = lds + (ksl * pl.tpg + tpl) * kRedPitch;
+  // sum the k-slices of each tile pair in slice order, ≤ 64 accumulators
+  // at a time through LDS
+  constexpr int kE = TS * TS;
 #pragma unroll
-    for (int u = 0; u < kTS; ++u)
+  for (int e0 = 0; e0 < kE; e0 += 64) {
+    if (ksl < pl.ks) {
+      float *slot = lds + (ksl * pl.tpg + tpl) * kRedPitch;
 #pragma unroll
-      for (int v = 0; v < kTS; ++v) slot[u * kTS + v] = acc[u][v];
-  }
-  __syncthreads();
-  const int outs = pl.tpg * kTS * kTS;
-  for (int o = tid; o < outs; o += kBlock) {
-    const int l = o / (kTS * kTS);
-    const int e = o - l * (kTS * kTS);
-    const int gtp = blockIdx.y * pl.tpg + l;
-    if (gtp >= pl.ntp) continue;
-    float sum = 0.0f;
-    for (int k = 0; k < pl.ks; ++k) sum += lds[(k * pl.tpg + l) * kRedPitch + e];
-    partial[(int64_t(c) * pl.ntp + gtp) * (kTS * kTS) + e] = sum;
+      for (int e = e0; e < e0 + 64 && e < kE; ++e)
+        slot[e - e0] = acc[e / TS][e % TS];
+    }
+    __syncthreads();
+    const int ne = kE - e0 < 64 ? kE - e0 : 64;
+    const int outs = pl.tpg * ne;
+    for (int o = tid; o < outs; o += kBlock) {
+      const int l = o / ne;
+      const int e = o - l * ne;
+      const int gtp = blockIdx.y * pl.tpg + l;
+      if (gtp >= pl.ntp) continue;
+      float sum = 0.0f;
+      for (int k = 0; k < pl.ks; ++k)
+        sum += lds[(k * pl.tpg + l) * kRedPitch + e];
+      partial[(int64_t(c) * pl.ntp + gtp) * kE + e0 + e] = sum;
+    }
+    __syncthreads();
   }
 }
 
@@ -253,7 +305,8 @@ __global__ __launch_bounds__(kSegBlock) void pairdist_segsq_kernel(
     const int *__restrict__ prefix, double *__restrict__ segsq) {
   __shared__ double red[kSegSlices][kWave];
   const int s = blockIdx.x;
-  const int per_seg = pl.ntp * kTS * kTS;
+  const int ee = pl.ts * pl.ts;
+  const int per_seg = pl.ntp * ee;
   const int lane = threadIdx.x & (kWave - 1), slice = threadIdx.x / kWave;
   const int r = blockIdx.y * kWave + lane;
   double sq = 0.0;
@@ -268,10 +321,10 @@ __global__ __launch_bounds__(kSegBlock) void pairdist_segsq_kernel(
   double t = 0.0;
 #pragma unroll
   for (int k = 0; k < kSegSlices; ++k) t += red[k][lane];
-  const int tp = r / (kTS * kTS), e = r % (kTS * kTS);
+  const int tp = r / ee, e = r % ee;
   int ti, tj;
   tp_to_tiles(tp, pl.nt, ti, tj);
-  const int i = ti * kTS + e / kTS, j = tj * kTS + e % kTS;
+  const int i = ti * pl.ts + e / pl.ts, j = tj * pl.ts + e % pl.ts;
   double *m = segsq + int64_t(s) * n * n;
   if (i == 0 && j == 1) {
     // the diagonal of this segment (one writer per segment)
@@ -358,7 +411,7 @@ extern "C" size_t fsagg_pairdist_workspace_bytes(int n, int64_t numel,
   const PairPlan pl = make_plan(n, numel, nseg);
   return align256(sizeof(int) * size_t(nseg + 1)) +
          align256(sizeof(float) * size_t(pl.max_chunks) * size_t(pl.ntp) *
-                  kTS * kTS) +
+                  size_t(pl.ts * pl.ts)) +
          align256(sizeof(double) * size_t(nseg) * size_t(n) * size_t(n));
 }
 
@@ -373,12 +426,16 @@ static int pairdist_segsq_impl(const float *const *rows, int n, int64_t numel,
       static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)));
   hipLaunchKernelGGL(chunk_prefix_kernel, dim3(1), dim3(1), 0, s, seg_off,
                      nseg, pl.chl, prefix);
-  if (numel > 0)
-    hipLaunchKernelGGL(pairdist_chunk_kernel,
-                       dim3(unsigned(pl.max_chunks), unsigned(pl.groups)),
-                       dim3(kBlock), 0, s, rows, n, pl, seg_off, nseg, prefix,
-                       partial);
-  const int per_seg = pl.ntp * kTS * kTS;
+  if (numel > 0) {
+    const dim3 grid(unsigned(pl.max_chunks), unsigned(pl.groups));
+    if (pl.ts == 10)
+      hipLaunchKernelGGL(pairdist_chunk_kernel<10>, grid, dim3(kBlock), 0, s,
+                         rows, n, pl, seg_off, nseg, prefix, partial);
+    else
+      hipLaunchKernelGGL(pairdist_chunk_kernel<8>, grid, dim3(kBlock), 0, s,
+                         rows, n, pl, seg_off, nseg, prefix, partial);
+  }
+  const int per_seg = pl.ntp * pl.ts * pl.ts;
   hipLaunchKernelGGL(pairdist_segsq_kernel,
                      dim3(unsigned(nseg), unsigned((per_seg + kWave - 1) / kWave)),
                      dim3(kSegBlock), 0, s, partial, n, pl, nseg, prefix, segsq);
@@ -404,8 +461,8 @@ extern "C" int fsagg_pairdist_f32(const float *const *rows, int n,
   const PairPlan pl = make_plan(n, numel, nseg);
   double *segsq = reinterpret_cast<double *>(
       static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)) +
-      align256(sizeof(float) * size_t(pl.max_chunks) * size_t(pl.ntp) * kTS *
-               kTS));
+      align256(sizeof(float) * size_t(pl.max_chunks) * size_t(pl.ntp) *
+               size_t(pl.ts * pl.ts)));
   pairdist_segsq_impl(rows, n, numel, seg_off, nseg, segsq, workspace, s);
   hipLaunchKernelGGL(pairdist_finish_kernel,
                      dim3(unsigned((n * n + kBlock - 1) / kBlock)),
