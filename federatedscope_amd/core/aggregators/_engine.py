@@ -20,7 +20,7 @@ import torch
 
 from ... import ops
 from ...layout import BucketLayout, ClientStack
-from ..auxiliaries.utils import param2tensor
+from ..auxiliaries.utils import as_float_tensor, param2tensor
 
 
 def compute_device(device=None):
@@ -111,7 +111,7 @@ class DeviceEngine:
             st.slab.zero_()
             self._stacks[key] = st
         if as_float:
-            models = [OrderedDict((k, param2tensor(v).float())
+            models = [OrderedDict((k, as_float_tensor(v))
                                   for k, v in m.items()) for m in models]
         st.load_many(models)
         return st
@@ -126,7 +126,7 @@ class DeviceEngine:
             if k not in model:
                 raise KeyError(k)
             v = param2tensor(model[k])
-            src[k] = v.float() if as_float else v
+            src[k] = as_float_tensor(v) if as_float else v
         layout.pack_device(src, flat)
         return flat
 
@@ -225,6 +225,9 @@ class DeviceEngine:
 
 def _as_float_proto(v):
     t = param2tensor(v)
-    if isinstance(t, torch.Tensor) and t.dtype != torch.float32:
+    if not isinstance(t, torch.Tensor):
+        import numpy as np
+        t = torch.as_tensor(np.asarray(t))
+    if t.dtype != torch.float32:
         return torch.empty(t.shape, dtype=torch.float32)
     return t

@@ -14,8 +14,8 @@ class AsynClientsAvgAggregator(ClientsAvgAggregator):
 
     def aggregate(self, agg_info):
         models = agg_info["client_feedback"]
-        if self.cfg.federate.use_ss:
-            raise NotImplementedError('secret sharing on the async path')
+        # use_ss: the reference hands recover_fun to _para_weighted_avg but
+        # never applies it on this path (:25-31, :53-84); neither do we
         staleness = [x[1] for x in agg_info['staleness']]
         weights = self._asyn_weights(models, staleness)
         out_dev = _first_device(models[0][1])

@@ -51,6 +51,17 @@ def param2tensor(param):
     return param
 
 
+def as_float_tensor(param):
+    """The robust and async rules' cast of a client value to fp32
+    (``x.float()`` for tensors, ``torch.FloatTensor(x)`` otherwise:
+    asyn_clients_avg_aggregator.py:74-77, krum_aggregator.py:48-53)."""
+    t = param2tensor(param)
+    if isinstance(t, torch.Tensor):
+        return t.float()
+    import numpy as np
+    return torch.as_tensor(np.asarray(t)).float()
+
+
 def merge_param_dict(raw_param, filtered_param):
     """Overlay the aggregate onto the model state_dict (utils.py:108-111)."""
     for key in filtered_param.keys():

@@ -15,7 +15,7 @@ from collections.abc import Mapping
 import torch
 
 from ...layout import BucketLayout, ClientStack, HostStager
-from ..auxiliaries.utils import param2tensor
+from ..auxiliaries.utils import as_float_tensor, param2tensor
 
 
 class StagedUpdate(Mapping):
@@ -90,7 +90,7 @@ class DeviceIngress:
         missing = [k for k in self.layout.keys if k not in model_para]
         if missing:
             raise KeyError('staged upload lacks keys %s' % missing)
-        src = {k: (param2tensor(model_para[k]).float() if self.as_float else
+        src = {k: (as_float_tensor(model_para[k]) if self.as_float else
                    param2tensor(model_para[k])) for k in self.layout.keys}
         on_host = any(v.device.type != 'cuda' for v in src.values())
         if on_host:

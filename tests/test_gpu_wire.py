@@ -190,3 +190,32 @@ def test_dissimilarity_metrics(name):
     obl = O.calc_blocal_dissim(last, clients)
     np.testing.assert_allclose(list(bl.values()), list(obl.values()),
                                rtol=1e-9)
+
+
+@pytest.mark.parametrize('nbits', [8, 16])
+def test_quant_plan_layouts(nbits):
+    """Wire layouts with only quantised keys, only fp32 keys, int16 codes,
+    and odd sizes (region offsets, scale table, gaps) through WireStager."""
+    from federatedscope_amd.core.compression import (
+        QuantPlan, WireStager, symmetric_uniform_quantization)
+    rng = np.random.default_rng(nbits)
+    shapes = [('conv1.weight', (3, 5, 7)), ('fc.bias', (13, )),
+              ('fc.weight', (1, )), ('bn.running_mean', (5, )),
+              ('conv2.weight', (2, 3))]
+    for keep in (None, 'weight', 'bias'):
+        m = OrderedDict((k, torch.from_numpy(
+            rng.standard_normal(s).astype(np.float32))) for k, s in shapes
+            if keep is None or k.endswith(keep) or
+            (keep == 'bias' and 'running' in k))
+        wire = symmetric_uniform_quantization(m, nbits=nbits)
+        plan = QuantPlan(wire)
+        st = WireStager(plan, 'cuda')
+        row = torch.full((plan.layout.numel, ), 9.0, device='cuda')
+        st.put(wire, row)
+        st.finish()
+        want = O.dequantize(OrderedDict((k, v.numpy()) for k, v in
+                                        wire.items()))
+        got = plan.layout.unpack(row)
+        assert list(got.keys()) == list(want.keys())
+        for k in want:
+            _same_bits(got[k], np.asarray(want[k], np.float32))
