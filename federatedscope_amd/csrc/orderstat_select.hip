@@ -13,7 +13,9 @@
 //     1 << 8·(d & 3) into word d / 4; n <= 255 keeps every byte from
 //     overflowing) places both needed ranks in their bins; one pass over its
 //     64 words finds both.  While the keys of the two bins would overflow
-//     the 64-slot list, the larger bin is refined by one more 8-bit digit.
+//     the 64-slot list, the bins are refined by their next 7-bit digits,
+//     both in one pass over the keys (rank 1's bins in histogram words
+//     [0, 32), rank 2's in [32, 64)).
 //  3. One compaction pass writes the keys of both bins to one per-lane LDS
 //     list (bin 1 before bin 2 in key order, so the sorted list holds both
 //     ranks) and, for the trimmed mean, sums every key strictly between the
@@ -53,9 +55,9 @@ struct RankSel {
 __device__ __forceinline__ uint32_t bin_mask(int lvl) {
   return lvl >= 32 ? 0u : (0xFFFFFFFFu << lvl);
 }
-// shift of the next 8-bit digit
-__device__ __forceinline__ int digit_shift(const RankSel &s) {
-  return s.lvl > 8 ? s.lvl - 8 : 0;
+// shift of the next digit of `width` bits
+__device__ __forceinline__ int digit_shift(const RankSel &s, int width = 8) {
+  return s.lvl > width ? s.lvl - width : 0;
 }
 
 __device__ __forceinline__ RankSel rank_init(uint32_t kmin, uint32_t kmax,
@@ -96,23 +98,6 @@ __device__ __forceinline__ void hist_add_all(uint32_t *H,
   }
 }
 
-// Refinement: the next digit of the keys of s's bin; lanes with !on (and
-// keys outside the bin) add zeros (no branch per key).
-template <int N>
-__device__ __forceinline__ void hist_add_bin(uint32_t *H,
-                                             const uint32_t (&k)[N], int n,
-                                             const RankSel &s, bool on) {
-  const int sh = digit_shift(s);
-  const uint32_t M = bin_mask(s.lvl);
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-    if (j >= N - kSelStep && j >= n) continue;
-    const uint32_t key = k[j];
-    const bool m = on && (key & M) == s.P;
-    atomicAdd(hist_word(H, key, sh), m ? hist_one(key, sh) : 0u);
-  }
-}
-
 // Locate rank r in the histogram given the word that holds it (w, x) and
 // the count before that word: returns the bin, the count below and in it.
 __device__ __forceinline__ uint32_t hist_bin(int w, uint32_t x, int before,
@@ -130,16 +115,16 @@ __device__ __forceinline__ uint32_t hist_bin(int w, uint32_t x, int before,
   return uint32_t(w) * 4u + byte;
 }
 
-// One pass over the 64 histogram words for rank ra (and rb if TWO): the
-// number of words whose inclusive prefix count is <= r is the word holding
-// r, and the last such prefix is the count before it.
-template <bool TWO>
+// One pass over W histogram words (from H) for rank ra (and rb if TWO):
+// the number of words whose inclusive prefix count is <= r is the word
+// holding r, and the last such prefix is the count before it.
+template <bool TWO, int W = 64>
 __device__ __forceinline__ void hist_scan(const uint32_t *H, int ra, int rb,
                                           uint32_t &da, int &ba, int &ca,
                                           uint32_t &db, int &bb, int &cb) {
   int cum = 0, na = 0, fa = 0, nb = 0, fb = 0;
 #pragma unroll 16
-  for (int w = 0; w < 64; ++w) {
+  for (int w = 0; w < W; ++w) {
     cum += int(__builtin_amdgcn_sad_u8(H[w * kWave], 0u, 0u));
     const bool ta = cum <= ra;
     na += ta;
@@ -150,19 +135,43 @@ __device__ __forceinline__ void hist_scan(const uint32_t *H, int ra, int rb,
       fb = tb ? cum : fb;
     }
   }
-  na = min(na, 63);
+  na = min(na, W - 1);
   da = hist_bin(na, H[na * kWave], fa, ra, ba, ca);
   if (TWO) {
-    nb = min(nb, 63);
+    nb = min(nb, W - 1);
     db = hist_bin(nb, H[nb * kWave], fb, rb, bb, cb);
+  }
+}
+
+// Refinement: the next 7-bit digit of the keys of BOTH ranks' bins in one
+// pass — rank 1's bin counts into histogram words [0, 32), rank 2's into
+// [32, 64) (the bins are disjoint unless shared, and then only rank 1's is
+// counted); other keys and lanes add zeros.
+template <int N>
+__device__ __forceinline__ void hist_add_dual(uint32_t *H,
+                                              const uint32_t (&k)[N], int n,
+                                              const RankSel &s1, bool on1,
+                                              const RankSel &s2, bool on2) {
+  const int sh1 = digit_shift(s1, 7), sh2 = digit_shift(s2, 7);
+  const uint32_t M1 = bin_mask(s1.lvl), M2 = bin_mask(s2.lvl);
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    if (j >= N - kSelStep && j >= n) continue;
+    const uint32_t key = k[j];
+    const bool m1 = on1 && (key & M1) == s1.P;
+    const bool m2 = on2 && (key & M2) == s2.P;
+    const uint32_t d = __builtin_amdgcn_ubfe(key, uint32_t(m2 ? sh2 : sh1),
+                                             7u) | (m2 ? 128u : 0u);
+    atomicAdd(&H[(d >> 2) * kWave],
+              (m1 || m2) ? 1u << ((d & 3u) * 8u) : 0u);
   }
 }
 
 // Narrow s to digit bin d (count b below it, c in it), if on.
 __device__ __forceinline__ void rank_apply(RankSel &s, bool on, uint32_t d,
-                                           int b, int c) {
+                                           int b, int c, int width = 8) {
   if (!on) return;
-  const int sh = digit_shift(s);
+  const int sh = digit_shift(s, width);
   s.below += b;
   s.cnt = c;
   s.P |= d << sh;
@@ -255,31 +264,27 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
   // kList / 2 keys while the list would overflow.
   bool shared = same_bin(s1, s2);
 #pragma unroll 1
-  for (int round = 0; round < 3; ++round) {
+  for (int round = 0; round < 4; ++round) {  // 7-bit digits: lvl 24 → 0
     const bool list1 = s1.lvl > 0, list2 = !shared && s2.lvl > 0;
     const int stored = (list1 ? s1.cnt : 0) + (list2 ? s2.cnt : 0);
     const bool need1 =
         list1 && stored > kList && (shared || s1.cnt > kList / 2);
     const bool need2 = list2 && stored > kList && s2.cnt > kList / 2;
     if (!__any(need1 || need2)) break;
-    if (__any(need1)) {
-      hist_clear(H);
-      hist_add_bin<N>(H, k, n, s1, need1);
-      uint32_t d1, d2;
-      int b1, c1, b2, c2;
-      hist_scan<true>(H, r1 - s1.below, r2 - s2.below, d1, b1, c1, d2, b2,
-                      c2);
-      rank_apply(s2, need1 && shared, d2, b2, c2);
-      rank_apply(s1, need1, d1, b1, c1);
-    }
-    if (__any(need2)) {
-      hist_clear(H);
-      hist_add_bin<N>(H, k, n, s2, need2);
-      uint32_t d2, dx;
-      int b2, c2, bx, cx;
-      hist_scan<false>(H, r2 - s2.below, 0, d2, b2, c2, dx, bx, cx);
-      rank_apply(s2, need2, d2, b2, c2);
-    }
+    hist_clear(H);
+    hist_add_dual<N>(H, k, n, s1, need1, s2, need2);
+    uint32_t d1, d2, d3 = 0;
+    int b1, c1, b2, c2, b3 = 0, c3 = 0;
+    // rank 1 (and rank 2 where it shares rank 1's bin) in words [0, 32)
+    hist_scan<true, 32>(H, r1 - s1.below, r2 - s2.below, d1, b1, c1, d2, b2,
+                        c2);
+    // rank 2 in its own bin: words [32, 64)
+    if (__any(need2))
+      hist_scan<false, 32>(H + 32 * kWave, r2 - s2.below, 0, d3, b3, c3, d3,
+                           b3, c3);
+    rank_apply(s2, need1 && shared, d2, b2, c2, 7);
+    rank_apply(s2, need2, d3, b3, c3, 7);
+    rank_apply(s1, need1, d1, b1, c1, 7);
     shared = same_bin(s1, s2);
   }
 
