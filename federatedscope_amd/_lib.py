@@ -75,6 +75,10 @@ SIGNATURES['fsagg_delta_wsum_f32'] = (
     _c_i, [_c_p, _c_p, _c_i, _c_i64, _c_p, _c_p, _c_p])
 SIGNATURES['fsagg_delta_sqnorm_f32'] = (
     _c_i, [_c_p, _c_i, _c_i64, _c_p, _c_p, _c_i, _c_p, _c_p, _c_sz, _c_p])
+SIGNATURES['fsagg_delta_sqnorm_keys_f32'] = (
+    _c_i, [_c_p, _c_i, _c_i64, _c_p, _c_p, _c_i, _c_p, _c_p, _c_sz, _c_p])
+SIGNATURES['fsagg_delta_wsum_keys_f32'] = (
+    _c_i, [_c_p, _c_p, _c_i, _c_i64, _c_p, _c_p, _c_i, _c_p, _c_p])
 
 _lib = None
 

@@ -3,7 +3,10 @@ calc_blocal_dissim / calc_l2_dissim,
 federatedscope/core/monitors/metric_calculator.py:309-372).
 
 Both read every client's update once more after (or instead of) the
-aggregation, so they reuse the device client stack: the per-client, per-key
+aggregation.  Device-resident client tensors (GPU dicts, or the server's
+staged stack rows) are read in place through a per-key pointer table
+(ops.KeyTable, no copy); host dicts are staged into a device stack first.
+The per-client, per-key
 ‖local − last‖² come from one fsagg_delta_sqnorm_f32 pass (fp64 sums), the
 global update Σ_i w_i (local_i − last) from fsagg_delta_wsum_f32 (the
 reference's fp32 op order, bit-exact) and its per-key ‖·‖² from a second
@@ -45,12 +48,39 @@ def _staged(last_model, local_updated_models):
     return lay, st, last, keys
 
 
+def _in_place(last_model, local_updated_models):
+    """A KeyTable over the clients' own tensors when every one of them is a
+    contiguous fp32 tensor on the compute device (device-resident dicts,
+    StagedUpdate views of the server's stack) — no staging copy; else
+    None (the caller stages)."""
+    from ..aggregators._engine import compute_device
+    dev = compute_device()
+    if dev.type != 'cuda':
+        return None
+    keys = list(local_updated_models[0][1].keys())
+    try:
+        table = ops.KeyTable([[m[k] for k in keys]
+                              for _, m in local_updated_models], dev)
+    except (KeyError, TypeError, AttributeError, ValueError):
+        return None
+    base = [param2tensor(last_model[k]).float().to(table.device).contiguous()
+            for k in keys]
+    if any(b.numel() != sz for b, sz in zip(base, table.sizes)):
+        return None
+    return table, base, keys
+
+
 def calc_l2_dissim(last_model, local_updated_models):
     """‖cat_k(local_k − last_k)‖₂ per client, and their mean
     (metric_calculator.py:360-372)."""
-    lay, st, last, keys = _staged(last_model, local_updated_models)
     n = len(local_updated_models)
-    sq = ops.delta_sqnorm(st.rows(list(range(n))), lay.segments(), base=last)
+    kt = _in_place(last_model, local_updated_models)
+    if kt is not None:
+        sq = ops.delta_sqnorm_keys(kt[0], base=kt[1])
+    else:
+        lay, st, last, keys = _staged(last_model, local_updated_models)
+        sq = ops.delta_sqnorm(st.rows(list(range(n))), lay.segments(),
+                              base=last)
     raw = [float(np.sqrt(v)) for v in sq.sum(1).cpu().tolist()]
     return {'raw': raw, 'mean': np.mean(raw)}
 
@@ -60,15 +90,23 @@ def calc_blocal_dissim(last_model, local_updated_models):
     (metric_calculator.py:309-357):
     sqrt(Σ_i w_i ‖g_ik‖² / ‖Σ_i w_i g_ik‖²), g_i = local_i − last,
     w = sample sizes normalised in float64."""
-    lay, st, last, keys = _staged(last_model, local_updated_models)
     n = len(local_updated_models)
     weights = np.asarray([tp[0] for tp in local_updated_models])
     weights = weights / np.sum(weights)
-    rows = st.rows(list(range(n)))
-    segs = lay.segments()
-    sq = ops.delta_sqnorm(rows, segs, base=last).cpu().numpy()
-    g = torch.empty(lay.numel, dtype=torch.float32, device=last.device)
-    ops.delta_wsum(rows, [float(w) for w in weights], last, g)
+    kt = _in_place(last_model, local_updated_models)
+    if kt is not None:
+        table, base, keys = kt
+        segs = table.offsets
+        sq = ops.delta_sqnorm_keys(table, base=base).cpu().numpy()
+        g = torch.empty(table.numel, dtype=torch.float32, device=table.device)
+        ops.delta_wsum_keys(table, [float(w) for w in weights], base, g)
+    else:
+        lay, st, last, keys = _staged(last_model, local_updated_models)
+        rows = st.rows(list(range(n)))
+        segs = lay.segments()
+        sq = ops.delta_sqnorm(rows, segs, base=last).cpu().numpy()
+        g = torch.empty(lay.numel, dtype=torch.float32, device=last.device)
+        ops.delta_wsum(rows, [float(w) for w in weights], last, g)
     gsq = ops.delta_sqnorm(ops.RowTable.from_tensors([g]), segs)
     gsq = gsq.cpu().numpy()[0]
     out = dict()

@@ -27,6 +27,17 @@ int check_launch(const char *what);
 
 constexpr int kWave = 64;
 
+// fp32 loads through a pointer read from a device table: the address space
+// is stated so the compiler emits global_load (not flat_load, which also
+// holds lgkmcnt); _nt marks data that is streamed once.
+typedef __attribute__((address_space(1))) const float global_f32;
+__device__ __forceinline__ float gload(const float *p) {
+  return *(global_f32 *)(p);
+}
+__device__ __forceinline__ float gload_nt(const float *p) {
+  return __builtin_nontemporal_load((global_f32 *)(p));
+}
+
 // Grid size for a streaming kernel: enough workgroups to fill 256 CUs a few
 // times over, never more than the work needs.
 inline unsigned stream_grid(int64_t work_items, int block, int64_t cap) {

@@ -49,13 +49,72 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// Where client `row`'s coordinate `start` (inside key `s`) lives: a flat
+// stack row, or (KEYS) the client's own tensor for key s — table entry
+// [row][s] of an n x nseg pointer table, so device-resident client dicts
+// are read in place instead of being staged into a stack first.
+template <bool KEYS>
+__device__ __forceinline__ const float *row_at(const float *const *rows,
+                                               int row, int nseg, int s,
+                                               const int64_t *seg_off,
+                                               int64_t p) {
+  if (KEYS) return rows[int64_t(row) * nseg + s] + (p - seg_off[s]);
+  return rows[row] + p;
+}
+
+template <bool KEYS>
+__device__ __forceinline__ const float *base_at(const float *base,
+                                                const float *const *base_keys,
+                                                int s, const int64_t *seg_off,
+                                                int64_t p) {
+  if (KEYS) return base_keys ? base_keys[s] + (p - seg_off[s]) : nullptr;
+  return base ? base + p : nullptr;
+}
+
+// One lane's fp64 Σ fl32(x - b)^2 over coordinates lane, lane + kBlock, ...
+// of a chunk: unguarded groups of 8 coordinates (all loads issued before
+// the first use), then a guarded tail.
+template <bool BASE>
+__device__ __forceinline__ double chunk_sqsum(const float *__restrict__ x,
+                                              const float *__restrict__ b,
+                                              int len) {
+  constexpr int G = 8;
+  const int full = len / (G * kBlock) * (G * kBlock);
+  double acc = 0.0;
+  int q = threadIdx.x;
+  for (; q < full; q += G * kBlock) {
+    float v[G], bv[G];
+#pragma unroll
+    for (int e = 0; e < G; ++e) {
+      v[e] = gload_nt(x + q + e * kBlock);
+      if (BASE) bv[e] = gload(b + q + e * kBlock);
+    }
+#pragma unroll
+    for (int e = 0; e < G; ++e) {
+      const float d = BASE ? __fsub_rn(v[e], bv[e]) : v[e];
+      acc += double(d) * double(d);
+    }
+  }
+  for (; q < len; q += kBlock) {
+    const float d = BASE ? __fsub_rn(gload(x + q), gload(b + q)) : gload(x + q);
+    acc += double(d) * double(d);
+  }
+  return acc;
+}
+
+// Block (chunk c, row): chunk_sqsum per lane (one fp64 accumulator, fixed
+// order), then the wave and block sums in order.
+template <bool KEYS>
 __global__ __launch_bounds__(kBlock) void delta_partial_kernel(
     const float *const *__restrict__ rows, const float *__restrict__ base,
+    const float *const *__restrict__ base_keys,
     const int64_t *__restrict__ seg_off, int nseg,
     const int *__restrict__ prefix, int64_t chl, double *__restrict__ partial,
     int n) {
   __shared__ double red[kBlock / kWave];
-  const int c = blockIdx.x, row = blockIdx.y;
+  // rows fastest: the n blocks of one chunk run together, so the chunk of
+  // `base` they all subtract stays in L2 instead of streaming n times
+  const int row = blockIdx.x, c = blockIdx.y;
   const int total = prefix[nseg];
   if (c >= total) return;
   int lo = 0, hi = nseg;  // segment: largest s with prefix[s] <= c
@@ -67,14 +126,13 @@ __global__ __launch_bounds__(kBlock) void delta_partial_kernel(
   const int64_t start = seg_off[lo] + int64_t(c - prefix[lo]) * chl;
   int64_t end = start + chl;
   if (end > seg_off[lo + 1]) end = seg_off[lo + 1];
-  const float *x = rows[row];
-  double acc = 0.0;
-  for (int64_t p = start + threadIdx.x; p < end; p += kBlock) {
-    const float g = base ? __fsub_rn(x[p], base[p]) : x[p];
-    acc += double(g) * double(g);
-  }
-  acc = wave_sum(acc);
-  if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = acc;
+  const int len = int(end - start);
+  const float *x = row_at<KEYS>(rows, row, nseg, lo, seg_off, start);
+  const float *b = base_at<KEYS>(base, base_keys, lo, seg_off, start);
+  const double acc = b ? chunk_sqsum<true>(x, b, len)
+                       : chunk_sqsum<false>(x, nullptr, len);
+  const double wsum = wave_sum(acc);
+  if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = wsum;
   __syncthreads();
   if (threadIdx.x == 0) {
     double t = 0.0;
@@ -84,31 +142,121 @@ __global__ __launch_bounds__(kBlock) void delta_partial_kernel(
   }
 }
 
-// sq[row][s] = Σ over segment s's chunks (chunk order)
-__global__ void delta_final_kernel(const double *__restrict__ partial,
-                                   const int *__restrict__ prefix, int nseg,
-                                   int n, double *__restrict__ sq) {
-  const int64_t q = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+// sq[row][s] = Σ over segment s's chunks: one wave per (row, s), lanes
+// striding the chunks, then the wave sum (a fixed order).
+__global__ __launch_bounds__(kBlock) void delta_final_kernel(
+    const double *__restrict__ partial, const int *__restrict__ prefix,
+    int nseg, int n, double *__restrict__ sq) {
+  const int64_t q = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
   if (q >= int64_t(n) * nseg) return;
   const int row = int(q / nseg), s = int(q % nseg);
   double t = 0.0;
-  for (int c = prefix[s]; c < prefix[s + 1]; ++c)
+  for (int c = prefix[s] + lane; c < prefix[s + 1]; c += kWave)
     t += partial[int64_t(c) * n + row];
-  sq[q] = t;
+  t = wave_sum(t);
+  if (lane == 0) sq[q] = t;
+}
+
+// Rows [0, n - n % 8) of the fast path: eight row pointers fetched together
+// (scalar loads), then 32 coordinates in flight; GUARD only for the grid's
+// last, partial block.  Returns the first row not yet added.
+template <bool KEYS, bool GUARD>
+__device__ __forceinline__ int wsum_rows(const float *const *__restrict__ rows,
+                                         const float *__restrict__ w, int n,
+                                         int nseg, int sb, int64_t q0,
+                                         const bool (&live)[4],
+                                         const float (&b)[4], float (&acc)[4]) {
+  constexpr int R = 8;
+  int i = 0;
+  for (; i + R <= n; i += R) {
+    const float *r[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+      r[u] = KEYS ? rows[int64_t(i + u) * nseg + sb] : rows[i + u];
+    float x[R][4];
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        x[u][e] = (!GUARD || live[e]) ? gload_nt(r[u] + q0 + e * kBlock)
+                                      : 0.0f;
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const float wu = w[i + u];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc[e] = add_rn(acc[e], mul_rn(wu, __fsub_rn(x[u][e], b[e])));
+    }
+  }
+  return i;
 }
 
 // out[p] = Σ_i fl32(w_i * fl32(x_i[p] - base[p])), list order, from +0:
 // the global update of calc_blocal_dissim (metric_calculator.py:342-349).
+// Four coordinates per lane (stride kBlock) and eight rows per step, so 32
+// loads are in flight; each coordinate still adds its rows in order.
+template <bool KEYS>
 __global__ __launch_bounds__(kBlock) void delta_wsum_kernel(
     const float *const *__restrict__ rows, const float *__restrict__ w, int n,
-    int64_t numel, const float *__restrict__ base, float *__restrict__ out) {
-  const int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (p >= numel) return;
-  const float b = base[p];
-  float acc = 0.0f;
-  for (int i = 0; i < n; ++i)
-    acc = add_rn(acc, mul_rn(w[i], __fsub_rn(rows[i][p], b)));
-  out[p] = acc;
+    int64_t numel, const float *__restrict__ base,
+    const float *const *__restrict__ base_keys,
+    const int64_t *__restrict__ seg_off, int nseg, float *__restrict__ out) {
+  const int64_t blk0 = int64_t(blockIdx.x) * 4 * kBlock;
+  const int64_t p0 = blk0 + threadIdx.x;
+  // KEYS: the key holding the block's first coordinate (a block-uniform,
+  // scalar search); when the block's 4*kBlock coordinates all lie in it,
+  // every row pointer is one scalar load, as in the flat form.
+  int sb = 0;
+  bool uniform = true;
+  if (KEYS) {
+    int lo = 0, hi = nseg;  // largest s with seg_off[s] <= blk0
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (seg_off[mid] <= blk0) lo = mid;
+      else hi = mid;
+    }
+    sb = lo;
+    uniform = seg_off[sb + 1] >= blk0 + 4 * kBlock || seg_off[sb + 1] >= numel;
+  }
+  if (p0 >= numel) return;
+  int64_t p[4];
+  int s[4];
+  bool live[4];
+  int sc = sb;
+  float b[4], acc[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    p[e] = p0 + int64_t(e) * kBlock;
+    live[e] = p[e] < numel;
+    if (KEYS && !uniform)
+      while (live[e] && p[e] >= seg_off[sc + 1]) ++sc;
+    s[e] = sc;
+    b[e] = live[e] ? gload(base_at<KEYS>(base, base_keys, s[e], seg_off, p[e]))
+                   : 0.0f;
+    acc[e] = 0.0f;
+  }
+  int i = 0;
+  if (!KEYS || uniform) {
+    const int64_t q0 = p0 - (KEYS ? seg_off[sb] : 0);  // row pointers per key
+    if (blk0 + 4 * kBlock <= numel)
+      i = wsum_rows<KEYS, false>(rows, w, n, nseg, sb, q0, live, b, acc);
+    else
+      i = wsum_rows<KEYS, true>(rows, w, n, nseg, sb, q0, live, b, acc);
+  }
+  // remaining rows (and every row of a block that straddles keys)
+  for (; i < n; ++i) {
+    const float wi = w[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float xv =
+          live[e] ? gload(row_at<KEYS>(rows, i, nseg, s[e], seg_off, p[e])) : 0.0f;
+      acc[e] = add_rn(acc[e], mul_rn(wi, __fsub_rn(xv, b[e])));
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (live[e]) out[p[e]] = acc[e];
 }
 
 }  // namespace
@@ -116,20 +264,86 @@ __global__ __launch_bounds__(kBlock) void delta_wsum_kernel(
 
 using namespace fsagg;
 
+namespace {
+
+int delta_wsum(const char *what, bool keys, const float *const *rows,
+               const float *weights, int n, int64_t numel, const float *base,
+               const float *const *base_keys, const int64_t *seg_off,
+               int nseg, float *out, fsagg_stream_t stream) {
+  if (!rows || !weights || !out || n < 1 || numel < 0 ||
+      (keys ? (!base_keys || !seg_off || nseg < 1) : !base)) {
+    set_error("%s: invalid argument (n=%d nseg=%d)", what, n, nseg);
+    return FSAGG_EINVAL;
+  }
+  if (numel == 0) return FSAGG_OK;
+  const dim3 grid(unsigned((numel + 4 * kBlock - 1) / (4 * kBlock)));
+  if (keys)
+    hipLaunchKernelGGL(delta_wsum_kernel<true>, grid, dim3(kBlock), 0,
+                       as_stream(stream), rows, weights, n, numel, nullptr,
+                       base_keys, seg_off, nseg, out);
+  else
+    hipLaunchKernelGGL(delta_wsum_kernel<false>, grid, dim3(kBlock), 0,
+                       as_stream(stream), rows, weights, n, numel, base,
+                       nullptr, nullptr, 0, out);
+  return check_launch(what);
+}
+
+int delta_sqnorm(const char *what, bool keys, const float *const *rows,
+                 int n, int64_t numel, const float *base,
+                 const float *const *base_keys, const int64_t *seg_off,
+                 int nseg, double *sq, void *workspace,
+                 size_t workspace_bytes, fsagg_stream_t stream) {
+  if (!rows || !seg_off || !sq || n < 1 || nseg < 1 || numel < 0 ||
+      delta_plan(numel, nseg).max_chunks > 65535) {
+    set_error("%s: invalid argument (n=%d nseg=%d)", what, n, nseg);
+    return FSAGG_EINVAL;
+  }
+  const size_t need = fsagg_delta_sqnorm_workspace_bytes(n, numel, nseg);
+  if (!workspace || workspace_bytes < need) {
+    set_error("%s: workspace %zu < %zu bytes", what, workspace_bytes, need);
+    return FSAGG_ESPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  const DeltaPlan pl = delta_plan(numel, nseg);
+  int *prefix = static_cast<int *>(workspace);
+  double *partial = reinterpret_cast<double *>(
+      static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)));
+  hipLaunchKernelGGL(delta_prefix_kernel, dim3(1), dim3(1), 0, s, seg_off,
+                     nseg, pl.chl, prefix);
+  const dim3 grid(unsigned(n), unsigned(pl.max_chunks));
+  if (keys)
+    hipLaunchKernelGGL(delta_partial_kernel<true>, grid, dim3(kBlock), 0, s,
+                       rows, nullptr, base_keys, seg_off, nseg, prefix,
+                       pl.chl, partial, n);
+  else
+    hipLaunchKernelGGL(delta_partial_kernel<false>, grid, dim3(kBlock), 0, s,
+                       rows, base, nullptr, seg_off, nseg, prefix, pl.chl,
+                       partial, n);
+  const int64_t waves = int64_t(n) * nseg;
+  const int64_t per = kBlock / kWave;
+  hipLaunchKernelGGL(delta_final_kernel, dim3(unsigned((waves + per - 1) / per)),
+                     dim3(kBlock), 0, s, partial, prefix, nseg, n, sq);
+  return check_launch(what);
+}
+
+}  // namespace
+
 extern "C" int fsagg_delta_wsum_f32(const float *const *rows,
                                     const float *weights, int n,
                                     int64_t numel, const float *base,
                                     float *out, fsagg_stream_t stream) {
-  if (!rows || !weights || !base || !out || n < 1 || numel < 0) {
-    set_error("fsagg_delta_wsum_f32: invalid argument (n=%d)", n);
-    return FSAGG_EINVAL;
-  }
-  if (numel == 0) return FSAGG_OK;
-  hipLaunchKernelGGL(delta_wsum_kernel,
-                     dim3(unsigned((numel + kBlock - 1) / kBlock)),
-                     dim3(kBlock), 0, as_stream(stream), rows, weights, n,
-                     numel, base, out);
-  return check_launch("fsagg_delta_wsum_f32");
+  return delta_wsum("fsagg_delta_wsum_f32", false, rows, weights, n, numel,
+                    base, nullptr, nullptr, 0, out, stream);
+}
+
+extern "C" int fsagg_delta_wsum_keys_f32(const float *const *keys,
+                                         const float *weights, int n,
+                                         int64_t numel,
+                                         const float *const *base_keys,
+                                         const int64_t *seg_off, int nseg,
+                                         float *out, fsagg_stream_t stream) {
+  return delta_wsum("fsagg_delta_wsum_keys_f32", true, keys, weights, n,
+                    numel, nullptr, base_keys, seg_off, nseg, out, stream);
 }
 
 extern "C" size_t fsagg_delta_sqnorm_workspace_bytes(int n, int64_t numel,
@@ -146,32 +360,17 @@ extern "C" int fsagg_delta_sqnorm_f32(const float *const *rows, int n,
                                       double *sq, void *workspace,
                                       size_t workspace_bytes,
                                       fsagg_stream_t stream) {
-  if (!rows || !seg_off || !sq || n < 1 || nseg < 1 || numel < 0 ||
-      n > 65535) {
-    set_error("fsagg_delta_sqnorm_f32: invalid argument (n=%d nseg=%d)", n,
-              nseg);
-    return FSAGG_EINVAL;
-  }
-  const size_t need = fsagg_delta_sqnorm_workspace_bytes(n, numel, nseg);
-  if (!workspace || workspace_bytes < need) {
-    set_error("fsagg_delta_sqnorm_f32: workspace %zu < %zu bytes",
-              workspace_bytes, need);
-    return FSAGG_ESPACE;
-  }
-  hipStream_t s = as_stream(stream);
-  const DeltaPlan pl = delta_plan(numel, nseg);
-  int *prefix = static_cast<int *>(workspace);
-  double *partial = reinterpret_cast<double *>(
-      static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)));
-  hipLaunchKernelGGL(delta_prefix_kernel, dim3(1), dim3(1), 0, s, seg_off,
-                     nseg, pl.chl, prefix);
-  hipLaunchKernelGGL(delta_partial_kernel,
-                     dim3(unsigned(pl.max_chunks), unsigned(n)), dim3(kBlock),
-                     0, s, rows, base, seg_off, nseg, prefix, pl.chl, partial,
-                     n);
-  const int64_t items = int64_t(n) * nseg;
-  hipLaunchKernelGGL(delta_final_kernel,
-                     dim3(unsigned((items + kBlock - 1) / kBlock)),
-                     dim3(kBlock), 0, s, partial, prefix, nseg, n, sq);
-  return check_launch("fsagg_delta_sqnorm_f32");
+  return delta_sqnorm("fsagg_delta_sqnorm_f32", false, rows, n, numel, base,
+                      nullptr, seg_off, nseg, sq, workspace, workspace_bytes,
+                      stream);
+}
+
+extern "C" int fsagg_delta_sqnorm_keys_f32(
+    const float *const *keys, int n, int64_t numel,
+    const float *const *base_keys, const int64_t *seg_off, int nseg,
+    double *sq, void *workspace, size_t workspace_bytes,
+    fsagg_stream_t stream) {
+  return delta_sqnorm("fsagg_delta_sqnorm_keys_f32", true, keys, n, numel,
+                      nullptr, base_keys, seg_off, nseg, sq, workspace,
+                      workspace_bytes, stream);
 }

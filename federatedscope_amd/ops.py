@@ -14,6 +14,18 @@ from . import _lib as L
 ALIGN_BYTES = 16
 
 
+def _h2d(values, dtype, device):
+    """A small host table (row pointers, weights, offsets) on ``device``:
+    staged through pinned memory and copied asynchronously on the current
+    stream, so a call never blocks the host on the GPU's queue (torch's
+    host allocator keeps the pinned block until the copy has run)."""
+    host = torch.tensor(values, dtype=dtype)
+    device = torch.device(device)
+    if device.type != 'cuda':
+        return host.to(device)
+    return host.pin_memory().to(device, non_blocking=True)
+
+
 def _stream(device):
     return ctypes_ptr(torch.cuda.current_stream(device).cuda_stream)
 
@@ -57,8 +69,7 @@ class RowTable:
         self.n = len(ptrs)
         self.numel = int(numel)
         self.device = torch.device(device)
-        self.table = torch.tensor(self.ptrs, dtype=torch.int64,
-                                  device=self.device)
+        self.table = _h2d(self.ptrs, torch.int64, self.device)
         self._keep = tuple(keepalive)
 
     @classmethod
@@ -104,8 +115,7 @@ class RowTable:
 
 
 def _fp32_dev(values, device):
-    return torch.tensor([float(v) for v in values], dtype=torch.float32,
-                        device=device)
+    return _h2d([float(v) for v in values], torch.float32, device)
 
 
 def _check_out(out, numel, device, what='out', align=ALIGN_BYTES):
@@ -178,10 +188,8 @@ def weighted_sum_typed(tensors, weights, out):
                          (odt, numel))
     if len(weights) != len(tensors):
         raise ValueError('weights length mismatch')
-    tab = torch.tensor([t.data_ptr() for t in tensors], dtype=torch.int64,
-                       device=dev)
-    w = torch.tensor([float(x) for x in weights], dtype=torch.float64,
-                     device=dev)
+    tab = _h2d([t.data_ptr() for t in tensors], torch.int64, dev)
+    w = _h2d([float(x) for x in weights], torch.float64, dev)
     L.check(L.load().fsagg_weighted_sum_typed(tab.data_ptr(), code,
                                               w.data_ptr(), len(tensors),
                                               numel, out.data_ptr(),
@@ -273,7 +281,7 @@ def pairdist(rows, seg_offsets, workspace=None):
     lib = L.load()
     need = lib.fsagg_pairdist_workspace_bytes(rows.n, rows.numel, nseg)
     ws = (workspace or _WS).get(rows.device, need)
-    seg = torch.tensor(offs, dtype=torch.int64, device=rows.device)
+    seg = _h2d(offs, torch.int64, rows.device)
     D = torch.empty((rows.n, rows.n), dtype=torch.float32, device=rows.device)
     L.check(lib.fsagg_pairdist_f32(rows.ptr(), rows.n, rows.numel,
                                    seg.data_ptr(), nseg, D.data_ptr(),
@@ -296,7 +304,7 @@ def pairdist_segsq(rows, seg_offsets, workspace=None):
     lib = L.load()
     need = lib.fsagg_pairdist_workspace_bytes(rows.n, rows.numel, nseg)
     ws = (workspace or _WS).get(rows.device, need)
-    seg = torch.tensor(offs, dtype=torch.int64, device=rows.device)
+    seg = _h2d(offs, torch.int64, rows.device)
     sq = torch.empty((nseg, rows.n, rows.n), dtype=torch.float64,
                      device=rows.device)
     L.check(lib.fsagg_pairdist_segsq_f32(rows.ptr(), rows.n, rows.numel,
@@ -421,10 +429,8 @@ def ss_recover(shares, mod, maximum, epsilon, total, recover=True):
     # the kernel reads two elements per lane (16-B loads)
     shares = [t if t.data_ptr() % ALIGN_BYTES == 0 else t.clone()
               for t in shares]
-    tab = torch.tensor([t.data_ptr() for t in shares], dtype=torch.int64,
-                       device=dev)
-    is_int = torch.tensor([t.dtype == torch.int64 for t in shares],
-                          dtype=torch.uint8, device=dev)
+    tab = _h2d([t.data_ptr() for t in shares], torch.int64, dev)
+    is_int = _h2d([t.dtype == torch.int64 for t in shares], torch.uint8, dev)
     out = torch.empty(shape, dtype=torch.float32 if recover else
                       torch.float64, device=dev)
     L.check(L.load().fsagg_ss_recover_f32(
@@ -449,7 +455,7 @@ def delta_sqnorm(rows, seg_offsets, base=None, workspace=None):
     lib = L.load()
     need = lib.fsagg_delta_sqnorm_workspace_bytes(rows.n, rows.numel, nseg)
     ws = (workspace or _WS).get(rows.device, need)
-    seg = torch.tensor(offs, dtype=torch.int64, device=rows.device)
+    seg = _h2d(offs, torch.int64, rows.device)
     sq = torch.empty((rows.n, nseg), dtype=torch.float64, device=rows.device)
     L.check(lib.fsagg_delta_sqnorm_f32(
         rows.ptr(), rows.n, rows.numel,
@@ -471,4 +477,96 @@ def delta_wsum(rows, weights, base, out):
                                           out.data_ptr(),
                                           _stream(rows.device)),
             'fsagg_delta_wsum_f32')
+    return out
+
+
+class KeyTable:
+    """Per-client, per-key device tensors addressed in place: an n x nseg
+    pointer table (entry [i][s] = client i's fp32 tensor for key s) plus the
+    keys' flat offsets.  No staging copy — the form of the metric passes for
+    client dicts that are already on the GPU.  Raises ValueError/TypeError
+    if a tensor is not a contiguous fp32 tensor of the first client's key
+    sizes on ``device`` (one lean pass: this runs once per client key)."""
+
+    def __init__(self, clients, device):
+        if not clients or not clients[0]:
+            raise ValueError('KeyTable needs at least one client and key')
+        device = torch.device(device)
+        if device.type != 'cuda':
+            raise ValueError('KeyTable needs a GPU device')
+        idx = torch.cuda.current_device() if device.index is None \
+            else device.index
+        self.device = torch.device('cuda', idx)
+        self.nseg = len(clients[0])
+        self.sizes = [int(t.numel()) for t in clients[0]]
+        f32 = torch.float32
+        ptrs = []
+        for i, row in enumerate(clients):
+            if len(row) != self.nseg:
+                raise ValueError('client %d has %d keys, client 0 has %d' %
+                                 (i, len(row), self.nseg))
+            for s, t in enumerate(row):
+                if t.dtype is not f32 or not t.is_contiguous() or \
+                        t.get_device() != idx or t.numel() != self.sizes[s]:
+                    raise ValueError(
+                        'client %d key %d must be a contiguous float32 '
+                        'tensor of %d elements on %s' %
+                        (i, s, self.sizes[s], self.device))
+                p = t.data_ptr()
+                if p % 4:
+                    raise ValueError('client %d key %d is not 4-byte '
+                                     'aligned' % (i, s))
+                ptrs.append(p)
+        self.n = len(clients)
+        offs = [0]
+        for sz in self.sizes:
+            offs.append(offs[-1] + sz)
+        self.offsets = offs
+        self.numel = offs[-1]
+        self.table = _h2d(ptrs, torch.int64, self.device)
+        self.seg = _h2d(offs, torch.int64, self.device)
+        self._keep = clients
+
+    def base_table(self, base):
+        """Device pointer table of the base model's per-key tensors."""
+        if len(base) != self.nseg:
+            raise ValueError('base has %d keys, clients %d' %
+                             (len(base), self.nseg))
+        for s, t in enumerate(base):
+            _check_f32_cuda(t, 'base key %d' % s, align=4)
+            if t.device != self.device or t.numel() != self.sizes[s]:
+                raise ValueError('base key %d does not match the clients' % s)
+        return _h2d([t.data_ptr() for t in base], torch.int64, self.device)
+
+
+def delta_sqnorm_keys(keys, base=None, workspace=None):
+    """:func:`delta_sqnorm` over a :class:`KeyTable` (``base``: per-key
+    tensors or None); bit-identical to the staged form."""
+    lib = L.load()
+    need = lib.fsagg_delta_sqnorm_workspace_bytes(keys.n, keys.numel,
+                                                  keys.nseg)
+    ws = (workspace or _WS).get(keys.device, need)
+    btab = keys.base_table(base) if base is not None else None
+    sq = torch.empty((keys.n, keys.nseg), dtype=torch.float64,
+                     device=keys.device)
+    L.check(lib.fsagg_delta_sqnorm_keys_f32(
+        keys.table.data_ptr(), keys.n, keys.numel,
+        None if btab is None else btab.data_ptr(), keys.seg.data_ptr(),
+        keys.nseg, sq.data_ptr(), ws.data_ptr(), ws.numel(),
+        _stream(keys.device)), 'fsagg_delta_sqnorm_keys_f32')
+    return sq
+
+
+def delta_wsum_keys(keys, weights, base, out):
+    """:func:`delta_wsum` over a :class:`KeyTable`; ``out`` is flat (keys
+    concatenated in table order)."""
+    _check_out(out, keys.numel, keys.device, align=4)
+    if len(weights) != keys.n:
+        raise ValueError('%d weights for %d clients' % (len(weights), keys.n))
+    btab = keys.base_table(base)
+    w = _fp32_dev(weights, keys.device)
+    L.check(L.load().fsagg_delta_wsum_keys_f32(
+        keys.table.data_ptr(), w.data_ptr(), keys.n, keys.numel,
+        btab.data_ptr(), keys.seg.data_ptr(), keys.nseg, out.data_ptr(),
+        _stream(keys.device)), 'fsagg_delta_wsum_keys_f32')
     return out

@@ -259,6 +259,28 @@ int fsagg_delta_wsum_f32(const float *const *rows, const float *weights,
                          fsagg_stream_t stream);
 
 /*
+ * Key-table forms of the two metric passes, for client dicts that are
+ * already device-resident (no staging copy): keys (device) is an n x nseg
+ * row-major table whose entry [i][s] points at client i's fp32 tensor for
+ * key s (seg_off[s+1] - seg_off[s] elements, any 4-byte alignment);
+ * base_keys (device) nseg pointers to the base model's tensors (may be NULL
+ * for the sqnorm).  numel = seg_off[nseg].  Results are bit-identical to the
+ * flat forms over the concatenated rows; the wsum's out stays flat.
+ * Reference: the same metric_calculator.py:309-372 loops, which index the
+ * clients' state dicts key by key.
+ */
+int fsagg_delta_sqnorm_keys_f32(const float *const *keys, int n,
+                                int64_t numel, const float *const *base_keys,
+                                const int64_t *seg_off, int nseg, double *sq,
+                                void *workspace, size_t workspace_bytes,
+                                fsagg_stream_t stream);
+int fsagg_delta_wsum_keys_f32(const float *const *keys, const float *weights,
+                              int n, int64_t numel,
+                              const float *const *base_keys,
+                              const int64_t *seg_off, int nseg, float *out,
+                              fsagg_stream_t stream);
+
+/*
  * Deterministic synthetic client updates (benchmarks / tests): fills the
  * [n][ld] slab X with u = hash(seed, client, index) mapped to [-1, 1),
  * index < numel; the same generator is restated on the host by the tests.

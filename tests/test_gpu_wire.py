@@ -219,3 +219,61 @@ def test_quant_plan_layouts(nbits):
         assert list(got.keys()) == list(want.keys())
         for k in want:
             _same_bits(got[k], np.asarray(want[k], np.float32))
+
+
+@pytest.mark.parametrize('name', case_names('dissim_'))
+def test_dissimilarity_metrics_in_place(name):
+    """Device-resident client dicts take the key-table path (no staging);
+    its sums are bit-identical to the staged path's."""
+    from federatedscope_amd.core.monitors import (calc_blocal_dissim,
+                                                  calc_l2_dissim)
+    _, clients, _, last, extra = load_case(name)
+    tl = OrderedDict((k, torch.from_numpy(v)) for k, v in last.items())
+    host = [(s, OrderedDict((k, torch.from_numpy(v)) for k, v in m.items()))
+            for s, m in clients]
+    dev = [(s, OrderedDict((k, v.cuda()) for k, v in m.items()))
+           for s, m in host]
+    assert calc_l2_dissim(tl, dev)['raw'] == calc_l2_dissim(tl, host)['raw']
+    np.testing.assert_allclose(calc_l2_dissim(tl, dev)['raw'],
+                               extra['l2_raw'], rtol=1e-5)
+    assert calc_blocal_dissim(tl, dev) == calc_blocal_dissim(tl, host)
+
+
+def test_delta_keys_match_flat_odd_layouts():
+    """KeyTable metric passes over odd-sized, empty and 4-byte-offset key
+    tensors equal the flat (staged) passes bit for bit."""
+    from federatedscope_amd import ops
+    g = torch.Generator(device='cuda').manual_seed(9)
+    sizes = [1, 0, 1023, 5, 300_001, 0, 7, 65_537]
+    n = 13
+    pool = torch.randn(n * (sum(sizes) + len(sizes)) + 8, device='cuda',
+                       generator=g)
+    clients, flat, off = [], [], 1   # start one element in: 4-B aligned
+    for i in range(n):
+        row = []
+        for sz in sizes:
+            row.append(pool[off:off + sz])
+            off += sz + 1
+        clients.append(row)
+        flat.append(torch.cat(row))
+    base = [torch.randn(sz, device='cuda', generator=g) for sz in sizes]
+    kt = ops.KeyTable(clients, 'cuda')
+    rows = ops.RowTable.from_tensors(flat)
+    bflat = torch.cat(base)
+    for b_keys, b_flat in ((base, bflat), (None, None)):
+        want = ops.delta_sqnorm(rows, kt.offsets, base=b_flat)
+        got = ops.delta_sqnorm_keys(kt, base=b_keys)
+        assert torch.equal(got, want)
+    w = [float(x) for x in np.random.default_rng(2).random(n)]
+    out_k = torch.full((kt.numel, ), 7.0, device='cuda')
+    out_f = torch.full((kt.numel, ), 7.0, device='cuda')
+    ops.delta_wsum_keys(kt, w, base, out_k)
+    ops.delta_wsum(rows, w, bflat, out_f)
+    assert torch.equal(out_k, out_f)
+    # the flat wsum against the oracle's op order (fp32, row order, from +0)
+    x = torch.stack(flat).cpu().numpy()
+    want = np.zeros(kt.numel, np.float32)
+    b = bflat.cpu().numpy()
+    for i in range(n):
+        want = want + np.float32(w[i]) * (x[i] - b)
+    assert out_f.cpu().numpy().tobytes() == want.tobytes()

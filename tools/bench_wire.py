@@ -176,7 +176,7 @@ def dissim_leg(n=100, P=6_000_000):
             ts.append(time.perf_counter() - t0)
         out[name + '_ms'] = round(min(ts) * 1e3, 2)
     return dict(leg='dissim', clients=n, params=P, **out,
-                what='device-resident client dicts staged + metric kernels')
+                what='device-resident client dicts read in place (ops.KeyTable) + metric kernels')
 
 
 def main():
