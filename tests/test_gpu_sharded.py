@@ -73,3 +73,24 @@ def test_sharded_krum_partials(world):
                                Dref[off.cpu().numpy()], rtol=1e-5)
     assert O.krum_select(O.krum_scores(D2.cpu().numpy(), 2), 4) == \
         O.krum_select(O.krum_scores(Dref, 2), 4)
+
+
+@pytest.mark.parametrize('chunks', [1, 3, 8])
+def test_pipelined_assembly_gpu_world1_bit_exact(chunks):
+    """PipelinedAssembly's piece plan driving the FedAvg kernel (one rank:
+    no collective) reproduces the unsharded result bit for bit."""
+    from federatedscope_amd import ops
+    from federatedscope_amd.core.sharding import PipelinedAssembly
+    n, P = 7, 100_003
+    dev, slab, ld = _setup(n, P)
+    w = O.fedavg_weights(list(range(3, n + 3)))
+    full = torch.empty(P, device=dev)
+    ops.weighted_sum(ops.RowTable.from_slab(slab, numel=P), w, full)
+    pa = PipelinedAssembly(P, chunks=chunks)
+
+    def compute(j, lo, hi, view):
+        ops.weighted_sum(ops.RowTable.from_slab(slab, col_offset=lo,
+                                                numel=hi - lo), w, view)
+
+    got = pa.run(compute, device=dev)
+    assert torch.equal(got, full)
