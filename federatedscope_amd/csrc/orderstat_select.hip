@@ -22,8 +22,10 @@
 //     bins in fp64.  The list is sorted in registers with the compile-time
 //     bitonic network (32 or 64 keys) and the ranks read off.
 // Histogram words and list slots are laid out [slot][lane], so the 64 lanes
-// of a wave always hit 64 distinct banks.  Word 64 is a per-lane dump slot
-// for the compaction stores of keys that match neither bin (branch-free).
+// of a wave always hit 64 distinct banks.  The compaction stores every key
+// at the list's current end (branch-free); a key outside both bins is
+// overwritten by the next one inside, and word 64 catches the stores made
+// once the list is full.
 //
 // Register budget: SEL_N keys + ~40 must stay within 256 VGPRs (2 waves per
 // SIMD); SEL_N moves in steps of kSelStep so no more than 7 are padding.
@@ -167,6 +169,28 @@ __device__ __forceinline__ void hist_add_dual(uint32_t *H,
   }
 }
 
+// Refinement of rank 1's bin alone (the common case: the median's two
+// ranks share a bin): the key's offset from the bin base, shifted to the
+// next 7-bit digit and clamped to 128, is the digit for keys in the bin; a
+// key outside it lands in bin 128 (word 32, outside the 32-word scan) or,
+// when the bin has fewer than 128 digits, in a digit above the bin's own —
+// after every key of the bin, so the scan for a rank inside the bin never
+// reaches it.  No compare/select per key.  (Lanes whose rank needs no
+// refinement count garbage and ignore the result; <= 255 keys per lane
+// keep every byte counter in range.)
+template <int N>
+__device__ __forceinline__ void hist_add_one(uint32_t *H,
+                                             const uint32_t (&k)[N], int n,
+                                             const RankSel &s) {
+  const int sh = digit_shift(s, 7);
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    if (j >= N - kSelStep && j >= n) continue;
+    const uint32_t d = min((k[j] - s.P) >> sh, 128u);
+    atomicAdd(&H[(d >> 2) * kWave], 1u << ((d << 3) & 31u));
+  }
+}
+
 // Narrow s to digit bin d (count b below it, c in it), if on.
 __device__ __forceinline__ void rank_apply(RankSel &s, bool on, uint32_t d,
                                            int b, int c, int width = 8) {
@@ -272,7 +296,10 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
     const bool need2 = list2 && stored > kList && s2.cnt > kList / 2;
     if (!__any(need1 || need2)) break;
     hist_clear(H);
-    hist_add_dual<N>(H, k, n, s1, need1, s2, need2);
+    if (__any(need2))
+      hist_add_dual<N>(H, k, n, s1, need1, s2, need2);
+    else
+      hist_add_one<N>(H, k, n, s1);
     uint32_t d1, d2, d3 = 0;
     int b1, c1, b2, c2, b3 = 0, c3 = 0;
     // rank 1 (and rank 2 where it shares rank 1's bin) in words [0, 32)
@@ -307,7 +334,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
         if (j >= N - kSelStep && j >= n) continue;
         const uint32_t key = k[j];
         const bool m = any && key - lo <= span;
-        H[(m ? min(c, kList) : kList) * kWave] = key;
+        H[min(c, kList) * kWave] = key;  // a miss: overwritten by next hit
         c += m;
       }
     } else {
@@ -324,7 +351,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
         const uint32_t key = k[j];
         const bool m = any && (key - l1 <= span1 || key - l2 <= span2);
         mid += key - mlo < mspan ? double(key2f(key)) : 0.0;
-        H[(m ? min(c, kList) : kList) * kWave] = key;
+        H[min(c, kList) * kWave] = key;  // a miss: overwritten by next hit
         c += m;
       }
     }
