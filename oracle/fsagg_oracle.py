@@ -305,14 +305,31 @@ def trimmed_mean_update(models, excluded_num, divisor=None):
 
     The reference sums ``cat([T, -top, bottom])`` with ATen's cascade sum
     (host-ISA dependent order); here the kept middle is summed in float64 and
-    rounded once, then divided in fp32 — compare under tolerance."""
+    rounded once, then divided in fp32 — compare under tolerance.  Columns
+    holding ±inf/NaN reproduce the reference's formula (NaN for k >= 1)."""
     first = models[0][1]
     out = OrderedDict()
     for k in first:
         T = np.stack([_to_float(d[k]) for _, d in models], 0)
         n = T.shape[0]
         S = np.sort(T, axis=0)
-        mid = S[excluded_num:n - excluded_num].astype(np.float64).sum(0)
+        with np.errstate(invalid='ignore'):
+            mid = S[excluded_num:n - excluded_num].astype(np.float64).sum(0)
+        # Non-finite columns follow the reference's formula literally: with
+        # k >= 1 an infinity (or NaN) is both in Σall and among the excluded
+        # top/bottom, so Σall − Σtop − Σbottom is inf − inf = NaN; with
+        # k == 0 it is Σall itself (±inf, or NaN for NaN / +inf with -inf).
+        bad = ~np.isfinite(T).all(0)
+        if bad.any():
+            has_nan = np.isnan(T).any(0)
+            pinf = (T == np.inf).any(0)
+            ninf = (T == -np.inf).any(0)
+            if excluded_num >= 1:
+                nf = np.full(T.shape[1], np.nan)
+            else:
+                nf = np.where(has_nan | (pinf & ninf), np.nan,
+                              np.where(pinf, np.inf, -np.inf))
+            mid = np.where(bad, nf, mid)
         div = (n - 2 * excluded_num) if divisor is None else divisor
         out[k] = (mid.astype(f32) / f32(div)).astype(f32)
     return out

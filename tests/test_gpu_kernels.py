@@ -212,3 +212,90 @@ def test_typed_weighted_sum(dt):
                               want.bits)
     else:
         assert got.numpy().tobytes() == np.asarray(want).tobytes()
+
+
+@pytest.mark.parametrize('n', [9, 65, 100, 200, 255, 300])
+def test_orderstat_nonfinite_columns_all_kernels(n):
+    """±inf / NaN columns through every order-statistic kernel (the
+    register network, the select kernels and the generic n > 255 path)."""
+    from federatedscope_amd import ops
+    P = 8
+    X = np.ones((n, P), np.float32)
+    X[0, 0] = np.nan
+    X[0, 1] = np.inf
+    X[0, 2] = -np.inf
+    X[1, 3] = np.inf
+    X[2, 3] = -np.inf
+    X[:, 4] = np.float32(np.arange(n) % 5)
+    X[3:, 5] = np.inf                    # mostly +inf
+    slab = torch.from_numpy(X).cuda()
+    rows = ops.RowTable.from_slab(slab)
+    out = torch.empty(P, device='cuda')
+    ops.coord_median(rows, out)
+    models = [(1, {'w': X[i]}) for i in range(n)]
+    want = O.median_update(models)['w']
+    assert np.array_equal(out.cpu().numpy(), want, equal_nan=True)
+    for k in (0, 1, n // 5):
+        if 2 * k >= n:
+            continue
+        ops.trimmed_mean(rows, k, out)
+        want = O.trimmed_mean_update(models, k)['w']
+        got = out.cpu().numpy()
+        assert np.array_equal(np.isnan(got), np.isnan(want)), (k, got, want)
+        fin = np.isfinite(want)
+        assert np.array_equal(got[~fin & ~np.isnan(want)],
+                              want[~fin & ~np.isnan(want)])
+        np.testing.assert_allclose(got[fin], want[fin], rtol=1e-6)
+
+
+@pytest.mark.parametrize('n', [100, 200, 255])
+def test_orderstat_refinement_stress(n):
+    """Columns built to drive the select kernel through every refinement
+    shape: a heavy cluster within a few ulps (bins refined down to lvl < 7),
+    two far clusters (dual refinement), a tight cluster next to a single
+    outlier, and wide dynamic ranges — median bit-exact, trimmed mean within
+    the summation tolerance."""
+    from federatedscope_amd import ops
+    rng = np.random.default_rng(100 + n)
+    cols = []
+    one = np.float32(1.0)
+    ulps = np.nextafter(one, np.float32(2)) - one
+    c = np.full(n, one, np.float32) + ulps * rng.integers(0, 4, n)
+    c[: n // 4] = 3.0
+    c[n // 4] = 2.0
+    cols.append(c)                                    # ulp cluster
+    c = np.where(rng.random(n) < 0.5,
+                 -5.0 + 1e-6 * rng.standard_normal(n),
+                 7.0 + 1e-6 * rng.standard_normal(n)).astype(np.float32)
+    cols.append(c)                                    # two tight clusters
+    c = (1e-3 * rng.standard_normal(n)).astype(np.float32)
+    c[0] = 1e30
+    cols.append(c)                                    # one huge outlier
+    c = (rng.standard_normal(n) * 10.0 ** rng.integers(-20, 20, n)).astype(
+        np.float32)
+    cols.append(c)                                    # wide exponents
+    c = np.float32(rng.integers(-2, 3, n)) + np.float32(1e-7) * \
+        np.float32(rng.integers(0, 2, n))
+    cols.append(c.astype(np.float32))                 # ties + near ties
+    c = rng.standard_normal(n).astype(np.float32)
+    c[rng.random(n) < 0.1] *= 100.0
+    cols.append(c)                                    # C5-like
+    X = np.stack(cols, 1).astype(np.float32)
+    X = np.repeat(X, 70, axis=1)                      # > one wave of columns
+    for j in range(X.shape[1]):
+        X[:, j] = X[rng.permutation(n), j]
+    P = X.shape[1]
+    slab = torch.from_numpy(np.ascontiguousarray(X)).cuda()
+    rows = ops.RowTable.from_slab(slab)
+    out = torch.empty(P, device='cuda')
+    models = [(1, {'w': X[i]}) for i in range(n)]
+    ops.coord_median(rows, out)
+    assert out.cpu().numpy().tobytes() == \
+        O.median_update(models)['w'].tobytes()
+    eps = np.finfo(np.float32).eps
+    for k in (1, n // 5, n // 2 - 1):
+        ops.trimmed_mean(rows, k, out)
+        want = O.trimmed_mean_update(models, k)['w']
+        mag = np.abs(np.sort(X, 0)[k:n - k]).sum(0) / (n - 2 * k)
+        err = np.abs(out.cpu().numpy().astype(np.float64) - want)
+        assert (err <= 2 * eps * (mag + np.abs(want))).all(), (k, err.max())

@@ -309,6 +309,39 @@ def order_stat_cases(rng):
                       out, init=init, extra=extra)
 
 
+def order_stat_nonfinite_cases(rng):
+    """±inf / NaN columns through MedianAggregator and TrimmedmeanAggregator
+    (k = 0 and k >= 1), so the oracle's non-finite rule is pinned to the
+    reference's own outputs."""
+    for n in (9, 20):
+        P = 8
+        shapes = OrderedDict([('w', (P, ))])
+        clients = rand_clients(rng, n, shapes)
+        W = np.stack([c[1]['w'].numpy() for c in clients])
+        W[0, 0] = np.nan
+        W[0, 1] = np.inf
+        W[0, 2] = -np.inf
+        W[1, 3] = np.inf
+        W[2, 3] = -np.inf
+        W[3:, 5] = np.inf
+        for i in range(n):
+            clients[i][1]['w'] = torch.from_numpy(W[i].copy())
+        init = OrderedDict([('w', torch.zeros(P))])
+        cfg = make_cfg(client_num=1000, f=1, tm_ratio=0.2)
+        out = run(MedianAggregator(model=DictModel(init), config=cfg),
+                  clients)
+        extra = {}
+        for ratio in (0.0, 0.1, 0.2):
+            cfg = make_cfg(client_num=1000, f=1, tm_ratio=ratio)
+            tm = run(TrimmedmeanAggregator(model=DictModel(init), config=cfg),
+                     clients)
+            for k, v in tm.items():
+                extra['tm|%s|%s' % (ratio, k)] = v.numpy()
+        save_case('orderstat_nonfinite_n%d' % n, {
+            'rule': 'median', 'tm_ratios': [0.0, 0.1, 0.2]}, clients, out,
+                  init=init, extra=extra)
+
+
 def bulyan_cases(rng):
     shapes = OrderedDict([('w', (3, 41)), ('b', (9, ))])
     for n, f, rate in ((11, 2, 1.0), (20, 4, 0.5), (40, 9, 1.0)):
@@ -373,6 +406,9 @@ def fedopt_cases(rng):
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(1)  # fed_runner.py:297-299
+    if sys.argv[1:] == ['nonfinite']:  # added later: its own seed
+        order_stat_nonfinite_cases(np.random.default_rng(20261016))
+        return 0
     rng = np.random.default_rng(20261015)
     fedavg_cases(rng)
     asyn_cases(rng)
