@@ -26,12 +26,17 @@
 //     the keys in fp32 in key order (the reference's
 //     `distance += torch.dist(...)`).
 // Deterministic: no atomics anywhere.
+#include <numeric>
+
 #include "common.h"
 
 namespace fsagg {
 namespace {
 
 constexpr int kBlock = 256;
+// the staged coordinate row of every client must fit the LDS many times
+// over (and the n²-sized workspace stay sane)
+constexpr int kMaxPairClients = 4096;
 constexpr int kRedPitch = 65;                  // LDS pitch of a reduction slot
 constexpr int kLdsFloats = kBlock * kRedPitch;  // 16640 floats = 65 KiB
 // register-prefetched staging items per thread (each 4 rows × 4
@@ -70,18 +75,24 @@ PairPlan make_plan(int n, int64_t numel, int nseg) {
   // pitch ≡ 28 (mod 32) words: conflict-free b128 staging writes and reads
   pl.ldsp = (pl.nt * pl.ts + 3) / 4 * 4 + 4;
   while (pl.ldsp % 32 != 28) pl.ldsp += 4;
-  pl.sub = kLdsFloats / pl.ldsp / kWave * kWave;  // a multiple of 64
-  // full stages are prefetched into stage_items(ts) float4 quads per thread
+  // Stage length: a multiple of lcm(4, ks), so every k-slice gets the same
+  // number of coordinates per stage (at n = 50, ks = 17: 204 coordinates,
+  // 12 per lane, where 192 gave 11 or 12) and float4 rows stay whole; at
+  // most what the LDS holds and, when the stage can be register-prefetched
+  // (stage_items(ts) float4 quads per thread), what the registers hold.
+  const int unit = std::lcm(4, pl.ks);
+  const int lds_cap = kLdsFloats / pl.ldsp;
   const int quads = (pl.nt * pl.ts + 3) / 4;
-  const int cap = stage_items(pl.ts) * kBlock / quads * 4 / kWave * kWave;
-  if (cap >= kWave && pl.sub > cap) pl.sub = cap;
-  if (pl.sub < kWave) pl.sub = kLdsFloats / pl.ldsp;
-  // ≈ 1000 chunks (two rounds of the 2 × 256 resident workgroups), a
-  // multiple of 64 coordinates so full stages stay 16-B aligned
+  const int reg_cap = stage_items(pl.ts) * kBlock / quads * 4;
+  const int limit = reg_cap >= unit && reg_cap < lds_cap ? reg_cap : lds_cap;
+  pl.sub = limit / unit * unit;
+  if (pl.sub < unit) pl.sub = limit >= 4 ? limit / 4 * 4 : limit;  // huge n
+  // ≈ 1000 chunks (two rounds of the 2 × 256 resident workgroups), whole
+  // stages (16-B aligned whenever the chunk start is)
   const int64_t target = 1024 - nseg > 256 ? 1024 - nseg : 256;
   int64_t chl = (numel + target - 1) / target;
   if (chl < 2048) chl = 2048;
-  pl.chl = (chl + 63) / 64 * 64;
+  pl.chl = (chl + pl.sub - 1) / pl.sub * pl.sub;
   pl.max_chunks = numel / chl + nseg + 1;
   return pl;
 }
@@ -447,7 +458,8 @@ extern "C" int fsagg_pairdist_f32(const float *const *rows, int n,
                                   int nseg, float *D, void *workspace,
                                   size_t workspace_bytes,
                                   fsagg_stream_t stream) {
-  if (!rows || !seg_off || !D || n < 2 || nseg < 1 || numel < 0) {
+  if (!rows || !seg_off || !D || n < 2 || n > kMaxPairClients ||
+      nseg < 1 || numel < 0) {
     set_error("fsagg_pairdist_f32: invalid argument (n=%d nseg=%d)", n, nseg);
     return FSAGG_EINVAL;
   }
@@ -476,7 +488,8 @@ extern "C" int fsagg_pairdist_segsq_f32(const float *const *rows, int n,
                                         void *workspace,
                                         size_t workspace_bytes,
                                         fsagg_stream_t stream) {
-  if (!rows || !seg_off || !segsq || n < 2 || nseg < 1 || numel < 0) {
+  if (!rows || !seg_off || !segsq || n < 2 || n > kMaxPairClients ||
+      nseg < 1 || numel < 0) {
     set_error("fsagg_pairdist_segsq_f32: invalid argument (n=%d nseg=%d)", n,
               nseg);
     return FSAGG_EINVAL;

@@ -131,7 +131,8 @@ int fsagg_trimmed_mean_f32(const float *const *rows, int n, int64_t numel,
  * — the sum over keys of per-key L2 distances of
  * KrumAggregator._calculate_distance (krum_aggregator.py:41-56) filled as in
  * _calculate_score (:58-73).  Per-key sums accumulate in fp32 within a chunk
- * and in fp64 across chunks (fixed order, deterministic).
+ * and in fp64 across chunks (fixed order, deterministic).  2 <= n <= 4096
+ * (FSAGG_EINVAL beyond).
  * Workspace: fsagg_pairdist_workspace_bytes(n, numel, nseg) bytes (device).
  */
 size_t fsagg_pairdist_workspace_bytes(int n, int64_t numel, int nseg);

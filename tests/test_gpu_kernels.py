@@ -299,3 +299,32 @@ def test_orderstat_refinement_stress(n):
         mag = np.abs(np.sort(X, 0)[k:n - k]).sum(0) / (n - 2 * k)
         err = np.abs(out.cpu().numpy().astype(np.float64) - want)
         assert (err <= 2 * eps * (mag + np.abs(want))).all(), (k, err.max())
+
+
+@pytest.mark.parametrize('n', [12, 50, 130, 255, 256, 300])
+def test_pairdist_aligned_rows_stage_plans(n):
+    """16-B aligned rows (the production ClientStack layout) take the
+    register-prefetched full-stage path; the client counts cover every stage
+    plan shape (k-slices > 1 with lcm(4, ks) stages, one k-slice, stages
+    capped by the LDS or by the prefetch registers)."""
+    from federatedscope_amd import ops
+    P = 6007
+    ld = ops.round_up(P, 64)
+    rng = np.random.default_rng(1000 + n)
+    X = np.zeros((n, ld), np.float32)
+    X[:, :P] = rng.standard_normal((n, P)).astype(np.float32)
+    offs = [0, 3, 2500, 2501, P]
+    slab = torch.from_numpy(X).cuda()
+    rows = ops.RowTable.from_slab(slab, numel=P)
+    assert rows.aligned16
+    D = ops.pairdist(rows, offs).cpu().numpy()
+    X64 = X[:, :P].astype(np.float64)
+    Dref = np.zeros((n, n), np.float32)
+    for s in range(len(offs) - 1):
+        blk = X64[:, offs[s]:offs[s + 1]]
+        for a in range(n):
+            Dref[a] += np.sqrt(((blk - blk[a]) ** 2).sum(1)).astype(
+                np.float32)
+    off = ~np.eye(n, dtype=bool)
+    np.testing.assert_allclose(D[off], Dref[off], rtol=2e-6)
+    assert np.isinf(np.diag(D)).all()
