@@ -37,6 +37,7 @@ constexpr int kBlock = 256;
 // the staged coordinate row of every client must fit the LDS many times
 // over (and the n²-sized workspace stay sane)
 constexpr int kMaxPairClients = 4096;
+constexpr int kPtrSlots = 512;                // LDS row-pointer table
 constexpr int kRedPitch = 65;                  // LDS pitch of a reduction slot
 constexpr int kLdsFloats = kBlock * kRedPitch;  // 16640 floats = 65 KiB
 // register-prefetched staging items per thread (each 4 rows × 4
@@ -152,6 +153,11 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     const int64_t *__restrict__ seg_off, int nseg,
     const int *__restrict__ prefix, float *__restrict__ partial) {
   __shared__ __attribute__((aligned(16))) float lds[kLdsFloats];
+  // client row pointers for the prefetch (n <= kPtrSlots, else no
+  // prefetch: stages are loaded by the scalar path): the per-lane
+  // pointer gather of a stage's items then costs LDS reads, which never
+  // wait behind the HBM loads already in flight (vmcnt is in order)
+  __shared__ const float *rowp[kPtrSlots];
   const int c = blockIdx.x;
   const int total = prefix[nseg];
   if (c >= total) return;
@@ -197,6 +203,9 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   // latency of one hides behind the FMAs of the other); 10×10 do not
   constexpr int kUnroll = TS == 8 ? 2 : 1;
   f4v pre[kStageItems][4];
+  // global (not flat) loads: a flat load also counts in lgkmcnt, so the
+  // compute loop's first LDS-read wait would wait for the whole prefetch
+  typedef __attribute__((address_space(1))) const f4v gf4v;
   auto fetch = [&](int64_t cs) {
 #pragma unroll
     for (int k = 0; k < kStageItems; ++k) {
@@ -206,8 +215,9 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = min(qd * 4 + e, n - 1);
+          const float *row = rowp[r];
           pre[k][e] = __builtin_nontemporal_load(
-              reinterpret_cast<const f4v *>(rows[r] + cs) + g);
+              (gf4v *)(row + cs) + g);
         }
       }
     }
@@ -245,7 +255,12 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     }
   };
 
-  const bool prefetch = vec && items <= kStageItems * kBlock;
+  const bool prefetch =
+      vec && items <= kStageItems * kBlock && n <= kPtrSlots;
+  if (n <= kPtrSlots) {
+    for (int r = tid; r < n; r += kBlock) rowp[r] = rows[r];
+    __syncthreads();
+  }
   if (prefetch && end - start >= pl.sub) fetch(start);
   for (int64_t cs = start; cs < end; cs += pl.sub) {
     const int len = int(end - cs < pl.sub ? end - cs : pl.sub);
