@@ -37,6 +37,20 @@ __device__ __forceinline__ float gload(const float *p) {
 __device__ __forceinline__ float gload_nt(const float *p) {
   return __builtin_nontemporal_load((global_f32 *)(p));
 }
+// Any element type.  (Why it matters: a pointer read from a table is
+// generic, so a plain dereference becomes flat_load, which also counts in
+// lgkmcnt — the next scalar load of a row pointer then waits for every
+// HBM load in flight.)
+template <typename T>
+__device__ __forceinline__ T gld(const T *p) {
+  typedef __attribute__((address_space(1))) const T gT;
+  return *(gT *)(p);
+}
+template <typename T>
+__device__ __forceinline__ T gld_nt(const T *p) {
+  typedef __attribute__((address_space(1))) const T gT;
+  return __builtin_nontemporal_load((gT *)(p));
+}
 
 // Grid size for a streaming kernel: enough workgroups to fill 256 CUs a few
 // times over, never more than the work needs.

@@ -32,7 +32,7 @@ __device__ __forceinline__ void load_column(const float *const *rows, int n,
                                             bool &nan, bool &nonfinite) {
   float x[N];
 #pragma unroll
-  for (int j = 0; j < N; ++j) x[j] = rows[j < n ? j : n - 1][p];
+  for (int j = 0; j < N; ++j) x[j] = gld_nt(rows[j < n ? j : n - 1] + p);
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     const bool real = j < n;
@@ -81,7 +81,7 @@ __device__ __forceinline__ uint32_t select_rank(const float *const *rows,
   for (int bit = 31; bit >= 0; --bit) {
     const uint32_t cand = prefix | ((1u << bit) - 1u);  // all lower bits set
     int cnt = 0;
-    for (int j = 0; j < n; ++j) cnt += f2key(rows[j][p]) <= cand;
+    for (int j = 0; j < n; ++j) cnt += f2key(gld(rows[j] + p)) <= cand;
     if (cnt <= rank) prefix |= 1u << bit;
   }
   return prefix;
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_generic_kernel(
   if (p >= numel) return;
   bool nan = false, nonfinite = false;
   for (int j = 0; j < n; ++j) {
-    const float x = rows[j][p];
+    const float x = gld(rows[j] + p);
     nan |= __builtin_isnan(x);
     nonfinite |= !__builtin_isfinite(x);
   }
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_generic_kernel(
       double acc = 0.0;
       int below = 0, eq_lo = 0, inside = 0;
       for (int j = 0; j < n; ++j) {
-        const float x = rows[j][p];
+        const float x = gld(rows[j] + p);
         const uint32_t key = f2key(x);
         below += key < klo;
         eq_lo += key == klo;
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_generic_kernel(
       // among the excluded values, so inf - inf (or a NaN) gives NaN;
       // with k == 0 the result is Σall itself.
       float all = 0.0f;
-      for (int j = 0; j < n; ++j) all = add_rn(all, rows[j][p]);
+      for (int j = 0; j < n; ++j) all = add_rn(all, gld(rows[j] + p));
       s = (kk == 0 && !nan) ? all : __builtin_nanf("");
     }
     r = __fdiv_rn(s, divisor);

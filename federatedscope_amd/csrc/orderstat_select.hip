@@ -400,7 +400,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
       if (kk == 0 && !nan) {
         s = 0.0f;
 #pragma unroll 1
-        for (int j = 0; j < n; ++j) s = add_rn(s, rows[j][p]);
+        for (int j = 0; j < n; ++j) s = add_rn(s, gld(rows[j] + p));
       }
     }
     r = __fdiv_rn(s, divisor);

@@ -251,7 +251,7 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
       const float *p3 = rows[min(r0 + 3, n - 1)] + cs;
       for (int cc = lane; cc < len; cc += kWave)
         *reinterpret_cast<float4 *>(lds + cc * pl.ldsp + r0) =
-            make_float4(p0[cc], p1[cc], p2[cc], p3[cc]);
+            make_float4(gld(p0 + cc), gld(p1 + cc), gld(p2 + cc), gld(p3 + cc));
     }
   };
 
@@ -401,10 +401,23 @@ __global__ __launch_bounds__(kBlock) void rownorm_partial_kernel(
   const int64_t lo = int64_t(blockIdx.x) * chunk;
   int64_t hi = lo + chunk;
   if (hi > numel) hi = numel;
-  const float *x = rows[row];
+  const float *x = rows[row] + lo;
+  const int64_t len = hi > lo ? hi - lo : 0;
+  // unguarded groups of 8 coordinates per lane (all loads issued before
+  // the first use), then a guarded tail
+  constexpr int G = 8;
+  const int64_t full = len / (G * kBlock) * (G * kBlock);
   double acc = 0.0;
-  for (int64_t p = lo + threadIdx.x; p < hi; p += kBlock) {
-    const double d = double(x[p]);
+  int64_t q = threadIdx.x;
+  for (; q < full; q += G * kBlock) {
+    float v[G];
+#pragma unroll
+    for (int e = 0; e < G; ++e) v[e] = gload_nt(x + q + e * kBlock);
+#pragma unroll
+    for (int e = 0; e < G; ++e) acc += double(v[e]) * double(v[e]);
+  }
+  for (; q < len; q += kBlock) {
+    const double d = double(gld(x + q));
     acc += d * d;
   }
   acc = wave_sum(acc);

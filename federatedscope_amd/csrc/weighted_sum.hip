@@ -172,11 +172,11 @@ __global__ void wsum_f32_tail_kernel(const float *const *__restrict__ rows,
                                      float *__restrict__ out) {
   const int64_t p = start + threadIdx.x;
   if (p >= numel) return;
-  float x = rows[0][p];
+  float x = gld(rows[0] + p);
   if (pre) x = mul_rn(x, pre[0]);
   float acc = mul_rn(x, w[0]);
   for (int i = 1; i < n; ++i) {
-    float t = rows[i][p];
+    float t = gld(rows[i] + p);
     if (pre) t = mul_rn(t, pre[i]);
     acc = add_rn(acc, mul_rn(t, w[i]));
   }
@@ -253,14 +253,14 @@ __global__ __launch_bounds__(kBlock) void wsum_typed_kernel(
   for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < numel;
        p += int64_t(gridDim.x) * kBlock) {
     if constexpr (DT == FSAGG_F64) {
-      double acc = __dmul_rn(static_cast<const double *>(rows[0])[p], w[0]);
+      double acc = __dmul_rn(gld(static_cast<const double *>(rows[0]) + p), w[0]);
       for (int i = 1; i < n; ++i)
         acc = __dadd_rn(acc,
-                        __dmul_rn(static_cast<const double *>(rows[i])[p], w[i]));
+                        __dmul_rn(gld(static_cast<const double *>(rows[i]) + p), w[i]));
       static_cast<double *>(out)[p] = acc;
     } else if constexpr (DT == FSAGG_F16) {
       auto ld = [&](int i) {
-        return __half2float(static_cast<const __half *>(rows[i])[p]);
+        return __half2float(__ushort_as_half(gld(static_cast<const unsigned short *>(rows[i]) + p)));
       };
       __half acc = __float2half(mul_f32_materialized(ld(0), float(w[0])));
       for (int i = 1; i < n; ++i) {
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(kBlock) void wsum_typed_kernel(
       static_cast<__half *>(out)[p] = acc;
     } else if constexpr (DT == FSAGG_BF16) {
       auto ld = [&](int i) {
-        return bf2f(static_cast<const uint16_t *>(rows[i])[p]);
+        return bf2f(gld(static_cast<const uint16_t *>(rows[i]) + p));
       };
       uint16_t acc = f2bf_rne(mul_rn(ld(0), float(w[0])));
       for (int i = 1; i < n; ++i) {
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(kBlock) void wsum_typed_kernel(
       static_cast<uint16_t *>(out)[p] = acc;
     } else {  // FSAGG_I64 -> f32
       auto ld = [&](int i) {
-        return static_cast<float>(static_cast<const int64_t *>(rows[i])[p]);
+        return static_cast<float>(gld(static_cast<const int64_t *>(rows[i]) + p));
       };
       float acc = mul_rn(ld(0), float(w[0]));
       for (int i = 1; i < n; ++i) acc = add_rn(acc, mul_rn(ld(i), float(w[i])));

@@ -70,6 +70,9 @@ __device__ __forceinline__ double py_mod(double a, double b) {
   return m;
 }
 
+typedef long long ll2v __attribute__((ext_vector_type(2)));
+typedef double d2v __attribute__((ext_vector_type(2)));
+
 // Two consecutive elements per lane (16-B loads of every share row), rows
 // taken four at a time so their loads are in flight together; the adds
 // stay in list order.
@@ -79,21 +82,21 @@ __device__ __forceinline__ void ss_load2(const void *row, bool is_int,
   if (is_int) {
     const int64_t *r = static_cast<const int64_t *>(row) + p;
     if (two) {
-      const longlong2 v = *reinterpret_cast<const longlong2 *>(r);
+      const ll2v v = gld(reinterpret_cast<const ll2v *>(r));
       x0 = __ll2double_rn(v.x);
       x1 = __ll2double_rn(v.y);
     } else {
-      x0 = __ll2double_rn(r[0]);
+      x0 = __ll2double_rn(gld(r));
       x1 = 0.0;
     }
   } else {
     const double *r = static_cast<const double *>(row) + p;
     if (two) {
-      const double2 v = *reinterpret_cast<const double2 *>(r);
+      const d2v v = gld(reinterpret_cast<const d2v *>(r));
       x0 = v.x;
       x1 = v.y;
     } else {
-      x0 = r[0];
+      x0 = gld(r);
       x1 = 0.0;
     }
   }
