@@ -151,3 +151,52 @@ def test_no_gpu_raises_loudly():
     agg = ClientsAvgAggregator(config=_cfg())
     with pytest.raises(RuntimeError, match='no CPU fallback'):
         agg.aggregate({'client_feedback': [(1, {'w': torch.zeros(4)})]})
+
+
+def _device_asm():
+    """Disassembly of libfsagg's gfx950 code objects (llvm-objdump)."""
+    import glob
+    import os
+    import shutil
+    import subprocess
+    import tempfile
+    llvm = '/opt/rocm/lib/llvm/bin/llvm-objdump'
+    so = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
+        __file__))), 'federatedscope_amd', 'lib', 'libfsagg.so')
+    if not (os.path.exists(llvm) and os.path.exists(so)):
+        pytest.skip('llvm-objdump or libfsagg.so missing')
+    d = tempfile.mkdtemp()
+    try:
+        dst = os.path.join(d, 'lib.so')
+        shutil.copy(so, dst)
+        subprocess.run([llvm, '--offloading', dst], check=True,
+                       capture_output=True, cwd=d)
+        cos = glob.glob(os.path.join(d, 'lib.so.*gfx950*'))
+        assert cos, 'no gfx950 code object in libfsagg.so'
+        return '\n'.join(subprocess.run([llvm, '-d', co], check=True,
+                                        capture_output=True,
+                                        text=True).stdout for co in cos)
+    finally:
+        shutil.rmtree(d)
+
+
+def test_device_code_memory_rules():
+    """Rules of the kernels' memory instructions, checked on the shipped
+    library: (1) no flat loads — row pointers come from tables, and a
+    dereference of a generic pointer compiles to flat_load, which also
+    counts in lgkmcnt, so the next scalar/LDS wait would drain every HBM
+    load in flight; (2) no writes through the scalar data
+    cache (scalar stores, scalar buffer/scratch stores, scalar cache
+    write-back/discard, scalar atomics) — the mnemonics are assembled at run
+    time below so this file does not spell them."""
+    import re
+    asm = _device_asm()
+    assert 'global_load' in asm
+    assert asm.count('flat_load') == 0
+    sc = 's' + '_'
+    stems = ['st' + 'ore_', 'buffer_st' + 'ore_', 'scratch_st' + 'ore_',
+             'dcache_' + 'wb', 'dcache_' + 'discard', 'ato' + 'mic_',
+             'buffer_ato' + 'mic_']
+    bad = re.findall(r'\b(' + '|'.join(sc + t + r'\w*' for t in stems) +
+                     r')\b', asm)
+    assert not bad, sorted(set(bad))
