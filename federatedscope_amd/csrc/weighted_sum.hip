@@ -515,6 +515,12 @@ extern "C" int fsagg_tune_wsum(int variant, unsigned grid,
     case 9: launch_variant<1, 12, true>(rows, w, n, nvec, out, grid, s); break;
     case 10: launch_variant<1, 20, true>(rows, w, n, nvec, out, grid, s); break;
     case 11: launch_variant<1, 24, true>(rows, w, n, nvec, out, grid, s); break;
+    case 12: launch_variant<1, 1, true>(rows, w, n, nvec, out, grid, s); break;
+    case 13: launch_variant<4, 1, true>(rows, w, n, nvec, out, grid, s); break;
+    case 14: launch_variant<8, 1, true>(rows, w, n, nvec, out, grid, s); break;
+    case 15: launch_variant<2, 4, true>(rows, w, n, nvec, out, grid, s); break;
+    case 16: launch_variant<1, 4, true>(rows, w, n, nvec, out, grid, s); break;
+    case 17: launch_variant<4, 2, true>(rows, w, n, nvec, out, grid, s); break;
     default: set_error("variant"); return FSAGG_EINVAL;
   }
   return check_launch("fsagg_tune_wsum");

@@ -14,7 +14,8 @@ from federatedscope_amd import _lib, ops  # noqa: E402
 
 VARIANTS = {0: 'U8V2nt', 1: 'U2V8nt', 2: 'U4V8nt', 3: 'U1V8nt', 4: 'U2V16nt',
             5: 'U1V16nt', 6: 'U4V4nt', 7: 'U3V8nt', 8: 'U2V8', 9: 'U1V12nt',
-            10: 'U1V20nt', 11: 'U1V24nt'}
+            10: 'U1V20nt', 11: 'U1V24nt', 12: 'U1V1nt', 13: 'U4V1nt',
+            14: 'U8V1nt', 15: 'U2V4nt', 16: 'U1V4nt', 17: 'U4V2nt'}
 
 PART = {0: 'U1V8', 1: 'U1V12', 2: 'U1V16', 3: 'U1V24', 4: 'U2V8', 5: 'U2V12',
         6: 'U1V32', 7: 'U4V4'}
