@@ -65,7 +65,7 @@ SIGNATURES['fsagg_server_opt_step_f32'] = (
 _c_d = ctypes.c_double
 FSAGG_WIRE_F32, FSAGG_WIRE_I8, FSAGG_WIRE_I16 = 0, 1, 2
 SIGNATURES['fsagg_wire_unpack_f32'] = (
-    _c_i, [_c_p, _c_p, _c_p, _c_i, _c_i64, _c_p, _c_p])
+    _c_i, [_c_p, _c_i64, _c_p, _c_p, _c_i, _c_i, _c_i64, _c_p, _c_i64, _c_p])
 SIGNATURES['fsagg_ss_recover_f32'] = (
     _c_i, [_c_p, _c_p, _c_i, _c_i64, _c_d, _c_d, _c_d, _c_d, _c_i, _c_p, _c_p,
            _c_p])

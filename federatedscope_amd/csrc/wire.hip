@@ -34,12 +34,26 @@ static_assert(sizeof(WireSeg) == 32, "WireSeg is part of the ABI");
 
 // grid = (ceil(max_len / (kBlock * kPerThread)), nseg): one y-row per
 // segment, consecutive threads take consecutive elements.
+// Segments are device data the host cannot see at launch time, so each
+// block checks its own against the stated extents (src_bytes of packed
+// input, out_len of the row) and skips one that does not fit: a malformed
+// table writes nothing instead of faulting.
 __global__ __launch_bounds__(kBlock) void wire_unpack_kernel(
     const unsigned char *__restrict__ src, const WireSeg *__restrict__ segs,
-    const float *__restrict__ scales, float *__restrict__ out) {
+    const float *__restrict__ scales, int nscale, int64_t src_bytes,
+    int64_t out_len, float *__restrict__ out) {
   const WireSeg sg = segs[blockIdx.y];
   const int64_t base = int64_t(blockIdx.x) * kBlock * kPerThread;
   if (base >= sg.len) return;
+  const int64_t width = sg.kind == FSAGG_WIRE_I8 ? 1
+                        : sg.kind == FSAGG_WIRE_I16 ? 2 : 4;
+  if (sg.len < 0 || sg.src < 0 || sg.dst < 0 || sg.src % width ||
+      sg.src > src_bytes || sg.len > (src_bytes - sg.src) / width ||
+      sg.dst > out_len || sg.len > out_len - sg.dst ||
+      (sg.kind != FSAGG_WIRE_F32 && sg.kind != FSAGG_WIRE_I8 &&
+       sg.kind != FSAGG_WIRE_I16) ||
+      sg.scale_idx >= nscale)
+    return;
   const float s = sg.scale_idx >= 0 ? scales[sg.scale_idx] : 1.0f;
 #pragma unroll
   for (int e = 0; e < kPerThread; ++e) {
@@ -155,11 +169,13 @@ __global__ __launch_bounds__(kBlock) void ss_recover_kernel(
 
 using namespace fsagg;
 
-extern "C" int fsagg_wire_unpack_f32(const void *src, const void *segs,
-                                     const float *scales, int nseg,
-                                     int64_t max_len, float *out,
+extern "C" int fsagg_wire_unpack_f32(const void *src, int64_t src_bytes,
+                                     const void *segs, const float *scales,
+                                     int nscale, int nseg, int64_t max_len,
+                                     float *out, int64_t out_len,
                                      fsagg_stream_t stream) {
-  if (!src || !segs || !out || nseg < 0 || max_len < 0) {
+  if (!src || !segs || !out || nseg < 0 || max_len < 0 || src_bytes < 0 ||
+      out_len < 0 || nscale < 0 || (nscale > 0 && !scales)) {
     set_error("fsagg_wire_unpack_f32: invalid argument");
     return FSAGG_EINVAL;
   }
@@ -173,7 +189,8 @@ extern "C" int fsagg_wire_unpack_f32(const void *src, const void *segs,
                      dim3(unsigned((max_len + per - 1) / per), unsigned(nseg)),
                      dim3(kBlock), 0, as_stream(stream),
                      static_cast<const unsigned char *>(src),
-                     static_cast<const WireSeg *>(segs), scales, out);
+                     static_cast<const WireSeg *>(segs), scales, nscale,
+                     src_bytes, out_len, out);
   return check_launch("fsagg_wire_unpack_f32");
 }
 

@@ -404,10 +404,13 @@ def wire_unpack(src, segs, nseg, max_len, scales, out, src_bytes=None,
         raise ValueError('packed upload larger than the staging buffer')
     if max_dst is not None and max_dst > out.numel():
         raise ValueError('segments write past the end of the row')
+    # the kernel re-checks every segment against these extents on the device
     L.check(L.load().fsagg_wire_unpack_f32(
-        src.data_ptr(), segs.data_ptr(), scales.data_ptr(), int(nseg),
-        int(max_len), out.data_ptr(), _stream(out.device)),
-        'fsagg_wire_unpack_f32')
+        src.data_ptr(), int(src.numel() if src_bytes is None else src_bytes),
+        segs.data_ptr(), scales.data_ptr(), int(scales.numel()), int(nseg),
+        int(max_len), out.data_ptr(),
+        int(out.numel() if max_dst is None else max_dst),
+        _stream(out.device)), 'fsagg_wire_unpack_f32')
     return out
 
 

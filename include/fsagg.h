@@ -202,15 +202,19 @@ int fsagg_server_opt_step_f32(float *param, const float *avg, float *state0,
  *   (federatedscope/core/compression/utils.py:70-90; int8/int16 codes times
  *   the fp32 scale tensor, one fp32 rounding), fused with the H2D scatter;
  * kind FSAGG_WIRE_F32: out[dst + i] = src_f32[i] (unquantised keys).
- * scales (device) holds the upload's per-key fp32 scales; max_len is the
- * longest segment.  Replaces Server.callback_funcs_model_para's
+ * scales (device) holds the upload's nscale per-key fp32 scales; max_len
+ * is the longest segment.  src_bytes / out_len are the extents of the
+ * packed input and of the fp32 row: the segment table lives on the device,
+ * so each segment is checked there, and one that does not fit both (or
+ * names an unknown kind / scale) is skipped — it writes nothing.  Replaces Server.callback_funcs_model_para's
  * dequantisation step (federatedscope/core/workers/server.py:946-960).
  */
 enum fsagg_wire_kind { FSAGG_WIRE_F32 = 0, FSAGG_WIRE_I8 = 1,
                        FSAGG_WIRE_I16 = 2 };
-int fsagg_wire_unpack_f32(const void *src, const void *segs,
-                          const float *scales, int nseg, int64_t max_len,
-                          float *out, fsagg_stream_t stream);
+int fsagg_wire_unpack_f32(const void *src, int64_t src_bytes,
+                          const void *segs, const float *scales, int nscale,
+                          int nseg, int64_t max_len, float *out,
+                          int64_t out_len, fsagg_stream_t stream);
 
 /*
  * Secret-sharing FedAvg (cfg.federate.use_ss) in one pass:

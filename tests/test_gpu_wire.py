@@ -277,3 +277,38 @@ def test_delta_keys_match_flat_odd_layouts():
     for i in range(n):
         want = want + np.float32(w[i]) * (x[i] - b)
     assert out_f.cpu().numpy().tobytes() == want.tobytes()
+
+
+def test_wire_unpack_skips_malformed_segments():
+    """The segment table is device data: segments that overrun the packed
+    input or the row, or name an unknown kind / scale, are skipped on the
+    device (nothing written, no fault); the valid ones still decode."""
+    from federatedscope_amd import _lib as L
+    from federatedscope_amd import ops
+    dev = torch.device('cuda')
+    f = np.arange(16, dtype=np.float32) + 1.0
+    src = torch.from_numpy(f.view(np.uint8).copy()).to(dev)      # 64 B
+    scales = torch.tensor([0.5], device=dev)
+    recs = [(0, 0, 4, L.FSAGG_WIRE_F32, -1),      # valid
+            (0, 98, 4, L.FSAGG_WIRE_F32, -1),     # row overrun
+            (60, 10, 4, L.FSAGG_WIRE_F32, -1),    # input overrun
+            (0, 20, 4, 7, -1),                    # unknown kind
+            (0, 30, 4, L.FSAGG_WIRE_I8, 5),       # scale index out of range
+            (0, 40, -3, L.FSAGG_WIRE_F32, -1),    # negative length
+            (1, 50, 2, L.FSAGG_WIRE_I16, 0),      # misaligned int16 source
+            (16, 60, 8, L.FSAGG_WIRE_I8, 0)]      # valid int8
+    arr = np.zeros(len(recs), dtype=ops.WIRE_SEG_DTYPE)
+    for i, r in enumerate(recs):
+        arr[i] = r
+    segs = torch.from_numpy(arr.view(np.uint8).copy()).to(dev)
+    out = torch.full((100, ), -1.0, device=dev)
+    ops.wire_unpack(src, segs, len(recs), 8, scales, out)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    assert o[:4].tolist() == [1.0, 2.0, 3.0, 4.0]
+    q = f.view(np.uint8)[16:24].view(np.int8).astype(np.float32)
+    assert o[60:68].tobytes() == (q * np.float32(0.5)).tobytes()
+    mask = np.ones(100, bool)
+    mask[:4] = False
+    mask[60:68] = False
+    assert (o[mask] == -1.0).all()
