@@ -200,3 +200,39 @@ def test_device_code_memory_rules():
     bad = re.findall(r'\b(' + '|'.join(sc + t + r'\w*' for t in stems) +
                      r')\b', asm)
     assert not bad, sorted(set(bad))
+
+
+def test_missing_library_fails_loudly():
+    """No CPU fallback: without libfsagg.so the product path raises."""
+    import subprocess
+    import sys
+    code = (
+        'import torch\n'
+        'from collections import OrderedDict\n'
+        'from types import SimpleNamespace\n'
+        'from federatedscope_amd import _lib\n'
+        'from federatedscope_amd.core.aggregators import '
+        'ClientsAvgAggregator\n'
+        'cfg = SimpleNamespace(federate=SimpleNamespace(ignore_weight=False,'
+        ' use_ss=False))\n'
+        'agg = ClientsAvgAggregator(config=cfg)\n'
+        'fb = [(1, OrderedDict(w=torch.ones(3))), '
+        '(2, OrderedDict(w=torch.zeros(3)))]\n'
+        'try:\n'
+        '    agg.aggregate({"client_feedback": fb})\n'
+        'except Exception as e:\n'
+        '    print("RAISED", type(e).__name__)\n'
+        'else:\n'
+        '    print("NO-ERROR")\n'
+        'try:\n'
+        '    _lib.load()\n'
+        'except _lib.FsaggError:\n'
+        '    print("LOAD-RAISED")\n')
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FSAGG_LIB='/nonexistent/libfsagg.so',
+               PYTHONPATH=root)
+    r = subprocess.run([sys.executable, '-c', code], env=env, cwd=root,
+                       capture_output=True, text=True, timeout=300)
+    assert 'RAISED' in r.stdout and 'NO-ERROR' not in r.stdout, r.stdout + \
+        r.stderr
+    assert 'LOAD-RAISED' in r.stdout
