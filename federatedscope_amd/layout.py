@@ -49,6 +49,28 @@ class BucketLayout:
         return (tuple(self.order), tuple(
             (k, self.shapes[k]) for k in self.keys), tuple(self.other.items()))
 
+    def chunk_tables(self, device):
+        """Device tables for fsagg_gather_rows_f32: key offsets, key lengths
+        and the bucket as chunks of <= FSAGG_STACK_CHUNK coordinates that
+        never straddle a key (built once per layout and device)."""
+        from .ops import _h2d
+        from ._lib import FSAGG_STACK_CHUNK as CH
+        device = torch.device(device)
+        cache = self.__dict__.setdefault('_chunk_tables', {})
+        if str(device) not in cache:
+            ck, cs = [], []
+            for s, k in enumerate(self.keys):
+                for st in range(0, self.numels[k], CH):
+                    ck.append(s)
+                    cs.append(st)
+            cache[str(device)] = (
+                _h2d([self.offsets[k] for k in self.keys], torch.int64,
+                     device),
+                _h2d([self.numels[k] for k in self.keys], torch.int64,
+                     device),
+                _h2d(ck, torch.int32, device), _h2d(cs, torch.int64, device))
+        return cache[str(device)]
+
     def segments(self, keys=None):
         """Element offsets [0, ..., numel] splitting the bucket per key
         (padding folded into the preceding key; zeros add nothing to sums of
@@ -172,10 +194,17 @@ class ClientStack:
         self.layout.pack_device(model, self.slab[i])
 
     def load_many(self, models):
-        """Stage every client: device-resident dicts by device copies, host
-        dicts through the double-buffered pinned stager."""
+        """Stage every client: device-resident fp32 dicts in ONE gather
+        launch (fsagg_gather_rows_f32), host dicts through the
+        double-buffered pinned stager, anything else (other dtypes, other
+        devices) by per-key device copies."""
         stager = None
+        gather = []
         for i, m in enumerate(models):
+            srcs = self._device_keys(m)
+            if srcs is not None:
+                gather.append((i, srcs))
+                continue
             on_host = any(param2tensor(m[k]).device.type != 'cuda'
                           for k in self.layout.keys if k in m)
             if on_host:
@@ -184,8 +213,52 @@ class ClientStack:
                 stager.put(self.layout, m, self.slab[i])
             else:
                 self.layout.pack_device(m, self.slab[i])
+        if gather:
+            self._gather(gather)
         if stager is not None:
             stager.finish()
+
+    def _device_keys(self, model):
+        """Data pointers of the model's fp32 keys when every present key is a
+        contiguous fp32 tensor of the layout's size on this stack's device
+        (0 for absent keys); else None."""
+        dev = self.device.index if self.device.index is not None else \
+            torch.cuda.current_device()
+        f32 = torch.float32
+        ptrs = []
+        lay = self.layout
+        for k in lay.keys:
+            if k not in model:
+                ptrs.append(0)
+                continue
+            t = model[k]
+            if not isinstance(t, torch.Tensor) or t.dtype is not f32 or \
+                    t.get_device() != dev or not t.is_contiguous() or \
+                    t.numel() != lay.numels[k]:
+                return None
+            ptrs.append(t.data_ptr() if t.numel() else 0)
+        return ptrs
+
+    def _gather(self, gather):
+        from . import _lib as L
+        from .ops import _h2d, _stream
+        lay = self.layout
+        if not lay.keys:
+            return
+        tabs = lay.chunk_tables(self.device)
+        base = self.slab.data_ptr()
+        ld = self.slab.stride(0) * 4
+        for b in range(0, len(gather), 65535):   # grid.y limit
+            part = gather[b:b + 65535]
+            src = _h2d([p for _, ptrs in part for p in ptrs], torch.int64,
+                       self.device)
+            dst = _h2d([base + i * ld for i, _ in part], torch.int64,
+                       self.device)
+            L.check(L.load().fsagg_gather_rows_f32(
+                src.data_ptr(), len(part), len(lay.keys), dst.data_ptr(),
+                tabs[0].data_ptr(), tabs[1].data_ptr(), tabs[2].data_ptr(),
+                tabs[3].data_ptr(), tabs[2].numel(), _stream(self.device)),
+                'fsagg_gather_rows_f32')
 
     def rows(self, idx=None, key=None):
         from .ops import RowTable

@@ -286,6 +286,24 @@ int fsagg_delta_wsum_keys_f32(const float *const *keys, const float *weights,
                               fsagg_stream_t stream);
 
 /*
+ * Stage device-resident client updates into the client stack in ONE launch
+ * (the per-key copies of ClientStack.load for GPU-resident state_dicts;
+ * federatedscope/core/workers/server.py:966-970 stores the dicts that the
+ * aggregators then read key by key).  src (device) is an n x nseg row-major
+ * table of fp32 key tensors (NULL: the client lacks that key, its row keeps
+ * its contents); dst_rows (device) n row pointers; key_off / key_len (device)
+ * nseg int64 offsets into a row and lengths; the bucket is listed as nchunk
+ * chunks (chunk_key int32, chunk_start int64, device) of at most
+ * FSAGG_STACK_CHUNK coordinates that never straddle a key.  n <= 65535.
+ */
+#define FSAGG_STACK_CHUNK 2048
+int fsagg_gather_rows_f32(const float *const *src, int n, int nseg,
+                          float *const *dst_rows, const int64_t *key_off,
+                          const int64_t *key_len, const int32_t *chunk_key,
+                          const int64_t *chunk_start, int nchunk,
+                          fsagg_stream_t stream);
+
+/*
  * Deterministic synthetic client updates (benchmarks / tests): fills the
  * [n][ld] slab X with u = hash(seed, client, index) mapped to [-1, 1),
  * index < numel; the same generator is restated on the host by the tests.

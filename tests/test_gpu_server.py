@@ -109,3 +109,47 @@ def test_staged_robust_rules_match_unstaged():
                          ).aggregate({'client_feedback': staged})
     for k in want:
         assert g[k].cpu().numpy().tobytes() == want[k].tobytes()
+
+
+def test_stack_gather_matches_per_key_copies():
+    """ClientStack.load_many: device-resident fp32 dicts go through one
+    fsagg_gather_rows_f32 launch; rows equal the per-key copies bit for bit,
+    absent keys leave the row untouched, and dicts the gather cannot take
+    (a non-contiguous or fp16 tensor) fall back to per-key copies."""
+    from collections import OrderedDict
+    from federatedscope_amd.layout import BucketLayout, ClientStack
+    dev = torch.device('cuda')
+    g = torch.Generator(device=dev).manual_seed(5)
+    shapes = [('a', (3, )), ('b', (2049, )), ('c', (0, )), ('d', (64, 70)),
+              ('e', (1, )), ('f', (5000, 3))]
+    tmpl = OrderedDict((k, torch.zeros(s)) for k, s in shapes)
+    lay = BucketLayout(tmpl)
+    n = 9
+    models = []
+    for i in range(n):
+        m = OrderedDict((k, torch.randn(s, device=dev, generator=g))
+                        for k, s in shapes)
+        if i == 2:
+            del m['d']                          # absent key
+        if i == 4:
+            m['b'] = torch.randn((2049, 2), device=dev,
+                                 generator=g)[:, 0]   # non-contiguous
+        if i == 6:
+            m['f'] = m['f'].half()              # other dtype: converted
+        models.append(m)
+    fast = ClientStack(lay, n, dev)
+    fast.slab.fill_(-3.0)
+    fast.load_many(models)
+    slow = ClientStack(lay, n, dev)
+    slow.slab.fill_(-3.0)
+    for i, m in enumerate(models):
+        lay.pack_device(m, slow.slab[i])
+    torch.cuda.synchronize()
+    assert torch.equal(fast.slab, slow.slab)
+    o, k = lay.offsets['d'], lay.numels['d']
+    assert (fast.slab[2, o:o + k] == -3.0).all()
+    for i in (0, 5, 8):
+        for key, s in shapes:
+            o, k = lay.offsets[key], lay.numels[key]
+            assert torch.equal(fast.slab[i, o:o + k],
+                               models[i][key].reshape(-1))

@@ -165,9 +165,89 @@ def orderstat_c5(dev, n=200, ratio=0.2):
     return res
 
 
+def dropin_rules(dev):
+    """The drop-in aggregators' whole aggregate() call (Python, staging of the
+    client dicts into the device stack, kernels, init + update) on
+    device-resident ConvNet2-h2048 dicts (12 keys, 6.6M params): Krum
+    (multi-Krum 5) and Bulyan at n = 50, f = 10; median, trimmed mean and
+    norm bounding at n = 200.  Wall clock with the GPU synchronised on both
+    sides; the result stays on the device."""
+    from collections import OrderedDict
+    from types import SimpleNamespace
+    from federatedscope_amd.core.aggregators import (
+        BulyanAggregator, KrumAggregator, MedianAggregator,
+        NormboundingAggregator, TrimmedmeanAggregator)
+
+    def cfg(f=0, agg_num=1, ratio=0.2, bound=5.0, client_num=1000):
+        bft = SimpleNamespace(krum_agg_num=agg_num,
+                              trimmedmean_excluded_ratio=ratio,
+                              normbounding_norm_bound=bound)
+        return SimpleNamespace(
+            federate=SimpleNamespace(ignore_weight=False, use_ss=False,
+                                     client_num=client_num,
+                                     sample_client_rate=1.0),
+            aggregator=SimpleNamespace(byzantine_node_num=f, BFT_args=bft),
+            asyn=SimpleNamespace(staleness_discount_factor=1.0))
+
+    class M(torch.nn.Module):
+        def __init__(self, sd):
+            super().__init__()
+            self._sd = sd
+
+        def state_dict(self, *a, **kw):
+            return OrderedDict((k, v.clone()) for k, v in self._sd.items())
+
+    g = torch.Generator(device=dev).manual_seed(7)
+    keys = [(k, s) for k, s in CONVNET2_H2048]
+    init = OrderedDict((k, torch.randn(s, device=dev, generator=g))
+                       for k, s in keys)
+    P = sum(v.numel() for v in init.values())
+
+    def clients(n):
+        return [(int(1 + i), OrderedDict(
+            (k, 1e-2 * torch.randn(s, device=dev, generator=g))
+            for k, s in keys)) for i in range(n)]
+
+    out = []
+    c50, c200 = clients(50), clients(200)
+    rules = [
+        ('krum_agg5', 50, KrumAggregator(model=M(init), device=dev,
+                                         config=cfg(f=10, agg_num=5))),
+        ('bulyan', 50, BulyanAggregator(model=M(init), device=dev,
+                                        config=cfg(f=10, client_num=50))),
+        ('median', 200, MedianAggregator(model=M(init), device=dev,
+                                         config=cfg())),
+        ('trimmed_mean', 200, TrimmedmeanAggregator(model=M(init),
+                                                    device=dev,
+                                                    config=cfg(ratio=0.2))),
+        ('normbounding', 200, NormboundingAggregator(model=M(init),
+                                                     device=dev,
+                                                     config=cfg(bound=5.0))),
+    ]
+    for name, n, agg in rules:
+        fb = c50 if n == 50 else c200
+        info = {'client_feedback': fb, 'recover_fun': None}
+        agg.aggregate(info)
+        ts = []
+        for _ in range(4):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            agg.aggregate(info)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        t = statistics.median(ts)
+        out.append({'rule': name, 'clients': n, 'params': P,
+                    'ms_aggregate': round(t * 1e3, 3),
+                    'GBps_algorithmic': round(4.0 * n * P / t / 1e9, 1),
+                    'what': 'aggregate() on device-resident dicts, '
+                            'staging + kernels + init+update'})
+        log('%s: %.2f ms' % (name, t * 1e3))
+    return out
+
+
 def main():
     dev = torch.device('cuda', 0)
-    which = sys.argv[1:] or ['krum', 'orderstat']
+    which = sys.argv[1:] or ['krum', 'orderstat', 'dropin']
     if 'krum' in which:
         t0 = time.time()
         print(json.dumps(krum_c4(dev)), flush=True)
@@ -175,6 +255,10 @@ def main():
         torch.cuda.empty_cache()
     if 'orderstat' in which:
         for r in orderstat_c5(dev):
+            print(json.dumps(r), flush=True)
+        torch.cuda.empty_cache()
+    if 'dropin' in which:
+        for r in dropin_rules(dev):
             print(json.dumps(r), flush=True)
 
 
