@@ -169,14 +169,14 @@ def dropin_rules(dev):
     """The drop-in aggregators' whole aggregate() call (Python, staging of the
     client dicts into the device stack, kernels, init + update) on
     device-resident ConvNet2-h2048 dicts (12 keys, 6.6M params): Krum
-    (multi-Krum 5) and Bulyan at n = 50, f = 10; median, trimmed mean and
-    norm bounding at n = 200.  Wall clock with the GPU synchronised on both
+    (multi-Krum 5) and Bulyan at n = 50, f = 10; FedAvg, median, trimmed
+    mean and norm bounding at n = 200.  Wall clock with the GPU synchronised on both
     sides; the result stays on the device."""
     from collections import OrderedDict
     from types import SimpleNamespace
     from federatedscope_amd.core.aggregators import (
-        BulyanAggregator, KrumAggregator, MedianAggregator,
-        NormboundingAggregator, TrimmedmeanAggregator)
+        BulyanAggregator, ClientsAvgAggregator, KrumAggregator,
+        MedianAggregator, NormboundingAggregator, TrimmedmeanAggregator)
 
     def cfg(f=0, agg_num=1, ratio=0.2, bound=5.0, client_num=1000):
         bft = SimpleNamespace(krum_agg_num=agg_num,
@@ -211,6 +211,8 @@ def dropin_rules(dev):
     out = []
     c50, c200 = clients(50), clients(200)
     rules = [
+        ('fedavg', 200, ClientsAvgAggregator(model=M(init), device=dev,
+                                             config=cfg())),
         ('krum_agg5', 50, KrumAggregator(model=M(init), device=dev,
                                          config=cfg(f=10, agg_num=5))),
         ('bulyan', 50, BulyanAggregator(model=M(init), device=dev,
