@@ -49,6 +49,15 @@ class BucketLayout:
         return (tuple(self.order), tuple(
             (k, self.shapes[k]) for k in self.keys), tuple(self.other.items()))
 
+    @property
+    def key_numels(self):
+        """[(key, numel)] of the fp32 keys in layout order."""
+        kn = self.__dict__.get('_key_numels')
+        if kn is None:
+            kn = self.__dict__['_key_numels'] = [(k, self.numels[k])
+                                                 for k in self.keys]
+        return kn
+
     def chunk_tables(self, device):
         """Device tables for fsagg_gather_rows_f32: key offsets, key lengths
         and the bucket as chunks of <= FSAGG_STACK_CHUNK coordinates that
@@ -221,22 +230,28 @@ class ClientStack:
     def _device_keys(self, model):
         """Data pointers of the model's fp32 keys when every present key is a
         contiguous fp32 tensor of the layout's size on this stack's device
-        (0 for absent keys); else None."""
+        (0 for absent keys); else None.  (A hot loop: one pass, one lookup
+        and the fewest tensor attribute reads per key.)"""
         dev = self.device.index if self.device.index is not None else \
             torch.cuda.current_device()
         f32 = torch.float32
+        Tensor = torch.Tensor
+        get = model.get
         ptrs = []
-        lay = self.layout
-        for k in lay.keys:
-            if k not in model:
-                ptrs.append(0)
+        push = ptrs.append
+        for k, nm in self.layout.key_numels:
+            t = get(k)
+            if t is None:
+                if k in model:      # an explicit None value: not ours
+                    return None
+                push(0)
                 continue
-            t = model[k]
-            if not isinstance(t, torch.Tensor) or t.dtype is not f32 or \
-                    t.get_device() != dev or not t.is_contiguous() or \
-                    t.numel() != lay.numels[k]:
+            if t.__class__ is not Tensor and not isinstance(t, Tensor):
                 return None
-            ptrs.append(t.data_ptr() if t.numel() else 0)
+            if t.dtype is not f32 or t.get_device() != dev or \
+                    t.numel() != nm or not t.is_contiguous():
+                return None
+            push(t.data_ptr() if nm else 0)
         return ptrs
 
     def _gather(self, gather):
