@@ -222,6 +222,17 @@ def main():
         ps = min(args.cpu_sample, P)
         log('cpu baseline: numpy oracle, %d clients x %d params' % (n, ps))
         t_cpu, exact = cpu_baseline_leg(slab, n, ps, weights, out)
+        import numpy
+        np_version = numpy.__version__
+        cpu_model = 'unknown CPU'
+        try:
+            with open('/proc/cpuinfo') as f:
+                for line in f:
+                    if line.startswith('model name'):
+                        cpu_model = line.split(':', 1)[1].strip()
+                        break
+        except OSError:
+            pass
         cpu = {
             'value': round(4.0 * n * ps / t_cpu / 1e9, 3),
             'unit': 'GB/s',
@@ -231,7 +242,9 @@ def main():
                        'clients_avg_aggregator.py:60-100, 1 thread like '
                        'fed_runner.py:299) on the first %d params of the '
                        'same %d synthetic clients; best of 3; GPU output '
-                       'bit-exact on this sample: %s' % (ps, n, exact)),
+                       'bit-exact on this sample: %s; host %s, numpy %s, '
+                       'torch %s' % (ps, n, exact, cpu_model,
+                                     np_version, torch.__version__)),
         }
         log('cpu baseline %.3f s -> %.3f GB/s, bit-exact=%s' %
             (t_cpu, cpu['value'], exact))
