@@ -1,17 +1,21 @@
 #!/usr/bin/env python3
 """Aggregation-engine benchmark (BASELINE.json metric).
 
-A "step" is one FedAvg reduction (fsagg_weighted_sum_f32) over one batch of
-synthetic client updates that are already resident in HBM: configs[2] of
-BASELINE.json, 100 clients × 25,000,000 fp32 parameters per GPU.
+A "step" is one FedAvg reduction (fsagg_weighted_sum_f32) of configs[2] of
+BASELINE.json — 100 clients x 25,000,000 fp32 parameters, synthetic updates
+already resident in HBM — whose FULL result ends up on every GPU.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py
---gpus N ...): FedAvg is per-coordinate, so every rank owns its own parameter
-range (rank r generates indices [r·P, (r+1)·P) of the global model) and runs
-the full client loop over it — no data-path collective, bit-exact, weak
-scaling; value = Σ_ranks 4·n·P bytes ÷ max-over-ranks step time.
+--gpus N ...) is STRONG scaling of that fixed model: the parameter range is
+cut into ``chunks`` rounds of N block-cyclic pieces (core/sharding.py
+PipelinedAssembly), rank r holds piece (j, r) of every client and runs the
+full client loop over it (bit-identical to one GPU: no arithmetic crosses
+GPUs), and round j's pieces are all-gathered in place over RCCL/xGMI while
+round j+1 computes.  value = 4·n·P bytes / max-over-ranks step time.
+Secondary fields: the same sharded compute with the output left sharded
+(no collective), and the weak-scaling rate (every rank its own 100 x 25M).
 
-Prints ONE JSON line on rank 0 (see the driver contract in DESIGN.md).
+Prints ONE JSON line on rank 0 (driver contract: DESIGN.md §6).
 """
 import argparse
 import json
@@ -25,6 +29,7 @@ sys.path.insert(0, ROOT)
 METRIC = ('aggregated-GB/s device-resident (clients×params fp32), '
           '1/2/4/8 MI355X; % HBM roofline')
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+SEED = 2026
 
 
 def log(*a):
@@ -48,26 +53,64 @@ def sample_sizes(n, seed=0):
             for i in range(n)]
 
 
-def cpu_baseline_leg(slab, n, P_sample, weights, out_dev):
-    """Time the CPU oracle (a numpy port of _para_weighted_avg, one thread)
-    on the first P_sample columns of the same synthetic clients; check the
-    GPU result bit-exact on that sample."""
-    import numpy as np
-    import oracle
-    host = slab[:, :P_sample].cpu().numpy()
-    models = [(0, {'w': host[i]}) for i in range(n)]
-    # ref weights are the reference's doubles; sizes do not matter here
-    want = None
-    times = []
-    for rep in range(4):
-        t0 = time.perf_counter()
-        got = oracle.para_weighted_avg(models, weights=weights)
-        times.append(time.perf_counter() - t0)
-        want = got['w']
-    t = min(times[1:]) if len(times) > 1 else times[0]
-    gpu = out_dev[:P_sample].cpu().numpy()
-    exact = bool(gpu.tobytes() == want.astype(np.float32).tobytes())
-    return t, exact
+def host_cores():
+    """CPU threads this process is granted.  The GPU box runs us on a share
+    of a large machine (os.cpu_count() and the affinity mask count all of
+    its CPUs) and states the share in OMP_NUM_THREADS."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    omp = os.environ.get('OMP_NUM_THREADS', '')
+    return min(n, int(omp)) if omp.isdigit() and int(omp) > 0 else n
+
+
+def cpu_model():
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown CPU'
+
+
+def cpu_baseline_leg(rows_slab, weights, P, n_sample, dev):
+    """Time oracle/torch_cpu.py (the reference's per-key ``tmp = x*w;
+    acc += tmp`` loop in torch CPU ops, clients_avg_aggregator.py:60-100)
+    on the first ``n_sample`` clients at full width (25M params, the
+    reference's shape class), at 1 thread (fed_runner.py:297-299) and at
+    all of this process's cores; best of 3 after a warm-up.  The GPU kernel
+    reduces the same clients with the same weights and must match bit for
+    bit."""
+    import torch
+    from federatedscope_amd import ops
+    from oracle.torch_cpu import para_weighted_avg_torch
+    host = rows_slab[:n_sample, :P].cpu()
+    models = [(0, {'w': host[i]}) for i in range(n_sample)]
+    w = weights[:n_sample]
+    ref_out = torch.empty(P, dtype=torch.float32, device=dev)
+    ops.weighted_sum(ops.RowTable.from_slab(rows_slab, rows=range(n_sample),
+                                            numel=P), w, ref_out)
+    gpu = ref_out.cpu()
+    prev = torch.get_num_threads()
+    res = {}
+    exact = True
+    for threads in (1, host_cores()):
+        torch.set_num_threads(threads)
+        para_weighted_avg_torch(models[:2], w)      # warm-up
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            got = para_weighted_avg_torch(models, w)['w']
+            ts.append(time.perf_counter() - t0)
+        exact = exact and torch.equal(got, gpu)
+        res[threads] = min(ts)
+        log('cpu baseline %d thread(s): %.3f s -> %.3f GB/s' %
+            (threads, res[threads], 4.0 * n_sample * P / res[threads] / 1e9))
+    torch.set_num_threads(prev)
+    return res, exact
 
 
 def e2e_leg(args, dev, weights, sizes):
@@ -123,6 +166,61 @@ def e2e_leg(args, dev, weights, sizes):
     print(json.dumps(rec), flush=True)
 
 
+class Dist:
+    """The job's process group (RCCL over xGMI when N > 1)."""
+
+    def __init__(self, gpus):
+        import torch
+        import torch.distributed as dist
+        self.dist = dist
+        self.world = int(os.environ.get('WORLD_SIZE', '1'))
+        self.rank = int(os.environ.get('RANK', '0'))
+        self.local = int(os.environ.get('LOCAL_RANK', '0'))
+        if self.world != gpus:
+            log('note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE' %
+                (gpus, self.world))
+        torch.cuda.set_device(self.local)
+        self.dev = torch.device('cuda', self.local)
+        if self.world > 1:
+            dist.init_process_group('nccl', rank=self.rank,
+                                    world_size=self.world,
+                                    device_id=self.dev)
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier(device_ids=[self.local])
+
+    def max(self, x):
+        import torch
+        if self.world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def timed_steps(D, fn, steps, warmup):
+    """W untimed steps, then K steps between barrier + synchronize pairs;
+    returns the max-over-ranks seconds per step."""
+    import torch
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    D.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    D.barrier()
+    torch.cuda.synchronize()
+    return D.max((time.perf_counter() - t0) / steps)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -130,10 +228,16 @@ def main():
     ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--clients', type=int, default=100)
     ap.add_argument('--params', type=int, default=25_000_000,
-                    help='parameters per GPU (configs[2]: 25M)')
-    ap.add_argument('--cpu-sample', type=int, default=5_000_000,
-                    help='columns of the workload timed on the CPU baseline')
+                    help='total model parameters (configs[2]: 25M), split '
+                         'over the GPUs')
+    ap.add_argument('--chunks', type=int, default=0,
+                    help='pipeline rounds of the assembly (0: 1 on one GPU, '
+                         '4 otherwise)')
+    ap.add_argument('--cpu-clients', type=int, default=20,
+                    help='clients (full width) timed on the CPU baseline')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-weak', action='store_true',
+                    help='skip the secondary weak-scaling phase (N > 1)')
     ap.add_argument('--e2e', action='store_true',
                     help='also time host dicts -> aggregate() -> host dicts')
     ap.add_argument('--layout', default='flat', choices=['flat', 'resnet50'])
@@ -142,73 +246,105 @@ def main():
     args = ap.parse_args()
 
     import torch
-    import torch.distributed as dist
     from federatedscope_amd import ops
     from federatedscope_amd.core.aggregators._engine import fedavg_weights
+    from federatedscope_amd.core.sharding import PipelinedAssembly
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world != args.gpus:
-        log('note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE' %
-            (args.gpus, world))
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
-    if world > 1:
-        dist.init_process_group('nccl', rank=rank, world_size=world,
-                                device_id=dev)
-
-    def barrier():
-        if world > 1:
-            dist.barrier(device_ids=[local])
-
+    D = Dist(args.gpus)
+    world, rank, dev = D.world, D.rank, D.dev
     n, P = args.clients, args.params
-    ld = ops.round_up(P, 64)
-    log('rank %d/%d on %s: %d clients x %d params (%.2f GB)' %
-        (rank, world, torch.cuda.get_device_name(dev), n, P, 4 * n * ld / 1e9))
-    slab = torch.empty((n, ld), dtype=torch.float32, device=dev)
-    ops.fill_uniform(slab, P, seed=2026, index_offset=rank * P)
-    out = torch.empty(P, dtype=torch.float32, device=dev)
-    rows = ops.RowTable.from_slab(slab, numel=P)
+    chunks = args.chunks or (1 if world == 1 else 4)
+    pa = PipelinedAssembly(P, chunks=chunks)
     sizes = sample_sizes(n)
     weights = fedavg_weights(sizes)
     w_dev = torch.tensor(weights, dtype=torch.float32, device=dev)
+    log('rank %d/%d on %s: %d clients x %d params, %d round(s) of %d-param '
+        'pieces (%.2f GB per rank)' %
+        (rank, world, torch.cuda.get_device_name(dev), n, P, chunks, pa.pc,
+         4.0 * n * pa.local_numel() / 1e9))
+
+    # this rank's pieces of every client: global coordinates [lo, hi) of
+    # the same counter-hash model at every N
+    pieces = []
+    for j, (lo, hi) in enumerate(pa.local_pieces()):
+        slab = torch.empty((n, pa.pc), dtype=torch.float32, device=dev)
+        if hi > lo:
+            ops.fill_uniform(slab, hi - lo, seed=SEED, index_offset=lo)
+        pieces.append((slab, ops.RowTable.from_slab(slab,
+                                                    numel=max(hi - lo, 1))))
+    out = torch.empty(pa.padded, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize()
 
+    # per-launch HIP events on the launch stream (the roofline's kernel time)
+    events = []
+    record = [False]
+
+    def compute(j, lo, hi, view):
+        if record[0]:
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            ops.weighted_sum(pieces[j][1], w_dev, view)
+            b.record(stream)
+            events.append((a, b, hi - lo))
+        else:
+            ops.weighted_sum(pieces[j][1], w_dev, view)
+
     def step():
-        ops.weighted_sum(rows, w_dev, out)
+        pa.run(compute, out=out)
+
+    def sharded_only():
+        for j, (lo, hi) in enumerate(pa.local_pieces()):
+            if hi > lo:
+                compute(j, lo, hi, out[lo:hi])
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        step()
-        ev[i][1].record(stream)
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    t_step = wall / args.steps
-    if world > 1:
-        tt = torch.tensor([t_step], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_step = float(tt.item())
-    algo_bytes = 4.0 * n * P + 4.0 * P + 4.0 * n  # read rows + write out + w
-    value = world * 4.0 * n * P / t_step / 1e9
-    achieved = algo_bytes / (kern_ms / 1e3) / 1e9
-    log('step %.3f ms  kernel %.3f ms  achieved %.0f GB/s' %
-        (t_step * 1e3, kern_ms, achieved))
+    record[0] = True
+    t_step = timed_steps(D, step, args.steps, 0)
+    record[0] = False
+    launches = [(a.elapsed_time(b), m) for a, b, m in events]
+    kern_ms = sum(t for t, _ in launches) / args.steps      # per rank
+    mean_launch_ms = sum(t for t, _ in launches) / len(launches)
+    mean_launch_p = sum(m for _, m in launches) / len(launches)
+    kern_ms = D.max(kern_ms)
+    t_sharded = timed_steps(D, sharded_only, args.steps, args.warmup) \
+        if world > 1 else t_step
+
+    # assembly check: columns of every rank's pieces (other ranks' too),
+    # regenerated here and reduced by the same kernel, must equal what the
+    # all-gather delivered, bit for bit
+    ok = True
+    probe = min(65536, pa.pc)
+    for j in range(chunks):
+        for r in range(world):
+            lo, hi = pa.piece(j, r)
+            for a in sorted({lo, max(lo, hi - probe)}):
+                b = min(a + probe, hi)
+                if b <= a:
+                    continue
+                tmp = torch.empty((n, ops.round_up(b - a, 64)),
+                                  dtype=torch.float32, device=dev)
+                ops.fill_uniform(tmp, b - a, seed=SEED, index_offset=a)
+                chk = torch.empty(ops.round_up(b - a, 4),
+                                  dtype=torch.float32, device=dev)
+                ops.weighted_sum(ops.RowTable.from_slab(tmp, numel=b - a),
+                                 w_dev, chk)
+                ok = ok and torch.equal(chk[:b - a], out[a:b])
+    ok = D.max(0.0 if ok else 1.0) == 0.0
+
+    algo_launch = 4.0 * n * mean_launch_p + 4.0 * mean_launch_p + 4.0 * n
+    achieved = algo_launch / (mean_launch_ms / 1e3) / 1e9
+    value = 4.0 * n * P / t_step / 1e9
+    log('step %.3f ms (kernels %.3f ms/rank, sharded-output step %.3f ms), '
+        'launch %.3f ms -> %.0f GB/s, assembled result bit-exact: %s' %
+        (t_step * 1e3, kern_ms, t_sharded * 1e3, mean_launch_ms, achieved,
+         ok))
 
     traffic = None
-    if os.path.exists(args.traffic):
+    if world == 1 and os.path.exists(args.traffic):
         try:
             with open(args.traffic) as f:
                 tr = json.load(f)
@@ -219,35 +355,45 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        ps = min(args.cpu_sample, P)
-        log('cpu baseline: numpy oracle, %d clients x %d params' % (n, ps))
-        t_cpu, exact = cpu_baseline_leg(slab, n, ps, weights, out)
-        import numpy
-        np_version = numpy.__version__
-        cpu_model = 'unknown CPU'
-        try:
-            with open('/proc/cpuinfo') as f:
-                for line in f:
-                    if line.startswith('model name'):
-                        cpu_model = line.split(':', 1)[1].strip()
-                        break
-        except OSError:
-            pass
+        k = min(args.cpu_clients, n)
+        log('cpu baseline: torch CPU op-for-op FedAvg, %d clients x %d '
+            'params' % (k, P))
+        res, exact = cpu_baseline_leg(pieces[0][0], weights, P, k, dev)
+        cores = host_cores()
         cpu = {
-            'value': round(4.0 * n * ps / t_cpu / 1e9, 3),
+            'value': round(4.0 * k * P / res[1] / 1e9, 3),
             'unit': 'GB/s',
             'cores': 1,
             'kind': 'port',
-            'sample': ('oracle.para_weighted_avg (numpy restatement of '
-                       'clients_avg_aggregator.py:60-100, 1 thread like '
-                       'fed_runner.py:299) on the first %d params of the '
-                       'same %d synthetic clients; best of 3; GPU output '
-                       'bit-exact on this sample: %s; host %s, numpy %s, '
-                       'torch %s' % (ps, n, exact, cpu_model,
-                                     np_version, torch.__version__)),
+            'all_cores': {'cores': cores,
+                          'value': round(4.0 * k * P / res[cores] / 1e9, 3)},
+            'sample': ('oracle/torch_cpu.py: the reference loop of '
+                       'clients_avg_aggregator.py:60-100 in torch %s CPU '
+                       'ops (tmp = x*w; acc += tmp per client), on the first '
+                       '%d of the same %d synthetic clients at full width '
+                       '(%d params); torch.set_num_threads(1) as '
+                       'fed_runner.py:299, and %d threads; best of 3; GPU '
+                       'kernel on the same clients bit-exact: %s; host %s' %
+                       (torch.__version__, k, n, P, cores, exact,
+                        cpu_model())),
         }
-        log('cpu baseline %.3f s -> %.3f GB/s, bit-exact=%s' %
-            (t_cpu, cpu['value'], exact))
+
+    weak = None
+    if world > 1 and not args.no_weak:
+        del pieces
+        torch.cuda.empty_cache()
+        ld = ops.round_up(P, 64)
+        slab = torch.empty((n, ld), dtype=torch.float32, device=dev)
+        ops.fill_uniform(slab, P, seed=SEED, index_offset=rank * P)
+        rows = ops.RowTable.from_slab(slab, numel=P)
+        wout = torch.empty(ld, dtype=torch.float32, device=dev)
+        t_weak = timed_steps(D, lambda: ops.weighted_sum(rows, w_dev, wout),
+                             args.steps, args.warmup)
+        weak = {'value': round(world * 4.0 * n * P / t_weak / 1e9, 2),
+                'ms_per_step': round(t_weak * 1e3, 4),
+                'what': 'every rank its own %d x %d (no collective)' %
+                        (n, P)}
+        del slab, rows
 
     if rank == 0:
         rec = {
@@ -259,18 +405,21 @@ def main():
             'warmup': args.warmup,
             'ms_per_step': round(t_step * 1e3, 4),
             'higher_is_better': True,
-            'scaling': 'weak',
+            'scaling': 'strong',
             'vs_baseline': None,
             'dtype': 'f32',
             'data': 'synthetic: counter-hash uniform[-1,1) generated on '
                     'device; sample sizes 1+hash(i) mod 1000',
             'config': {
                 'workload': 'configs[2]: FedAvg weighted sum, %d clients x '
-                            '%d fp32 params per GPU (param-range shard per '
-                            'rank, no collective)' % (n, P),
+                            '%d fp32 params in total, param-range sharded '
+                            'over %d GPU(s), full result assembled on every '
+                            'GPU' % (n, P, world),
                 'clients': n,
-                'params_per_gpu': P,
-                'parallelism': 'param-range x%d' % world,
+                'params': P,
+                'parallelism': ('param-range x%d, %d pipelined all-gather '
+                                'rounds' % (world, chunks)) if world > 1
+                else 'single GPU',
             },
             'roofline': {
                 'bound': 'hbm',
@@ -281,14 +430,20 @@ def main():
                 'traffic': traffic,
             },
             'cpu_baseline': cpu,
+            'per_rank_kernel_ms': round(kern_ms, 4),
+            'exposed_assembly_ms': round(max(t_step * 1e3 - kern_ms, 0.0), 4),
+            'sharded_output': {
+                'ms_per_step': round(t_sharded * 1e3, 4),
+                'value': round(4.0 * n * P / t_sharded / 1e9, 2)},
+            'weak_scaling': weak,
+            'assembled_bit_exact': ok,
         }
         print(json.dumps(rec), flush=True)
     if args.e2e and world == 1:
-        del slab, rows
+        del pieces
         torch.cuda.empty_cache()
         e2e_leg(args, dev, weights, sizes)
-    if world > 1:
-        dist.destroy_process_group()
+    D.close()
 
 
 if __name__ == '__main__':

@@ -198,6 +198,12 @@ class DeviceEngine:
         arrival) → StagedSet."""
         from ..workers.ingress import StagedUpdate
         dicts = [m for _, m in models]
+        # every staged slot must have landed before anything reads it, on
+        # every path below (a list can mix staged uploads with stale ones
+        # that were buffered as plain dicts)
+        for ing in {id(d.ingress): d.ingress for d in dicts
+                    if isinstance(d, StagedUpdate)}.values():
+            ing.sync()
         if all(isinstance(d, StagedUpdate) for d in dicts):
             ing = dicts[0].ingress
             if all(d.ingress is ing for d in dicts) and \
@@ -206,7 +212,6 @@ class DeviceEngine:
                     for i, d in enumerate(dicts):
                         if len(d) != len(ing.layout.keys):
                             raise KeyError('client %d lacks keys' % i)
-                ing.sync()
                 return StagedSet(ing.layout, ing.stack,
                                  [d.slot for d in dicts])
         layout = self._layout(dicts[0], as_float=as_float)

@@ -81,12 +81,25 @@ class DeviceIngress:
         self.next_slot = 0
         self._stager = None
 
-    def receive(self, sample_size, model_para):
-        """Stage one upload; returns (sample_size, StagedUpdate)."""
+    def _slot(self, slot=None):
+        """The stack row for the next upload: ``slot`` (a sender's earlier
+        upload of this round, overwritten in place) or a fresh one."""
+        if slot is not None:
+            return slot
         if self.next_slot >= self.stack.capacity:
+            # copies into the old slab may still be in flight on the side
+            # stream: order them before the growth copy (and the old slab's
+            # release) on the current stream
+            self.sync()
             self.stack.ensure(self.stack.capacity * 2)
         slot = self.next_slot
         self.next_slot += 1
+        return slot
+
+    def receive(self, sample_size, model_para, slot=None):
+        """Stage one upload; returns (sample_size, StagedUpdate).  ``slot``
+        reuses the row of the same sender's earlier upload this round."""
+        slot = self._slot(slot)
         missing = [k for k in self.layout.keys if k not in model_para]
         if missing:
             raise KeyError('staged upload lacks keys %s' % missing)
@@ -101,7 +114,7 @@ class DeviceIngress:
             self.layout.pack_device(src, self.stack.slab[slot])
         return sample_size, StagedUpdate(self, slot, model_para.keys())
 
-    def receive_quantized(self, sample_size, wire):
+    def receive_quantized(self, sample_size, wire, slot=None):
         """Stage one quantised upload (the wire dict of
         symmetric_uniform_quantization): the codes cross PCIe as int8/int16
         and are dequantised into the slot by fsagg_wire_unpack_f32 — the
@@ -110,10 +123,7 @@ class DeviceIngress:
         if self.plan is None:
             raise RuntimeError('ingress was not built for quantised uploads')
         from ..compression.wire import WireStager
-        if self.next_slot >= self.stack.capacity:
-            self.stack.ensure(self.stack.capacity * 2)
-        slot = self.next_slot
-        self.next_slot += 1
+        slot = self._slot(slot)
         if self._stager is None:
             self._stager = WireStager(self.plan, self.device)
         self._stager.put(wire, self.stack.slab[slot])

@@ -58,11 +58,17 @@ class AggregationServer:
                                                  self.sample_client_num,
                                                  device=self.device,
                                                  quantized=staged_quant)
+                # a sender that uploads twice in one round overwrites its
+                # buffer entry (server.py:966-970): reuse its stack row
+                prev = self.msg_buffer['train'].get(round, {}).get(sender)
+                slot = prev[1].slot if prev and getattr(
+                    prev[1], 'ingress', None) is self.ingress else None
                 if staged_quant:
                     # dequantised on the device as the upload is staged
-                    content = self.ingress.receive_quantized(*content)
+                    content = self.ingress.receive_quantized(*content,
+                                                             slot=slot)
                 else:
-                    content = self.ingress.receive(*content)
+                    content = self.ingress.receive(*content, slot=slot)
             self.msg_buffer['train'].setdefault(round, dict())[sender] = \
                 content
         elif round >= self.state - self.staleness_toleration:

@@ -119,8 +119,7 @@ class BucketLayout:
             return out_row
         st = HostStager(out_row.device, nbuf=1)
         st.put(self, model, out_row)
-        st.finish()
-        st.events[0].synchronize()
+        st.finish()      # the consumer stream waits for the copy
         return out_row
 
     def unpack(self, flat, keys=None):
@@ -132,10 +131,18 @@ class BucketLayout:
         return out
 
 
+# Pinned staging buffers are shared by every HostStager of the process, so
+# the event of the last DMA that read each slot lives next to the slot: a
+# stager must not overwrite a buffer an earlier stager's copy is still
+# reading (e.g. the init model packed right after the client uploads).
 _PINNED = {}
+_PINNED_EV = {}
 
 
 def _pinned(numel, slot=0):
+    ev = _PINNED_EV.pop(slot, None)
+    if ev is not None:
+        ev.synchronize()              # the DMA that last read this slot
     b = _PINNED.get(slot)
     if b is None or b.numel() < numel:
         b = torch.empty(numel, dtype=torch.float32, pin_memory=True)
@@ -157,22 +164,20 @@ class HostStager:
         # the consumer stream (the stack is reused across rounds)
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         self.nbuf = nbuf
-        self.events = [None] * nbuf
+        self.last = None
         self.i = 0
 
     def put(self, layout, model, dst_row):
         slot = self.i % self.nbuf
         self.i += 1
-        ev = self.events[slot]
-        if ev is not None:
-            ev.synchronize()          # the DMA that last read this buffer
         host = _pinned(layout.numel, slot)
         layout.pack_host(model, host)
         with torch.cuda.stream(self.stream):
             dst_row.copy_(host, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self.stream)
-        self.events[slot] = ev
+        _PINNED_EV[slot] = ev
+        self.last = ev
 
     def finish(self):
         torch.cuda.current_stream(self.device).wait_stream(self.stream)

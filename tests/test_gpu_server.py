@@ -153,3 +153,82 @@ def test_stack_gather_matches_per_key_copies():
             o, k = lay.offsets[key], lay.numels[key]
             assert torch.equal(fast.slab[i, o:o + k],
                                models[i][key].reshape(-1))
+
+
+def test_large_host_dicts_median_pinned_reuse():
+    """~100 MB of host dicts through MedianAggregator: the init
+    model is packed into the shared pinned buffer right after the clients'
+    DMAs were queued from it, so the stager must wait for them.  Against
+    the same clients handed over as device dicts (no pinned staging)."""
+    from federatedscope_amd.core.aggregators import MedianAggregator
+    g = torch.Generator().manual_seed(12)
+    n, shapes = 9, [('w', (2_700_000, )), ('b', (17, ))]
+    clients = [(i + 1, OrderedDict((k, torch.randn(s, generator=g))
+                                   for k, s in shapes)) for i in range(n)]
+    init = OrderedDict((k, torch.randn(s, generator=g)) for k, s in shapes)
+
+    class M(torch.nn.Module):
+        def state_dict(self, *a, **kw):
+            return init
+
+    host = MedianAggregator(model=M(), config=_cfg(f=1, client_num=50))
+    got = host.aggregate({'client_feedback': clients})
+    dev = [(s, OrderedDict((k, v.cuda()) for k, v in d.items()))
+           for s, d in clients]
+    want = MedianAggregator(model=M(), config=_cfg(f=1, client_num=50)
+                            ).aggregate({'client_feedback': dev})
+    for k in want:
+        assert torch.equal(got[k], want[k].cpu()), k
+    ref = O.median_aggregate([(s, OrderedDict((k, v.numpy()) for k, v in
+                                              d.items())) for s, d in clients],
+                             OrderedDict((k, v.numpy())
+                                         for k, v in init.items()))
+    for k in ref:
+        assert got[k].numpy().tobytes() == ref[k].tobytes(), k
+
+
+def test_staged_with_stale_host_dicts_and_resend():
+    """stage_on_arrival with staleness_toleration > 0: the
+    round's list mixes staged slots with stale uploads buffered as host
+    dicts; a sender that uploads twice in one round keeps its row.  The
+    result equals the unstaged server's bit for bit."""
+    from federatedscope_amd.core.aggregators import AsynClientsAvgAggregator
+    from federatedscope_amd.core.workers.server import AggregationServer
+    g = torch.Generator().manual_seed(4)
+    shapes = [('w', (300_001, )), ('b', (5, ))]
+
+    def upload():
+        return (int(torch.randint(1, 50, (1, ), generator=g)),
+                OrderedDict((k, torch.randn(s, generator=g))
+                            for k, s in shapes))
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.w = torch.nn.Parameter(torch.zeros(300_001))
+            self.b = torch.nn.Parameter(torch.zeros(5))
+
+    script = []
+    for r in range(3):
+        if r > 0:
+            script.append((r - 1, 9, upload()))      # stale, tolerated
+        script.append((r, 1, upload()))
+        script.append((r, 1, upload()))              # resend: overwrites
+        for c in (2, 3, 4):
+            script.append((r, c, upload()))
+    results = []
+    for stage in (True, False):
+        model = M()
+        srv = AggregationServer(model, AsynClientsAvgAggregator(
+            model=model, config=_cfg()), sample_client_num=4,
+            staleness_toleration=2, stage_on_arrival=stage)
+        for r, c, (s, d) in script:
+            srv.callback_funcs_model_para(
+                r, c, (s, OrderedDict((k, v.clone()) for k, v in d.items())))
+        assert srv.state == 3
+        results.append([OrderedDict((k, v.detach().cpu().clone())
+                                    for k, v in h.items())
+                        for h in srv.history])
+    for a, b in zip(*results):
+        for k in a:
+            assert torch.equal(a[k], b[k]), k

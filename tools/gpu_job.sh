@@ -21,8 +21,8 @@ for step in "$@"; do
   i=$((i+1))
   case $step in
     smoke) run smoke 240 python __graft_entry__.py smoke ;;
-    pytest) run pytest_gpu 600 python -m pytest tests -m gpu -x -q ;;
-    pytestall) run pytest_gpu 600 python -m pytest tests -m gpu -q ;;
+    pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    pytestall) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
     bench) run bench 420 python bench.py ;;
     *) echo "step$i: $step" >> gpurun_out/steps.log; run "step$i" 600 bash -c "$step" ;;
   esac
