@@ -58,20 +58,21 @@ def _first_device(model):
 
 
 class StagedSet:
-    """The client list of one aggregate() call, resident in a ClientStack:
-    client i lives in stack row ``slots[i]``."""
+    """The client list of one aggregate() call as a row set: client i's
+    key s is ``rs`` entry (i, s) — a slot of a ClientStack (staged uploads)
+    or the client's own device tensor (read in place)."""
 
-    def __init__(self, layout, stack, slots):
+    def __init__(self, layout, rs, stack=None, slots=None):
         self.layout = layout
+        self.rs = rs
+        self.n = rs.n
         self.stack = stack
-        self.slots = list(slots)
-        self.n = len(self.slots)
+        self.slots = slots
 
-    def rows(self, sel=None, key=None):
-        """RowTable over clients ``sel`` (indices into the client list, in
-        reduction order; default all), optionally one key's sub-range."""
-        idx = self.slots if sel is None else [self.slots[i] for i in sel]
-        return self.stack.rows(idx, key=key)
+    def rows(self, sel=None):
+        """The clients ``sel`` (indices into the client list, in reduction
+        order; default all) as a RowSet."""
+        return self.rs if sel is None else self.rs.subset(sel)
 
 
 class DeviceEngine:
@@ -81,6 +82,7 @@ class DeviceEngine:
         self._dev_req = device
         self._dev = None
         self._layouts = {}
+        self._fast_layouts = {}
         self._stacks = {}
 
     @property
@@ -130,6 +132,41 @@ class DeviceEngine:
         layout.pack_device(src, flat)
         return flat
 
+    def _key_table(self, layout, dicts):
+        """(ptrs [n][nseg], aligned16) when every present layout key of
+        every dict is a contiguous fp32 tensor of the layout's shape on the
+        compute device (the C++ walk of csrc/host/keytable.cpp), else
+        None."""
+        import numpy as np
+        from ... import _lib
+        dev = self.compute_device
+        kl = layout.__dict__.get('_key_list')
+        if kl is None:
+            kl = layout.__dict__['_key_list'] = (
+                list(layout.keys), [layout.shapes[k] for k in layout.keys])
+        if not kl[0] or not all(isinstance(d, dict) for d in dicts):
+            return None
+        res = _lib.host().key_table(dicts, kl[0], kl[1], dev.index)
+        if res is None:
+            return None
+        raw, _, aligned = res
+        return (np.frombuffer(raw, dtype=np.int64).reshape(len(dicts),
+                                                           len(kl[0])),
+                aligned)
+
+    def _base(self, layout, model, as_float=False):
+        """The server model as the kernels' ``base`` operand: its own device
+        tensors when they are fp32 on the compute device (no copy), else a
+        packed device bucket."""
+        if isinstance(model, dict):
+            kt = self._key_table(layout, [model])
+            if kt is not None and kt[1] and (kt[0] != 0).all():
+                return ops.BaseRows.from_pointers(layout, kt[0][0],
+                                                  self.compute_device,
+                                                  keepalive=(model, ))
+        return ops.BaseRows.from_bucket(self._bucket(layout, model,
+                                                     as_float=as_float))
+
     # -- result emission -----------------------------------------------------
     @staticmethod
     def _emit(layout, flat, keys, out_device, extra=None):
@@ -152,7 +189,10 @@ class DeviceEngine:
 
         Returns (layout, flat fp32 bucket on the GPU, {non-fp32 key: tensor},
         key order).  ``models`` is the client_feedback list of
-        (sample_size, dict); ``weights`` the per-client Python doubles."""
+        (sample_size, dict); ``weights`` the per-client Python doubles.
+        Keys some clients lack are reduced over the clients that have them,
+        weights NOT renormalised (clients_avg_aggregator.py:74-75): their
+        row-set entries are NULL and the kernel skips them."""
         dicts = [m for _, m in models]
         template = dicts[0]
         n = len(dicts)
@@ -163,22 +203,9 @@ class DeviceEngine:
                           device=self.compute_device)
         base = None
         if base_model is not None:
-            base = self._bucket(layout, base_model, as_float=as_float)
-        ops.weighted_sum(st.rows(), weights, out, prescale=prescale,
-                         base=base)
-        # keys some clients lack: reduce over the clients that have them,
-        # weights NOT renormalised (clients_avg_aggregator.py:74-75)
-        for k in layout.keys:
-            have = [i for i in range(n) if k in dicts[i]]
-            if len(have) == n:
-                continue
-            o, m = layout.offsets[k], layout.numels[k]
-            ops.weighted_sum(
-                st.rows(have, key=k), [weights[i] for i in have],
-                out[o:o + m],
-                prescale=None if prescale is None else
-                [prescale[i] for i in have],
-                base=None if base is None else base[o:o + m])
+            base = self._base(layout, base_model, as_float=as_float)
+        ops.weighted_sum_rows(st.rows(), weights, out, prescale=prescale,
+                              base=base)
         extra = OrderedDict()
         for k, dt in layout.other.items():
             have = [i for i in range(n) if k in dicts[i]]
@@ -194,8 +221,9 @@ class DeviceEngine:
         return layout, out, extra, list(template.keys())
 
     def _staged(self, models, as_float=False, require_all=False):
-        """Stage the client list (or reuse what DeviceIngress staged on
-        arrival) → StagedSet."""
+        """The client list as a row set: slots DeviceIngress staged on
+        arrival, the clients' own device tensors read in place, or (host
+        dicts, other devices, other dtypes) rows of a device stack."""
         from ..workers.ingress import StagedUpdate
         dicts = [m for _, m in models]
         # every staged slot must have landed before anything reads it, on
@@ -212,16 +240,39 @@ class DeviceEngine:
                     for i, d in enumerate(dicts):
                         if len(d) != len(ing.layout.keys):
                             raise KeyError('client %d lacks keys' % i)
-                return StagedSet(ing.layout, ing.stack,
-                                 [d.slot for d in dicts])
-        layout = self._layout(dicts[0], as_float=as_float)
+                slots = [d.slot for d in dicts]
+                return StagedSet(ing.layout, ops.RowSet.from_stack(
+                    ing.stack, slots), ing.stack, slots)
+        # device-resident fp32 dicts: read in place through a key table
+        d0 = dicts[0]
+        fk = (tuple(d0.keys()), bool(as_float))
+        layout = self._fast_layouts.get(fk)
+        if layout is None:
+            layout = self._layout(d0, as_float=as_float)
+            self._fast_layouts[fk] = layout
+        if not layout.other:
+            kt = self._key_table(layout, dicts)
+            if kt is not None and kt[1]:
+                ptrs = kt[0]
+                if require_all and not (ptrs != 0).all():
+                    i, s = [int(x[0]) for x in (ptrs == 0).nonzero()]
+                    raise KeyError('client %d lacks key %r' %
+                                   (i, layout.keys[s]))
+                return StagedSet(layout, ops.RowSet.from_pointers(
+                    layout, ptrs, self.compute_device, keepalive=(dicts, )))
+        # staged through a device stack
+        layout = self._layout(d0, as_float=as_float)
+        present = [[k in d for k in layout.keys] for d in dicts]
         if require_all:
-            for i, d in enumerate(dicts):
-                for k in layout.keys:
-                    if k not in d:
+            for i, row in enumerate(present):
+                for k, ok in zip(layout.keys, row):
+                    if not ok:
                         raise KeyError('client %d lacks key %r' % (i, k))
         stack = self._stack(layout, dicts, as_float=as_float)
-        return StagedSet(layout, stack, range(len(dicts)))
+        slots = list(range(len(dicts)))
+        return StagedSet(layout, ops.RowSet.from_stack(stack, slots,
+                                                       present=present),
+                         stack, slots)
 
     def _stage_all(self, models, as_float=True):
         """Pack every client (robust rules need all keys in all clients)."""

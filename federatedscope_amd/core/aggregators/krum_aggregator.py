@@ -1,7 +1,8 @@
 """Krum / multi-Krum (federatedscope/core/aggregators/krum_aggregator.py:6-90).
 
-Device path: all client updates are staged as fp32 rows; fsagg_pairdist_f32
-computes the per-key L2 distances for every pair and the n×n matrix (sum over
+Device path: the client updates are read where they lie (a row set: the
+clients' own device tensors, or their staged stack rows);
+fsagg_pairdist_rows_segsq_f32 + fsagg_pairdist_finish_f64 compute the per-key L2 distances for every pair and the n×n matrix (sum over
 keys, +inf diagonal) in one pass over the stack; the n×n matrix (≤ 200² floats)
 comes back to the host where the score/sort/select logic runs with the same
 torch CPU ops as the reference (:75-87); the selected clients are then
@@ -39,7 +40,7 @@ class KrumAggregator(ClientsAvgAggregator):
     def distance_matrix(self, models):
         """D (host fp32 [n, n]) as _calculate_score fills it (:58-73)."""
         st = self._stage_all(models)
-        return ops.pairdist(st.rows(), st.layout.segments()).cpu(), st
+        return ops.pairdist_rows(st.rows()).cpu(), st
 
     def _calculate_score(self, models):
         D, _ = self.distance_matrix([(0, m) for m in models])
@@ -54,8 +55,8 @@ class KrumAggregator(ClientsAvgAggregator):
         self.last_selection = sel
         sizes = [models[i][0] for i in sel]
         weights = fedavg_weights(sizes, self.cfg.federate.ignore_weight)
-        base = self._bucket(layout, self.model.state_dict(), as_float=True)
+        base = self._base(layout, self.model.state_dict(), as_float=True)
         out = torch.empty(layout.numel, dtype=torch.float32,
                           device=self.compute_device)
-        ops.weighted_sum(st.rows(sel), weights, out, base=base)
+        ops.weighted_sum_rows(st.rows(sel), weights, out, base=base)
         return layout, out, list(models[0][1].keys())

@@ -1,5 +1,5 @@
 """Coordinate-wise median (federatedscope/core/aggregators/
-median_aggregator.py:10-52) on the GPU: fsagg_coord_median_f32 computes
+median_aggregator.py:10-52) on the GPU: fsagg_coord_median_rows_f32 computes
 (median(T) - median(-T))/2 per coordinate (bit-exact) and adds the server's
 init model in the same kernel."""
 import torch
@@ -21,8 +21,8 @@ class MedianAggregator(ClientsAvgAggregator):
         out_dev = _first_device(models[0][1])
         st = self._stage_all(models)
         layout = st.layout
-        base = self._bucket(layout, self.model.state_dict(), as_float=True)
+        base = self._base(layout, self.model.state_dict(), as_float=True)
         out = torch.empty(layout.numel, dtype=torch.float32,
                           device=self.compute_device)
-        ops.coord_median(st.rows(), out, base=base)
+        ops.coord_median_rows(st.rows(), out, base=base)
         return self._emit(layout, out, list(models[0][1].keys()), out_dev)

@@ -1,7 +1,7 @@
 """Coordinate-wise trimmed mean (federatedscope/core/aggregators/
 trimmedmean_aggregator.py:10-57) on the GPU: drop the k = int(n·ratio)
 largest and smallest of each coordinate, average the rest, add init — one
-fsagg_trimmed_mean_f32 launch over the client stack."""
+fsagg_trimmed_mean_rows_f32 launch over the clients' rows."""
 import torch
 
 from ... import ops
@@ -26,8 +26,8 @@ class TrimmedmeanAggregator(ClientsAvgAggregator):
         layout = st.layout
         n = len(models)
         k = int(n * self.excluded_ratio)
-        base = self._bucket(layout, self.model.state_dict(), as_float=True)
+        base = self._base(layout, self.model.state_dict(), as_float=True)
         out = torch.empty(layout.numel, dtype=torch.float32,
                           device=self.compute_device)
-        ops.trimmed_mean(st.rows(), k, out, base=base)
+        ops.trimmed_mean_rows(st.rows(), k, out, base=base)
         return self._emit(layout, out, list(models[0][1].keys()), out_dev)

@@ -1,0 +1,106 @@
+// _fsagg_host: the host half of the row-set boundary (include/fsagg.h
+// fsagg_rows), as a CPython extension.
+//
+// The reference's aggregators walk every client's state_dict key by key in
+// Python (clients_avg_aggregator.py:70-91: `for key in avg_model: for i in
+// range(len(models)): ... local_model[key]`).  When the uploads are already
+// device tensors, the device engine needs exactly one thing from that walk:
+// the n x nkeys table of data pointers (and the proof that every tensor is
+// a contiguous fp32 tensor of the layout's shape on the right GPU).  Doing
+// the walk in Python costs ~1 us per tensor (five attribute reads each);
+// here it is one dict lookup and a few inline TensorImpl reads per tensor.
+//
+// key_table(dicts, keys, shapes, device_index)
+//   dicts  list of dict (client state_dicts; OrderedDict is a dict)
+//   keys   list of str (the layout's fp32 keys, in bucket order)
+//   shapes list of tuple[int] (each key's shape, as client 0 holds it)
+// returns (bytes ptrs, int missing, bool aligned16) — ptrs is n*len(keys)
+// native int64 data pointers, 0 where a client lacks the key — or None when
+// any present value is not a contiguous float32 tensor of that shape on
+// cuda:device_index, or an element of dicts is not a dict.  None is not an
+// error: the caller then stages the dicts instead.
+#include <Python.h>
+#include <torch/csrc/autograd/python_variable.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace {
+
+PyObject *key_table(PyObject *, PyObject *args) {
+  PyObject *dicts, *keys, *shapes;
+  int device_index;
+  if (!PyArg_ParseTuple(args, "O!O!O!i", &PyList_Type, &dicts, &PyList_Type,
+                        &keys, &PyList_Type, &shapes, &device_index))
+    return nullptr;
+  const Py_ssize_t n = PyList_GET_SIZE(dicts);
+  const Py_ssize_t nk = PyList_GET_SIZE(keys);
+  if (PyList_GET_SIZE(shapes) != nk) {
+    PyErr_SetString(PyExc_ValueError, "keys and shapes differ in length");
+    return nullptr;
+  }
+  std::vector<std::vector<int64_t>> shp(nk);
+  for (Py_ssize_t s = 0; s < nk; ++s) {
+    PyObject *t = PyList_GET_ITEM(shapes, s);
+    PyObject *seq = PySequence_Fast(t, "shape must be a sequence");
+    if (!seq) return nullptr;
+    const Py_ssize_t d = PySequence_Fast_GET_SIZE(seq);
+    for (Py_ssize_t j = 0; j < d; ++j) {
+      const long long v = PyLong_AsLongLong(PySequence_Fast_GET_ITEM(seq, j));
+      if (v == -1 && PyErr_Occurred()) {
+        Py_DECREF(seq);
+        return nullptr;
+      }
+      shp[s].push_back(v);
+    }
+    Py_DECREF(seq);
+  }
+  std::string buf(size_t(n) * size_t(nk) * sizeof(int64_t), '\0');
+  auto *out = reinterpret_cast<int64_t *>(&buf[0]);
+  Py_ssize_t missing = 0;
+  bool aligned = true;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject *d = PyList_GET_ITEM(dicts, i);
+    if (!PyDict_Check(d)) Py_RETURN_NONE;
+    for (Py_ssize_t s = 0; s < nk; ++s) {
+      PyObject *v = PyDict_GetItemWithError(d, PyList_GET_ITEM(keys, s));
+      if (!v) {
+        if (PyErr_Occurred()) return nullptr;
+        out[i * nk + s] = 0;
+        ++missing;
+        continue;
+      }
+      if (!THPVariable_Check(v)) Py_RETURN_NONE;
+      const at::Tensor &t = THPVariable_Unpack(v);
+      if (t.scalar_type() != at::kFloat || !t.is_cuda() ||
+          t.get_device() != device_index || !t.is_contiguous())
+        Py_RETURN_NONE;
+      const auto sz = t.sizes();
+      if (sz.size() != shp[s].size()) Py_RETURN_NONE;
+      for (size_t j = 0; j < sz.size(); ++j)
+        if (sz[j] != shp[s][j]) Py_RETURN_NONE;
+      const auto p = reinterpret_cast<uintptr_t>(t.data_ptr());
+      if (p == 0 && t.numel() > 0) Py_RETURN_NONE;
+      aligned = aligned && (p & 15u) == 0;
+      out[i * nk + s] = int64_t(p);
+    }
+  }
+  PyObject *bytes = PyBytes_FromStringAndSize(buf.data(), Py_ssize_t(buf.size()));
+  if (!bytes) return nullptr;
+  return Py_BuildValue("(NnO)", bytes, missing, aligned ? Py_True : Py_False);
+}
+
+PyMethodDef kMethods[] = {
+    {"key_table", key_table, METH_VARARGS,
+     "key_table(dicts, keys, shapes, device_index) -> (bytes, missing, "
+     "aligned16) or None"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_fsagg_host",
+                       "Host half of libfsagg's row-set boundary.", -1,
+                       kMethods};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__fsagg_host(void) { return PyModule_Create(&kModule); }

@@ -92,6 +92,52 @@ __device__ __forceinline__ float nonfinite_sum(const uint32_t (&k)[N], int n,
 
 enum Mode { kMedian = 0, kTrimmed = 1 };
 
+// Where a block's coordinates and clients live.  Flat form (chunks ==
+// nullptr): block b covers [b·kBlock, …) of [0, numel) and client j's row
+// is tab[j]; row-set form (include/fsagg.h fsagg_rows): block b is chunk b
+// (one key segment, <= kBlock coordinates) and client j's row of segment
+// seg is tab[j·si + seg·ss] (a virtual base: coordinate p is row[p]).
+struct RowSrc {
+  const float *const *tab;
+  int64_t si, ss;
+  const fsagg_chunk *chunks;
+  int64_t numel;
+  const float *base;          // flat base (tab form), or
+  const float *const *btab;   // per-segment virtual bases, stride bss
+  int64_t bss;
+};
+
+struct BlockRows {
+  const float *const *rows;  // client j: rows[j * si]
+  int64_t si;
+  int64_t lo;                // first coordinate
+  int len;                   // live lanes
+  const float *base;
+};
+
+__device__ __forceinline__ BlockRows block_rows(const RowSrc &rs, int b) {
+  BlockRows br;
+  int seg = 0;
+  if (rs.chunks) {
+    br.lo = rs.chunks[b].lo;
+    br.len = rs.chunks[b].len;
+    seg = rs.chunks[b].seg;
+  } else {
+    br.lo = int64_t(b) * kBlock;
+    const int64_t r = rs.numel - br.lo;
+    br.len = r < kBlock ? int(r) : kBlock;
+  }
+  br.rows = rs.tab + int64_t(seg) * rs.ss;
+  br.si = rs.si;
+  br.base = rs.btab ? rs.btab[int64_t(seg) * rs.bss] : rs.base;
+  return br;
+}
+
+inline unsigned rows_grid(const RowSrc &rs, int nchunk) {
+  return rs.chunks ? unsigned(nchunk)
+                   : unsigned((rs.numel + kBlock - 1) / kBlock);
+}
+
 
 // The select kernel for register-array size N serves N - kSelStep < n <= N.
 constexpr int kSelStep = 8;
@@ -99,9 +145,8 @@ constexpr int kSelStep = 8;
 // Launch the range-adaptive select kernel for 64 < n <= N (orderstat_select.hip,
 // one translation unit per N).
 template <int N, int MODE>
-void launch_select(const float *const *rows, int n, int64_t numel, int kk,
-                   float divisor, const float *base, float *out,
-                   hipStream_t s);
+void launch_select(const RowSrc &rs, unsigned grid, int n, int kk,
+                   float divisor, float *out, hipStream_t s);
 
 }  // namespace os
 }  // namespace fsagg

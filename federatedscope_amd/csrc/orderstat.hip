@@ -27,12 +27,14 @@ namespace {
 // — a per-row `if (j < n)` splits the loop into N basic blocks and every
 // load then waits out its own HBM round trip.
 template <int N>
-__device__ __forceinline__ void load_column(const float *const *rows, int n,
-                                            int64_t p, uint32_t (&k)[N],
-                                            bool &nan, bool &nonfinite) {
+__device__ __forceinline__ void load_column(const float *const *rows,
+                                            int64_t si, int n, int64_t p,
+                                            uint32_t (&k)[N], bool &nan,
+                                            bool &nonfinite) {
   float x[N];
 #pragma unroll
-  for (int j = 0; j < N; ++j) x[j] = gld_nt(rows[j < n ? j : n - 1] + p);
+  for (int j = 0; j < N; ++j)
+    x[j] = gld_nt(rows[(j < n ? j : n - 1) * si] + p);
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     const bool real = j < n;
@@ -44,13 +46,14 @@ __device__ __forceinline__ void load_column(const float *const *rows, int n,
 
 template <int N, int MODE>
 __global__ __launch_bounds__(kBlock) void orderstat_reg_kernel(
-    const float *const *__restrict__ rows, int n, int64_t numel, int kk,
-    float divisor, const float *__restrict__ base, float *__restrict__ out) {
-  const int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (p >= numel) return;
+    RowSrc rs, int n, int kk, float divisor, float *__restrict__ out) {
+  const BlockRows br = block_rows(rs, blockIdx.x);
+  if (int(threadIdx.x) >= br.len) return;
+  const int64_t p = br.lo + threadIdx.x;
+  const float *__restrict__ base = br.base;
   uint32_t k[N];
   bool nan = false, nonfinite = false;
-  load_column<N>(rows, n, p, k, nan, nonfinite);
+  load_column<N>(br.rows, br.si, n, p, k, nan, nonfinite);
   bitonic_sort<N>(k);
   using Seq = std::make_integer_sequence<int, N>;
   float r;
@@ -69,19 +72,20 @@ __global__ __launch_bounds__(kBlock) void orderstat_reg_kernel(
     }
     r = __fdiv_rn(s, divisor);
   }
-  if (base) r = add_rn(base[p], r);
+  if (base) r = add_rn(gld(base + p), r);
   out[p] = r;
 }
 
 // ---- generic n: radix select (binary search on the key bits) -----------
 __device__ __forceinline__ uint32_t select_rank(const float *const *rows,
-                                                int n, int64_t p, int rank) {
+                                                int64_t si, int n, int64_t p,
+                                                int rank) {
   // smallest key v such that #(key <= v) > rank
   uint32_t prefix = 0;
   for (int bit = 31; bit >= 0; --bit) {
     const uint32_t cand = prefix | ((1u << bit) - 1u);  // all lower bits set
     int cnt = 0;
-    for (int j = 0; j < n; ++j) cnt += f2key(gld(rows[j] + p)) <= cand;
+    for (int j = 0; j < n; ++j) cnt += f2key(gld(rows[j * si] + p)) <= cand;
     if (cnt <= rank) prefix |= 1u << bit;
   }
   return prefix;
@@ -89,32 +93,35 @@ __device__ __forceinline__ uint32_t select_rank(const float *const *rows,
 
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void orderstat_generic_kernel(
-    const float *const *__restrict__ rows, int n, int64_t numel, int kk,
-    float divisor, const float *__restrict__ base, float *__restrict__ out) {
-  const int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (p >= numel) return;
+    RowSrc rs, int n, int kk, float divisor, float *__restrict__ out) {
+  const BlockRows br = block_rows(rs, blockIdx.x);
+  if (int(threadIdx.x) >= br.len) return;
+  const int64_t p = br.lo + threadIdx.x;
+  const float *const *__restrict__ rows = br.rows;
+  const int64_t si = br.si;
+  const float *__restrict__ base = br.base;
   bool nan = false, nonfinite = false;
   for (int j = 0; j < n; ++j) {
-    const float x = gld(rows[j] + p);
+    const float x = gld(rows[j * si] + p);
     nan |= __builtin_isnan(x);
     nonfinite |= !__builtin_isfinite(x);
   }
   float r;
   if constexpr (MODE == kMedian) {
-    const float lo = key2f(select_rank(rows, n, p, (n - 1) / 2));
-    const float hi = key2f(select_rank(rows, n, p, n / 2));
+    const float lo = key2f(select_rank(rows, si, n, p, (n - 1) / 2));
+    const float hi = key2f(select_rank(rows, si, n, p, n / 2));
     r = __fdiv_rn(lo - (-hi), 2.0f);
     if (nan) r = __builtin_nanf("");
   } else {
-    const uint32_t klo = select_rank(rows, n, p, kk);
-    const uint32_t khi = select_rank(rows, n, p, n - kk - 1);
+    const uint32_t klo = select_rank(rows, si, n, p, kk);
+    const uint32_t khi = select_rank(rows, si, n, p, n - kk - 1);
     float s;
     if (!nonfinite) {
       // kept ranks [kk, n-kk): strictly inside (klo, khi) plus tie copies
       double acc = 0.0;
       int below = 0, eq_lo = 0, inside = 0;
       for (int j = 0; j < n; ++j) {
-        const float x = gld(rows[j] + p);
+        const float x = gld(rows[j * si] + p);
         const uint32_t key = f2key(x);
         below += key < klo;
         eq_lo += key == klo;
@@ -136,31 +143,29 @@ __global__ __launch_bounds__(kBlock) void orderstat_generic_kernel(
       // among the excluded values, so inf - inf (or a NaN) gives NaN;
       // with k == 0 the result is Σall itself.
       float all = 0.0f;
-      for (int j = 0; j < n; ++j) all = add_rn(all, gld(rows[j] + p));
+      for (int j = 0; j < n; ++j) all = add_rn(all, gld(rows[j * si] + p));
       s = (kk == 0 && !nan) ? all : __builtin_nanf("");
     }
     r = __fdiv_rn(s, divisor);
   }
-  if (base) r = add_rn(base[p], r);
+  if (base) r = add_rn(gld(base + p), r);
   out[p] = r;
 }
 
 template <int MODE>
-int launch(const float *const *rows, int n, int64_t numel, int kk,
-           float divisor, const float *base, float *out, hipStream_t s) {
-  const unsigned grid = unsigned((numel + kBlock - 1) / kBlock);
+int launch(const RowSrc &rs, int nchunk, int n, int kk, float divisor,
+           float *out, hipStream_t s) {
+  const unsigned grid = rows_grid(rs, nchunk);
 #define FSAGG_OS(NN)                                                        \
   hipLaunchKernelGGL((orderstat_reg_kernel<NN, MODE>), dim3(grid),         \
-                     dim3(kBlock), 0, s, rows, n, numel, kk, divisor, base, \
-                     out)
+                     dim3(kBlock), 0, s, rs, n, kk, divisor, out)
   if (n <= 4) FSAGG_OS(4);
   else if (n <= 8) FSAGG_OS(8);
   else if (n <= 16) FSAGG_OS(16);
   else if (n <= 32) FSAGG_OS(32);
   else if (n <= 64) FSAGG_OS(64);
-#define FSAGG_RX(NN) \
-  launch_select<NN, MODE>(rows, n, numel, kk, divisor, base, out, s)
-  else if (n <= 255 && numel <= (int64_t(1) << 30)) {
+#define FSAGG_RX(NN) launch_select<NN, MODE>(rs, grid, n, kk, divisor, out, s)
+  else if (n <= 255 && rs.numel <= (int64_t(1) << 30)) {
     switch ((n + kSelStep - 1) / kSelStep * kSelStep) {
     case 72: FSAGG_RX(72); break;
     case 80: FSAGG_RX(80); break;
@@ -189,13 +194,28 @@ int launch(const float *const *rows, int n, int64_t numel, int kk,
     }
   } else {
     hipLaunchKernelGGL((orderstat_generic_kernel<MODE>), dim3(grid),
-                       dim3(kBlock), 0, s, rows, n, numel, kk, divisor, base,
-                       out);
+                       dim3(kBlock), 0, s, rs, n, kk, divisor, out);
   }
 #undef FSAGG_OS
 #undef FSAGG_RX
-  return check_launch(MODE == kMedian ? "fsagg_coord_median_f32"
-                                      : "fsagg_trimmed_mean_f32");
+  return check_launch(MODE == kMedian ? "coordinate median"
+                                      : "trimmed mean");
+}
+
+RowSrc flat_src(const float *const *rows, int64_t numel, const float *base) {
+  return RowSrc{rows, 1, 0, nullptr, numel, base, nullptr, 0};
+}
+
+// the row-set entry points' shared argument checks
+bool rows_args_ok(const fsagg_rows *rows, const fsagg_chunk *chunks,
+                  int nchunk, int64_t numel, int64_t base_ss, float *out,
+                  const char *what) {
+  if (!rows || !rows->tab || rows->n < 1 || rows->nseg < 1 || !out ||
+      nchunk < 0 || (nchunk > 0 && !chunks) || numel < 0 || base_ss < 0) {
+    set_error("%s: invalid argument", what);
+    return false;
+  }
+  return true;
 }
 
 }  // namespace
@@ -213,7 +233,7 @@ extern "C" int fsagg_coord_median_f32(const float *const *rows, int n,
     return FSAGG_EINVAL;
   }
   if (numel == 0) return FSAGG_OK;
-  return launch<kMedian>(rows, n, numel, 0, 2.0f, base, out,
+  return launch<kMedian>(flat_src(rows, numel, base), 0, n, 0, 2.0f, out,
                          as_stream(stream));
 }
 
@@ -226,6 +246,44 @@ extern "C" int fsagg_trimmed_mean_f32(const float *const *rows, int n,
     return FSAGG_EINVAL;
   }
   if (numel == 0) return FSAGG_OK;
-  return launch<kTrimmed>(rows, n, numel, k, divisor, base, out,
+  return launch<kTrimmed>(flat_src(rows, numel, base), 0, n, k, divisor, out,
+                          as_stream(stream));
+}
+
+extern "C" int fsagg_coord_median_rows_f32(const fsagg_rows *rows,
+                                           const fsagg_chunk *chunks,
+                                           int nchunk, int64_t numel,
+                                           const float *const *base,
+                                           int64_t base_ss, float *out,
+                                           fsagg_stream_t stream) {
+  if (!rows_args_ok(rows, chunks, nchunk, numel, base_ss, out,
+                    "fsagg_coord_median_rows_f32"))
+    return FSAGG_EINVAL;
+  if (nchunk == 0) return FSAGG_OK;
+  const RowSrc rs{rows->tab, rows->si, rows->ss, chunks, numel, nullptr,
+                  base, base_ss};
+  return launch<kMedian>(rs, nchunk, rows->n, 0, 2.0f, out,
+                         as_stream(stream));
+}
+
+extern "C" int fsagg_trimmed_mean_rows_f32(const fsagg_rows *rows,
+                                           const fsagg_chunk *chunks,
+                                           int nchunk, int64_t numel, int k,
+                                           float divisor,
+                                           const float *const *base,
+                                           int64_t base_ss, float *out,
+                                           fsagg_stream_t stream) {
+  if (!rows_args_ok(rows, chunks, nchunk, numel, base_ss, out,
+                    "fsagg_trimmed_mean_rows_f32"))
+    return FSAGG_EINVAL;
+  if (k < 0 || 2 * k >= rows->n) {
+    set_error("fsagg_trimmed_mean_rows_f32: invalid k=%d for n=%d", k,
+              rows->n);
+    return FSAGG_EINVAL;
+  }
+  if (nchunk == 0) return FSAGG_OK;
+  const RowSrc rs{rows->tab, rows->si, rows->ss, chunks, numel, nullptr,
+                  base, base_ss};
+  return launch<kTrimmed>(rs, nchunk, rows->n, k, divisor, out,
                           as_stream(stream));
 }

@@ -235,20 +235,24 @@ __device__ __forceinline__ void list_select(const uint32_t *H, int cnt,
 
 template <int N, int MODE>
 __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
-    const float *const *__restrict__ rows, int n, int64_t numel, int kk,
-    float divisor, const float *__restrict__ base, float *__restrict__ out) {
+    RowSrc rs, int n, int kk, float divisor, float *__restrict__ out) {
   __shared__ uint32_t lds[kSelLds];
   uint32_t *H = lds + (threadIdx.x / kWave) * kSelWords * kWave +
                 (threadIdx.x & (kWave - 1));
-  const int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-  const bool live = p < numel;
+  const BlockRows br = block_rows(rs, blockIdx.x);
+  const float *const *__restrict__ rows = br.rows;
+  const int64_t si = br.si;
+  const float *__restrict__ base = br.base;
+  const int64_t p = br.lo + threadIdx.x;
+  const bool live = int(threadIdx.x) < br.len;
   __builtin_assume(n > N - kSelStep && n <= N);  // dispatch
   uint32_t k[N];
   {
-    const uint32_t off = live ? uint32_t(p) : 0u;  // numel <= 2^30: launch
+    // coordinates < 2^30 (launch); dead lanes re-read the chunk's first
+    const uint32_t off = uint32_t(live ? p : br.lo);
 #pragma unroll
     for (int j = 0; j < N; ++j)
-      k[j] = __float_as_uint(ld_nt(rows[j < n ? j : n - 1], off));
+      k[j] = __float_as_uint(ld_nt(rows[(j < n ? j : n - 1) * si], off));
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       const uint32_t key = f2key(__uint_as_float(k[j]));
@@ -400,34 +404,29 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
       if (kk == 0 && !nan) {
         s = 0.0f;
 #pragma unroll 1
-        for (int j = 0; j < n; ++j) s = add_rn(s, gld(rows[j] + p));
+        for (int j = 0; j < n; ++j) s = add_rn(s, gld(rows[j * si] + p));
       }
     }
     r = __fdiv_rn(s, divisor);
   }
-  if (base) r = add_rn(base[p], r);
+  if (base) r = add_rn(gld(base + p), r);
   out[p] = r;
 }
 
 }  // namespace
 
 template <int N, int MODE>
-void launch_select(const float *const *rows, int n, int64_t numel, int kk,
-                   float divisor, const float *base, float *out,
-                   hipStream_t s) {
-  const unsigned grid = unsigned((numel + kBlock - 1) / kBlock);
+void launch_select(const RowSrc &rs, unsigned grid, int n, int kk,
+                   float divisor, float *out, hipStream_t s) {
   hipLaunchKernelGGL((orderstat_select_kernel<N, MODE>), dim3(grid),
-                     dim3(kBlock), 0, s, rows, n, numel, kk, divisor, base,
-                     out);
+                     dim3(kBlock), 0, s, rs, n, kk, divisor, out);
 }
 
-template void launch_select<SEL_N, kMedian>(const float *const *, int,
-                                            int64_t, int, float,
-                                            const float *, float *,
+template void launch_select<SEL_N, kMedian>(const RowSrc &, unsigned, int,
+                                            int, float, float *,
                                             hipStream_t);
-template void launch_select<SEL_N, kTrimmed>(const float *const *, int,
-                                             int64_t, int, float,
-                                             const float *, float *,
+template void launch_select<SEL_N, kTrimmed>(const RowSrc &, unsigned, int,
+                                             int, float, float *,
                                              hipStream_t);
 
 }  // namespace os

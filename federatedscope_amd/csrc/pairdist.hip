@@ -100,13 +100,16 @@ PairPlan make_plan(int n, int64_t numel, int nseg) {
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-__global__ void chunk_prefix_kernel(const int64_t *__restrict__ seg_off,
+// Key segment s covers [seg_lo[s], seg_end[s]); the flat API passes its
+// contiguous offsets as seg_lo = seg_off, seg_end = seg_off + 1.
+__global__ void chunk_prefix_kernel(const int64_t *__restrict__ seg_lo,
+                                    const int64_t *__restrict__ seg_end,
                                     int nseg, int64_t chl, int *prefix) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   int acc = 0;
   prefix[0] = 0;
   for (int s = 0; s < nseg; ++s) {
-    const int64_t len = seg_off[s + 1] - seg_off[s];
+    const int64_t len = seg_end[s] - seg_lo[s];
     acc += int((len + chl - 1) / chl);
     prefix[s + 1] = acc;
   }
@@ -149,8 +152,9 @@ __device__ __forceinline__ void read_tile(const float *col, int t,
 
 template <int TS>
 __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
-    const float *const *__restrict__ rows, int n, PairPlan pl,
-    const int64_t *__restrict__ seg_off, int nseg,
+    const float *const *__restrict__ tab, int64_t si, int64_t ss, int n,
+    PairPlan pl, const int64_t *__restrict__ seg_lo,
+    const int64_t *__restrict__ seg_end, int nseg,
     const int *__restrict__ prefix, float *__restrict__ partial) {
   __shared__ __attribute__((aligned(16))) float lds[kLdsFloats];
   // client row pointers for the prefetch (n <= kPtrSlots, else no
@@ -169,9 +173,11 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     else hi = mid;
   }
   const int s = lo;
-  const int64_t start = seg_off[s] + int64_t(c - prefix[s]) * pl.chl;
+  const int64_t start = seg_lo[s] + int64_t(c - prefix[s]) * pl.chl;
   int64_t end = start + pl.chl;
-  if (end > seg_off[s + 1]) end = seg_off[s + 1];
+  if (end > seg_end[s]) end = seg_end[s];
+  // client r's row of this key segment: rows[r * si] (a virtual base)
+  const float *const *__restrict__ rows = tab + int64_t(s) * ss;
 
   const int tid = threadIdx.x;
   const int tpl = tid % pl.tpg;
@@ -190,7 +196,7 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   const int items = quads * groups;
   bool vec = (start & 3) == 0;
   for (int r = 0; r < n; ++r)
-    vec = vec && (reinterpret_cast<uintptr_t>(rows[r]) & 15u) == 0;
+    vec = vec && (reinterpret_cast<uintptr_t>(rows[r * si]) & 15u) == 0;
 
   float acc[TS][TS];
 #pragma unroll
@@ -245,10 +251,10 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     const int wave = tid / kWave, lane = tid & (kWave - 1);
     for (int qd = wave; qd < quads; qd += kBlock / kWave) {
       const int r0 = qd * 4;
-      const float *p0 = rows[min(r0, n - 1)] + cs;
-      const float *p1 = rows[min(r0 + 1, n - 1)] + cs;
-      const float *p2 = rows[min(r0 + 2, n - 1)] + cs;
-      const float *p3 = rows[min(r0 + 3, n - 1)] + cs;
+      const float *p0 = rows[min(r0, n - 1) * si] + cs;
+      const float *p1 = rows[min(r0 + 1, n - 1) * si] + cs;
+      const float *p2 = rows[min(r0 + 2, n - 1) * si] + cs;
+      const float *p3 = rows[min(r0 + 3, n - 1) * si] + cs;
       for (int cc = lane; cc < len; cc += kWave)
         *reinterpret_cast<float4 *>(lds + cc * pl.ldsp + r0) =
             make_float4(gld(p0 + cc), gld(p1 + cc), gld(p2 + cc), gld(p3 + cc));
@@ -258,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   const bool prefetch =
       vec && items <= kStageItems * kBlock && n <= kPtrSlots;
   if (n <= kPtrSlots) {
-    for (int r = tid; r < n; r += kBlock) rowp[r] = rows[r];
+    for (int r = tid; r < n; r += kBlock) rowp[r] = rows[r * si];
     __syncthreads();
   }
   if (prefetch && end - start >= pl.sub) fetch(start);
@@ -439,10 +445,95 @@ __global__ void rownorm_final_kernel(const double *__restrict__ partial, int n,
   sq[row] = t;
 }
 
+// ---- per-(client, key) squared norms over a row set (fp64) --------------
+// Block (c, i) sums chunk c of client i (fixed lane order + one LDS tree) →
+// partial[i][c]; then one lane per client adds its chunks in chunk order
+// into sq[i][seg].  NULL entries (absent keys) contribute nothing.
+__global__ __launch_bounds__(kBlock) void rows_sqnorm_partial_kernel(
+    const float *const *__restrict__ tab, int64_t si, int64_t ss,
+    const fsagg_chunk *__restrict__ chunks, int nchunk,
+    double *__restrict__ partial) {
+  __shared__ double red[kBlock / kWave];
+  const int c = blockIdx.x, i = blockIdx.y;
+  const int64_t lo = chunks[c].lo;
+  const int len = chunks[c].len;
+  const float *row = tab[int64_t(i) * si + int64_t(chunks[c].seg) * ss];
+  double acc = 0.0;
+  if (row) {
+    constexpr int G = 8;
+    int q = threadIdx.x;
+    for (; q + (G - 1) * kBlock < len; q += G * kBlock) {
+      float v[G];
+#pragma unroll
+      for (int e = 0; e < G; ++e) v[e] = gload_nt(row + lo + q + e * kBlock);
+#pragma unroll
+      for (int e = 0; e < G; ++e) acc += double(v[e]) * double(v[e]);
+    }
+    for (; q < len; q += kBlock) {
+      const double d = double(gld(row + lo + q));
+      acc += d * d;
+    }
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < kBlock / kWave; ++w) t += red[w];
+    partial[int64_t(i) * nchunk + c] = t;
+  }
+}
+
+__global__ void rows_sqnorm_final_kernel(const fsagg_chunk *__restrict__ chunks,
+                                         int nchunk, int n, int nseg,
+                                         const double *__restrict__ partial,
+                                         double *__restrict__ sq) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double *o = sq + int64_t(i) * nseg;
+  for (int s = 0; s < nseg; ++s) o[s] = 0.0;
+  for (int c = 0; c < nchunk; ++c)
+    o[chunks[c].seg] += partial[int64_t(i) * nchunk + c];
+}
+
 }  // namespace
 }  // namespace fsagg
 
 using namespace fsagg;
+
+extern "C" size_t fsagg_rows_sqnorm_workspace_bytes(int n, int nchunk) {
+  if (n < 1 || nchunk < 1) return 0;
+  return sizeof(double) * size_t(n) * size_t(nchunk);
+}
+
+extern "C" int fsagg_rows_sqnorm_f32(const fsagg_rows *rows,
+                                     const fsagg_chunk *chunks, int nchunk,
+                                     double *sq, void *workspace,
+                                     size_t workspace_bytes,
+                                     fsagg_stream_t stream) {
+  if (!rows || !rows->tab || rows->n < 1 || rows->n > 65535 ||
+      rows->nseg < 1 || !sq || nchunk < 0 || (nchunk > 0 && !chunks)) {
+    set_error("fsagg_rows_sqnorm_f32: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  const size_t need = fsagg_rows_sqnorm_workspace_bytes(rows->n, nchunk);
+  if (need && (!workspace || workspace_bytes < need)) {
+    set_error("fsagg_rows_sqnorm_f32: workspace %zu < %zu bytes",
+              workspace_bytes, need);
+    return FSAGG_ESPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  double *partial = static_cast<double *>(workspace);
+  if (nchunk > 0)
+    hipLaunchKernelGGL(rows_sqnorm_partial_kernel,
+                       dim3(unsigned(nchunk), unsigned(rows->n)), dim3(kBlock),
+                       0, s, rows->tab, rows->si, rows->ss, chunks, nchunk,
+                       partial);
+  hipLaunchKernelGGL(rows_sqnorm_final_kernel,
+                     dim3(unsigned((rows->n + 63) / 64)), dim3(64), 0, s,
+                     chunks, nchunk, rows->n, rows->nseg, partial, sq);
+  return check_launch("fsagg_rows_sqnorm_f32");
+}
 
 extern "C" size_t fsagg_pairdist_workspace_bytes(int n, int64_t numel,
                                                  int nseg) {
@@ -455,24 +546,27 @@ extern "C" size_t fsagg_pairdist_workspace_bytes(int n, int64_t numel,
 }
 
 // Enqueue the chunk and per-segment kernels; segsq receives [nseg][n][n].
-static int pairdist_segsq_impl(const float *const *rows, int n, int64_t numel,
-                               const int64_t *seg_off, int nseg,
-                               double *segsq, void *workspace,
+static int pairdist_segsq_impl(const float *const *tab, int64_t si,
+                               int64_t ss, int n, int64_t numel,
+                               const int64_t *seg_lo, const int64_t *seg_end,
+                               int nseg, double *segsq, void *workspace,
                                hipStream_t s) {
   const PairPlan pl = make_plan(n, numel, nseg);
   int *prefix = static_cast<int *>(workspace);
   float *partial = reinterpret_cast<float *>(
       static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)));
-  hipLaunchKernelGGL(chunk_prefix_kernel, dim3(1), dim3(1), 0, s, seg_off,
-                     nseg, pl.chl, prefix);
+  hipLaunchKernelGGL(chunk_prefix_kernel, dim3(1), dim3(1), 0, s, seg_lo,
+                     seg_end, nseg, pl.chl, prefix);
   if (numel > 0) {
     const dim3 grid(unsigned(pl.max_chunks), unsigned(pl.groups));
     if (pl.ts == 10)
       hipLaunchKernelGGL(pairdist_chunk_kernel<10>, grid, dim3(kBlock), 0, s,
-                         rows, n, pl, seg_off, nseg, prefix, partial);
+                         tab, si, ss, n, pl, seg_lo, seg_end, nseg, prefix,
+                         partial);
     else
       hipLaunchKernelGGL(pairdist_chunk_kernel<8>, grid, dim3(kBlock), 0, s,
-                         rows, n, pl, seg_off, nseg, prefix, partial);
+                         tab, si, ss, n, pl, seg_lo, seg_end, nseg, prefix,
+                         partial);
   }
   const int per_seg = pl.ntp * pl.ts * pl.ts;
   hipLaunchKernelGGL(pairdist_segsq_kernel,
@@ -503,7 +597,8 @@ extern "C" int fsagg_pairdist_f32(const float *const *rows, int n,
       static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)) +
       align256(sizeof(float) * size_t(pl.max_chunks) * size_t(pl.ntp) *
                size_t(pl.ts * pl.ts)));
-  pairdist_segsq_impl(rows, n, numel, seg_off, nseg, segsq, workspace, s);
+  pairdist_segsq_impl(rows, 1, 0, n, numel, seg_off, seg_off + 1, nseg, segsq,
+                      workspace, s);
   hipLaunchKernelGGL(pairdist_finish_kernel,
                      dim3(unsigned((n * n + kBlock - 1) / kBlock)),
                      dim3(kBlock), 0, s, segsq, n, nseg, D);
@@ -528,9 +623,34 @@ extern "C" int fsagg_pairdist_segsq_f32(const float *const *rows, int n,
               workspace_bytes, need);
     return FSAGG_ESPACE;
   }
-  pairdist_segsq_impl(rows, n, numel, seg_off, nseg, segsq, workspace,
-                      as_stream(stream));
+  pairdist_segsq_impl(rows, 1, 0, n, numel, seg_off, seg_off + 1, nseg, segsq,
+                      workspace, as_stream(stream));
   return check_launch("fsagg_pairdist_segsq_f32");
+}
+
+extern "C" int fsagg_pairdist_rows_segsq_f32(const fsagg_rows *rows,
+                                             const int64_t *seg_lo,
+                                             const int64_t *seg_end,
+                                             int64_t numel, double *segsq,
+                                             void *workspace,
+                                             size_t workspace_bytes,
+                                             fsagg_stream_t stream) {
+  if (!rows || !rows->tab || !seg_lo || !seg_end || !segsq || rows->n < 2 ||
+      rows->n > kMaxPairClients || rows->nseg < 1 || numel < 0) {
+    set_error("fsagg_pairdist_rows_segsq_f32: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  const size_t need =
+      fsagg_pairdist_workspace_bytes(rows->n, numel, rows->nseg);
+  if (!workspace || workspace_bytes < need) {
+    set_error("fsagg_pairdist_rows_segsq_f32: workspace %zu < %zu bytes",
+              workspace_bytes, need);
+    return FSAGG_ESPACE;
+  }
+  pairdist_segsq_impl(rows->tab, rows->si, rows->ss, rows->n, numel, seg_lo,
+                      seg_end, rows->nseg, segsq, workspace,
+                      as_stream(stream));
+  return check_launch("fsagg_pairdist_rows_segsq_f32");
 }
 
 extern "C" int fsagg_pairdist_finish_f64(const double *segsq, int n, int nseg,

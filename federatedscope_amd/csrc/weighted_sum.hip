@@ -223,6 +223,137 @@ void launch_wsum(const float *const *rows, const float *w, const float *pre,
 }
 
 // ---------------------------------------------------------------------------
+// row sets: clients' key tensors read in place (include/fsagg.h fsagg_rows)
+// ---------------------------------------------------------------------------
+// One chunk of <= kBlock·V float4 coordinates of one key segment.  The
+// chunk's client rows are wave-uniform scalar loads of the pointer table; a
+// NULL entry is a client that lacks the key and is skipped (the reference's
+// `if key not in local_model: continue`, clients_avg_aggregator.py:74-75) —
+// the first present client initialises the accumulator.  Same per-lane
+// streaming shape as wsum_tile: all V loads of one client in flight before
+// any is consumed.
+template <int V, bool PRE, bool BASE, bool GUARD>
+__device__ __forceinline__ void wsum_rows_chunk(
+    const float *const *__restrict__ rows, int64_t si, int n, int64_t lo,
+    int nvec, const float *__restrict__ w, const float *__restrict__ pre,
+    const float *__restrict__ base, float *__restrict__ out) {
+  int idx[V];
+  bool ok[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    idx[v] = v * kBlock + int(threadIdx.x);
+    ok[v] = !GUARD || idx[v] < nvec;
+  }
+  f4 acc[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) acc[v] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+  bool first = true;
+  for (int i = 0; i < n; ++i) {
+    const float *row = rows[int64_t(i) * si];
+    if (row == nullptr) continue;
+    const f4 *r = reinterpret_cast<const f4 *>(row + lo);
+    f4 x[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+      x[v] = ok[v] ? ld4<true>(r + idx[v]) : f4{0.0f, 0.0f, 0.0f, 0.0f};
+    const float wi = w[i];
+    const float s = PRE ? pre[i] : 1.0f;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      f4 t = x[v];
+      if (PRE) t = mul4(t, s);
+      acc[v] = first ? mul4(t, wi) : add4(acc[v], mul4(t, wi));
+    }
+    first = false;
+  }
+  f4 *o = reinterpret_cast<f4 *>(out + lo);
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    if (!ok[v]) continue;
+    f4 a = acc[v];
+    if (BASE) a = add4(ld4<false>(reinterpret_cast<const f4 *>(base + lo) +
+                                  idx[v]), a);
+    o[idx[v]] = a;
+  }
+}
+
+template <int V, bool PRE, bool BASE>
+__global__ __launch_bounds__(kBlock) void wsum_rows_kernel(
+    const float *const *__restrict__ tab, int64_t si, int64_t ss, int n,
+    const fsagg_chunk *__restrict__ chunks, int nchunk,
+    const float *__restrict__ w, const float *__restrict__ pre,
+    const float *const *__restrict__ btab, int64_t bss,
+    float *__restrict__ out) {
+  for (int c = blockIdx.x; c < nchunk; c += gridDim.x) {
+    const int64_t lo = chunks[c].lo;
+    const int len = chunks[c].len;
+    const int seg = chunks[c].seg;
+    const float *const *rows = tab + int64_t(seg) * ss;
+    const float *base = BASE ? btab[int64_t(seg) * bss] : nullptr;
+    const int nvec = len >> 2;
+    if (nvec == kBlock * V)
+      wsum_rows_chunk<V, PRE, BASE, false>(rows, si, n, lo, nvec, w, pre,
+                                           base, out);
+    else
+      wsum_rows_chunk<V, PRE, BASE, true>(rows, si, n, lo, nvec, w, pre,
+                                          base, out);
+    // the key's last (< 4) coordinates
+    const int t = int(threadIdx.x);
+    if (t < (len & 3)) {
+      const int64_t p = lo + 4 * int64_t(nvec) + t;
+      float acc = 0.0f;
+      bool first = true;
+      for (int i = 0; i < n; ++i) {
+        const float *row = rows[int64_t(i) * si];
+        if (row == nullptr) continue;
+        float x = gld(row + p);
+        if (PRE) x = mul_rn(x, pre[i]);
+        acc = first ? mul_rn(x, w[i]) : add_rn(acc, mul_rn(x, w[i]));
+        first = false;
+      }
+      if (BASE) acc = add_rn(gld(base + p), acc);
+      out[p] = acc;
+    }
+  }
+}
+
+// V of the flat launcher (launch_wsum) for a bucket of `numel` coordinates
+int wsum_vec_width(int64_t numel) {
+  const int64_t nvec = numel / 4;
+  auto tiles = [&](int v) { return (nvec + 256 * v - 1) / (256 * v); };
+  if (tiles(24) >= 1000) return 24;
+  if (tiles(16) >= 1000) return 16;
+  if (tiles(8) >= 1000) return 8;
+  if (tiles(4) >= 1000) return 4;
+  return 1;
+}
+
+template <int V, bool PRE, bool BASE>
+void launch_wsum_rows(const fsagg_rows &rs, const fsagg_chunk *chunks,
+                      int nchunk, const float *w, const float *pre,
+                      const float *const *btab, int64_t bss, float *out,
+                      hipStream_t s) {
+  const unsigned grid = stream_grid(nchunk, 1, 256 * 16);
+  hipLaunchKernelGGL((wsum_rows_kernel<V, PRE, BASE>), dim3(grid),
+                     dim3(kBlock), 0, s, rs.tab, rs.si, rs.ss, rs.n, chunks,
+                     nchunk, w, pre, btab, bss, out);
+}
+
+template <int V>
+void launch_wsum_rows_v(const fsagg_rows &rs, const fsagg_chunk *chunks,
+                        int nchunk, const float *w, const float *pre,
+                        const float *const *btab, int64_t bss, float *out,
+                        hipStream_t s) {
+  if (pre) {
+    if (btab) launch_wsum_rows<V, true, true>(rs, chunks, nchunk, w, pre, btab, bss, out, s);
+    else launch_wsum_rows<V, true, false>(rs, chunks, nchunk, w, pre, btab, bss, out, s);
+  } else {
+    if (btab) launch_wsum_rows<V, false, true>(rs, chunks, nchunk, w, pre, btab, bss, out, s);
+    else launch_wsum_rows<V, false, false>(rs, chunks, nchunk, w, pre, btab, bss, out, s);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // non-fp32 buckets
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint16_t f2bf_rne(float f) {
@@ -379,6 +510,43 @@ extern "C" int fsagg_weighted_sum_f32(const float *const *rows,
                        weights, prescale, n, nvec * 4, numel, base, out);
   }
   return check_launch("fsagg_weighted_sum_f32");
+}
+
+extern "C" int64_t fsagg_wsum_chunk_elems(int64_t numel) {
+  return int64_t(1024) * wsum_vec_width(numel < 0 ? 0 : numel);
+}
+
+extern "C" int fsagg_weighted_sum_rows_f32(const fsagg_rows *rows,
+                                           const fsagg_chunk *chunks,
+                                           int nchunk, int64_t chunk_elems,
+                                           const float *weights,
+                                           const float *prescale,
+                                           const float *const *base,
+                                           int64_t base_ss, float *out,
+                                           fsagg_stream_t stream) {
+  if (!rows || !rows->tab || rows->n < 1 || rows->nseg < 1 || !weights ||
+      !out || nchunk < 0 || (nchunk > 0 && !chunks) || base_ss < 0) {
+    set_error("fsagg_weighted_sum_rows_f32: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  if (!aligned16(out)) {
+    set_error("fsagg_weighted_sum_rows_f32: out must be 16-byte aligned");
+    return FSAGG_EINVAL;
+  }
+  if (nchunk == 0) return FSAGG_OK;
+  hipStream_t s = as_stream(stream);
+  switch (chunk_elems) {
+    case 1024 * 24: launch_wsum_rows_v<24>(*rows, chunks, nchunk, weights, prescale, base, base_ss, out, s); break;
+    case 1024 * 16: launch_wsum_rows_v<16>(*rows, chunks, nchunk, weights, prescale, base, base_ss, out, s); break;
+    case 1024 * 8: launch_wsum_rows_v<8>(*rows, chunks, nchunk, weights, prescale, base, base_ss, out, s); break;
+    case 1024 * 4: launch_wsum_rows_v<4>(*rows, chunks, nchunk, weights, prescale, base, base_ss, out, s); break;
+    case 1024: launch_wsum_rows_v<1>(*rows, chunks, nchunk, weights, prescale, base, base_ss, out, s); break;
+    default:
+      set_error("fsagg_weighted_sum_rows_f32: chunk_elems %lld is not a "
+                "fsagg_wsum_chunk_elems() unit", (long long)chunk_elems);
+      return FSAGG_EINVAL;
+  }
+  return check_launch("fsagg_weighted_sum_rows_f32");
 }
 
 extern "C" int fsagg_weighted_sum_typed(const void *const *rows, int in_dtype,

@@ -80,6 +80,54 @@ class BucketLayout:
                 _h2d(ck, torch.int32, device), _h2d(cs, torch.int64, device))
         return cache[str(device)]
 
+    def row_chunks(self, unit, device, lo=0, hi=None):
+        """Device chunk table (struct fsagg_chunk, include/fsagg.h) of the
+        fp32 keys' coordinates inside [lo, hi), cut into pieces of at most
+        ``unit`` that never straddle a key (padding between keys is never
+        part of a chunk).  Cached per (unit, range, device); returns
+        (uint8 device tensor, nchunk)."""
+        import numpy as np
+        from .ops import CHUNK_DTYPE, _h2d_bytes
+        hi = self.numel if hi is None else hi
+        device = torch.device(device)
+        cache = self.__dict__.setdefault('_row_chunks', {})
+        ck = (int(unit), int(lo), int(hi), str(device))
+        if ck not in cache:
+            parts = []
+            for s, k in enumerate(self.keys):
+                a = max(self.offsets[k], lo)
+                b = min(self.offsets[k] + self.numels[k], hi)
+                if b <= a:
+                    continue
+                st = np.arange(a, b, unit, dtype=np.int64)
+                part = np.zeros(len(st), dtype=CHUNK_DTYPE)
+                part['lo'] = st
+                part['len'] = np.minimum(unit, b - st)
+                part['seg'] = s
+                parts.append(part)
+            arr = np.concatenate(parts) if parts else \
+                np.zeros(0, dtype=CHUNK_DTYPE)
+            cache[ck] = (_h2d_bytes(arr, device) if len(arr) else None,
+                         len(arr))
+        return cache[ck]
+
+    def seg_bounds(self, device, lo=0, hi=None):
+        """Device int64 arrays (seg_lo, seg_end) of each fp32 key's exact
+        coordinates clipped to [lo, hi) (empty segments where a key lies
+        outside), cached per range and device."""
+        hi = self.numel if hi is None else hi
+        device = torch.device(device)
+        cache = self.__dict__.setdefault('_seg_bounds', {})
+        ck = (int(lo), int(hi), str(device))
+        if ck not in cache:
+            from .ops import _h2d
+            a = [min(max(self.offsets[k], lo), hi) for k in self.keys]
+            b = [min(max(self.offsets[k] + self.numels[k], lo), hi)
+                 for k in self.keys]
+            cache[ck] = (_h2d(a, torch.int64, device),
+                         _h2d(b, torch.int64, device))
+        return cache[ck]
+
     def segments(self, keys=None):
         """Element offsets [0, ..., numel] splitting the bucket per key
         (padding folded into the preceding key; zeros add nothing to sums of

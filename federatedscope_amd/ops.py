@@ -5,6 +5,7 @@ BEFORE anything is launched (a malformed launch on a GPU box can fault the
 whole node), then calls the HIP kernel on the current torch stream of the
 tensors' device.  PyTorch is only the device-memory / stream container here.
 """
+import ctypes
 import math
 
 import torch
@@ -24,6 +25,21 @@ def _h2d(values, dtype, device):
     if device.type != 'cuda':
         return host.to(device)
     return host.pin_memory().to(device, non_blocking=True)
+
+
+def _h2d_bytes(arr, device):
+    """A numpy record array as a uint8 device tensor (pinned, async)."""
+    import numpy as np
+    host = torch.from_numpy(
+        np.ascontiguousarray(arr).view(np.uint8).reshape(-1).copy())
+    return host.pin_memory().to(torch.device(device), non_blocking=True)
+
+
+def _h2d_np(arr, device):
+    """A numpy array as a device tensor of its dtype (pinned, async)."""
+    import numpy as np
+    host = torch.from_numpy(np.ascontiguousarray(arr).reshape(-1).copy())
+    return host.pin_memory().to(torch.device(device), non_blocking=True)
 
 
 def _stream(device):
@@ -573,3 +589,230 @@ def delta_wsum_keys(keys, weights, base, out):
         btab.data_ptr(), keys.seg.data_ptr(), keys.nseg, out.data_ptr(),
         _stream(keys.device)), 'fsagg_delta_wsum_keys_f32')
     return out
+
+
+# -- row sets: client key tensors read in place (include/fsagg.h) -----------
+import numpy as _np  # noqa: E402
+
+CHUNK_DTYPE = _np.dtype([('lo', '<i8'), ('len', '<i4'), ('seg', '<i4')])
+
+
+class RowSet:
+    """``n`` clients x the fp32 key segments of a :class:`BucketLayout`,
+    addressed in place (struct fsagg_rows): entry (i, s) is client i's
+    virtual base for key s — its key tensor's address minus 4 x the key's
+    bucket offset, or its stack row (where bucket coordinates are row
+    coordinates).  0 = the client lacks the key.  ``table`` is the host
+    copy ([n][1] for a stack without absent keys, else [n][nseg])."""
+
+    def __init__(self, layout, table, device, keepalive=(), aligned16=True):
+        table = _np.ascontiguousarray(table, dtype=_np.int64)
+        if table.ndim != 2 or table.shape[0] < 1:
+            raise ValueError('row table must be [n][1] or [n][nseg]')
+        self.layout = layout
+        self.host = table
+        self.n = table.shape[0]
+        self.nseg = max(len(layout.keys), 1)
+        if table.shape[1] == 1:
+            self.si, self.ss = 1, 0
+        elif table.shape[1] == self.nseg:
+            self.si, self.ss = self.nseg, 1
+        else:
+            raise ValueError('row table has %d columns for %d keys' %
+                             (table.shape[1], self.nseg))
+        self.device = torch.device(device)
+        self.aligned16 = bool(aligned16)
+        self.missing = int((table == 0).sum())
+        self.tab = _h2d_np(table, self.device)
+        self.struct = L.Rows(self.tab.data_ptr(), self.si, self.ss, self.n,
+                             self.nseg)
+        self._keep = tuple(keepalive)
+
+    @classmethod
+    def from_stack(cls, stack, slots, present=None):
+        """Rows ``slots`` of a ClientStack; ``present`` (bool [n][nseg])
+        marks absent keys (NULL entries)."""
+        _check_f32_cuda(stack.slab, 'stack')
+        base = stack.slab.data_ptr()
+        ld = stack.slab.stride(0) * 4
+        rows = _np.array([base + int(s) * ld for s in slots], dtype=_np.int64)
+        tab = rows[:, None]
+        if present is not None and not _np.all(present):
+            tab = _np.where(_np.asarray(present, bool), tab, 0)
+        return cls(stack.layout, tab, stack.device, keepalive=(stack.slab, ),
+                   aligned16=ld % ALIGN_BYTES == 0 and
+                   base % ALIGN_BYTES == 0)
+
+    @classmethod
+    def from_pointers(cls, layout, ptrs, device, keepalive=(),
+                      aligned16=True):
+        """[n][nseg] real data pointers of the clients' key tensors (0:
+        absent), in layout key order."""
+        ptrs = _np.asarray(ptrs, dtype=_np.int64)
+        offs = _np.array([layout.offsets[k] for k in layout.keys],
+                         dtype=_np.int64)
+        virt = _np.where(ptrs != 0, ptrs - 4 * offs[None, :], 0)
+        return cls(layout, virt, device, keepalive=keepalive,
+                   aligned16=aligned16)
+
+    def subset(self, sel):
+        """The clients ``sel`` (indices, in the new reduction order)."""
+        idx = _np.asarray([int(i) for i in sel], dtype=_np.int64)
+        if len(idx) == 0 or idx.min() < 0 or idx.max() >= self.n:
+            raise IndexError('row selection outside the %d clients' % self.n)
+        return RowSet(self.layout, self.host[idx], self.device,
+                      keepalive=self._keep, aligned16=self.aligned16)
+
+    def ptr(self):
+        return ctypes.byref(self.struct)
+
+
+class BaseRows:
+    """The ``base`` operand of the row-set kernels (the server's init model
+    of the robust rules' init + update): per-key virtual bases of device
+    tensors, or one flat bucket."""
+
+    def __init__(self, tab, bss, keepalive=()):
+        self.tab = tab
+        self.bss = bss
+        self._keep = tuple(keepalive)
+
+    @classmethod
+    def from_bucket(cls, flat):
+        _check_f32_cuda(flat, 'base bucket')
+        return cls(_h2d([flat.data_ptr()], torch.int64, flat.device), 0,
+                   keepalive=(flat, ))
+
+    @classmethod
+    def from_pointers(cls, layout, ptrs, device, keepalive=()):
+        ptrs = _np.asarray(ptrs, dtype=_np.int64).reshape(-1)
+        offs = _np.array([layout.offsets[k] for k in layout.keys],
+                         dtype=_np.int64)
+        virt = ptrs - 4 * offs
+        return cls(_h2d_np(virt, device), 1,
+                   keepalive=keepalive)
+
+    def ptr(self):
+        return self.tab.data_ptr()
+
+
+def _rows_out(rs, out, align):
+    _check_f32_cuda(out, 'out', align=align)
+    if out.device != rs.device or out.numel() < rs.layout.numel:
+        raise ValueError('out must hold the %d-element bucket on %s' %
+                         (rs.layout.numel, rs.device))
+
+
+def weighted_sum_rows(rs, weights, out, prescale=None, base=None, lo=0,
+                      hi=None):
+    """:func:`weighted_sum` over a row set, on the keys' coordinates in
+    [lo, hi) of the flat ``out`` bucket; absent keys are skipped per
+    client (the reference's missing-key rule, in the same launch)."""
+    if len(weights) != rs.n:
+        raise ValueError('%d weights for %d rows' % (len(weights), rs.n))
+    if not rs.aligned16:
+        raise ValueError('weighted_sum_rows needs 16-byte aligned key '
+                         'tensors')
+    _rows_out(rs, out, ALIGN_BYTES)
+    lib = L.load()
+    unit = lib.fsagg_wsum_chunk_elems(rs.layout.numel)
+    chunks, nchunk = rs.layout.row_chunks(unit, rs.device, lo, hi)
+    if nchunk == 0:
+        return out
+    w = weights if isinstance(weights, torch.Tensor) else _fp32_dev(
+        weights, rs.device)
+    pre = None
+    if prescale is not None:
+        if len(prescale) != rs.n:
+            raise ValueError('prescale length mismatch')
+        pre = prescale if isinstance(prescale, torch.Tensor) else _fp32_dev(
+            prescale, rs.device)
+    L.check(lib.fsagg_weighted_sum_rows_f32(
+        rs.ptr(), chunks.data_ptr(), nchunk, unit, w.data_ptr(),
+        pre.data_ptr() if pre is not None else None,
+        base.ptr() if base is not None else None,
+        base.bss if base is not None else 0, out.data_ptr(),
+        _stream(rs.device)), 'fsagg_weighted_sum_rows_f32')
+    return out
+
+
+def _require_all(rs, what):
+    if rs.missing:
+        raise KeyError('%s needs every client to hold every key (%d absent)'
+                       % (what, rs.missing))
+
+
+def coord_median_rows(rs, out, base=None, lo=0, hi=None):
+    _require_all(rs, 'median')
+    _rows_out(rs, out, 4)
+    chunks, nchunk = rs.layout.row_chunks(L.FSAGG_ROWS_OS_CHUNK, rs.device,
+                                          lo, hi)
+    if nchunk == 0:
+        return out
+    L.check(L.load().fsagg_coord_median_rows_f32(
+        rs.ptr(), chunks.data_ptr(), nchunk, rs.layout.numel,
+        base.ptr() if base is not None else None,
+        base.bss if base is not None else 0, out.data_ptr(),
+        _stream(rs.device)), 'fsagg_coord_median_rows_f32')
+    return out
+
+
+def trimmed_mean_rows(rs, k, out, divisor=None, base=None, lo=0, hi=None):
+    _require_all(rs, 'trimmed mean')
+    if k < 0 or 2 * k >= rs.n:
+        raise ValueError('trimmed mean needs 0 <= 2k < n (k=%d n=%d)' %
+                         (k, rs.n))
+    _rows_out(rs, out, 4)
+    chunks, nchunk = rs.layout.row_chunks(L.FSAGG_ROWS_OS_CHUNK, rs.device,
+                                          lo, hi)
+    if nchunk == 0:
+        return out
+    div = float(rs.n - 2 * k if divisor is None else divisor)
+    L.check(L.load().fsagg_trimmed_mean_rows_f32(
+        rs.ptr(), chunks.data_ptr(), nchunk, rs.layout.numel, int(k), div,
+        base.ptr() if base is not None else None,
+        base.bss if base is not None else 0, out.data_ptr(),
+        _stream(rs.device)), 'fsagg_trimmed_mean_rows_f32')
+    return out
+
+
+def pairdist_rows_segsq(rs, lo=0, hi=None, workspace=None):
+    """Per-key squared pair distances [nseg][n][n] (fp64) over the keys'
+    coordinates in [lo, hi) (a rank's range: summed across ranks by the
+    caller, then :func:`pairdist_finish`)."""
+    _require_all(rs, 'Krum')
+    if rs.n < 2:
+        raise ValueError('Krum needs at least two clients')
+    lay = rs.layout
+    seg_lo, seg_end = lay.seg_bounds(rs.device, lo, hi)
+    lib = L.load()
+    need = lib.fsagg_pairdist_workspace_bytes(rs.n, lay.numel, rs.nseg)
+    ws = (workspace or _WS).get(rs.device, need)
+    sq = torch.empty((rs.nseg, rs.n, rs.n), dtype=torch.float64,
+                     device=rs.device)
+    L.check(lib.fsagg_pairdist_rows_segsq_f32(
+        rs.ptr(), seg_lo.data_ptr(), seg_end.data_ptr(), lay.numel,
+        sq.data_ptr(), ws.data_ptr(), ws.numel(), _stream(rs.device)),
+        'fsagg_pairdist_rows_segsq_f32')
+    return sq
+
+
+def pairdist_rows(rs, workspace=None):
+    """Krum's distance matrix D[n][n] (fp32, device) over a row set."""
+    return pairdist_finish(pairdist_rows_segsq(rs, workspace=workspace))
+
+
+def rows_sqnorm(rs, lo=0, hi=None, workspace=None):
+    """[n][nseg] fp64 per-client, per-key Σx² over [lo, hi) (0 for absent
+    keys)."""
+    lib = L.load()
+    unit = lib.fsagg_wsum_chunk_elems(rs.layout.numel)
+    chunks, nchunk = rs.layout.row_chunks(unit, rs.device, lo, hi)
+    need = lib.fsagg_rows_sqnorm_workspace_bytes(rs.n, max(nchunk, 1))
+    ws = (workspace or _WS).get(rs.device, need)
+    sq = torch.empty((rs.n, rs.nseg), dtype=torch.float64, device=rs.device)
+    L.check(lib.fsagg_rows_sqnorm_f32(
+        rs.ptr(), chunks.data_ptr() if chunks is not None else None, nchunk,
+        sq.data_ptr(), ws.data_ptr(), ws.numel(), _stream(rs.device)),
+        'fsagg_rows_sqnorm_f32')
+    return sq

@@ -34,7 +34,7 @@ extern "C" {
 
 typedef void *fsagg_stream_t; /* hipStream_t */
 
-#define FSAGG_VERSION 1
+#define FSAGG_VERSION 2
 
 enum fsagg_status {
   FSAGG_OK = 0,
@@ -302,6 +302,97 @@ int fsagg_gather_rows_f32(const float *const *src, int n, int nseg,
                           const int64_t *key_len, const int32_t *chunk_key,
                           const int64_t *chunk_start, int nchunk,
                           fsagg_stream_t stream);
+
+/*
+ * ---- Client rows read in place ("row sets") ------------------------------
+ * The reference's aggregators index every client's state_dict key by key
+ * (clients_avg_aggregator.py:70-91, median_aggregator.py:45-48,
+ * krum_aggregator.py:48-53); when the uploads are already device tensors
+ * (the reference's multi-GPU mode receives them on cuda:0,
+ * core/parallel/parallel_runner.py:282-293), the kernels below read them
+ * where they lie — no staging copy into a stack.
+ *
+ * A row set addresses client i's value of bucket coordinate p, p inside key
+ * segment s, at  tab[i*si + s*ss][p]  — each entry is a "virtual base":
+ * the key tensor's pointer minus 4 * (the key's bucket offset).  A stacked
+ * slab is the special case ss = 0 (every segment of client i starts at its
+ * row), a [n][nseg] key table is si = nseg, ss = 1.  A NULL entry means the
+ * client lacks that key: the weighted sum skips it (the reference's
+ * `if key not in local_model: continue`), the order statistics and Krum
+ * require every entry.
+ * The bucket is processed as a device array of chunks that never straddle
+ * a key, built once per layout by the caller: chunk c covers coordinates
+ * [lo, lo + len) of segment seg, len <= the call's chunk unit.
+ */
+typedef struct fsagg_rows {
+  const float *const *tab; /* (device) row-pointer table */
+  int64_t si, ss;          /* table strides per client / per segment */
+  int n;                   /* clients */
+  int nseg;                /* key segments */
+} fsagg_rows;
+
+typedef struct fsagg_chunk {
+  int64_t lo;  /* first bucket coordinate */
+  int32_t len; /* coordinates in the chunk */
+  int32_t seg; /* key segment */
+} fsagg_chunk;
+
+/* Chunk unit (coordinates) the weighted-sum row-set kernel expects for a
+ * bucket of `numel` coordinates (its per-lane vector width x 1024). */
+int64_t fsagg_wsum_chunk_elems(int64_t numel);
+
+/*
+ * fsagg_weighted_sum_f32 over a row set: out[p] for every chunk coordinate,
+ * clients in table order, NULL entries skipped (the first present client
+ * initialises the accumulator, as client 0 does in the reference).
+ * base (device) nseg' virtual base pointers with stride base_ss (0: one
+ * entry for every segment), or NULL.  out is a flat bucket.  Every non-NULL
+ * entry, base entry and out must be 16-byte aligned at every chunk start
+ * (chunk lo multiple of 4); chunk_elems = fsagg_wsum_chunk_elems(...).
+ */
+int fsagg_weighted_sum_rows_f32(const fsagg_rows *rows,
+                                const fsagg_chunk *chunks, int nchunk,
+                                int64_t chunk_elems, const float *weights,
+                                const float *prescale,
+                                const float *const *base, int64_t base_ss,
+                                float *out, fsagg_stream_t stream);
+
+/* Coordinate-wise median / trimmed mean over a row set (chunk unit
+ * FSAGG_ROWS_OS_CHUNK, no NULL entries); same results as the flat forms.
+ * numel = the bucket extent (every chunk inside [0, numel)). */
+#define FSAGG_ROWS_OS_CHUNK 256
+int fsagg_coord_median_rows_f32(const fsagg_rows *rows,
+                                const fsagg_chunk *chunks, int nchunk,
+                                int64_t numel, const float *const *base,
+                                int64_t base_ss, float *out,
+                                fsagg_stream_t stream);
+int fsagg_trimmed_mean_rows_f32(const fsagg_rows *rows,
+                                const fsagg_chunk *chunks, int nchunk,
+                                int64_t numel, int k, float divisor,
+                                const float *const *base, int64_t base_ss,
+                                float *out, fsagg_stream_t stream);
+
+/* Krum per-key squared distances over a row set: segment s covers
+ * [seg_lo[s], seg_end[s]) (device int64 arrays; keys may leave gaps between
+ * them, which are never read); numel = the bucket extent (for planning).
+ * Output as fsagg_pairdist_segsq_f32.  Workspace:
+ * fsagg_pairdist_workspace_bytes(n, numel, nseg). */
+int fsagg_pairdist_rows_segsq_f32(const fsagg_rows *rows,
+                                  const int64_t *seg_lo,
+                                  const int64_t *seg_end, int64_t numel,
+                                  double *segsq, void *workspace,
+                                  size_t workspace_bytes,
+                                  fsagg_stream_t stream);
+
+/* Per-(client, key segment) squared L2 norms over a row set in fp64:
+ * sq[i][s] = Σ_{p in s} x_i[p]^2 (0 for a NULL entry), summed in a fixed
+ * order (deterministic).  The norm of NormboundingAggregator's flattened
+ * update over the server keys a client holds (normbounding_aggregator.py:
+ * 35-57).  Any chunk unit.  Workspace: fsagg_rows_sqnorm_workspace_bytes. */
+size_t fsagg_rows_sqnorm_workspace_bytes(int n, int nchunk);
+int fsagg_rows_sqnorm_f32(const fsagg_rows *rows, const fsagg_chunk *chunks,
+                          int nchunk, double *sq, void *workspace,
+                          size_t workspace_bytes, fsagg_stream_t stream);
 
 /*
  * Deterministic synthetic client updates (benchmarks / tests): fills the

@@ -1,0 +1,226 @@
+"""Row sets on the GPU: the clients' own device tensors read in place
+(include/fsagg.h fsagg_rows) must give exactly what the staged stack gives.
+
+* the row-set kernels over a key table equal the same kernels over the
+  stack rows bit for bit, and the flat kernels over the slab (weighted sum,
+  median, trimmed mean: per coordinate, so bit-identical; Krum: the same
+  chunking → identical, the flat form's padded segments → within 1e-6);
+* NULL entries implement the reference's missing-key rule in one launch;
+* the drop-in aggregators take the in-place path for device dicts (no
+  stack is built) and return what they return for host dicts."""
+from collections import OrderedDict
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [1, 0, 1023, 5, 300_001, 3, 7, 65_537, 24_577, 16]
+
+
+def _clients(n, sizes=SIZES, seed=9, scale=1.0):
+    g = torch.Generator(device='cuda').manual_seed(seed)
+    return [OrderedDict(('k%d' % j, scale * torch.randn(
+        sz, device='cuda', generator=g)) for j, sz in enumerate(sizes))
+        for _ in range(n)]
+
+
+def _sets(clients):
+    from federatedscope_amd import ops
+    from federatedscope_amd.layout import BucketLayout, ClientStack
+    lay = BucketLayout(OrderedDict((k, v.cpu()) for k, v in
+                                   clients[0].items()))
+    st = ClientStack(lay, len(clients), 'cuda')
+    st.slab.zero_()
+    st.load_many(clients)
+    ptrs = np.array([[c[k].data_ptr() for k in lay.keys] for c in clients],
+                    dtype=np.int64)
+    keyed = ops.RowSet.from_pointers(lay, ptrs, 'cuda', keepalive=clients)
+    stacked = ops.RowSet.from_stack(st, range(len(clients)))
+    return lay, st, keyed, stacked
+
+
+def _key_ranges(lay, a, b):
+    return all(torch.equal(a[lay.offsets[k]:lay.offsets[k] + lay.numels[k]],
+                           b[lay.offsets[k]:lay.offsets[k] + lay.numels[k]])
+               for k in lay.keys)
+
+
+@pytest.mark.parametrize('n', [1, 13, 100])
+def test_weighted_sum_rows_matches_flat(n):
+    from federatedscope_amd import ops
+    clients = _clients(n)
+    lay, st, keyed, stacked = _sets(clients)
+    rng = np.random.default_rng(n)
+    w = [float(x) for x in rng.random(n)]
+    pre = [float(x) for x in rng.random(n) + 0.5]
+    base = torch.randn(lay.numel, device='cuda')
+    outs = []
+    for rs in (keyed, stacked):
+        for kw in ({}, {'prescale': pre},
+                   {'base': ops.BaseRows.from_bucket(base)}):
+            o = torch.full((lay.numel, ), 7.0, device='cuda')
+            ops.weighted_sum_rows(rs, w, o, **kw)
+            outs.append(o)
+    flat = []
+    for kw in ({}, {'prescale': pre}, {'base': base}):
+        o = torch.full((lay.numel, ), 7.0, device='cuda')
+        ops.weighted_sum(ops.RowTable.from_slab(st.slab, numel=lay.numel),
+                         w, o, **kw)
+        flat.append(o)
+    for i in range(3):
+        assert _key_ranges(lay, outs[i], flat[i])
+        assert _key_ranges(lay, outs[3 + i], flat[i])
+    # and the first against the oracle's op order
+    want = O.para_weighted_avg([(0, OrderedDict((k, v.cpu().numpy())
+                                                for k, v in c.items()))
+                                for c in clients], weights=w)
+    got = lay.unpack(outs[0])
+    for k in lay.keys:
+        assert got[k].cpu().numpy().tobytes() == want[k].tobytes(), k
+
+
+def test_weighted_sum_rows_missing_keys_one_launch():
+    """NULL entries: each key reduced over the clients that hold it, the
+    weights not renormalised (clients_avg_aggregator.py:74-75)."""
+    from federatedscope_amd import ops
+    n = 9
+    clients = _clients(n, seed=4)
+    lay, st, _, _ = _sets(clients)
+    ptrs = np.array([[c[k].data_ptr() for k in lay.keys] for c in clients],
+                    dtype=np.int64)
+    drop = [(3, 'k2'), (5, 'k4'), (8, 'k4'), (1, 'k0'), (6, 'k8')]
+    for i, k in drop:
+        ptrs[i, lay.keys.index(k)] = 0
+    rs = ops.RowSet.from_pointers(lay, ptrs, 'cuda', keepalive=clients)
+    assert rs.missing == len(drop)
+    w = [float(x) for x in np.random.default_rng(1).random(n)]
+    out = torch.zeros(lay.numel, device='cuda')
+    ops.weighted_sum_rows(rs, w, out)
+    host = [(0, OrderedDict((k, v.cpu().numpy()) for k, v in c.items()
+                            if (i, k) not in drop))
+            for i, c in enumerate(clients)]
+    want = O.para_weighted_avg(host, weights=w)
+    got = lay.unpack(out)
+    for k in lay.keys:
+        assert got[k].cpu().numpy().tobytes() == want[k].tobytes(), k
+    with pytest.raises(KeyError):
+        ops.coord_median_rows(rs, out)
+
+
+@pytest.mark.parametrize('n', [7, 64, 100, 200])
+def test_order_statistics_rows_match_flat(n):
+    from federatedscope_amd import ops
+    sizes = [1, 1023, 5, 70_001, 3, 257]
+    clients = _clients(n, sizes=sizes, seed=n)
+    lay, st, keyed, stacked = _sets(clients)
+    base = torch.randn(lay.numel, device='cuda')
+    rows = ops.RowTable.from_slab(st.slab, numel=lay.numel)
+    k = int(n * 0.2)
+    for rs in (keyed, stacked):
+        a = torch.full((lay.numel, ), 3.0, device='cuda')
+        b = torch.full((lay.numel, ), 3.0, device='cuda')
+        ops.coord_median_rows(rs, a, base=ops.BaseRows.from_bucket(base))
+        ops.coord_median(rows, b, base=base)
+        assert _key_ranges(lay, a, b)
+        ops.trimmed_mean_rows(rs, k, a)
+        ops.trimmed_mean(rows, k, b)
+        assert _key_ranges(lay, a, b)
+        ops.trimmed_mean_rows(rs, k, a, divisor=3.0,
+                              base=ops.BaseRows.from_bucket(base))
+        ops.trimmed_mean(rows, k, b, divisor=3.0, base=base)
+        assert _key_ranges(lay, a, b)
+
+
+@pytest.mark.parametrize('n', [5, 50])
+def test_pairdist_rows(n):
+    from federatedscope_amd import ops
+    clients = _clients(n, sizes=[1, 1023, 5, 300_001, 3, 65_537], seed=2,
+                       scale=0.1)
+    lay, st, keyed, stacked = _sets(clients)
+    D1 = ops.pairdist_rows(keyed)
+    D2 = ops.pairdist_rows(stacked)
+    assert torch.equal(D1, D2)     # same chunking → same sums
+    D3 = ops.pairdist(ops.RowTable.from_slab(st.slab, numel=lay.numel),
+                      lay.segments())
+    off = ~torch.eye(n, dtype=torch.bool, device='cuda')
+    assert torch.allclose(D1[off], D3[off], rtol=1e-6, atol=0)
+    X = [np.concatenate([c[k].cpu().numpy().astype(np.float64).ravel()
+                         for k in lay.keys]) for c in clients]
+    sq = ops.rows_sqnorm(keyed).cpu().numpy()
+    for i in range(n):
+        for s, k in enumerate(lay.keys):
+            v = clients[i][k].cpu().numpy().astype(np.float64)
+            assert sq[i, s] == pytest.approx((v * v).sum(), rel=1e-12,
+                                             abs=1e-300)
+        assert sq[i].sum() == pytest.approx((X[i] ** 2).sum(), rel=1e-12)
+
+
+def _cfg(**kw):
+    bft = SimpleNamespace(krum_agg_num=kw.get('agg_num', 3),
+                          trimmedmean_excluded_ratio=0.2,
+                          normbounding_norm_bound=kw.get('bound', 5.0))
+    return SimpleNamespace(
+        federate=SimpleNamespace(ignore_weight=False, use_ss=False,
+                                 client_num=kw.get('client_num', 1000),
+                                 sample_client_rate=1.0),
+        aggregator=SimpleNamespace(byzantine_node_num=kw.get('f', 2),
+                                   BFT_args=bft),
+        asyn=SimpleNamespace(staleness_discount_factor=1.0))
+
+
+def test_dropin_device_dicts_read_in_place():
+    """Device dicts → no ClientStack is built; the results equal the host
+    dicts' (staged) results bit for bit, for every rule; the server model
+    on the device is read in place too."""
+    from federatedscope_amd.core.aggregators import (
+        BulyanAggregator, ClientsAvgAggregator, KrumAggregator,
+        MedianAggregator, NormboundingAggregator, TrimmedmeanAggregator)
+    n = 23
+    sizes = [(5, 3), (1, ), (130, ), (33, 2), (4097, )]
+    g = torch.Generator().manual_seed(21)
+    host = [(int(torch.randint(1, 90, (1, ), generator=g)), OrderedDict(
+        ('p%d' % j, 0.1 * torch.randn(s, generator=g))
+        for j, s in enumerate(sizes))) for _ in range(n)]
+    dev = [(s, OrderedDict((k, v.cuda()) for k, v in d.items()))
+           for s, d in host]
+    init_h = OrderedDict(('p%d' % j, torch.randn(s, generator=g))
+                         for j, s in enumerate(sizes))
+    init_d = OrderedDict((k, v.cuda()) for k, v in init_h.items())
+
+    class M(torch.nn.Module):
+        def __init__(self, sd):
+            super().__init__()
+            self.sd = sd
+
+        def state_dict(self, *a, **kw):
+            return self.sd
+
+    rules = [(ClientsAvgAggregator, {}), (KrumAggregator, {}),
+             (BulyanAggregator, {'f': 4, 'client_num': n}),
+             (MedianAggregator, {}), (TrimmedmeanAggregator, {}),
+             (NormboundingAggregator, {'bound': 0.5})]
+    for cls, kw in rules:
+        a = cls(model=M(init_d), device='cuda', config=_cfg(**kw))
+        got = a.aggregate({'client_feedback': dev, 'recover_fun': None})
+        assert not a._stacks, cls          # nothing staged
+        b = cls(model=M(init_h), device='cuda', config=_cfg(**kw))
+        want = b.aggregate({'client_feedback': host, 'recover_fun': None})
+        assert list(got) == list(want)
+        for k in want:
+            assert got[k].device.type == 'cuda'
+            assert torch.equal(got[k].cpu(), want[k]), (cls.__name__, k)
+    # an unaligned view (4-B offset) is staged instead, same result
+    off = [(s, OrderedDict((k, torch.cat([torch.zeros(1, device='cuda'),
+                                           v.reshape(-1)])[1:].view(v.shape))
+                           for k, v in d.items())) for s, d in dev]
+    a = ClientsAvgAggregator(device='cuda', config=_cfg())
+    got = a.aggregate({'client_feedback': off, 'recover_fun': None})
+    want = ClientsAvgAggregator(device='cuda', config=_cfg()).aggregate(
+        {'client_feedback': host, 'recover_fun': None})
+    for k in want:
+        assert torch.equal(got[k].cpu(), want[k]), k

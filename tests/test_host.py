@@ -32,7 +32,7 @@ def test_library_exports_header():
     for s in syms:
         assert hasattr(lib, s), s
     assert sorted(_lib.SIGNATURES) == syms
-    assert lib.fsagg_version() == 1
+    assert lib.fsagg_version() == 2
 
 
 def test_library_rejects_bad_args_without_gpu():
@@ -46,6 +46,34 @@ def test_library_rejects_bad_args_without_gpu():
     assert lib.fsagg_pairdist_workspace_bytes(50, 6603902, 12) > 0
     # trimmed mean with 2k >= n is rejected before any launch
     assert lib.fsagg_trimmed_mean_f32(1, 4, 10, 2, 0.0, None, 1, None) == -1
+    # row-set entry points reject a missing table / a bad chunk unit
+    rows = _lib.Rows(0, 1, 0, 4, 1)
+    assert lib.fsagg_weighted_sum_rows_f32(rows, None, 0, 1024, 1, None,
+                                           None, 0, 16, None) == -1
+    rows = _lib.Rows(16, 1, 0, 4, 1)
+    assert lib.fsagg_weighted_sum_rows_f32(rows, 16, 3, 1000, 16, None,
+                                           None, 0, 16, None) == -1
+    assert b'chunk_elems' in lib.fsagg_last_error()
+    assert lib.fsagg_trimmed_mean_rows_f32(rows, 16, 3, 100, 2, 1.0, None,
+                                           0, 16, None) == -1
+    assert lib.fsagg_wsum_chunk_elems(25_000_000) == 24 * 1024
+    assert lib.fsagg_wsum_chunk_elems(1000) == 1024
+
+
+def test_host_extension_key_table_without_gpu():
+    """csrc/host/keytable.cpp: CPU tensors (or non-dicts) are not device
+    rows: None, and the caller stages instead."""
+    import torch
+    from federatedscope_amd import _lib
+    h = _lib.host()
+    d = [{'a': torch.zeros(3), 'b': torch.zeros(2, 2)} for _ in range(3)]
+    assert h.key_table(d, ['a', 'b'], [(3, ), (2, 2)], 0) is None
+    assert h.key_table([object()], ['a'], [(3, )], 0) is None
+    # no keys at all: an empty table
+    raw, missing, aligned = h.key_table(d, [], [], 0)
+    assert raw == b'' and missing == 0 and aligned
+    with pytest.raises(ValueError):
+        h.key_table(d, ['a'], [], 0)
 
 
 def test_bucket_layout_alignment_and_dtypes():
