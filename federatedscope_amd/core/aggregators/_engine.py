@@ -160,7 +160,8 @@ class DeviceEngine:
         packed device bucket."""
         if isinstance(model, dict):
             kt = self._key_table(layout, [model])
-            if kt is not None and kt[1] and (kt[0] != 0).all():
+            if kt is not None and kt[1] and \
+                    not ops.absent(layout, kt[0]).any():
                 return ops.BaseRows.from_pointers(layout, kt[0][0],
                                                   self.compute_device,
                                                   keepalive=(model, ))
@@ -254,8 +255,9 @@ class DeviceEngine:
             kt = self._key_table(layout, dicts)
             if kt is not None and kt[1]:
                 ptrs = kt[0]
-                if require_all and not (ptrs != 0).all():
-                    i, s = [int(x[0]) for x in (ptrs == 0).nonzero()]
+                gone = ops.absent(layout, ptrs)
+                if require_all and gone.any():
+                    i, s = [int(x[0]) for x in gone.nonzero()]
                     raise KeyError('client %d lacks key %r' %
                                    (i, layout.keys[s]))
                 return StagedSet(layout, ops.RowSet.from_pointers(

@@ -597,6 +597,25 @@ import numpy as _np  # noqa: E402
 CHUNK_DTYPE = _np.dtype([('lo', '<i8'), ('len', '<i4'), ('seg', '<i4')])
 
 
+def _cuda_index(device):
+    d = torch.device(device)
+    if d.type == 'cuda' and d.index is None:
+        d = torch.device('cuda', torch.cuda.current_device())
+    return d
+
+
+def absent(layout, table):
+    """[n][m] bool: the NULL entries of a row table that name a non-empty
+    key (an empty tensor's NULL pointer is never dereferenced: no chunk
+    covers it)."""
+    table = _np.asarray(table)
+    if table.shape[1] == 1:
+        return table == 0
+    nonempty = _np.array([layout.numels[k] > 0 for k in layout.keys],
+                         dtype=bool)
+    return (table == 0) & nonempty[None, :]
+
+
 class RowSet:
     """``n`` clients x the fp32 key segments of a :class:`BucketLayout`,
     addressed in place (struct fsagg_rows): entry (i, s) is client i's
@@ -613,17 +632,20 @@ class RowSet:
         self.host = table
         self.n = table.shape[0]
         self.nseg = max(len(layout.keys), 1)
+        # on the device the table is segment-major: one chunk's n client
+        # pointers are contiguous (batched scalar loads, a small
+        # scalar-cache footprint per workgroup)
         if table.shape[1] == 1:
             self.si, self.ss = 1, 0
         elif table.shape[1] == self.nseg:
-            self.si, self.ss = self.nseg, 1
+            self.si, self.ss = 1, self.n
         else:
             raise ValueError('row table has %d columns for %d keys' %
                              (table.shape[1], self.nseg))
-        self.device = torch.device(device)
+        self.device = _cuda_index(device)
         self.aligned16 = bool(aligned16)
-        self.missing = int((table == 0).sum())
-        self.tab = _h2d_np(table, self.device)
+        self.missing = int(absent(layout, table).sum())
+        self.tab = _h2d_np(table.T, self.device)
         self.struct = L.Rows(self.tab.data_ptr(), self.si, self.ss, self.n,
                              self.nseg)
         self._keep = tuple(keepalive)
@@ -689,7 +711,7 @@ class BaseRows:
         offs = _np.array([layout.offsets[k] for k in layout.keys],
                          dtype=_np.int64)
         virt = ptrs - 4 * offs
-        return cls(_h2d_np(virt, device), 1,
+        return cls(_h2d_np(virt, _cuda_index(device)), 1,
                    keepalive=keepalive)
 
     def ptr(self):
