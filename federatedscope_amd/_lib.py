@@ -87,8 +87,7 @@ SIGNATURES['fsagg_gather_rows_f32'] = (
 
 class Rows(ctypes.Structure):
     """struct fsagg_rows (include/fsagg.h): a row set's pointer table."""
-    _fields_ = [('tab', _c_p), ('si', _c_i64), ('ss', _c_i64), ('n', _c_i),
-                ('nseg', _c_i)]
+    _fields_ = [('tab', _c_p), ('ss', _c_i64), ('n', _c_i), ('nseg', _c_i)]
 
 
 _rows_p = ctypes.POINTER(Rows)

@@ -58,21 +58,36 @@ def _first_device(model):
 
 
 class StagedSet:
-    """The client list of one aggregate() call as a row set: client i's
-    key s is ``rs`` entry (i, s) — a slot of a ClientStack (staged uploads)
-    or the client's own device tensor (read in place)."""
+    """The client list of one aggregate() call as row sets.  Unsharded: one
+    piece, the whole bucket, whose row set is a slot of a ClientStack
+    (staged uploads) or the clients' own device tensors (read in place).
+    Sharded by parameter range: this rank's pieces of the
+    bucket, each (j, lo, hi, rows), plus the PipelinedAssembly ``plan``
+    that all-gathers the pieces of every rank."""
 
-    def __init__(self, layout, rs, stack=None, slots=None):
+    def __init__(self, layout, rs=None, stack=None, slots=None, pieces=None,
+                 plan=None):
         self.layout = layout
         self.rs = rs
-        self.n = rs.n
         self.stack = stack
         self.slots = slots
+        self.plan = plan
+        self.pieces = pieces if pieces is not None else \
+            [(0, 0, layout.numel, rs)]
+        self.n = self.pieces[0][3].n
 
     def rows(self, sel=None):
         """The clients ``sel`` (indices into the client list, in reduction
-        order; default all) as a RowSet."""
+        order; default all) as one RowSet over the whole bucket."""
+        if self.plan is not None or self.rs is None:
+            raise RuntimeError('a sharded client set has per-piece rows')
         return self.rs if sel is None else self.rs.subset(sel)
+
+    def subset(self, sel):
+        """The clients ``sel`` in the new reduction order (every piece)."""
+        rs = None if self.rs is None else self.rs.subset(sel)
+        pieces = [(j, lo, hi, r.subset(sel)) for j, lo, hi, r in self.pieces]
+        return StagedSet(self.layout, rs, pieces=pieces, plan=self.plan)
 
 
 class DeviceEngine:
@@ -84,6 +99,79 @@ class DeviceEngine:
         self._layouts = {}
         self._fast_layouts = {}
         self._stacks = {}
+        self._plans = {}
+
+    # -- parameter-range sharding across the ranks of a process group --------
+    def _shard(self):
+        """(Comm, chunks) when the config asks for the aggregation to be
+        sharded by parameter range over the default process group
+        (``aggregator.shard_by_param_range``, pipelined over
+        ``aggregator.shard_chunks`` rounds) and that group has > 1 rank;
+        else None.  Every rank then calls aggregate() with the same client
+        list (SPMD) and receives the full result."""
+        agg = getattr(getattr(self, 'cfg', None), 'aggregator', None)
+        if not getattr(agg, 'shard_by_param_range', False):
+            return None
+        import torch.distributed as dist
+        if not dist.is_initialized() or dist.get_world_size() == 1:
+            return None
+        from ..sharding import Comm
+        comm = self.__dict__.get('_comm')
+        if comm is None:
+            comm = self._comm = Comm()
+        return comm, int(getattr(agg, 'shard_chunks', 2) or 1)
+
+    def _plan(self, layout, comm, chunks):
+        from ..sharding import PipelinedAssembly
+        key = (layout.signature(), chunks)
+        pa = self._plans.get(key)
+        if pa is None:
+            pa = self._plans[key] = PipelinedAssembly(layout.numel,
+                                                      chunks=chunks,
+                                                      comm=comm)
+        return pa
+
+    def _run_pieces(self, st, fn):
+        """Flat result bucket on the compute device from fn(rows, out, lo,
+        hi) over the set's pieces; sharded, the ranks' pieces are
+        all-gathered (the gather of round j overlapping round j+1) so every
+        rank holds the whole bucket.  Coordinates are bucket coordinates."""
+        dev = self.compute_device
+        if st.plan is None:
+            out = torch.empty(st.layout.numel, dtype=torch.float32,
+                              device=dev)
+            for _, lo, hi, rs in st.pieces:
+                fn(rs, out, lo, hi)
+            return out
+        out = torch.empty(st.plan.padded, dtype=torch.float32, device=dev)
+        rows = {j: rs for j, _, _, rs in st.pieces}
+        st.plan.run(lambda j, lo, hi, view: fn(rows[j], out, lo, hi),
+                    out=out)
+        return out
+
+    def _sum_pieces(self, st, fn):
+        """Σ over this rank's pieces of fn(rows, lo, hi), summed across the
+        ranks when sharded (the exchange Krum and norm bounding need)."""
+        acc = None
+        for _, lo, hi, rs in st.pieces:
+            if hi <= lo and acc is not None:
+                continue
+            v = fn(rs, lo, max(hi, lo))
+            acc = v if acc is None else acc.add_(v)
+        if st.plan is not None:
+            st.plan.comm.all_reduce_sum(acc)
+        return acc
+
+    def _pairdist(self, st):
+        """Krum's distance matrix D (fp32 [n][n], device) of a client set."""
+        segsq = self._sum_pieces(
+            st, lambda rs, lo, hi: ops.pairdist_rows_segsq(rs, lo, hi))
+        return ops.pairdist_finish(segsq)
+
+    def _sqnorms(self, st):
+        """[n][nseg] fp64 per-client, per-key squared norms."""
+        return self._sum_pieces(
+            st, lambda rs, lo, hi: ops.rows_sqnorm(rs, lo, hi))
 
     @property
     def compute_device(self):
@@ -200,13 +288,11 @@ class DeviceEngine:
         st = staged if staged is not None else self._staged(
             models, as_float=as_float)
         layout = st.layout
-        out = torch.empty(layout.numel, dtype=torch.float32,
-                          device=self.compute_device)
         base = None
         if base_model is not None:
             base = self._base(layout, base_model, as_float=as_float)
-        ops.weighted_sum_rows(st.rows(), weights, out, prescale=prescale,
-                              base=base)
+        out = self._run_pieces(st, lambda rs, o, lo, hi: ops.weighted_sum_rows(
+            rs, weights, o, prescale=prescale, base=base, lo=lo, hi=hi))
         extra = OrderedDict()
         for k, dt in layout.other.items():
             have = [i for i in range(n) if k in dicts[i]]
@@ -222,9 +308,45 @@ class DeviceEngine:
         return layout, out, extra, list(template.keys())
 
     def _staged(self, models, as_float=False, require_all=False):
-        """The client list as a row set: slots DeviceIngress staged on
+        """The client list as row sets (sharded by parameter range when the
+        config asks for it, see :meth:`_shard`)."""
+        sh = self._shard()
+        st = self._staged_rows(models, as_float, require_all,
+                               whole=sh is None)
+        if sh is None:
+            return st
+        comm, chunks = sh
+        plan = self._plan(st.layout, comm, chunks)
+        spans = plan.local_pieces()
+        if st.rs is not None:          # whole-bucket rows: restrict
+            pieces = [(j, lo, hi, st.rs) for j, (lo, hi) in enumerate(spans)]
+            return StagedSet(st.layout, st.rs, pieces=pieces, plan=plan)
+        # host (or foreign-device) dicts: stage this rank's pieces only
+        from ...layout import RangeStack
+        dicts = [m for _, m in models]
+        if as_float:
+            dicts = [OrderedDict((k, as_float_tensor(v))
+                                 for k, v in m.items()) for m in dicts]
+        key = ('range', st.layout.signature(), chunks)
+        rst = self._stacks.get(key)
+        if rst is None or rst.capacity < len(dicts):
+            rst = RangeStack(st.layout, spans, len(dicts),
+                             self.compute_device)
+            self._stacks[key] = rst
+        rst.load_many(dicts)
+        present = st.slots          # the presence matrix (see below)
+        pieces = [(j, lo, hi, ops.RowSet.from_stack(
+            rst, range(len(dicts)), present=present, offset=rst.offset(j)))
+            for j, (lo, hi) in enumerate(spans)]
+        return StagedSet(st.layout, pieces=pieces, plan=plan)
+
+    def _staged_rows(self, models, as_float=False, require_all=False,
+                     whole=True):
+        """The client list as one row set: slots DeviceIngress staged on
         arrival, the clients' own device tensors read in place, or (host
-        dicts, other devices, other dtypes) rows of a device stack."""
+        dicts, other devices, other dtypes) rows of a device stack.  With
+        ``whole=False`` the stack is not built: the StagedSet then carries
+        only the layout and, in ``slots``, the key-presence matrix."""
         from ..workers.ingress import StagedUpdate
         dicts = [m for _, m in models]
         # every staged slot must have landed before anything reads it, on
@@ -270,6 +392,9 @@ class DeviceEngine:
                 for k, ok in zip(layout.keys, row):
                     if not ok:
                         raise KeyError('client %d lacks key %r' % (i, k))
+        if not whole:
+            return StagedSet(layout, slots=present,
+                             pieces=[(0, 0, 0, _NoRows(len(dicts)))])
         stack = self._stack(layout, dicts, as_float=as_float)
         slots = list(range(len(dicts)))
         return StagedSet(layout, ops.RowSet.from_stack(stack, slots,
@@ -279,6 +404,13 @@ class DeviceEngine:
     def _stage_all(self, models, as_float=True):
         """Pack every client (robust rules need all keys in all clients)."""
         return self._staged(models, as_float=as_float, require_all=True)
+
+
+class _NoRows:
+    """Placeholder rows of a not-yet-staged client set (client count)."""
+
+    def __init__(self, n):
+        self.n = n
 
 
 def _as_float_proto(v):

@@ -24,7 +24,7 @@ class BulyanAggregator(ClientsAvgAggregator):
         st = self._stage_all(models)
         layout = st.layout
         n = len(models)
-        D = ops.pairdist_rows(st.rows()).cpu()
+        D = self._pairdist(st).cpu()
         scores = krum_scores(D, self.byzantine_node_num)
         index_order = torch.sort(scores)[1].numpy()
         keep = n - int(2 * self.sample_client_rate * self.byzantine_node_num)
@@ -33,7 +33,7 @@ class BulyanAggregator(ClientsAvgAggregator):
         k = int(self.sample_client_rate * self.byzantine_node_num)
         gamma = len(sel) - 2 * k
         base = self._base(layout, self.model.state_dict(), as_float=True)
-        out = torch.empty(layout.numel, dtype=torch.float32,
-                          device=self.compute_device)
-        ops.trimmed_mean_rows(st.rows(sel), k, out, divisor=gamma, base=base)
+        out = self._run_pieces(st.subset(sel), lambda rs, o, lo, hi:
+                               ops.trimmed_mean_rows(rs, k, o, divisor=gamma,
+                                                     base=base, lo=lo, hi=hi))
         return self._emit(layout, out, list(models[0][1].keys()), out_dev)

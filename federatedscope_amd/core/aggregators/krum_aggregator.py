@@ -40,7 +40,7 @@ class KrumAggregator(ClientsAvgAggregator):
     def distance_matrix(self, models):
         """D (host fp32 [n, n]) as _calculate_score fills it (:58-73)."""
         st = self._stage_all(models)
-        return ops.pairdist_rows(st.rows()).cpu(), st
+        return self._pairdist(st).cpu(), st
 
     def _calculate_score(self, models):
         D, _ = self.distance_matrix([(0, m) for m in models])
@@ -56,7 +56,7 @@ class KrumAggregator(ClientsAvgAggregator):
         sizes = [models[i][0] for i in sel]
         weights = fedavg_weights(sizes, self.cfg.federate.ignore_weight)
         base = self._base(layout, self.model.state_dict(), as_float=True)
-        out = torch.empty(layout.numel, dtype=torch.float32,
-                          device=self.compute_device)
-        ops.weighted_sum_rows(st.rows(sel), weights, out, base=base)
+        out = self._run_pieces(st.subset(sel), lambda rs, o, lo, hi:
+                               ops.weighted_sum_rows(rs, weights, o,
+                                                     base=base, lo=lo, hi=hi))
         return layout, out, list(models[0][1].keys())

@@ -2,8 +2,6 @@
 median_aggregator.py:10-52) on the GPU: fsagg_coord_median_rows_f32 computes
 (median(T) - median(-T))/2 per coordinate (bit-exact) and adds the server's
 init model in the same kernel."""
-import torch
-
 from ... import ops
 from ._engine import _first_device
 from .clients_avg_aggregator import ClientsAvgAggregator
@@ -22,7 +20,6 @@ class MedianAggregator(ClientsAvgAggregator):
         st = self._stage_all(models)
         layout = st.layout
         base = self._base(layout, self.model.state_dict(), as_float=True)
-        out = torch.empty(layout.numel, dtype=torch.float32,
-                          device=self.compute_device)
-        ops.coord_median_rows(st.rows(), out, base=base)
+        out = self._run_pieces(st, lambda rs, o, lo, hi: ops.coord_median_rows(
+            rs, o, base=base, lo=lo, hi=hi))
         return self._emit(layout, out, list(models[0][1].keys()), out_dev)

@@ -31,7 +31,7 @@ class NormboundingAggregator(ClientsAvgAggregator):
                 'norm bounding with client keys that differ from the server '
                 'model keys')
         n = len(models)
-        sq = ops.rows_sqnorm(st.rows()).sum(1).cpu().numpy()
+        sq = self._sqnorms(st).sum(1).cpu().numpy()
         pre = []
         bound32 = np.float32(self.norm_bound)
         for i in range(n):

@@ -2,8 +2,6 @@
 trimmedmean_aggregator.py:10-57) on the GPU: drop the k = int(n·ratio)
 largest and smallest of each coordinate, average the rest, add init — one
 fsagg_trimmed_mean_rows_f32 launch over the clients' rows."""
-import torch
-
 from ... import ops
 from ._engine import _first_device
 from .clients_avg_aggregator import ClientsAvgAggregator
@@ -27,7 +25,6 @@ class TrimmedmeanAggregator(ClientsAvgAggregator):
         n = len(models)
         k = int(n * self.excluded_ratio)
         base = self._base(layout, self.model.state_dict(), as_float=True)
-        out = torch.empty(layout.numel, dtype=torch.float32,
-                          device=self.compute_device)
-        ops.trimmed_mean_rows(st.rows(), k, out, base=base)
+        out = self._run_pieces(st, lambda rs, o, lo, hi: ops.trimmed_mean_rows(
+            rs, k, o, base=base, lo=lo, hi=hi))
         return self._emit(layout, out, list(models[0][1].keys()), out_dev)

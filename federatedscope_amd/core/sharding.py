@@ -41,6 +41,50 @@ def local_segments(seg_offsets, lo, hi):
     return [min(max(int(o), lo), hi) - lo for o in seg_offsets]
 
 
+class Comm:
+    """The sharded path's two collectives over a torch.distributed group.
+
+    On RCCL ("nccl", xGMI) device tensors go to the collective directly.
+    The gloo backend (CPU tests, two ranks sharing one GPU in the GPU
+    tests) takes host tensors: device operands are staged through host
+    memory and the call completes synchronously."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() \
+            else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.backend = dist.get_backend(group) if dist.is_initialized() \
+            else None
+        self.host_staged = self.backend == 'gloo'
+
+    def all_gather_into(self, out, inp, async_op=False):
+        """out = cat of every rank's ``inp`` (equal sizes), in rank order.
+        Returns a work handle when asynchronous, else None."""
+        if self.world == 1:
+            out.copy_(inp)
+            return None
+        if not (self.host_staged and inp.device.type == 'cuda'):
+            return dist.all_gather_into_tensor(out, inp, group=self.group,
+                                               async_op=async_op)
+        ci = inp.detach().cpu()
+        parts = [torch.empty_like(ci) for _ in range(self.world)]
+        dist.all_gather(parts, ci, group=self.group)
+        out.copy_(torch.cat(parts))
+        return None
+
+    def all_reduce_sum(self, t):
+        if self.world == 1:
+            return t
+        if self.host_staged and t.device.type == 'cuda':
+            c = t.detach().cpu()
+            dist.all_reduce(c, op=dist.ReduceOp.SUM, group=self.group)
+            t.copy_(c)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
+
+
 def assemble(shard, ranges, numel=None, group=None):
     """All-gather disjoint output shards into the full vector (every rank)."""
     world = dist.get_world_size(group)
@@ -121,13 +165,13 @@ class PipelinedAssembly:
     single-GPU reduction; the only traffic is the output itself (4·P bytes,
     ring all-gather over xGMI)."""
 
-    def __init__(self, numel, chunks=4, group=None, align=ALIGN):
+    def __init__(self, numel, chunks=4, group=None, align=ALIGN, comm=None):
         if chunks < 1:
             raise ValueError('chunks must be >= 1')
-        self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() \
-            else 1
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.comm = comm if comm is not None else Comm(group)
+        self.group = self.comm.group
+        self.world = self.comm.world
+        self.rank = self.comm.rank
         self.numel = int(numel)
         self.chunks = int(chunks)
         per = self.world * self.chunks
@@ -166,9 +210,11 @@ class PipelinedAssembly:
             if hi > lo:
                 compute(j, lo, hi, out[slot:slot + (hi - lo)])
             if W > 1:
-                works.append(dist.all_gather_into_tensor(
+                w = self.comm.all_gather_into(
                     out[j * W * pc:(j + 1) * W * pc], out[slot:slot + pc],
-                    group=self.group, async_op=True))
+                    async_op=True)
+                if w is not None:
+                    works.append(w)
         for w in works:
             w.wait()
         return out[:self.numel]

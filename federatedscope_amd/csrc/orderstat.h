@@ -96,10 +96,10 @@ enum Mode { kMedian = 0, kTrimmed = 1 };
 // nullptr): block b covers [b·kBlock, …) of [0, numel) and client j's row
 // is tab[j]; row-set form (include/fsagg.h fsagg_rows): block b is chunk b
 // (one key segment, <= kBlock coordinates) and client j's row of segment
-// seg is tab[j·si + seg·ss] (a virtual base: coordinate p is row[p]).
+// seg is tab[seg·ss + j] (a virtual base: coordinate p is row[p]).
 struct RowSrc {
   const float *const *tab;
-  int64_t si, ss;
+  int64_t ss;
   const fsagg_chunk *chunks;
   int64_t numel;
   const float *base;          // flat base (tab form), or
@@ -108,8 +108,7 @@ struct RowSrc {
 };
 
 struct BlockRows {
-  const float *const *rows;  // client j: rows[j * si]
-  int64_t si;
+  const float *const *rows;  // client j: rows[j]
   int64_t lo;                // first coordinate
   int len;                   // live lanes
   const float *base;
@@ -128,7 +127,6 @@ __device__ __forceinline__ BlockRows block_rows(const RowSrc &rs, int b) {
     br.len = r < kBlock ? int(r) : kBlock;
   }
   br.rows = rs.tab + int64_t(seg) * rs.ss;
-  br.si = rs.si;
   br.base = rs.btab ? rs.btab[int64_t(seg) * rs.bss] : rs.base;
   return br;
 }

@@ -27,14 +27,12 @@ namespace {
 // — a per-row `if (j < n)` splits the loop into N basic blocks and every
 // load then waits out its own HBM round trip.
 template <int N>
-__device__ __forceinline__ void load_column(const float *const *rows,
-                                            int64_t si, int n, int64_t p,
-                                            uint32_t (&k)[N], bool &nan,
-                                            bool &nonfinite) {
+__device__ __forceinline__ void load_column(const float *const *rows, int n,
+                                            int64_t p, uint32_t (&k)[N],
+                                            bool &nan, bool &nonfinite) {
   float x[N];
 #pragma unroll
-  for (int j = 0; j < N; ++j)
-    x[j] = gld_nt(rows[(j < n ? j : n - 1) * si] + p);
+  for (int j = 0; j < N; ++j) x[j] = gld_nt(rows[j < n ? j : n - 1] + p);
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     const bool real = j < n;
@@ -53,7 +51,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_reg_kernel(
   const float *__restrict__ base = br.base;
   uint32_t k[N];
   bool nan = false, nonfinite = false;
-  load_column<N>(br.rows, br.si, n, p, k, nan, nonfinite);
+  load_column<N>(br.rows, n, p, k, nan, nonfinite);
   bitonic_sort<N>(k);
   using Seq = std::make_integer_sequence<int, N>;
   float r;
@@ -78,14 +76,13 @@ __global__ __launch_bounds__(kBlock) void orderstat_reg_kernel(
 
 // ---- generic n: radix select (binary search on the key bits) -----------
 __device__ __forceinline__ uint32_t select_rank(const float *const *rows,
-                                                int64_t si, int n, int64_t p,
-                                                int rank) {
+                                                int n, int64_t p, int rank) {
   // smallest key v such that #(key <= v) > rank
   uint32_t prefix = 0;
   for (int bit = 31; bit >= 0; --bit) {
     const uint32_t cand = prefix | ((1u << bit) - 1u);  // all lower bits set
     int cnt = 0;
-    for (int j = 0; j < n; ++j) cnt += f2key(gld(rows[j * si] + p)) <= cand;
+    for (int j = 0; j < n; ++j) cnt += f2key(gld(rows[j] + p)) <= cand;
     if (cnt <= rank) prefix |= 1u << bit;
   }
   return prefix;
@@ -98,30 +95,29 @@ __global__ __launch_bounds__(kBlock) void orderstat_generic_kernel(
   if (int(threadIdx.x) >= br.len) return;
   const int64_t p = br.lo + threadIdx.x;
   const float *const *__restrict__ rows = br.rows;
-  const int64_t si = br.si;
   const float *__restrict__ base = br.base;
   bool nan = false, nonfinite = false;
   for (int j = 0; j < n; ++j) {
-    const float x = gld(rows[j * si] + p);
+    const float x = gld(rows[j] + p);
     nan |= __builtin_isnan(x);
     nonfinite |= !__builtin_isfinite(x);
   }
   float r;
   if constexpr (MODE == kMedian) {
-    const float lo = key2f(select_rank(rows, si, n, p, (n - 1) / 2));
-    const float hi = key2f(select_rank(rows, si, n, p, n / 2));
+    const float lo = key2f(select_rank(rows, n, p, (n - 1) / 2));
+    const float hi = key2f(select_rank(rows, n, p, n / 2));
     r = __fdiv_rn(lo - (-hi), 2.0f);
     if (nan) r = __builtin_nanf("");
   } else {
-    const uint32_t klo = select_rank(rows, si, n, p, kk);
-    const uint32_t khi = select_rank(rows, si, n, p, n - kk - 1);
+    const uint32_t klo = select_rank(rows, n, p, kk);
+    const uint32_t khi = select_rank(rows, n, p, n - kk - 1);
     float s;
     if (!nonfinite) {
       // kept ranks [kk, n-kk): strictly inside (klo, khi) plus tie copies
       double acc = 0.0;
       int below = 0, eq_lo = 0, inside = 0;
       for (int j = 0; j < n; ++j) {
-        const float x = gld(rows[j * si] + p);
+        const float x = gld(rows[j] + p);
         const uint32_t key = f2key(x);
         below += key < klo;
         eq_lo += key == klo;
@@ -143,7 +139,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_generic_kernel(
       // among the excluded values, so inf - inf (or a NaN) gives NaN;
       // with k == 0 the result is Σall itself.
       float all = 0.0f;
-      for (int j = 0; j < n; ++j) all = add_rn(all, gld(rows[j * si] + p));
+      for (int j = 0; j < n; ++j) all = add_rn(all, gld(rows[j] + p));
       s = (kk == 0 && !nan) ? all : __builtin_nanf("");
     }
     r = __fdiv_rn(s, divisor);
@@ -203,7 +199,7 @@ int launch(const RowSrc &rs, int nchunk, int n, int kk, float divisor,
 }
 
 RowSrc flat_src(const float *const *rows, int64_t numel, const float *base) {
-  return RowSrc{rows, 1, 0, nullptr, numel, base, nullptr, 0};
+  return RowSrc{rows, 0, nullptr, numel, base, nullptr, 0};
 }
 
 // the row-set entry points' shared argument checks
@@ -260,8 +256,8 @@ extern "C" int fsagg_coord_median_rows_f32(const fsagg_rows *rows,
                     "fsagg_coord_median_rows_f32"))
     return FSAGG_EINVAL;
   if (nchunk == 0) return FSAGG_OK;
-  const RowSrc rs{rows->tab, rows->si, rows->ss, chunks, numel, nullptr,
-                  base, base_ss};
+  const RowSrc rs{rows->tab, rows->ss, chunks, numel, nullptr, base,
+                  base_ss};
   return launch<kMedian>(rs, nchunk, rows->n, 0, 2.0f, out,
                          as_stream(stream));
 }
@@ -282,8 +278,8 @@ extern "C" int fsagg_trimmed_mean_rows_f32(const fsagg_rows *rows,
     return FSAGG_EINVAL;
   }
   if (nchunk == 0) return FSAGG_OK;
-  const RowSrc rs{rows->tab, rows->si, rows->ss, chunks, numel, nullptr,
-                  base, base_ss};
+  const RowSrc rs{rows->tab, rows->ss, chunks, numel, nullptr, base,
+                  base_ss};
   return launch<kTrimmed>(rs, nchunk, rows->n, k, divisor, out,
                           as_stream(stream));
 }

@@ -241,7 +241,6 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
                 (threadIdx.x & (kWave - 1));
   const BlockRows br = block_rows(rs, blockIdx.x);
   const float *const *__restrict__ rows = br.rows;
-  const int64_t si = br.si;
   const float *__restrict__ base = br.base;
   const int64_t p = br.lo + threadIdx.x;
   const bool live = int(threadIdx.x) < br.len;
@@ -252,7 +251,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
     const uint32_t off = uint32_t(live ? p : br.lo);
 #pragma unroll
     for (int j = 0; j < N; ++j)
-      k[j] = __float_as_uint(ld_nt(rows[(j < n ? j : n - 1) * si], off));
+      k[j] = __float_as_uint(ld_nt(rows[j < n ? j : n - 1], off));
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       const uint32_t key = f2key(__uint_as_float(k[j]));
@@ -404,7 +403,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
       if (kk == 0 && !nan) {
         s = 0.0f;
 #pragma unroll 1
-        for (int j = 0; j < n; ++j) s = add_rn(s, gld(rows[j * si] + p));
+        for (int j = 0; j < n; ++j) s = add_rn(s, gld(rows[j] + p));
       }
     }
     r = __fdiv_rn(s, divisor);

@@ -152,7 +152,7 @@ __device__ __forceinline__ void read_tile(const float *col, int t,
 
 template <int TS>
 __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
-    const float *const *__restrict__ tab, int64_t si, int64_t ss, int n,
+    const float *const *__restrict__ tab, int64_t ss, int n,
     PairPlan pl, const int64_t *__restrict__ seg_lo,
     const int64_t *__restrict__ seg_end, int nseg,
     const int *__restrict__ prefix, float *__restrict__ partial) {
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   const int64_t start = seg_lo[s] + int64_t(c - prefix[s]) * pl.chl;
   int64_t end = start + pl.chl;
   if (end > seg_end[s]) end = seg_end[s];
-  // client r's row of this key segment: rows[r * si] (a virtual base)
+  // client r's row of this key segment: rows[r] (a virtual base)
   const float *const *__restrict__ rows = tab + int64_t(s) * ss;
 
   const int tid = threadIdx.x;
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   const int items = quads * groups;
   bool vec = (start & 3) == 0;
   for (int r = 0; r < n; ++r)
-    vec = vec && (reinterpret_cast<uintptr_t>(rows[r * si]) & 15u) == 0;
+    vec = vec && (reinterpret_cast<uintptr_t>(rows[r]) & 15u) == 0;
 
   float acc[TS][TS];
 #pragma unroll
@@ -251,10 +251,10 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     const int wave = tid / kWave, lane = tid & (kWave - 1);
     for (int qd = wave; qd < quads; qd += kBlock / kWave) {
       const int r0 = qd * 4;
-      const float *p0 = rows[min(r0, n - 1) * si] + cs;
-      const float *p1 = rows[min(r0 + 1, n - 1) * si] + cs;
-      const float *p2 = rows[min(r0 + 2, n - 1) * si] + cs;
-      const float *p3 = rows[min(r0 + 3, n - 1) * si] + cs;
+      const float *p0 = rows[min(r0, n - 1)] + cs;
+      const float *p1 = rows[min(r0 + 1, n - 1)] + cs;
+      const float *p2 = rows[min(r0 + 2, n - 1)] + cs;
+      const float *p3 = rows[min(r0 + 3, n - 1)] + cs;
       for (int cc = lane; cc < len; cc += kWave)
         *reinterpret_cast<float4 *>(lds + cc * pl.ldsp + r0) =
             make_float4(gld(p0 + cc), gld(p1 + cc), gld(p2 + cc), gld(p3 + cc));
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   const bool prefetch =
       vec && items <= kStageItems * kBlock && n <= kPtrSlots;
   if (n <= kPtrSlots) {
-    for (int r = tid; r < n; r += kBlock) rowp[r] = rows[r * si];
+    for (int r = tid; r < n; r += kBlock) rowp[r] = rows[r];
     __syncthreads();
   }
   if (prefetch && end - start >= pl.sub) fetch(start);
@@ -450,14 +450,14 @@ __global__ void rownorm_final_kernel(const double *__restrict__ partial, int n,
 // partial[i][c]; then one lane per client adds its chunks in chunk order
 // into sq[i][seg].  NULL entries (absent keys) contribute nothing.
 __global__ __launch_bounds__(kBlock) void rows_sqnorm_partial_kernel(
-    const float *const *__restrict__ tab, int64_t si, int64_t ss,
+    const float *const *__restrict__ tab, int64_t ss,
     const fsagg_chunk *__restrict__ chunks, int nchunk,
     double *__restrict__ partial) {
   __shared__ double red[kBlock / kWave];
   const int c = blockIdx.x, i = blockIdx.y;
   const int64_t lo = chunks[c].lo;
   const int len = chunks[c].len;
-  const float *row = tab[int64_t(i) * si + int64_t(chunks[c].seg) * ss];
+  const float *row = tab[int64_t(chunks[c].seg) * ss + i];
   double acc = 0.0;
   if (row) {
     constexpr int G = 8;
@@ -484,16 +484,25 @@ __global__ __launch_bounds__(kBlock) void rows_sqnorm_partial_kernel(
   }
 }
 
+// One lane per (client, segment): the segment's chunks are contiguous in
+// the table (built key by key) — binary-search the first, add in order.
 __global__ void rows_sqnorm_final_kernel(const fsagg_chunk *__restrict__ chunks,
                                          int nchunk, int n, int nseg,
                                          const double *__restrict__ partial,
                                          double *__restrict__ sq) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  double *o = sq + int64_t(i) * nseg;
-  for (int s = 0; s < nseg; ++s) o[s] = 0.0;
-  for (int c = 0; c < nchunk; ++c)
-    o[chunks[c].seg] += partial[int64_t(i) * nchunk + c];
+  const int64_t q = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (q >= int64_t(n) * nseg) return;
+  const int i = int(q / nseg), s = int(q % nseg);
+  int lo = 0, hi = nchunk;  // first chunk with seg >= s
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (chunks[mid].seg < s) lo = mid + 1;
+    else hi = mid;
+  }
+  double t = 0.0;
+  for (int c = lo; c < nchunk && chunks[c].seg == s; ++c)
+    t += partial[int64_t(i) * nchunk + c];
+  sq[q] = t;
 }
 
 }  // namespace
@@ -527,10 +536,10 @@ extern "C" int fsagg_rows_sqnorm_f32(const fsagg_rows *rows,
   if (nchunk > 0)
     hipLaunchKernelGGL(rows_sqnorm_partial_kernel,
                        dim3(unsigned(nchunk), unsigned(rows->n)), dim3(kBlock),
-                       0, s, rows->tab, rows->si, rows->ss, chunks, nchunk,
-                       partial);
+                       0, s, rows->tab, rows->ss, chunks, nchunk, partial);
+  const int64_t pairs = int64_t(rows->n) * rows->nseg;
   hipLaunchKernelGGL(rows_sqnorm_final_kernel,
-                     dim3(unsigned((rows->n + 63) / 64)), dim3(64), 0, s,
+                     dim3(unsigned((pairs + 255) / 256)), dim3(256), 0, s,
                      chunks, nchunk, rows->n, rows->nseg, partial, sq);
   return check_launch("fsagg_rows_sqnorm_f32");
 }
@@ -546,8 +555,8 @@ extern "C" size_t fsagg_pairdist_workspace_bytes(int n, int64_t numel,
 }
 
 // Enqueue the chunk and per-segment kernels; segsq receives [nseg][n][n].
-static int pairdist_segsq_impl(const float *const *tab, int64_t si,
-                               int64_t ss, int n, int64_t numel,
+static int pairdist_segsq_impl(const float *const *tab, int64_t ss, int n,
+                               int64_t numel,
                                const int64_t *seg_lo, const int64_t *seg_end,
                                int nseg, double *segsq, void *workspace,
                                hipStream_t s) {
@@ -561,11 +570,11 @@ static int pairdist_segsq_impl(const float *const *tab, int64_t si,
     const dim3 grid(unsigned(pl.max_chunks), unsigned(pl.groups));
     if (pl.ts == 10)
       hipLaunchKernelGGL(pairdist_chunk_kernel<10>, grid, dim3(kBlock), 0, s,
-                         tab, si, ss, n, pl, seg_lo, seg_end, nseg, prefix,
+                         tab, ss, n, pl, seg_lo, seg_end, nseg, prefix,
                          partial);
     else
       hipLaunchKernelGGL(pairdist_chunk_kernel<8>, grid, dim3(kBlock), 0, s,
-                         tab, si, ss, n, pl, seg_lo, seg_end, nseg, prefix,
+                         tab, ss, n, pl, seg_lo, seg_end, nseg, prefix,
                          partial);
   }
   const int per_seg = pl.ntp * pl.ts * pl.ts;
@@ -597,7 +606,7 @@ extern "C" int fsagg_pairdist_f32(const float *const *rows, int n,
       static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)) +
       align256(sizeof(float) * size_t(pl.max_chunks) * size_t(pl.ntp) *
                size_t(pl.ts * pl.ts)));
-  pairdist_segsq_impl(rows, 1, 0, n, numel, seg_off, seg_off + 1, nseg, segsq,
+  pairdist_segsq_impl(rows, 0, n, numel, seg_off, seg_off + 1, nseg, segsq,
                       workspace, s);
   hipLaunchKernelGGL(pairdist_finish_kernel,
                      dim3(unsigned((n * n + kBlock - 1) / kBlock)),
@@ -623,7 +632,7 @@ extern "C" int fsagg_pairdist_segsq_f32(const float *const *rows, int n,
               workspace_bytes, need);
     return FSAGG_ESPACE;
   }
-  pairdist_segsq_impl(rows, 1, 0, n, numel, seg_off, seg_off + 1, nseg, segsq,
+  pairdist_segsq_impl(rows, 0, n, numel, seg_off, seg_off + 1, nseg, segsq,
                       workspace, as_stream(stream));
   return check_launch("fsagg_pairdist_segsq_f32");
 }
@@ -647,7 +656,7 @@ extern "C" int fsagg_pairdist_rows_segsq_f32(const fsagg_rows *rows,
               workspace_bytes, need);
     return FSAGG_ESPACE;
   }
-  pairdist_segsq_impl(rows->tab, rows->si, rows->ss, rows->n, numel, seg_lo,
+  pairdist_segsq_impl(rows->tab, rows->ss, rows->n, numel, seg_lo,
                       seg_end, rows->nseg, segsq, workspace,
                       as_stream(stream));
   return check_launch("fsagg_pairdist_rows_segsq_f32");

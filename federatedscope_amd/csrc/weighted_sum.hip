@@ -234,7 +234,7 @@ void launch_wsum(const float *const *rows, const float *w, const float *pre,
 // any is consumed.
 template <int V, bool PRE, bool BASE, bool GUARD>
 __device__ __forceinline__ void wsum_rows_chunk(
-    const float *const *__restrict__ rows, int64_t si, int n, int64_t lo,
+    const float *const *__restrict__ rows, int n, int64_t lo,
     int nvec, const float *__restrict__ w, const float *__restrict__ pre,
     const float *__restrict__ base, float *__restrict__ out) {
   int idx[V];
@@ -244,12 +244,26 @@ __device__ __forceinline__ void wsum_rows_chunk(
     idx[v] = v * kBlock + int(threadIdx.x);
     ok[v] = !GUARD || idx[v] < nvec;
   }
+  // the first present client initialises the accumulator
+  int i0 = 0;
+  while (i0 < n && rows[i0] == nullptr) ++i0;
   f4 acc[V];
+  if (i0 < n) {
+    const f4 *r = reinterpret_cast<const f4 *>(rows[i0] + lo);
+    const float w0 = w[i0];
+    const float s0 = PRE ? pre[i0] : 1.0f;
 #pragma unroll
-  for (int v = 0; v < V; ++v) acc[v] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-  bool first = true;
-  for (int i = 0; i < n; ++i) {
-    const float *row = rows[int64_t(i) * si];
+    for (int v = 0; v < V; ++v) {
+      f4 x = ok[v] ? ld4<true>(r + idx[v]) : f4{0.0f, 0.0f, 0.0f, 0.0f};
+      if (PRE) x = mul4(x, s0);
+      acc[v] = mul4(x, w0);
+    }
+  } else {
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[v] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+  }
+  for (int i = i0 + 1; i < n; ++i) {
+    const float *row = rows[i];
     if (row == nullptr) continue;
     const f4 *r = reinterpret_cast<const f4 *>(row + lo);
     f4 x[V];
@@ -262,9 +276,8 @@ __device__ __forceinline__ void wsum_rows_chunk(
     for (int v = 0; v < V; ++v) {
       f4 t = x[v];
       if (PRE) t = mul4(t, s);
-      acc[v] = first ? mul4(t, wi) : add4(acc[v], mul4(t, wi));
+      acc[v] = add4(acc[v], mul4(t, wi));
     }
-    first = false;
   }
   f4 *o = reinterpret_cast<f4 *>(out + lo);
 #pragma unroll
@@ -279,7 +292,7 @@ __device__ __forceinline__ void wsum_rows_chunk(
 
 template <int V, bool PRE, bool BASE>
 __global__ __launch_bounds__(kBlock) void wsum_rows_kernel(
-    const float *const *__restrict__ tab, int64_t si, int64_t ss, int n,
+    const float *const *__restrict__ tab, int64_t ss, int n,
     const fsagg_chunk *__restrict__ chunks, int nchunk,
     const float *__restrict__ w, const float *__restrict__ pre,
     const float *const *__restrict__ btab, int64_t bss,
@@ -292,11 +305,11 @@ __global__ __launch_bounds__(kBlock) void wsum_rows_kernel(
     const float *base = BASE ? btab[int64_t(seg) * bss] : nullptr;
     const int nvec = len >> 2;
     if (nvec == kBlock * V)
-      wsum_rows_chunk<V, PRE, BASE, false>(rows, si, n, lo, nvec, w, pre,
-                                           base, out);
+      wsum_rows_chunk<V, PRE, BASE, false>(rows, n, lo, nvec, w, pre, base,
+                                           out);
     else
-      wsum_rows_chunk<V, PRE, BASE, true>(rows, si, n, lo, nvec, w, pre,
-                                          base, out);
+      wsum_rows_chunk<V, PRE, BASE, true>(rows, n, lo, nvec, w, pre, base,
+                                          out);
     // the key's last (< 4) coordinates
     const int t = int(threadIdx.x);
     if (t < (len & 3)) {
@@ -304,7 +317,7 @@ __global__ __launch_bounds__(kBlock) void wsum_rows_kernel(
       float acc = 0.0f;
       bool first = true;
       for (int i = 0; i < n; ++i) {
-        const float *row = rows[int64_t(i) * si];
+        const float *row = rows[i];
         if (row == nullptr) continue;
         float x = gld(row + p);
         if (PRE) x = mul_rn(x, pre[i]);
@@ -335,7 +348,7 @@ void launch_wsum_rows(const fsagg_rows &rs, const fsagg_chunk *chunks,
                       hipStream_t s) {
   const unsigned grid = stream_grid(nchunk, 1, 256 * 16);
   hipLaunchKernelGGL((wsum_rows_kernel<V, PRE, BASE>), dim3(grid),
-                     dim3(kBlock), 0, s, rs.tab, rs.si, rs.ss, rs.n, chunks,
+                     dim3(kBlock), 0, s, rs.tab, rs.ss, rs.n, chunks,
                      nchunk, w, pre, btab, bss, out);
 }
 

@@ -336,3 +336,75 @@ class ClientStack:
         return RowTable.from_slab(self.slab, rows=idx,
                                   col_offset=self.layout.offsets[key],
                                   numel=self.layout.numels[key])
+
+
+class RangeStack:
+    """Device slab ``[capacity][local]`` holding, per client, this rank's
+    pieces of the bucket (global coordinate ranges ``pieces``), back to
+    back at ``loc[j]`` — the parameter-range shard of the client stack
+    (SURVEY §8(e)).  Duck-types the layout interface HostStager packs
+    through (``numel``, ``pack_host``)."""
+
+    ALIGN = 64
+
+    def __init__(self, layout, pieces, capacity, device):
+        self.layout = layout
+        self.pieces = [(int(a), int(b)) for a, b in pieces]
+        self.loc = []
+        off = 0
+        for a, b in self.pieces:
+            self.loc.append(off)
+            off += -(-max(b - a, 0) // self.ALIGN) * self.ALIGN
+        self.numel = max(off, self.ALIGN)
+        self.device = torch.device(device)
+        self.slab = torch.zeros((max(1, capacity), self.numel),
+                                dtype=torch.float32, device=self.device)
+        # per piece: [(key, key elem start, local start, length)]
+        self.spans = []
+        for (a, b), loc in zip(self.pieces, self.loc):
+            sp = []
+            for k in layout.keys:
+                o, m = layout.offsets[k], layout.numels[k]
+                x, y = max(a, o), min(b, o + m)
+                if y > x:
+                    sp.append((k, x - o, loc + x - a, y - x))
+            self.spans.append(sp)
+
+    @property
+    def capacity(self):
+        return self.slab.shape[0]
+
+    def offset(self, j):
+        """Row element of bucket coordinate 0 for piece j (RowSet offset)."""
+        return self.loc[j] - self.pieces[j][0]
+
+    def pack_host(self, model, out):
+        for sp in self.spans:
+            for k, src, dst, ln in sp:
+                if k in model:
+                    out[dst:dst + ln].copy_(
+                        param2tensor(model[k]).reshape(-1)[src:src + ln])
+        return out
+
+    def load_many(self, models):
+        """Stage each client's pieces: host dicts through the pinned
+        double-buffered stager (only this rank's share crosses PCIe),
+        device tensors by slice copies."""
+        stager = None
+        for i, m in enumerate(models):
+            on_host = any(param2tensor(m[k]).device.type != 'cuda'
+                          for k in self.layout.keys if k in m)
+            if on_host:
+                if stager is None:
+                    stager = HostStager(self.device)
+                stager.put(self, m, self.slab[i])
+            else:
+                row = self.slab[i]
+                for sp in self.spans:
+                    for k, src, dst, ln in sp:
+                        if k in m:
+                            row[dst:dst + ln].copy_(
+                                param2tensor(m[k]).reshape(-1)[src:src + ln],
+                                non_blocking=True)
+        if stager is not None:
+            stager.finish()

@@ -636,9 +636,9 @@ class RowSet:
         # pointers are contiguous (batched scalar loads, a small
         # scalar-cache footprint per workgroup)
         if table.shape[1] == 1:
-            self.si, self.ss = 1, 0
+            self.ss = 0
         elif table.shape[1] == self.nseg:
-            self.si, self.ss = 1, self.n
+            self.ss = self.n
         else:
             raise ValueError('row table has %d columns for %d keys' %
                              (table.shape[1], self.nseg))
@@ -646,16 +646,17 @@ class RowSet:
         self.aligned16 = bool(aligned16)
         self.missing = int(absent(layout, table).sum())
         self.tab = _h2d_np(table.T, self.device)
-        self.struct = L.Rows(self.tab.data_ptr(), self.si, self.ss, self.n,
+        self.struct = L.Rows(self.tab.data_ptr(), self.ss, self.n,
                              self.nseg)
         self._keep = tuple(keepalive)
 
     @classmethod
-    def from_stack(cls, stack, slots, present=None):
+    def from_stack(cls, stack, slots, present=None, offset=0):
         """Rows ``slots`` of a ClientStack; ``present`` (bool [n][nseg])
-        marks absent keys (NULL entries)."""
+        marks absent keys (NULL entries).  Bucket coordinate p is at row
+        element p + ``offset`` (a range stack holds a piece of the bucket)."""
         _check_f32_cuda(stack.slab, 'stack')
-        base = stack.slab.data_ptr()
+        base = stack.slab.data_ptr() + 4 * int(offset)
         ld = stack.slab.stride(0) * 4
         rows = _np.array([base + int(s) * ld for s in slots], dtype=_np.int64)
         tab = rows[:, None]
@@ -806,14 +807,16 @@ def pairdist_rows_segsq(rs, lo=0, hi=None, workspace=None):
     if rs.n < 2:
         raise ValueError('Krum needs at least two clients')
     lay = rs.layout
+    hi = lay.numel if hi is None else hi
     seg_lo, seg_end = lay.seg_bounds(rs.device, lo, hi)
     lib = L.load()
-    need = lib.fsagg_pairdist_workspace_bytes(rs.n, lay.numel, rs.nseg)
+    extent = max(hi - lo, 1)       # plans ~1000 chunks over the range
+    need = lib.fsagg_pairdist_workspace_bytes(rs.n, extent, rs.nseg)
     ws = (workspace or _WS).get(rs.device, need)
     sq = torch.empty((rs.nseg, rs.n, rs.n), dtype=torch.float64,
                      device=rs.device)
     L.check(lib.fsagg_pairdist_rows_segsq_f32(
-        rs.ptr(), seg_lo.data_ptr(), seg_end.data_ptr(), lay.numel,
+        rs.ptr(), seg_lo.data_ptr(), seg_end.data_ptr(), extent,
         sq.data_ptr(), ws.data_ptr(), ws.numel(), _stream(rs.device)),
         'fsagg_pairdist_rows_segsq_f32')
     return sq

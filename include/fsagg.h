@@ -313,10 +313,11 @@ int fsagg_gather_rows_f32(const float *const *src, int n, int nseg,
  * where they lie — no staging copy into a stack.
  *
  * A row set addresses client i's value of bucket coordinate p, p inside key
- * segment s, at  tab[i*si + s*ss][p]  — each entry is a "virtual base":
+ * segment s, at  tab[s*ss + i][p]  — each entry is a "virtual base":
  * the key tensor's pointer minus 4 * (the key's bucket offset).  A stacked
  * slab is the special case ss = 0 (every segment of client i starts at its
- * row), a [n][nseg] key table is si = nseg, ss = 1.  A NULL entry means the
+ * row), a segment-major [nseg][n] key table has ss = n (one chunk's client
+ * pointers are contiguous: batched scalar loads).  A NULL entry means the
  * client lacks that key: the weighted sum skips it (the reference's
  * `if key not in local_model: continue`), the order statistics and Krum
  * require every entry.
@@ -326,7 +327,7 @@ int fsagg_gather_rows_f32(const float *const *src, int n, int nseg,
  */
 typedef struct fsagg_rows {
   const float *const *tab; /* (device) row-pointer table */
-  int64_t si, ss;          /* table strides per client / per segment */
+  int64_t ss;              /* table stride per key segment (0 or >= n) */
   int n;                   /* clients */
   int nseg;                /* key segments */
 } fsagg_rows;
