@@ -47,10 +47,10 @@ def test_library_rejects_bad_args_without_gpu():
     # trimmed mean with 2k >= n is rejected before any launch
     assert lib.fsagg_trimmed_mean_f32(1, 4, 10, 2, 0.0, None, 1, None) == -1
     # row-set entry points reject a missing table / a bad chunk unit
-    rows = _lib.Rows(0, 1, 0, 4, 1)
+    rows = _lib.Rows(0, 0, 4, 1)
     assert lib.fsagg_weighted_sum_rows_f32(rows, None, 0, 1024, 1, None,
                                            None, 0, 16, None) == -1
-    rows = _lib.Rows(16, 1, 0, 4, 1)
+    rows = _lib.Rows(16, 0, 4, 1)
     assert lib.fsagg_weighted_sum_rows_f32(rows, 16, 3, 1000, 16, None,
                                            None, 0, 16, None) == -1
     assert b'chunk_elems' in lib.fsagg_last_error()
