@@ -167,34 +167,48 @@ def e2e_leg(args, dev, weights, sizes):
 
 
 class Dist:
-    """The job's process group (RCCL over xGMI when N > 1)."""
+    """The job's process group: RCCL ("nccl") over xGMI when N > 1.  The
+    gloo backend is for the multi-process tests on a one-GPU box (ranks
+    then share the visible GPUs round-robin; collectives go through host
+    memory, see core/sharding.Comm)."""
 
-    def __init__(self, gpus):
+    def __init__(self, gpus, backend='nccl'):
         import torch
         import torch.distributed as dist
         self.dist = dist
+        self.backend = backend
         self.world = int(os.environ.get('WORLD_SIZE', '1'))
         self.rank = int(os.environ.get('RANK', '0'))
         self.local = int(os.environ.get('LOCAL_RANK', '0'))
         if self.world != gpus:
             log('note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE' %
                 (gpus, self.world))
+        if backend == 'gloo':
+            self.local %= max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(self.local)
         self.dev = torch.device('cuda', self.local)
         if self.world > 1:
-            dist.init_process_group('nccl', rank=self.rank,
-                                    world_size=self.world,
-                                    device_id=self.dev)
+            if backend == 'nccl':
+                dist.init_process_group('nccl', rank=self.rank,
+                                        world_size=self.world,
+                                        device_id=self.dev)
+            else:
+                dist.init_process_group(backend, rank=self.rank,
+                                        world_size=self.world)
 
     def barrier(self):
         if self.world > 1:
-            self.dist.barrier(device_ids=[self.local])
+            if self.backend == 'nccl':
+                self.dist.barrier(device_ids=[self.local])
+            else:
+                self.dist.barrier()
 
     def max(self, x):
         import torch
         if self.world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=self.dev)
+        dev = self.dev if self.backend == 'nccl' else 'cpu'
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -241,6 +255,9 @@ def main():
     ap.add_argument('--e2e', action='store_true',
                     help='also time host dicts -> aggregate() -> host dicts')
     ap.add_argument('--layout', default='flat', choices=['flat', 'resnet50'])
+    ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
+                    help='process-group backend (gloo: multi-process tests '
+                         'on one GPU)')
     ap.add_argument('--traffic', default=os.path.join(
         ROOT, 'profiles', 'traffic_fedavg_c3.json'))
     args = ap.parse_args()
@@ -250,7 +267,7 @@ def main():
     from federatedscope_amd.core.aggregators._engine import fedavg_weights
     from federatedscope_amd.core.sharding import PipelinedAssembly
 
-    D = Dist(args.gpus)
+    D = Dist(args.gpus, args.backend)
     world, rank, dev = D.world, D.rank, D.dev
     n, P = args.clients, args.params
     chunks = args.chunks or (1 if world == 1 else 4)

@@ -1,0 +1,60 @@
+"""Two ranks (gloo, sharing the box's one GPU) through the multi-GPU code
+paths with the real libfsagg kernels:
+
+* bench.py's strong-scaling step (PipelinedAssembly: block-cyclic
+  parameter pieces, an all-gather per round) must assemble the full
+  FedAvg result bit-exact on every rank;
+* the drop-in aggregators in ``aggregator.shard_by_param_range`` mode
+  (tests/_world2_worker.py) must reproduce the reference's goldens.
+
+On the 8-GPU node the same code runs over RCCL (bench.py's default
+backend); the collectives differ only in core/sharding.Comm."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run2(args, timeout=110):
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes', '1',
+           '--nproc-per-node', '2', '--master-addr', '127.0.0.1',
+           '--master-port', str(_port())] + args
+    env = dict(os.environ, OMP_NUM_THREADS='4')
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True,
+                       timeout=timeout, env=env)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    return [json.loads(l) for l in p.stdout.splitlines()
+            if l.startswith('{')]
+
+
+def test_bench_strong_scaling_world2():
+    recs = _run2(['bench.py', '--gpus', '2', '--backend', 'gloo',
+                  '--clients', '10', '--params', '1000003', '--steps', '3',
+                  '--warmup', '1', '--no-cpu-baseline', '--no-weak'])
+    assert len(recs) == 1
+    r = recs[0]
+    assert r['n_gpus'] == 2 and r['scaling'] == 'strong'
+    assert r['assembled_bit_exact'] is True
+    assert r['config']['params'] == 1000003
+
+
+def test_sharded_aggregators_world2():
+    recs = _run2([os.path.join('tests', '_world2_worker.py')])
+    assert sorted(r['rank'] for r in recs) == [0, 1]
+    for r in recs:
+        assert 'synthetic' in r['ok'] and len(r['ok']) >= 18, r
