@@ -484,14 +484,15 @@ __global__ __launch_bounds__(kBlock) void rows_sqnorm_partial_kernel(
   }
 }
 
-// One lane per (client, segment): the segment's chunks are contiguous in
-// the table (built key by key) — binary-search the first, add in order.
-__global__ void rows_sqnorm_final_kernel(const fsagg_chunk *__restrict__ chunks,
-                                         int nchunk, int n, int nseg,
-                                         const double *__restrict__ partial,
-                                         double *__restrict__ sq) {
-  const int64_t q = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (q >= int64_t(n) * nseg) return;
+// One wave per (client, segment): the segment's chunks are contiguous in
+// the table (built key by key) — binary-search the first, lane l adds
+// chunks first + l, first + l + 64, … in order, then a fixed shuffle tree.
+__global__ __launch_bounds__(kBlock) void rows_sqnorm_final_kernel(
+    const fsagg_chunk *__restrict__ chunks, int nchunk, int n, int nseg,
+    const double *__restrict__ partial, double *__restrict__ sq) {
+  const int64_t q = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  if (q >= int64_t(n) * nseg) return;  // whole waves leave together
   const int i = int(q / nseg), s = int(q % nseg);
   int lo = 0, hi = nchunk;  // first chunk with seg >= s
   while (lo < hi) {
@@ -499,10 +500,18 @@ __global__ void rows_sqnorm_final_kernel(const fsagg_chunk *__restrict__ chunks,
     if (chunks[mid].seg < s) lo = mid + 1;
     else hi = mid;
   }
+  int end = lo;  // first chunk with seg > s
+  hi = nchunk;
+  while (end < hi) {
+    const int mid = (end + hi) >> 1;
+    if (chunks[mid].seg <= s) end = mid + 1;
+    else hi = mid;
+  }
   double t = 0.0;
-  for (int c = lo; c < nchunk && chunks[c].seg == s; ++c)
-    t += partial[int64_t(i) * nchunk + c];
-  sq[q] = t;
+  const double *row = partial + int64_t(i) * nchunk;
+  for (int c = lo + lane; c < end; c += kWave) t += row[c];
+  t = wave_sum(t);
+  if (lane == 0) sq[q] = t;
 }
 
 }  // namespace
@@ -537,10 +546,11 @@ extern "C" int fsagg_rows_sqnorm_f32(const fsagg_rows *rows,
     hipLaunchKernelGGL(rows_sqnorm_partial_kernel,
                        dim3(unsigned(nchunk), unsigned(rows->n)), dim3(kBlock),
                        0, s, rows->tab, rows->ss, chunks, nchunk, partial);
-  const int64_t pairs = int64_t(rows->n) * rows->nseg;
+  const int64_t waves = int64_t(rows->n) * rows->nseg;
+  const int64_t per = kBlock / kWave;
   hipLaunchKernelGGL(rows_sqnorm_final_kernel,
-                     dim3(unsigned((pairs + 255) / 256)), dim3(256), 0, s,
-                     chunks, nchunk, rows->n, rows->nseg, partial, sq);
+                     dim3(unsigned((waves + per - 1) / per)), dim3(kBlock), 0,
+                     s, chunks, nchunk, rows->n, rows->nseg, partial, sq);
   return check_launch("fsagg_rows_sqnorm_f32");
 }
 

@@ -205,17 +205,58 @@ def _to_float(v):
 # ---------------------------------------------------------------------------
 # Online running mean  (clients_avg_aggregator.py:115-148)
 # ---------------------------------------------------------------------------
+def _online_mul(t, k):
+    """python int k * tensor t (clients_avg_aggregator.py:136-138): the
+    tensor's dtype; reduced floats computed in float32 (ATen's opmath) and
+    rounded once."""
+    t = np.asarray(t)
+    if t.dtype == np.int64:
+        return t * np.int64(k)
+    if t.dtype == np.float16:
+        return (t.astype(np.float32) * np.float32(k)).astype(np.float16)
+    if t.dtype == np.float64:
+        return t * np.float64(k)
+    return t.astype(np.float32) * np.float32(k)
+
+
+_ONLINE_RANK = {np.dtype(np.int64): 0, np.dtype(np.float16): 1,
+                np.dtype(np.float32): 2, np.dtype(np.float64): 3}
+
+
+def _online_add(a, b):
+    """tensor + tensor: ATen's promotion (int64 < f16 < f32 < f64), both
+    operands cast to the common type, reduced floats added in float32."""
+    ct = max(a.dtype, b.dtype, key=lambda d: _ONLINE_RANK[np.dtype(d)])
+    if ct == np.float16:
+        return (a.astype(np.float16).astype(np.float32) +
+                b.astype(np.float16).astype(np.float32)).astype(np.float16)
+    return a.astype(ct) + b.astype(ct)
+
+
+def _online_div(c, d):
+    """tensor / python int: integers become float32 (true division)."""
+    if c.dtype == np.int64:
+        return c.astype(np.float32) / np.float32(d)
+    if c.dtype == np.float16:
+        return (c.astype(np.float32) / np.float32(d)).astype(np.float16)
+    if c.dtype == np.float64:
+        return c / np.float64(d)
+    return c / np.float32(d)
+
+
 def online_aggregate(init, clients):
     """reset(): zeros like the server model; inc((s, x)) per client:
-    m = (cnt*m + s*x) / (cnt + s); cnt += s."""
-    m = OrderedDict((k, np.zeros_like(v)) for k, v in init.items())
+    m = (cnt*m + s*x) / (cnt + s) with ATen's dtype rules per op
+    (clients_avg_aggregator.py:115-142); cnt += s."""
+    m = OrderedDict((k, np.zeros_like(np.asarray(v))) for k, v in
+                    init.items())
     cnt = 0
     for s, x in clients:
         for k in m:
             if k not in x:
                 continue
-            m[k] = ((f32(cnt) * m[k] + f32(s) * x[k]) / f32(cnt + s)).astype(
-                m[k].dtype)
+            m[k] = _online_div(_online_add(_online_mul(m[k], cnt),
+                                           _online_mul(x[k], s)), cnt + s)
         cnt += s
     return m
 
@@ -505,14 +546,16 @@ def _py_mod(a, b):
     return np.where(m == 0, np.copysign(0.0, b), m)
 
 
-def ss_fedavg(models, mod_number, maximum, epsilon):
+def ss_fedavg(models, mod_number, maximum, epsilon, ignore_weight=False):
     """clients_avg_aggregator.py:79-98 with AdditiveSecretSharing
-    .fixedpoint2float (secret_sharing.py:93-98): Σ shares (float64, weight
-    1.0, list order), x %= mod, x > maximum ? -(mod - x)/eps : x/eps,
+    .fixedpoint2float (secret_sharing.py:93-98): Σ shares·w (float64, list
+    order; w = 1.0, or 1/n with ignore_weight, which the reference tests
+    first, :77-82), x %= mod, x > maximum ? -(mod - x)/eps : x/eps,
     ÷ total sample size, → fp32."""
     total = 0
     for s, _ in models:
         total += s
+    w = 1.0 / len(models) if ignore_weight else 1.0
     mod = np.float64(float(mod_number))
     mx = np.float64(float(maximum))
     eps = np.float64(epsilon)
@@ -522,7 +565,7 @@ def ss_fedavg(models, mod_number, maximum, epsilon):
         for _, m in models:
             if key not in m:
                 continue
-            x = np.asarray(m[key]).astype(np.float64) * 1.0
+            x = np.asarray(m[key]).astype(np.float64) * w
             acc = x if acc is None else acc + x
         x = _py_mod(acc, mod)
         r = np.where(x > mx, -1 * (mod - x) / eps, x / eps)

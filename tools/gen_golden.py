@@ -403,11 +403,118 @@ def fedopt_cases(rng):
                       init=init if r == 0 else None)
 
 
+def normbound_missing_key_cases(rng):
+    """Clients whose keys differ from the server model's
+    (normbounding_aggregator.py:49-70): the norm runs over the server keys
+    a client holds, and a scaled client is rebuilt from a deepcopy of the
+    server model — keys it lacks come back as the SERVER's values."""
+    shapes = OrderedDict([('w', (7, 33)), ('b', (7, )), ('bn.x', (4, ))])
+    for tag, bound in (('scaled', 0.5), ('mixed', 2.0), ('none', 1e6)):
+        for variant in ('peer', 'first', 'extra'):
+            cfg = make_cfg(norm_bound=bound)
+            clients = rand_clients(rng, 9, shapes, scale=0.3)
+            # a spread of norms so that 'mixed' scales some clients only
+            for i, (_, d) in enumerate(clients):
+                for k in d:
+                    d[k] = d[k] * float(0.2 + 0.25 * i)
+            if variant == 'peer':
+                del clients[3][1]['b']
+                del clients[6][1]['bn.x']
+            elif variant == 'first':
+                del clients[0][1]['bn.x']
+                del clients[4][1]['w']
+            else:   # a key the server model does not have
+                clients[5][1]['extra.w'] = torch.from_numpy(
+                    rng.standard_normal(5).astype(np.float32))
+                del clients[2][1]['b']
+            init = OrderedDict((k, torch.from_numpy(
+                rng.standard_normal(s).astype(np.float32))) for k, s in
+                               shapes.items())
+            agg = NormboundingAggregator(model=DictModel(init), config=cfg)
+            out = run(agg, clients)
+            save_case('normbound_keys_%s_%s' % (tag, variant), {
+                'rule': 'normbounding', 'bound': bound}, clients, out,
+                      init=init)
+
+
+def online_dtype_cases(rng):
+    """OnlineClientsAvgAggregator.inc with non-fp32 keys
+    (clients_avg_aggregator.py:125-142): ATen promotes — an int64 buffer's
+    running mean becomes fp32 at the first division, an fp16 upload of an
+    fp32 key is multiplied in fp16, an fp64 upload promotes the key."""
+    init = OrderedDict([
+        ('w', torch.from_numpy(rng.standard_normal((5, 7)).astype(
+            np.float32))),
+        ('n', torch.tensor(int(rng.integers(0, 100)), dtype=torch.long)),
+        ('h', torch.from_numpy(rng.standard_normal(6).astype(
+            np.float32)).half()),
+        ('c', torch.from_numpy(rng.integers(-50, 50, 4))),
+    ])
+    agg = OnlineClientsAvgAggregator(model=DictModel(init),
+                                     config=make_cfg())
+    agg.reset()
+    clients = []
+    for i in range(6):
+        d = OrderedDict()
+        wv = rng.standard_normal((5, 7)).astype(np.float32)
+        d['w'] = torch.from_numpy(wv).half() if i % 3 == 1 else \
+            torch.from_numpy(wv)
+        d['n'] = torch.tensor(int(rng.integers(0, 10**6)), dtype=torch.long)
+        hv = rng.standard_normal(6)
+        d['h'] = torch.from_numpy(hv) if i == 4 else \
+            torch.from_numpy(hv.astype(np.float32)).half() if i % 2 else \
+            torch.from_numpy(hv.astype(np.float32))
+        if i != 2:
+            d['c'] = torch.from_numpy(rng.integers(-1000, 1000, 4))
+        clients.append((int(rng.integers(1, 300)), d))
+    for s, d in copy.deepcopy(clients):
+        agg.inc((s, d))
+    out = agg.aggregate({})
+    # the server model's state_dict order (parameters, then buffers) is
+    # the order the reference iterates: save init in that order
+    order = list(DictModel(init).state_dict().keys())
+    save_case('online_dtypes_n6', {'rule': 'online'}, clients, out,
+              init=OrderedDict((k, init[k]) for k in order))
+
+
+def fedopt_more_cases(rng):
+    """FedOpt configs the device path first lacked: Adam(amsgrad) and a
+    float64 server model (fedopt_aggregator.py:26-44 runs any
+    torch.optim config)."""
+    shapes = OrderedDict([('w', (5, 21)), ('b', (5, ))])
+    for tag, opt, dt in (
+            ('AdamAms', {'type': 'Adam', 'lr': 0.01, 'amsgrad': True},
+             torch.float32),
+            ('SGDm64', {'type': 'SGD', 'lr': 0.5, 'momentum': 0.9,
+                        'weight_decay': 0.01}, torch.float64),
+            ('Adam64', {'type': 'Adam', 'lr': 0.01}, torch.float64)):
+        cfg = make_cfg(fedopt=opt)
+        init = OrderedDict((k, torch.from_numpy(
+            rng.standard_normal(s)).to(dt)) for k, s in shapes.items())
+        agg = FedOptAggregator(config=cfg, model=DictModel(init))
+        rounds, outs = [], []
+        for r in range(3):
+            clients = rand_clients(rng, 4, shapes, dtype=dt)
+            rounds.append(clients)
+            outs.append(OrderedDict((k, v.detach().clone())
+                                    for k, v in run(agg, clients).items()))
+        for r in range(3):
+            save_case('fedopt_%s_%d' % (tag, r), {
+                'rule': 'fedopt', 'opt': opt, 'round': r}, rounds[r],
+                      outs[r], init=init if r == 0 else None)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(1)  # fed_runner.py:297-299
     if sys.argv[1:] == ['nonfinite']:  # added later: its own seed
         order_stat_nonfinite_cases(np.random.default_rng(20261016))
+        return 0
+    if sys.argv[1:] == ['round2']:     # round 2 cases: their own seed
+        rng = np.random.default_rng(20261017)
+        normbound_missing_key_cases(rng)
+        online_dtype_cases(rng)
+        fedopt_more_cases(rng)
         return 0
     rng = np.random.default_rng(20261015)
     fedavg_cases(rng)
