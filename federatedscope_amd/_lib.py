@@ -48,27 +48,33 @@ SIGNATURES = {
 
 
 
+_c_d = ctypes.c_double
+
+
 class OptParams(ctypes.Structure):
     """struct fsagg_opt_params (include/fsagg.h)."""
-    _fields_ = [('kind', _c_i), ('flags', _c_i), ('lr', _c_f),
-                ('momentum', _c_f), ('dampening', _c_f),
-                ('weight_decay', _c_f), ('beta1', _c_f), ('beta2', _c_f),
-                ('eps', _c_f), ('step_size', _c_f),
-                ('bias_correction2_sqrt', _c_f)]
+    _fields_ = [('kind', _c_i), ('flags', _c_i), ('lr', _c_d),
+                ('momentum', _c_d), ('dampening', _c_d),
+                ('weight_decay', _c_d), ('beta1', _c_d), ('beta2', _c_d),
+                ('eps', _c_d), ('step_size', _c_d),
+                ('bias_correction2_sqrt', _c_d)]
 
 
 FSAGG_OPT_SGD, FSAGG_OPT_ADAM = 0, 1
-FSAGG_OPT_NESTEROV, FSAGG_OPT_FIRST_STEP = 1, 2
+FSAGG_OPT_NESTEROV, FSAGG_OPT_FIRST_STEP, FSAGG_OPT_AMSGRAD = 1, 2, 4
 SIGNATURES['fsagg_server_opt_step_f32'] = (
-    _c_i, [_c_p, _c_p, _c_p, _c_p, _c_i64, ctypes.POINTER(OptParams), _c_p])
+    _c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, ctypes.POINTER(OptParams),
+           _c_p])
+SIGNATURES['fsagg_server_opt_step_f64'] = (
+    _c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, ctypes.POINTER(OptParams),
+           _c_p])
 
-_c_d = ctypes.c_double
 FSAGG_WIRE_F32, FSAGG_WIRE_I8, FSAGG_WIRE_I16 = 0, 1, 2
 SIGNATURES['fsagg_wire_unpack_f32'] = (
     _c_i, [_c_p, _c_i64, _c_p, _c_p, _c_i, _c_i, _c_i64, _c_p, _c_i64, _c_p])
 SIGNATURES['fsagg_ss_recover_f32'] = (
-    _c_i, [_c_p, _c_p, _c_i, _c_i64, _c_d, _c_d, _c_d, _c_d, _c_i, _c_p, _c_p,
-           _c_p])
+    _c_i, [_c_p, _c_p, _c_i, _c_i64, _c_d, _c_d, _c_d, _c_d, _c_d, _c_i, _c_p,
+           _c_p, _c_p])
 SIGNATURES['fsagg_delta_sqnorm_workspace_bytes'] = (_c_sz, [_c_i, _c_i64,
                                                             _c_i])
 SIGNATURES['fsagg_delta_wsum_f32'] = (
@@ -103,6 +109,8 @@ SIGNATURES['fsagg_trimmed_mean_rows_f32'] = (
 SIGNATURES['fsagg_pairdist_rows_segsq_f32'] = (
     _c_i, [_rows_p, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_sz, _c_p])
 
+SIGNATURES['fsagg_online_inc_typed'] = (
+    _c_i, [_c_p, _c_i, _c_p, _c_i, _c_p, _c_i, _c_i64, _c_i64, _c_i64, _c_p])
 SIGNATURES['fsagg_rows_sqnorm_workspace_bytes'] = (_c_sz, [_c_i, _c_i])
 SIGNATURES['fsagg_rows_sqnorm_f32'] = (
     _c_i, [_rows_p, _c_p, _c_i, _c_p, _c_p, _c_sz, _c_p])

@@ -265,10 +265,10 @@ class DeviceEngine:
         views = layout.unpack(flat)
         out = OrderedDict()
         for k in keys:
-            if k in views:
-                out[k] = views[k]
-            elif extra is not None and k in extra:
+            if extra is not None and k in extra:
                 out[k] = extra[k].to(out_device)
+            elif k in views:
+                out[k] = views[k]
         return out
 
     # -- the FedAvg core ----------------------------------------------------

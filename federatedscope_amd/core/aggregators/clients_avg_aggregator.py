@@ -41,10 +41,6 @@ class ClientsAvgAggregator(DeviceEngine, _ModelIO, Aggregator):
 
         Returns a state_dict in client 0's key order on client 0's device."""
         if self.cfg.federate.use_ss:
-            if self.cfg.federate.ignore_weight:
-                raise NotImplementedError(
-                    'use_ss with ignore_weight (1/n-weighted fixed-point '
-                    'shares) has no device path')
             return self._ss_avg(models, recover_fun)
         weights = self._weights(models)
         out_dev = _first_device(models[0][1])
@@ -54,14 +50,17 @@ class ClientsAvgAggregator(DeviceEngine, _ModelIO, Aggregator):
     def _ss_avg(self, models, recover_fun):
         """The use_ss branch (clients_avg_aggregator.py:79-98): every upload
         is the client's share sum of sample_size·params in fixed point;
-        weight 1.0, Σ in float64 (numpy), then fixedpoint2float, ÷ total,
-        fp32 — fused in fsagg_ss_recover_f32.  Without a recover function
-        the float64 sums are returned (the reference leaves them numpy)."""
+        weight 1.0 — or 1/n when ignore_weight is set too, which the
+        reference tests first (:77-82) — Σ in float64 (numpy), then
+        fixedpoint2float, ÷ total, fp32 — fused in fsagg_ss_recover_f32.
+        Without a recover function the float64 sums are returned (the
+        reference leaves them numpy)."""
         from ..secret_sharing import ss_params
         dev = self.compute_device
         total = 0
         for size, _ in models:
             total += size
+        w = 1.0 / len(models) if self.cfg.federate.ignore_weight else 1.0
         params = ss_params(recover_fun) if recover_fun else None
         avg = OrderedDict()
         keys = list(models[0][1].keys())
@@ -71,11 +70,13 @@ class ClientsAvgAggregator(DeviceEngine, _ModelIO, Aggregator):
                       if key in m]
             if params is None:
                 avg[key] = ops.ss_recover(shares, 1.0, 0.0, 1.0, 1.0,
-                                          recover=False).to(out_dev)
+                                          recover=False,
+                                          weight=w).to(out_dev)
             else:
                 mod, maximum, eps = params
                 avg[key] = ops.ss_recover(shares, mod, maximum, eps,
-                                          float(total)).to(out_dev)
+                                          float(total),
+                                          weight=w).to(out_dev)
         return avg
 
 
@@ -97,9 +98,17 @@ def _share_to_device(x, dev):
     return t.to(dev).contiguous()
 
 
+_DT_CODE = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2,
+            torch.float64: 3, torch.int64: 4}
+
+
 class OnlineClientsAvgAggregator(ClientsAvgAggregator):
     """Streaming running mean (clients_avg_aggregator.py:103-148):
-    m = (cnt*m + s*x) / (cnt + s) per client, on the GPU."""
+    m = (cnt*m + s*x) / (cnt + s) per client, on the GPU.  fp32 keys with
+    fp32 uploads live in one bucket and take one launch per upload; any
+    other dtype pair follows ATen's promotion per key
+    (fsagg_online_inc_typed) — an int64 counter becomes a float32 mean, an
+    fp64 upload promotes its key."""
     def __init__(self, model=None, device='cpu', src_device='cpu',
                  config=None):
         super().__init__(model, device, config)
@@ -108,15 +117,37 @@ class OnlineClientsAvgAggregator(ClientsAvgAggregator):
     def reset(self):
         sd = self.model.state_dict()
         self._layout_m = self._layout(sd)
+        dev = self.compute_device
         self._m = torch.zeros(self._layout_m.numel, dtype=torch.float32,
-                              device=self.compute_device)
-        # non-fp32 model entries (e.g. BN counters) stay zeros of their dtype
+                              device=dev)
+        # keys held outside the fp32 bucket (other dtypes, or promoted)
         self._m_other = OrderedDict(
-            (k, torch.zeros_like(sd[k], device=self.src_device))
-            for k in self._layout_m.other)
+            (k, torch.zeros(param2tensor(sd[k]).shape, dtype=dt, device=dev))
+            for k, dt in self._layout_m.other.items())
         self._keys = list(sd.keys())
         self._x = torch.zeros_like(self._m)
         self.cnt = 0
+
+    def _typed_inc(self, k, m, x, sample_size):
+        """One key through fsagg_online_inc_typed; returns the new value."""
+        from ... import _lib as L
+        if m.dtype not in _DT_CODE or x.dtype not in _DT_CODE:
+            raise TypeError('online aggregation of %s/%s key %r' %
+                            (m.dtype, x.dtype, k))
+        ct = torch.promote_types(m.dtype, x.dtype)
+        odt = torch.float32 if ct == torch.int64 else ct
+        x = x.to(m.device).contiguous()
+        m = m.contiguous()
+        out = m if odt == m.dtype else torch.empty(m.shape, dtype=odt,
+                                                   device=m.device)
+        if m.numel() != x.numel():
+            raise ValueError('upload of key %r has %d elements, the model '
+                             '%d' % (k, x.numel(), m.numel()))
+        L.check(L.load().fsagg_online_inc_typed(
+            m.data_ptr(), _DT_CODE[m.dtype], x.data_ptr(), _DT_CODE[x.dtype],
+            out.data_ptr(), _DT_CODE[ct], int(self.cnt), int(sample_size),
+            m.numel(), ops._stream(m.device)), 'fsagg_online_inc_typed')
+        return out
 
     def inc(self, content):
         if not isinstance(content, tuple):
@@ -124,22 +155,35 @@ class OnlineClientsAvgAggregator(ClientsAvgAggregator):
                 "{} is not a tuple (sample_size, model_para)".format(content))
         sample_size, model_params = content
         lay = self._layout_m
-        for k in lay.other:
-            if k in model_params:
-                raise NotImplementedError(
-                    'online aggregation of non-fp32 key %r' % k)
-        lay.pack_device(OrderedDict(
-            (k, param2tensor(model_params[k])) for k in lay.keys
-            if k in model_params), self._x)
-        if all(k in model_params for k in lay.keys):
-            ops.online_inc(self._m, self._x, self.cnt, sample_size)
-        else:
-            for k in lay.keys:
-                if k not in model_params:
-                    continue
-                o, m = lay.offsets[k], lay.numels[k]
-                ops.online_inc(self._m[o:o + m], self._x[o:o + m], self.cnt,
-                               sample_size)
+        fast = []
+        for k in lay.keys:
+            if k in model_params and k not in self._m_other and \
+                    param2tensor(model_params[k]).dtype == torch.float32:
+                fast.append(k)
+        if fast:
+            lay.pack_device(OrderedDict(
+                (k, param2tensor(model_params[k])) for k in fast), self._x)
+            if len(fast) == len(lay.keys):
+                ops.online_inc(self._m, self._x, self.cnt, sample_size)
+            else:
+                for k in fast:
+                    o, m = lay.offsets[k], lay.numels[k]
+                    ops.online_inc(self._m[o:o + m], self._x[o:o + m],
+                                   self.cnt, sample_size)
+        for k in self._keys:
+            if k not in model_params or k in fast:
+                continue
+            x = param2tensor(model_params[k])
+            if k in self._m_other:
+                m = self._m_other[k]
+            else:                    # an fp32 bucket key, non-fp32 upload
+                o, n = lay.offsets[k], lay.numels[k]
+                m = self._m[o:o + n].view(lay.shapes[k])
+            new = self._typed_inc(k, m, x, sample_size)
+            if k in self._m_other or new.dtype != torch.float32:
+                self._m_other[k] = new          # promoted keys leave the
+            elif new is not m:                  # bucket for good
+                m.copy_(new)
         self.cnt += sample_size
 
     @property

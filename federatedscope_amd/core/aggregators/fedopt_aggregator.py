@@ -48,26 +48,27 @@ class FedOptAggregator(ClientsAvgAggregator):
                 'FedOpt server optimizer %r is not on the device path '
                 '(supported: %s)' % (self.opt_type, ', '.join(_SUPPORTED)))
         self.kw = opt
+        if opt.get('maximize', False):
+            raise NotImplementedError('maximize=True')
         if self.opt_type == 'SGD':
             self.momentum = float(opt.get('momentum', 0.0))
             self.dampening = float(opt.get('dampening', 0.0))
             self.weight_decay = float(opt.get('weight_decay', 0.0))
             self.nesterov = bool(opt.get('nesterov', False))
-            if opt.get('maximize', False):
-                raise NotImplementedError('maximize=True')
+            self.amsgrad = False
         else:
             betas = opt.get('betas', (0.9, 0.999))
             self.beta1, self.beta2 = float(betas[0]), float(betas[1])
             self.eps = float(opt.get('eps', 1e-8))
             self.weight_decay = float(opt.get('weight_decay', 0.0))
-            if opt.get('amsgrad', False) or opt.get('maximize', False):
-                raise NotImplementedError('amsgrad / maximize')
+            self.amsgrad = bool(opt.get('amsgrad', False))
         fo = config.fedopt
         self._annealing = bool(getattr(fo, 'annealing', False))
         self._anneal_step = int(getattr(fo, 'annealing_step_size', 2000))
         self._anneal_gamma = float(getattr(fo, 'annealing_gamma', 0.5))
         self._rounds = 0
-        self._state = {}     # layout signature -> (s0, s1, steps)
+        self._state = {}     # layout signature -> [s0, s1, s2, steps]
+        self._state64 = {}   # float64 parameter -> [s0, s1, s2, steps]
 
     def _lr(self):
         if not self._annealing:
@@ -75,44 +76,84 @@ class FedOptAggregator(ClientsAvgAggregator):
         return self.lr0 * self._anneal_gamma ** (self._rounds //
                                                  self._anneal_step)
 
-    def aggregate(self, agg_info):
+    def _new_model(self, agg_info):
+        """super().aggregate(agg_info) of the reference (:30): the FedAvg —
+        or, with federate.use_ss, the secret-sharing average — as (layout,
+        fp32 bucket, {other-dtype key: device tensor})."""
         models = agg_info["client_feedback"]
+        if self.cfg.federate.use_ss:
+            recover_fun = agg_info.get('recover_fun')
+            avg = self._ss_avg(models, recover_fun)
+            dev = self.compute_device
+            avg = OrderedDict((k, torch.as_tensor(v)) for k, v in avg.items())
+            layout = self._layout(avg)
+            extra = OrderedDict((k, avg[k].to(dev)) for k in layout.other)
+            return layout, self._bucket(layout, avg), extra
         weights = fedavg_weights([s for s, _ in models],
                                  self.cfg.federate.ignore_weight)
-        layout, avg, extra, keys = self._weighted_avg_device(models, weights)
+        layout, avg, extra, _ = self._weighted_avg_device(models, weights)
+        return layout, avg, extra
+
+    def _states(self, store, key, like):
+        st = store.get(key)
+        if st is None:
+            adam = self.opt_type == 'Adam'
+            st = store[key] = [
+                torch.zeros_like(like),
+                torch.zeros_like(like) if adam else None,
+                torch.zeros_like(like) if adam and self.amsgrad else None, 0]
+        return st
+
+    def _step(self, fn, param, avg, st):
+        """One optimizer step of a contiguous device parameter range."""
+        hp = self._params(first=(st[3] == 0), step=st[3] + 1)
+        L.check(fn(param.data_ptr(), avg.data_ptr(), st[0].data_ptr(),
+                   st[1].data_ptr() if st[1] is not None else None,
+                   st[2].data_ptr() if st[2] is not None else None,
+                   param.numel(), ctypes.byref(hp), _stream(param.device)),
+                'fedopt step')
+
+    def aggregate(self, agg_info):
+        layout, avg, extra = self._new_model(agg_info)
+        lib = L.load()
         named = OrderedDict(self.model.named_parameters())
+        # parameters the aggregate holds (fedopt_aggregator.py:37-40); other
+        # state_dict entries (buffers) are returned unchanged
         step_keys = [k for k in named if k in layout.keys]
         for k in named:
-            if k in extra:
-                raise NotImplementedError('FedOpt on non-fp32 parameter %r' %
-                                          k)
-        param = self._bucket(layout, OrderedDict(
-            (k, named[k].detach() if k in named else torch.zeros(
-                layout.shapes[k])) for k in layout.keys))
-        sig = layout.signature()
-        if sig not in self._state:
-            s0 = torch.zeros_like(param)
-            s1 = torch.zeros_like(param) if self.opt_type == 'Adam' else None
-            self._state[sig] = [s0, s1, 0]
-        st = self._state[sig]
-        hp = self._params(first=(st[2] == 0), step=st[2] + 1)
-        lib = L.load()
-        for k in step_keys:      # per key: params the optimizer owns
-            o, m = layout.offsets[k], layout.numels[k]
-            for t in (param, avg, st[0]):
-                _check_f32_cuda(t[o:o + m], 'FedOpt bucket')
-            L.check(lib.fsagg_server_opt_step_f32(
-                param[o:o + m].data_ptr(), avg[o:o + m].data_ptr(),
-                st[0][o:o + m].data_ptr(),
-                st[1][o:o + m].data_ptr() if st[1] is not None else None,
-                m, ctypes.byref(hp), _stream(param.device)),
-                'fsagg_server_opt_step_f32')
-        st[2] += 1
+            if k in extra and extra[k].dtype != torch.float64:
+                raise NotImplementedError(
+                    'FedOpt on %s parameter %r' % (extra[k].dtype, k))
+        dev = self.compute_device
+        if step_keys:
+            param = self._bucket(layout, OrderedDict(
+                (k, named[k].detach() if k in named else torch.zeros(
+                    layout.shapes[k])) for k in layout.keys))
+            st = self._states(self._state, layout.signature(), param)
+            for k in step_keys:      # per key: params the optimizer owns
+                o, m = layout.offsets[k], layout.numels[k]
+                for t in (param, avg, st[0]):
+                    _check_f32_cuda(t[o:o + m], 'FedOpt bucket')
+                self._step(lib.fsagg_server_opt_step_f32, param[o:o + m],
+                           avg[o:o + m], [t[o:o + m] if t is not None
+                                          else None for t in st[:3]] +
+                           [st[3]])
+            st[3] += 1
+            views = layout.unpack(param)
+            with torch.no_grad():
+                for k in step_keys:
+                    named[k].data.copy_(views[k])
+        for k in named:              # float64 parameters, one key each
+            if k not in extra:
+                continue
+            p64 = named[k].detach().to(dev, torch.float64).contiguous()
+            a64 = extra[k].to(dev, torch.float64).contiguous()
+            st = self._states(self._state64, k, p64)
+            self._step(lib.fsagg_server_opt_step_f64, p64, a64, st)
+            st[3] += 1
+            with torch.no_grad():
+                named[k].data.copy_(p64)
         self._rounds += 1
-        views = layout.unpack(param)
-        with torch.no_grad():
-            for k in step_keys:
-                named[k].data.copy_(views[k])
         return self.model.state_dict()
 
     def _params(self, first, step):
@@ -133,7 +174,8 @@ class FedOptAggregator(ClientsAvgAggregator):
             bc2 = 1 - self.beta2**step
             hp.step_size = lr / bc1
             hp.bias_correction2_sqrt = bc2**0.5
-            hp.flags = L.FSAGG_OPT_FIRST_STEP if first else 0
+            hp.flags = (L.FSAGG_OPT_FIRST_STEP if first else 0) | \
+                (L.FSAGG_OPT_AMSGRAD if self.amsgrad else 0)
         return hp
 
 

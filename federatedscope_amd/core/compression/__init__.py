@@ -1,6 +1,4 @@
-from .utils import (symmetric_uniform_quantization,
-                    symmetric_uniform_dequantization)
+from .utils import symmetric_uniform_dequantization
 from .wire import QuantPlan, WireStager
 
-__all__ = ['symmetric_uniform_quantization',
-           'symmetric_uniform_dequantization', 'QuantPlan', 'WireStager']
+__all__ = ['symmetric_uniform_dequantization', 'QuantPlan', 'WireStager']

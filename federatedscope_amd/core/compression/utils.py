@@ -1,9 +1,8 @@
-"""Symmetric uniform quantisation of uploads (drop-in for
-federatedscope/core/compression/utils.py).
+"""Server side of the symmetric uniform quantisation of uploads (drop-in
+for the dequantisation half of federatedscope/core/compression/utils.py).
 
-* ``symmetric_uniform_quantization`` is the CLIENT side (utils.py:8-61): it
-  stays a restatement in torch ops on whatever device the model lives —
-  clients are not the server's hot path.
+* Quantisation is the CLIENTS' job (utils.py:8-61) and is not rebuilt here:
+  FederatedScope's own client code keeps producing the wire dicts.
 * ``symmetric_uniform_dequantization`` is the SERVER side (utils.py:64-90,
   called from Server.callback_funcs_model_para, server.py:946-960): the
   ``value * alpha`` of every ``*.weight_quant`` key runs in libfsagg's
@@ -12,54 +11,10 @@ federatedscope/core/compression/utils.py).
   host tensors out.  The server's staged path (WireStager) decodes uploads
   straight into the device client stack instead.
 """
-import logging
-
 import torch
 
 from ... import _lib as L
 from ... import ops
-
-logger = logging.getLogger(__name__)
-
-
-def _symmetric_uniform_quantization(x, nbits, stochastic=False):
-    """utils.py:8-29, op for op."""
-    assert (torch.isnan(x).sum() == 0)
-    assert (torch.isinf(x).sum() == 0)
-    c = torch.max(torch.abs(x))
-    s = c / (2**(nbits - 1) - 1)
-    if s == 0:
-        return x, s
-    qx = x / s
-    if stochastic:
-        noise = qx.new(qx.shape).uniform_(-0.5, 0.5)
-        qx.add_(noise)
-    qx.clamp_(-(2**(nbits - 1) - 1), (2**(nbits - 1) - 1)).round_()
-    return qx, s
-
-
-def symmetric_uniform_quantization(state_dict, nbits=8):
-    """utils.py:32-61: quantise the weights of conv / fc layers to int8 or
-    int16 with one fp32 scale per tensor."""
-    if nbits == 8:
-        quant_data_type = torch.int8
-    elif nbits == 16:
-        quant_data_type = torch.int16
-    else:
-        logger.info(f'The provided value of nbits ({nbits}) is invalid, and '
-                    f'we change it to 8')
-        nbits = 8
-        quant_data_type = torch.int8
-    quant_state_dict = dict()
-    for key, value in state_dict.items():
-        if ('fc' in key or 'conv' in key) and 'weight' == key.split('.')[-1]:
-            q_weight, w_s = _symmetric_uniform_quantization(value, nbits=nbits)
-            quant_state_dict[key.replace(
-                'weight', 'weight_quant')] = q_weight.type(quant_data_type)
-            quant_state_dict[key.replace('weight', 'weight_scale')] = w_s
-        else:
-            quant_state_dict[key] = value
-    return quant_state_dict
 
 
 def scale_to_f32(alpha):

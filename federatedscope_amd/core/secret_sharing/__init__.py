@@ -1,3 +1,3 @@
-from .secret_sharing import AdditiveSecretSharing, SecretSharing, ss_params
+from .secret_sharing import ss_params
 
-__all__ = ['AdditiveSecretSharing', 'SecretSharing', 'ss_params']
+__all__ = ['ss_params']

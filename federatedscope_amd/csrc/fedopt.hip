@@ -5,11 +5,13 @@
 // takes one torch.optim step on the server model.  Here the step is one
 // fused elementwise pass over the device buckets — param, FedAvg result and
 // the optimizer state are each read once and param/state written once
-// (SGD: 16 B/elem with momentum, Adam: 24 B/elem) — following the
-// arithmetic of torch's single-tensor CPU kernels (the reference runs the
-// optimizer on CPU tensors): `add(alpha)` is a fused multiply-add
-// (Vectorized fmadd), `lerp` with weight < 0.5 is self + w·(end − self) as an
-// fma, `addcmul`/`addcdiv` are self + (v·t1)·t2 and self + (v·t1)/t2.
+// (SGD: 16 B/elem with momentum, Adam: 24 B/elem, +8 with amsgrad) —
+// following the arithmetic of torch's single-tensor CPU kernels (the
+// reference runs the optimizer on CPU tensors): `add(alpha)` is a fused
+// multiply-add (Vectorized fmadd), `lerp` with weight < 0.5 is
+// self + w·(end − self) as an fma, `addcmul`/`addcdiv` are
+// self + (v·t1)·t2 and self + (v·t1)/t2.  float32 and float64 parameters
+// (the Python scalars enter as the tensor's type, as ATen casts them).
 #include "common.h"
 
 namespace fsagg {
@@ -17,58 +19,126 @@ namespace {
 
 constexpr int kBlock = 256;
 
-__device__ __forceinline__ float fma_rn(float a, float b, float c) {
+__device__ __forceinline__ float fma_t(float a, float b, float c) {
   return __builtin_fmaf(a, b, c);
 }
+__device__ __forceinline__ double fma_t(double a, double b, double c) {
+  return __builtin_fma(a, b, c);
+}
+// single-rounded ops of either type, never contracted
+__device__ __forceinline__ float mul_t(float a, float b) { return __fmul_rn(a, b); }
+__device__ __forceinline__ double mul_t(double a, double b) { return __dmul_rn(a, b); }
+__device__ __forceinline__ float add_t(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ double add_t(double a, double b) { return __dadd_rn(a, b); }
+__device__ __forceinline__ float sub_t(float a, float b) { return __fsub_rn(a, b); }
+__device__ __forceinline__ double sub_t(double a, double b) { return __dsub_rn(a, b); }
+__device__ __forceinline__ float div_t(float a, float b) { return __fdiv_rn(a, b); }
+__device__ __forceinline__ double div_t(double a, double b) { return __ddiv_rn(a, b); }
+__device__ __forceinline__ float sqrt_t(float a) { return __fsqrt_rn(a); }
+__device__ __forceinline__ double sqrt_t(double a) { return __dsqrt_rn(a); }
 
+template <typename T>
 __global__ __launch_bounds__(kBlock) void sgd_step_kernel(
-    float *__restrict__ param, const float *__restrict__ avg,
-    float *__restrict__ buf, int64_t numel, fsagg_opt_params hp) {
+    T *__restrict__ param, const T *__restrict__ avg, T *__restrict__ buf,
+    int64_t numel, fsagg_opt_params hp) {
   const bool nesterov = hp.flags & FSAGG_OPT_NESTEROV;
   const bool first = hp.flags & FSAGG_OPT_FIRST_STEP;
+  const T lr = T(hp.lr), wd = T(hp.weight_decay), mom = T(hp.momentum);
+  const T keep = T(1.0 - hp.dampening);  // Python's 1 - dampening
   for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < numel;
        p += int64_t(gridDim.x) * kBlock) {
-    const float x = param[p];
-    float g = x - avg[p];  // grads = model - new_model  (fedopt_aggregator.py:35)
-    if (hp.weight_decay != 0.0f) g = fma_rn(x, hp.weight_decay, g);
-    if (hp.momentum != 0.0f) {
-      float b;
+    const T x = param[p];
+    T g = sub_t(x, avg[p]);  // grads = model - new_model  (fedopt_aggregator.py:35)
+    if (hp.weight_decay != 0.0) g = fma_t(x, wd, g);
+    if (hp.momentum != 0.0) {
+      T b;
       if (first) {
         b = g;  // torch.clone(grad)
       } else {
-        b = mul_rn(buf[p], hp.momentum);
-        b = fma_rn(g, 1.0f - hp.dampening, b);
+        b = mul_t(buf[p], mom);
+        b = fma_t(g, keep, b);
       }
       buf[p] = b;
-      g = nesterov ? fma_rn(b, hp.momentum, g) : b;
+      g = nesterov ? fma_t(b, mom, g) : b;
     }
-    param[p] = fma_rn(g, -hp.lr, x);
+    param[p] = fma_t(g, -lr, x);
   }
 }
 
+template <typename T, bool AMS>
 __global__ __launch_bounds__(kBlock) void adam_step_kernel(
-    float *__restrict__ param, const float *__restrict__ avg,
-    float *__restrict__ m1, float *__restrict__ m2, int64_t numel,
+    T *__restrict__ param, const T *__restrict__ avg, T *__restrict__ m1,
+    T *__restrict__ m2, T *__restrict__ vmax, int64_t numel,
     fsagg_opt_params hp) {
-  const float w1 = 1.0f - hp.beta1;
-  const float w2 = 1.0f - hp.beta2;
+  const T w1 = T(1.0 - hp.beta1);  // lerp weight, Python's 1 - beta1
+  const T w2 = T(1.0 - hp.beta2);  // addcmul value
+  const T b2 = T(hp.beta2), wd = T(hp.weight_decay), eps = T(hp.eps);
+  const T bc2 = T(hp.bias_correction2_sqrt), neg_step = T(-hp.step_size);
   for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < numel;
        p += int64_t(gridDim.x) * kBlock) {
-    const float x = param[p];
-    float g = x - avg[p];
-    if (hp.weight_decay != 0.0f) g = fma_rn(x, hp.weight_decay, g);
-    float a = m1[p];
+    const T x = param[p];
+    T g = sub_t(x, avg[p]);
+    if (hp.weight_decay != 0.0) g = fma_t(x, wd, g);
+    T a = m1[p];
     // exp_avg.lerp_(grad, 1 - beta1)
-    a = (w1 < 0.5f) ? fma_rn(w1, g - a, a) : g - mul_rn(g - a, 1.0f - w1);
-    float v = mul_rn(m2[p], hp.beta2);
-    v = add_rn(v, mul_rn(mul_rn(w2, g), g));      // addcmul_(g, g, 1 - beta2)
-    const float denom =
-        add_rn(__fdiv_rn(__fsqrt_rn(v), hp.bias_correction2_sqrt), hp.eps);
+    a = (w1 < T(0.5)) ? fma_t(w1, sub_t(g, a), a)
+                      : sub_t(g, mul_t(sub_t(g, a), sub_t(T(1), w1)));
+    T v = mul_t(m2[p], b2);
+    v = add_t(v, mul_t(mul_t(w2, g), g));  // addcmul_(g, g, 1 - beta2)
     m1[p] = a;
     m2[p] = v;
+    T vd = v;
+    if (AMS) {  // torch.maximum(max_exp_avg_sq, exp_avg_sq, out=...)
+      const T mx = vmax[p];
+      vd = (mx != mx || v != v) ? (mx != mx ? mx : v) : (mx > v ? mx : v);
+      vmax[p] = vd;
+    }
+    const T denom = add_t(div_t(sqrt_t(vd), bc2), eps);
     // param.addcdiv_(exp_avg, denom, value=-step_size)
-    param[p] = add_rn(x, __fdiv_rn(mul_rn(-hp.step_size, a), denom));
+    param[p] = add_t(x, div_t(mul_t(neg_step, a), denom));
   }
+}
+
+template <typename T>
+int opt_step(T *param, const T *avg, T *state0, T *state1, T *state2,
+             int64_t numel, const fsagg_opt_params *hp, fsagg_stream_t stream,
+             const char *what) {
+  if (!param || !avg || !hp || numel < 0) {
+    set_error("%s: invalid argument", what);
+    return FSAGG_EINVAL;
+  }
+  if (numel == 0) return FSAGG_OK;
+  const unsigned grid = stream_grid(numel, kBlock, 256 * 8);
+  hipStream_t s = as_stream(stream);
+  switch (hp->kind) {
+    case FSAGG_OPT_SGD:
+      if (hp->momentum != 0.0 && !state0) {
+        set_error("%s: SGD momentum needs state0", what);
+        return FSAGG_EINVAL;
+      }
+      hipLaunchKernelGGL(sgd_step_kernel<T>, dim3(grid), dim3(kBlock), 0, s,
+                         param, avg, state0, numel, *hp);
+      break;
+    case FSAGG_OPT_ADAM:
+      if (!state0 || !state1 || ((hp->flags & FSAGG_OPT_AMSGRAD) && !state2)) {
+        set_error("%s: Adam needs state0 and state1 (and state2 with "
+                  "amsgrad)", what);
+        return FSAGG_EINVAL;
+      }
+      if (hp->flags & FSAGG_OPT_AMSGRAD)
+        hipLaunchKernelGGL((adam_step_kernel<T, true>), dim3(grid),
+                           dim3(kBlock), 0, s, param, avg, state0, state1,
+                           state2, numel, *hp);
+      else
+        hipLaunchKernelGGL((adam_step_kernel<T, false>), dim3(grid),
+                           dim3(kBlock), 0, s, param, avg, state0, state1,
+                           state2, numel, *hp);
+      break;
+    default:
+      set_error("%s: unknown optimizer kind %d", what, hp->kind);
+      return FSAGG_EINVAL;
+  }
+  return check_launch(what);
 }
 
 }  // namespace
@@ -78,37 +148,18 @@ using namespace fsagg;
 
 extern "C" int fsagg_server_opt_step_f32(float *param, const float *avg,
                                          float *state0, float *state1,
-                                         int64_t numel,
+                                         float *state2, int64_t numel,
                                          const fsagg_opt_params *hp,
                                          fsagg_stream_t stream) {
-  if (!param || !avg || !hp || numel < 0) {
-    set_error("fsagg_server_opt_step_f32: invalid argument");
-    return FSAGG_EINVAL;
-  }
-  if (numel == 0) return FSAGG_OK;
-  const unsigned grid = stream_grid(numel, kBlock, 256 * 8);
-  hipStream_t s = as_stream(stream);
-  switch (hp->kind) {
-    case FSAGG_OPT_SGD:
-      if (hp->momentum != 0.0f && !state0) {
-        set_error("fsagg_server_opt_step_f32: SGD momentum needs state0");
-        return FSAGG_EINVAL;
-      }
-      hipLaunchKernelGGL(sgd_step_kernel, dim3(grid), dim3(kBlock), 0, s,
-                         param, avg, state0, numel, *hp);
-      break;
-    case FSAGG_OPT_ADAM:
-      if (!state0 || !state1) {
-        set_error("fsagg_server_opt_step_f32: Adam needs state0 and state1");
-        return FSAGG_EINVAL;
-      }
-      hipLaunchKernelGGL(adam_step_kernel, dim3(grid), dim3(kBlock), 0, s,
-                         param, avg, state0, state1, numel, *hp);
-      break;
-    default:
-      set_error("fsagg_server_opt_step_f32: unknown optimizer kind %d",
-                hp->kind);
-      return FSAGG_EINVAL;
-  }
-  return check_launch("fsagg_server_opt_step_f32");
+  return opt_step<float>(param, avg, state0, state1, state2, numel, hp,
+                         stream, "fsagg_server_opt_step_f32");
+}
+
+extern "C" int fsagg_server_opt_step_f64(double *param, const double *avg,
+                                         double *state0, double *state1,
+                                         double *state2, int64_t numel,
+                                         const fsagg_opt_params *hp,
+                                         fsagg_stream_t stream) {
+  return opt_step<double>(param, avg, state0, state1, state2, numel, hp,
+                          stream, "fsagg_server_opt_step_f64");
 }

@@ -445,6 +445,93 @@ __global__ __launch_bounds__(kBlock) void online_inc_kernel(
   }
 }
 
+// Online running mean with ATen's dtype rules (clients_avg_aggregator.py:
+// 136-139 on tensors of any of f32/f16/bf16/f64/i64): a = cnt*m in m's
+// type, b = s*x in x's type (reduced floats computed in float and rounded
+// once — ATen's opmath), c = a + b in the promoted type (both operands cast
+// to it first), out = c / (cnt + s) — integers become float32 (true
+// division).  Values travel as doubles (exact for every float type) or
+// int64.  A per-element type switch: this path carries the odd keys (BN
+// counters, fp16 uploads), never the bulk.
+struct TV {
+  double f;
+  int64_t i;
+};
+
+__device__ __forceinline__ TV load_tv(const void *p, int dt, int64_t k) {
+  TV v{0.0, 0};
+  switch (dt) {
+    case FSAGG_F32: v.f = gld(static_cast<const float *>(p) + k); break;
+    case FSAGG_F64: v.f = gld(static_cast<const double *>(p) + k); break;
+    case FSAGG_F16:
+      v.f = __half2float(__ushort_as_half(
+          gld(static_cast<const unsigned short *>(p) + k)));
+      break;
+    case FSAGG_BF16: v.f = bf2f(gld(static_cast<const uint16_t *>(p) + k)); break;
+    default: v.i = gld(static_cast<const int64_t *>(p) + k); break;
+  }
+  return v;
+}
+
+// round a float-computed value to type dt (dt a float type)
+__device__ __forceinline__ double round_to(float x, int dt) {
+  if (dt == FSAGG_F16) return __half2float(__float2half(x));
+  if (dt == FSAGG_BF16) return bf2f(f2bf_rne(x));
+  return x;
+}
+
+// convert a value of type `from` to type `to` (to a float type)
+__device__ __forceinline__ double cast_to(TV v, int from, int to) {
+  if (to == FSAGG_F64) return from == FSAGG_I64 ? double(v.i) : v.f;
+  const float x = from == FSAGG_I64 ? float(v.i) : float(v.f);
+  return round_to(x, to);
+}
+
+// python int k * tensor value of type dt
+__device__ __forceinline__ TV mul_scalar(TV v, int64_t k, int dt) {
+  TV r{0.0, 0};
+  if (dt == FSAGG_I64) {
+    r.i = int64_t(uint64_t(v.i) * uint64_t(k));
+  } else if (dt == FSAGG_F64) {
+    r.f = __dmul_rn(v.f, double(k));
+  } else {
+    r.f = round_to(mul_rn(float(v.f), float(k)), dt);
+  }
+  return r;
+}
+
+__global__ __launch_bounds__(kBlock) void online_typed_kernel(
+    const void *__restrict__ m, int mdt, const void *__restrict__ x, int xdt,
+    void *__restrict__ out, int cdt, int64_t cnt, int64_t s, int64_t numel) {
+  const int odt = cdt == FSAGG_I64 ? FSAGG_F32 : cdt;
+  for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < numel;
+       p += int64_t(gridDim.x) * kBlock) {
+    const TV a = mul_scalar(load_tv(m, mdt, p), cnt, mdt);
+    const TV b = mul_scalar(load_tv(x, xdt, p), s, xdt);
+    double r;
+    if (cdt == FSAGG_I64) {
+      const int64_t c = int64_t(uint64_t(a.i) + uint64_t(b.i));
+      r = __fdiv_rn(float(c), float(cnt + s));
+    } else if (cdt == FSAGG_F64) {
+      r = __ddiv_rn(__dadd_rn(cast_to(a, mdt, cdt), cast_to(b, xdt, cdt)),
+                    double(cnt + s));
+    } else {
+      const float c = float(round_to(
+          add_rn(float(cast_to(a, mdt, cdt)), float(cast_to(b, xdt, cdt))),
+          cdt));
+      r = round_to(__fdiv_rn(c, float(cnt + s)), cdt);
+    }
+    switch (odt) {
+      case FSAGG_F32: static_cast<float *>(out)[p] = float(r); break;
+      case FSAGG_F64: static_cast<double *>(out)[p] = r; break;
+      case FSAGG_F16:
+        static_cast<__half *>(out)[p] = __float2half(float(r));
+        break;
+      default: static_cast<uint16_t *>(out)[p] = f2bf_rne(float(r)); break;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void add_kernel(
     const float *__restrict__ a, const float *__restrict__ b,
     float *__restrict__ out, int64_t nvec, int64_t numel) {
@@ -605,6 +692,25 @@ extern "C" int fsagg_online_inc_f32(float *m, const float *x, float cnt,
                      dim3(kBlock), 0, as_stream(stream), m, x, cnt, s, denom,
                      numel);
   return check_launch("fsagg_online_inc_f32");
+}
+
+extern "C" int fsagg_online_inc_typed(const void *m, int m_dtype,
+                                      const void *x, int x_dtype, void *out,
+                                      int common_dtype, int64_t cnt,
+                                      int64_t s, int64_t numel,
+                                      fsagg_stream_t stream) {
+  auto ok = [](int d) { return d >= FSAGG_F32 && d <= FSAGG_I64; };
+  if (!m || !x || !out || numel < 0 || !ok(m_dtype) || !ok(x_dtype) ||
+      !ok(common_dtype)) {
+    set_error("fsagg_online_inc_typed: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  if (numel == 0) return FSAGG_OK;
+  hipLaunchKernelGGL(online_typed_kernel,
+                     dim3(stream_grid(numel, kBlock, 256 * 8)), dim3(kBlock),
+                     0, as_stream(stream), m, m_dtype, x, x_dtype, out,
+                     common_dtype, cnt, s, numel);
+  return check_launch("fsagg_online_inc_typed");
 }
 
 extern "C" int fsagg_add_f32(const float *a, const float *b, float *out,

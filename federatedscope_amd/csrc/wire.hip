@@ -131,13 +131,14 @@ __device__ __forceinline__ float ss_recover_one(double acc, double mod,
 
 __global__ __launch_bounds__(kBlock) void ss_recover_kernel(
     const void *const *__restrict__ rows, const uint8_t *__restrict__ is_int,
-    int n, int64_t numel, double mod, double maximum, double epsilon,
-    double total, int recover, float *__restrict__ out,
+    int n, int64_t numel, double weight, double mod, double maximum,
+    double epsilon, double total, int recover, float *__restrict__ out,
     double *__restrict__ out_sum) {
   const int64_t p = 2 * (int64_t(blockIdx.x) * kBlock + threadIdx.x);
   if (p >= numel) return;
   const bool two = p + 1 < numel;
-  // avg = x_0 * 1.0, then avg += x_i * 1.0 in list order (float64)
+  // avg = x_0 * w, then avg += x_i * w in list order (float64; w = 1.0, or
+  // 1/n with ignore_weight — x * 1.0 is exact)
   double a0 = 0.0, a1 = 0.0;
   int i = 0;
   for (; i + kSsRows <= n; i += kSsRows) {
@@ -147,13 +148,17 @@ __global__ __launch_bounds__(kBlock) void ss_recover_kernel(
       ss_load2(rows[i + u], is_int[i + u], p, two, x[u][0], x[u][1]);
 #pragma unroll
     for (int u = 0; u < kSsRows; ++u) {
-      a0 = (i + u == 0) ? x[u][0] : __dadd_rn(a0, x[u][0]);
-      a1 = (i + u == 0) ? x[u][1] : __dadd_rn(a1, x[u][1]);
+      const double y0 = __dmul_rn(x[u][0], weight);
+      const double y1 = __dmul_rn(x[u][1], weight);
+      a0 = (i + u == 0) ? y0 : __dadd_rn(a0, y0);
+      a1 = (i + u == 0) ? y1 : __dadd_rn(a1, y1);
     }
   }
   for (; i < n; ++i) {
     double x0, x1;
     ss_load2(rows[i], is_int[i], p, two, x0, x1);
+    x0 = __dmul_rn(x0, weight);
+    x1 = __dmul_rn(x1, weight);
     a0 = i == 0 ? x0 : __dadd_rn(a0, x0);
     a1 = i == 0 ? x1 : __dadd_rn(a1, x1);
   }
@@ -198,10 +203,10 @@ extern "C" int fsagg_wire_unpack_f32(const void *src, int64_t src_bytes,
 
 extern "C" int fsagg_ss_recover_f32(const void *const *rows,
                                     const uint8_t *row_is_int, int n,
-                                    int64_t numel, double mod, double maximum,
-                                    double epsilon, double total, int recover,
-                                    float *out, double *out_sum,
-                                    fsagg_stream_t stream) {
+                                    int64_t numel, double weight, double mod,
+                                    double maximum, double epsilon,
+                                    double total, int recover, float *out,
+                                    double *out_sum, fsagg_stream_t stream) {
   if (!rows || !row_is_int || n < 1 || numel < 0 ||
       (recover && !out) || (!recover && !out_sum)) {
     set_error("fsagg_ss_recover_f32: invalid argument (n=%d)", n);
@@ -212,7 +217,7 @@ extern "C" int fsagg_ss_recover_f32(const void *const *rows,
   hipLaunchKernelGGL(ss_recover_kernel,
                      dim3(unsigned((pairs + kBlock - 1) / kBlock)),
                      dim3(kBlock), 0, as_stream(stream), rows, row_is_int, n,
-                     numel, mod, maximum, epsilon, total, recover, out,
-                     out_sum);
+                     numel, weight, mod, maximum, epsilon, total, recover,
+                     out, out_sum);
   return check_launch("fsagg_ss_recover_f32");
 }

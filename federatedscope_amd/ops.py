@@ -430,10 +430,12 @@ def wire_unpack(src, segs, nseg, max_len, scales, out, src_bytes=None,
     return out
 
 
-def ss_recover(shares, mod, maximum, epsilon, total, recover=True):
+def ss_recover(shares, mod, maximum, epsilon, total, recover=True,
+               weight=1.0):
     """Secret-sharing FedAvg of one key: ``shares`` are per-client device
-    tensors (float64 or int64, same shape).  Returns fp32 (recovered, divided
-    by ``total``) or, with ``recover=False``, the float64 share sums."""
+    tensors (float64 or int64, same shape), each multiplied by ``weight``
+    (float64) and summed in list order.  Returns fp32 (recovered, divided
+    by ``total``) or, with ``recover=False``, the float64 sums."""
     if not shares:
         raise ValueError('no shares')
     dev = shares[0].device
@@ -453,7 +455,8 @@ def ss_recover(shares, mod, maximum, epsilon, total, recover=True):
     out = torch.empty(shape, dtype=torch.float32 if recover else
                       torch.float64, device=dev)
     L.check(L.load().fsagg_ss_recover_f32(
-        tab.data_ptr(), is_int.data_ptr(), len(shares), numel, float(mod),
+        tab.data_ptr(), is_int.data_ptr(), len(shares), numel,
+        float(weight), float(mod),
         float(maximum), float(epsilon), float(total), 1 if recover else 0,
         out.data_ptr() if recover else None,
         None if recover else out.data_ptr(), _stream(dev)),

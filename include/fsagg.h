@@ -95,6 +95,20 @@ int fsagg_weighted_sum_typed(const void *const *rows, int in_dtype,
 int fsagg_online_inc_f32(float *m, const float *x, float cnt, float s,
                          float denom, int64_t numel, fsagg_stream_t stream);
 
+/*
+ * The same running mean for keys that are not float32 on both sides, with
+ * ATen's dtype rules (clients_avg_aggregator.py:136-139 on any tensors):
+ * a = cnt*m in m's type, b = s*x in x's type, c = a + b in common_dtype
+ * (torch.promote_types of the two), out = c / (cnt + s) in common_dtype —
+ * float32 when common_dtype is FSAGG_I64 (true division).  Reduced floats
+ * are computed in float and rounded once per op.  out may alias m when
+ * their types agree.
+ */
+int fsagg_online_inc_typed(const void *m, int m_dtype, const void *x,
+                           int x_dtype, void *out, int common_dtype,
+                           int64_t cnt, int64_t s, int64_t numel,
+                           fsagg_stream_t stream);
+
 /* out = a + b elementwise (the robust rules' init + update; e.g.
  * median_aggregator.py:37-41).  out may alias a or b. */
 int fsagg_add_f32(const float *a, const float *b, float *out, int64_t numel,
@@ -172,23 +186,30 @@ int fsagg_row_sqnorm_f32(const float *const *rows, int n, int64_t numel,
  * FedOpt server step on the aggregated bucket (fedopt_aggregator.py:26-44):
  * per element g = param - avg, then one torch.optim step in place on param
  * and the optimizer state buckets (SGD: state0 = momentum buffer; Adam:
- * state0 = exp_avg, state1 = exp_avg_sq).  Scalars are the host's doubles
- * rounded to fp32 (Adam's step_size = lr / (1 - beta1^t) and
- * bias_correction2_sqrt = sqrt(1 - beta2^t) are computed on the host, as
- * torch does).  Tolerance-pinned: ATen's CPU optimizer arithmetic (fmadd in
- * the vectorised body) is ISA-dependent.
+ * state0 = exp_avg, state1 = exp_avg_sq, state2 = max_exp_avg_sq with
+ * amsgrad).  Scalars are the host's doubles; the kernels convert them to the
+ * parameter type as ATen does (Adam's step_size = lr / (1 - beta1^t) and
+ * bias_correction2_sqrt = (1 - beta2^t)^0.5 are computed on the host, as
+ * torch does).  Tolerance-pinned: ATen's CPU optimizer arithmetic (fmadd
+ * in the vectorised body) is ISA-dependent.  _f32 for float32 parameters,
+ * _f64 for float64 ones.
  */
 enum fsagg_opt_kind { FSAGG_OPT_SGD = 0, FSAGG_OPT_ADAM = 1 };
-enum fsagg_opt_flags { FSAGG_OPT_NESTEROV = 1, FSAGG_OPT_FIRST_STEP = 2 };
+enum fsagg_opt_flags { FSAGG_OPT_NESTEROV = 1, FSAGG_OPT_FIRST_STEP = 2,
+                       FSAGG_OPT_AMSGRAD = 4 };
 typedef struct fsagg_opt_params {
   int kind;
   int flags;
-  float lr, momentum, dampening, weight_decay;
-  float beta1, beta2, eps, step_size, bias_correction2_sqrt;
+  double lr, momentum, dampening, weight_decay;
+  double beta1, beta2, eps, step_size, bias_correction2_sqrt;
 } fsagg_opt_params;
 int fsagg_server_opt_step_f32(float *param, const float *avg, float *state0,
-                              float *state1, int64_t numel,
+                              float *state1, float *state2, int64_t numel,
                               const fsagg_opt_params *hp,
+                              fsagg_stream_t stream);
+int fsagg_server_opt_step_f64(double *param, const double *avg,
+                              double *state0, double *state1, double *state2,
+                              int64_t numel, const fsagg_opt_params *hp,
                               fsagg_stream_t stream);
 
 /*
@@ -218,8 +239,11 @@ int fsagg_wire_unpack_f32(const void *src, int64_t src_bytes,
 
 /*
  * Secret-sharing FedAvg (cfg.federate.use_ss) in one pass:
- *     acc = Σ_i double(x_i[p])      (list order, weight 1.0; int64 shares
- *                                    converted round-to-nearest, as numpy)
+ *     acc = Σ_i double(x_i[p]) * w  (list order; w = 1.0, or 1/n when
+ *                                    ignore_weight is also set — the
+ *                                    reference tests it first, :77-82;
+ *                                    int64 shares converted round-to-
+ *                                    nearest, as numpy)
  *     if recover:  x = acc mod `mod` (numpy float remainder)
  *                  r = x > maximum ? -(mod - x) / epsilon : x / epsilon
  *                  out[p] = fl32(r / total)
@@ -233,9 +257,10 @@ int fsagg_wire_unpack_f32(const void *src, int64_t src_bytes,
  * Every share row must be 16-byte aligned.
  */
 int fsagg_ss_recover_f32(const void *const *rows, const uint8_t *row_is_int,
-                         int n, int64_t numel, double mod, double maximum,
-                         double epsilon, double total, int recover,
-                         float *out, double *out_sum, fsagg_stream_t stream);
+                         int n, int64_t numel, double weight, double mod,
+                         double maximum, double epsilon, double total,
+                         int recover, float *out, double *out_sum,
+                         fsagg_stream_t stream);
 
 /*
  * Per-row, per-key squared L2 distance to a base row, in fp64:

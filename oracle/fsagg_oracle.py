@@ -467,21 +467,31 @@ def _fma32(a, b, c):
 
 class FedOptState:
     """Server optimizer state carried across rounds (torch.optim semantics,
-    ATen's vectorised fmadd for add(alpha); tolerance-pinned)."""
+    ATen's vectorised fmadd for add(alpha); tolerance-pinned).  float32
+    parameters use an exact fp32 fma; float64 ones plain float64 ops (numpy
+    has no fma: a few ulps apart, within the float64 tolerance)."""
 
     def __init__(self, params, opt):
-        self.params = OrderedDict((k, np.asarray(v, f32).copy())
+        first = np.asarray(next(iter(params.values())))
+        self.dt = np.float64 if first.dtype == np.float64 else f32
+        self.params = OrderedDict((k, np.asarray(v, self.dt).copy())
                                   for k, v in params.items())
         self.opt = dict(opt)
         self.buf = {}
         self.m = {}
         self.v = {}
+        self.vmax = {}
         self.t = 0
+
+    def _fma(self, a, b, c):
+        if self.dt == f32:
+            return _fma32(a, b, c)
+        return np.float64(a) * np.float64(b) + np.asarray(c, np.float64)
 
     def step(self, models):
         avg = para_weighted_avg(models)
         o = self.opt
-
+        T = self.dt
         self.t += 1
         for k, x in self.params.items():
             if k not in avg:
@@ -489,30 +499,34 @@ class FedOptState:
             g = x - avg[k]
             wd = o.get('weight_decay', 0.0)
             if wd:
-                g = _fma32(x, wd, g)
+                g = self._fma(x, T(wd), g)
             if o['type'] == 'SGD':
                 mom = o.get('momentum', 0.0)
                 if mom:
                     if k not in self.buf:
                         self.buf[k] = g.copy()
                     else:
-                        self.buf[k] = _fma32(
-                            g, 1 - o.get('dampening', 0.0),
-                            self.buf[k] * f32(mom))
-                    g = _fma32(self.buf[k], mom, g) if o.get(
+                        self.buf[k] = self._fma(
+                            g, T(1 - o.get('dampening', 0.0)),
+                            self.buf[k] * T(mom))
+                    g = self._fma(self.buf[k], T(mom), g) if o.get(
                         'nesterov', False) else self.buf[k]
-                self.params[k] = _fma32(g, -o['lr'], x)
+                self.params[k] = self._fma(g, T(-o['lr']), x)
             else:
                 b1, b2 = o.get('betas', (0.9, 0.999))
                 eps = o.get('eps', 1e-8)
                 m = self.m.get(k, np.zeros_like(x))
                 v = self.v.get(k, np.zeros_like(x))
-                m = _fma32(f32(1 - b1), g - m, m)
-                v = v * f32(b2) + (f32(1 - b2) * g) * g
+                m = self._fma(T(1 - b1), g - m, m)
+                v = v * T(b2) + (T(1 - b2) * g) * g
                 bc1 = 1 - b1**self.t
                 bc2 = 1 - b2**self.t
-                denom = np.sqrt(v) / f32(bc2**0.5) + f32(eps)
-                self.params[k] = x + (f32(-(o['lr'] / bc1)) * m) / denom
+                vd = v
+                if o.get('amsgrad', False):
+                    vd = np.maximum(self.vmax.get(k, np.zeros_like(x)), v)
+                    self.vmax[k] = vd
+                denom = np.sqrt(vd) / T(bc2**0.5) + T(eps)
+                self.params[k] = x + (T(-(o['lr'] / bc1)) * m) / denom
                 self.m[k], self.v[k] = m, v
         return OrderedDict((k, v.copy()) for k, v in self.params.items())
 

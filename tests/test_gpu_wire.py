@@ -125,25 +125,44 @@ def test_wire_unpack_large_int8_int16_mix():
     assert (o[:16] == -7.0).all() and (o[d_f + 4099:d16] == -7.0).all()
 
 
+class _Recover:
+    """Stands in for ``AdditiveSecretSharing(...).fixedpoint2float`` — the
+    recover function the reference's server hands the aggregator.  The
+    device path only reads its fixed-point constants (core/secret_sharing
+    ss_params) and must never call it."""
+
+    def __init__(self, meta):
+        self.mod_number = int(meta['mod_number'])
+        self.maximum = int(meta['maximum'])
+        self.epsilon = meta['epsilon']
+
+    def __call__(self, x):
+        raise AssertionError('the device path called recover_fun')
+
+
 @pytest.mark.parametrize('name', case_names('ss_'))
 def test_secret_sharing_fedavg_bit_exact(name):
+    """Shares written by the reference's clients (secret_split + the share
+    exchange, tools/gen_golden_wire.py) through the use_ss branch, with and
+    without ignore_weight (weight 1/n in float64, :77-82)."""
     from federatedscope_amd.core.aggregators import ClientsAvgAggregator
-    from federatedscope_amd.core.secret_sharing import AdditiveSecretSharing
     meta, clients, out, _, _ = load_case(name)
-    ss = AdditiveSecretSharing(shared_party_num=len(clients))
-    assert str(ss.mod_number) == meta['mod_number']
-    agg = ClientsAvgAggregator(device='cuda', config=_cfg(use_ss=True))
+    iw = meta.get('ignore_weight', False)
+    c = _cfg(use_ss=True)
+    c.federate.ignore_weight = iw
+    agg = ClientsAvgAggregator(device='cuda', config=c)
     got = agg.aggregate({'client_feedback': clients,
-                         'recover_fun': ss.fixedpoint2float})
+                         'recover_fun': _Recover(meta)})
     assert list(got.keys()) == list(out.keys())
     for k in out:
         _same_bits(got[k], out[k])
-    # no recover function: the float64 share sums (numpy's x*1.0 + ...)
+    # no recover function: the float64 weighted share sums (numpy's x*w)
     sums = agg.aggregate({'client_feedback': clients, 'recover_fun': None})
+    w = 1.0 / len(clients) if iw else 1.0
     for k in out:
         acc = None
         for _, m in clients:
-            x = np.asarray(m[k]).astype(np.float64) * 1.0
+            x = np.asarray(m[k]).astype(np.float64) * w
             acc = x if acc is None else acc + x
         _same_bits(sums[k], acc)
 
@@ -192,33 +211,24 @@ def test_dissimilarity_metrics(name):
                                rtol=1e-9)
 
 
-@pytest.mark.parametrize('nbits', [8, 16])
-def test_quant_plan_layouts(nbits):
-    """Wire layouts with only quantised keys, only fp32 keys, int16 codes,
-    and odd sizes (region offsets, scale table, gaps) through WireStager."""
-    from federatedscope_amd.core.compression import (
-        QuantPlan, WireStager, symmetric_uniform_quantization)
-    rng = np.random.default_rng(nbits)
-    shapes = [('conv1.weight', (3, 5, 7)), ('fc.bias', (13, )),
-              ('fc.weight', (1, )), ('bn.running_mean', (5, )),
-              ('conv2.weight', (2, 3))]
-    for keep in (None, 'weight', 'bias'):
-        m = OrderedDict((k, torch.from_numpy(
-            rng.standard_normal(s).astype(np.float32))) for k, s in shapes
-            if keep is None or k.endswith(keep) or
-            (keep == 'bias' and 'running' in k))
-        wire = symmetric_uniform_quantization(m, nbits=nbits)
-        plan = QuantPlan(wire)
-        st = WireStager(plan, 'cuda')
-        row = torch.full((plan.layout.numel, ), 9.0, device='cuda')
-        st.put(wire, row)
-        st.finish()
-        want = O.dequantize(OrderedDict((k, v.numpy()) for k, v in
-                                        wire.items()))
-        got = plan.layout.unpack(row)
-        assert list(got.keys()) == list(want.keys())
-        for k in want:
-            _same_bits(got[k], np.asarray(want[k], np.float32))
+@pytest.mark.parametrize('name', case_names('quantlayout_'))
+def test_quant_plan_layouts(name):
+    """Wire dicts written by the reference's client-side quantisation for
+    layouts with only quantised keys, only fp32 keys, int16 codes and odd
+    sizes (region offsets, scale table, gaps) through WireStager, against
+    the reference's own dequantisation."""
+    from federatedscope_amd.core.compression import QuantPlan, WireStager
+    _, clients, out, _, _ = load_case(name)
+    wire = _torch_wire(clients[0][1])
+    plan = QuantPlan(wire)
+    st = WireStager(plan, 'cuda')
+    row = torch.full((plan.layout.numel, ), 9.0, device='cuda')
+    st.put(wire, row)
+    st.finish()
+    got = plan.layout.unpack(row)
+    assert list(got.keys()) == list(out.keys())
+    for k in out:
+        _same_bits(got[k], np.asarray(out[k], np.float32))
 
 
 @pytest.mark.parametrize('name', case_names('dissim_'))
