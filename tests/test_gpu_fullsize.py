@@ -1,0 +1,208 @@
+"""Parity at BASELINE.json's full sizes, inside ``pytest -m gpu``.
+
+* C2 — FEMNIST ConvNet2 (hidden 512, 12 trainable keys, 1,690,238 params)
+  x 100 device-resident clients through ClientsAvgAggregator: bit-exact in
+  full against the oracle.
+* C3 — 100 x 25,000,000: the headline kernel over the stacked slab and the
+  drop-in over 100 device tensors, bit-exact on column blocks (first,
+  middle, last — 64-bit offsets, the ragged tail) against the oracle.
+* C4 — Krum over 50 x 6,603,902 (ConvNet2 hidden 2048) with the SURVEY
+  §8(d) generator: the score margin asserted, the selection exact against
+  an fp64 restatement of the distances, the multi-Krum output bit-exact.
+* C5 — 200 x 6,603,902 with 10 % x100 outliers: median bit-exact and
+  trimmed mean (k = 40) within its tolerance on sampled column blocks.
+
+Inputs are generated on the device (seeded) and copied to the host for the
+numpy oracle (tests/ only)."""
+from collections import OrderedDict
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+CONVNET2 = lambda h: [  # noqa: E731  (cv/model/cnn.py:14-50, trainable)
+    ('conv1.weight', (32, 1, 5, 5)), ('conv1.bias', (32, )),
+    ('bn1.weight', (32, )), ('bn1.bias', (32, )),
+    ('conv2.weight', (64, 32, 5, 5)), ('conv2.bias', (64, )),
+    ('bn2.weight', (64, )), ('bn2.bias', (64, )),
+    ('fc1.weight', (h, 3136)), ('fc1.bias', (h, )),
+    ('fc2.weight', (62, h)), ('fc2.bias', (62, ))]
+
+
+def _cfg(**kw):
+    bft = SimpleNamespace(krum_agg_num=kw.get('agg_num', 1),
+                          trimmedmean_excluded_ratio=kw.get('ratio', 0.2),
+                          normbounding_norm_bound=1.0)
+    return SimpleNamespace(
+        federate=SimpleNamespace(ignore_weight=False, use_ss=False,
+                                 client_num=kw.get('client_num', 1000),
+                                 sample_client_rate=1.0),
+        aggregator=SimpleNamespace(byzantine_node_num=kw.get('f', 0),
+                                   BFT_args=bft))
+
+
+class _Model(torch.nn.Module):
+    def __init__(self, sd):
+        super().__init__()
+        self.sd = sd
+
+    def state_dict(self, *a, **kw):
+        return self.sd
+
+
+def _sizes(n, seed):
+    return [int(s) for s in np.random.default_rng(seed).integers(1, 1000, n)]
+
+
+def _clients(keys, n, seed, fn=None):
+    g = torch.Generator(device='cuda').manual_seed(seed)
+    out = []
+    for i in range(n):
+        d = OrderedDict()
+        for k, s in keys:
+            z = torch.randn(s, device='cuda', generator=g)
+            d[k] = fn(i, z) if fn else z
+        out.append(d)
+    return out
+
+
+def test_c2_convnet2_fedavg_full():
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    keys = CONVNET2(512)
+    assert sum(int(np.prod(s)) for _, s in keys) == 1_690_238
+    n = 100
+    dev = _clients(keys, n, 2)
+    sizes = _sizes(n, 2)
+    fb = [(s, d) for s, d in zip(sizes, dev)]
+    agg = ClientsAvgAggregator(device='cuda', config=_cfg())
+    got = agg.aggregate({'client_feedback': fb, 'recover_fun': None})
+    assert not agg._stacks                 # read in place
+    host = [(s, OrderedDict((k, v.cpu().numpy()) for k, v in d.items()))
+            for s, d in fb]
+    want = O.para_weighted_avg(host)
+    for k in want:
+        assert got[k].cpu().numpy().tobytes() == want[k].tobytes(), k
+
+
+def test_c3_fedavg_100x25M_blocks():
+    from federatedscope_amd import ops
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    n, P = 100, 25_000_000
+    slab = torch.empty((n, P), dtype=torch.float32, device='cuda')
+    ops.fill_uniform(slab, P, seed=31)
+    sizes = _sizes(n, 3)
+    w = O.fedavg_weights(sizes)
+    out = torch.empty(P, dtype=torch.float32, device='cuda')
+    ops.weighted_sum(ops.RowTable.from_slab(slab, numel=P), w, out)
+    fb = [(s, {'w': slab[i]}) for i, s in enumerate(sizes)]
+    got = ClientsAvgAggregator(device='cuda', config=_cfg()).aggregate(
+        {'client_feedback': fb, 'recover_fun': None})['w']
+    blk = 1 << 20
+    for a in (0, P // 2 - 12345, P - blk):
+        x = slab[:, a:a + blk].cpu().numpy()
+        want = O.para_weighted_avg([(s, {'w': x[i]})
+                                    for i, s in enumerate(sizes)],
+                                   weights=w)['w']
+        assert out[a:a + blk].cpu().numpy().tobytes() == want.tobytes(), a
+        assert got[a:a + blk].cpu().numpy().tobytes() == want.tobytes(), a
+
+
+def _fp64_distances(X, bounds):
+    """Σ over keys of per-key L2 distances, fp64 Gram form per key (fp64
+    keeps ‖a‖² + ‖b‖² − 2a·b far from cancellation at these scales)."""
+    n = X.shape[0]
+    D = np.zeros((n, n))
+    for a, b in bounds:
+        Y = X[:, a:b].astype(np.float64)
+        g = Y @ Y.T
+        d = np.diag(g)
+        D += np.sqrt(np.maximum(d[:, None] + d[None, :] - 2 * g, 0.0))
+    np.fill_diagonal(D, np.inf)
+    return D
+
+
+def test_c4_krum_50x6p6M_selection_and_average():
+    from federatedscope_amd.core.aggregators import KrumAggregator
+    n, f, agg_num = 50, 10, 5
+    keys = CONVNET2(2048)
+    P = sum(int(np.prod(s)) for _, s in keys)
+    assert P == 6_603_902
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(1234))
+    byz = set(perm[:f].tolist())
+    g = torch.Generator(device='cuda').manual_seed(1234)
+    base = OrderedDict((k, torch.randn(s, device='cuda', generator=g))
+                       for k, s in keys)
+    clients = []
+    for i in range(n):
+        d = OrderedDict()
+        for k, s in keys:
+            z = torch.randn(s, device='cuda', generator=g)
+            d[k] = (0.1 + 0.05 * z) if i in byz else \
+                (base[k] + 0.01 * (1 + 0.05 * i) * z)
+        clients.append(d)
+    sizes = _sizes(n, 4)
+    init = OrderedDict((k, torch.randn(s, device='cuda', generator=g))
+                       for k, s in keys)
+    agg = KrumAggregator(model=_Model(init), device='cuda',
+                         config=_cfg(f=f, agg_num=agg_num, client_num=n))
+    fb = [(s, d) for s, d in zip(sizes, clients)]
+    got = agg.aggregate({'client_feedback': fb})
+    # fp64 restatement of the distances → scores → selection
+    X = np.concatenate([np.stack([d[k].reshape(-1).cpu().numpy()
+                                  for d in clients]) for k, _ in keys], 1)
+    bounds, o = [], 0
+    for _, s in keys:
+        bounds.append((o, o + int(np.prod(s))))
+        o += int(np.prod(s))
+    D = _fp64_distances(X, bounds)
+    scores = np.sort(D, axis=1)[:, :n - f - 2].sum(-1)
+    srt = np.sort(scores)
+    assert (srt[1] - srt[0]) / srt[0] >= 1e-2          # the margin
+    want_sel = [int(i) for i in np.argsort(scores, kind='stable')[:agg_num]]
+    assert agg.last_selection == want_sel
+    assert not byz & set(want_sel)
+    host = [(sizes[i], OrderedDict((k, clients[i][k].cpu().numpy())
+                                   for k, _ in keys)) for i in want_sel]
+    want = O.add_init(OrderedDict((k, v.cpu().numpy())
+                                  for k, v in init.items()),
+                      O.para_weighted_avg(host))
+    for k in want:
+        assert got[k].cpu().numpy().tobytes() == want[k].tobytes(), k
+
+
+def test_c5_median_trimmed_200x6p6M_blocks():
+    from federatedscope_amd.core.aggregators import (MedianAggregator,
+                                                     TrimmedmeanAggregator)
+    n = 200
+    keys = [('w', (6_603_902, ))]
+    out_i = set(np.random.default_rng(2).choice(n, n // 10,
+                                                replace=False).tolist())
+    clients = _clients(keys, n, 2,
+                       lambda i, z: z * 100.0 if i in out_i else z)
+    g = torch.Generator(device='cuda').manual_seed(9)
+    init = OrderedDict([('w', torch.randn(6_603_902, device='cuda',
+                                          generator=g))])
+    fb = [(1, d) for d in clients]
+    med = MedianAggregator(model=_Model(init), device='cuda',
+                           config=_cfg(f=1)).aggregate(
+        {'client_feedback': fb})['w']
+    tm = TrimmedmeanAggregator(model=_Model(init), device='cuda',
+                               config=_cfg(f=1, ratio=0.2)).aggregate(
+        {'client_feedback': fb})['w']
+    k = int(n * 0.2)
+    eps = np.finfo(np.float32).eps
+    P, blk = 6_603_902, 1 << 16
+    for a in (0, 3_000_001, P - blk):
+        host = [(1, {'w': d['w'][a:a + blk].cpu().numpy()}) for d in clients]
+        ini = {'w': init['w'][a:a + blk].cpu().numpy()}
+        want = O.median_aggregate(host, ini)['w']
+        assert med[a:a + blk].cpu().numpy().tobytes() == want.tobytes(), a
+        ref = O.add_init(ini, O.trimmed_mean_update(host, k))['w']
+        got = tm[a:a + blk].cpu().numpy().astype(np.float64)
+        assert (np.abs(got - ref) <= 4 * eps * (np.abs(ref) +
+                                                np.abs(ini['w']))).all(), a
