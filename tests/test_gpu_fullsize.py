@@ -7,7 +7,8 @@
   drop-in over 100 device tensors, bit-exact on column blocks (first,
   middle, last — 64-bit offsets, the ragged tail) against the oracle.
 * C4 — Krum over 50 x 6,603,902 (ConvNet2 hidden 2048) with the SURVEY
-  §8(d) generator: the score margin asserted, the selection exact against
+  §8(d) generator: the score margin asserted (>= 1e-3: 500x the kernel's
+  distance error), the selection exact against
   an fp64 restatement of the distances, the multi-Krum output bit-exact.
 * C5 — 200 x 6,603,902 with 10 % x100 outliers: median bit-exact and
   trimmed mean (k = 40) within its tolerance on sampled column blocks.
@@ -162,7 +163,10 @@ def test_c4_krum_50x6p6M_selection_and_average():
     D = _fp64_distances(X, bounds)
     scores = np.sort(D, axis=1)[:, :n - f - 2].sum(-1)
     srt = np.sort(scores)
-    assert (srt[1] - srt[0]) / srt[0] >= 1e-2          # the margin
+    # the best-vs-second score margin (0.84 % with this generator and the
+    # 12-key layout) must dwarf the kernel's distance error (<= 2e-6
+    # relative, tests/test_gpu_kernels.py): 1e-3 leaves a 500x guard
+    assert (srt[1] - srt[0]) / srt[0] >= 1e-3
     want_sel = [int(i) for i in np.argsort(scores, kind='stable')[:agg_num]]
     assert agg.last_selection == want_sel
     assert not byz & set(want_sel)
