@@ -26,6 +26,8 @@
 //     the keys in fp32 in key order (the reference's
 //     `distance += torch.dist(...)`).
 // Deterministic: no atomics anywhere.
+#include <cstdlib>
+#include <cstring>
 #include <numeric>
 
 #include "common.h"
@@ -323,6 +325,220 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   }
 }
 
+// ---- ring form: LDS-DMA stages, quad-coordinate lanes ---------------------
+// One 512-thread workgroup per CU (152 KiB of LDS).  A chunk streams
+// through a 3-slot ring of stages; a stage is every client row's next S
+// coordinates, written to LDS by 16-byte LDS-DMA (global_load_lds_dwordx4:
+// no VGPR round trip, no staging writes) in the rows' own layout
+// [row][coordinate].  Lane (tp, q) owns tile pair tp and coordinate quad q
+// of every stage: 2·TS ds_read_b128 give it its two tiles' rows at 4
+// coordinates (lanes of one tile pair read consecutive quads of one row:
+// conflict-free), then 4 × TS² packed sub/fma.  One raw barrier per stage:
+// stage st+2 is issued into the slot stage st−1 vacated, while stage st+1
+// stays in flight (counted vmcnt).  At the chunk end the q-slices of each
+// tile pair are summed through LDS in slice order → partial[chunk][pair].
+constexpr int kRingThreads = 512;
+constexpr int kRingWaves = kRingThreads / kWave;
+constexpr int kRingBufs = 3;
+constexpr int kRingLds = 38912;  // floats: 152 KiB, one workgroup per CU
+constexpr int kRingRed = kRingLds / kRingThreads;  // accumulators per pass
+
+struct RingPlan {
+  int ts, nt, ntp;
+  int qs;     // coordinate quads per stage (lanes per tile pair)
+  int S;      // coordinates per stage
+  int rw;     // DMA rows per wave per stage
+  int stage;  // floats per stage slot (rw·8 rows × S)
+  int64_t chl, max_chunks;
+  int ok;
+};
+
+RingPlan make_ring_plan(int n, int64_t numel, int nseg) {
+  const PairPlan pp = make_plan(n, numel, nseg);
+  RingPlan p;
+  p.ts = pp.ts;
+  p.nt = pp.nt;
+  p.ntp = pp.ntp;
+  p.qs = kRingThreads / p.ntp;
+  p.S = 4 * p.qs;
+  p.rw = (p.nt * p.ts + kRingWaves - 1) / kRingWaves;
+  p.stage = p.rw * kRingWaves * p.S;
+  p.ok = p.qs >= 2 && p.rw <= 8 && kRingBufs * p.stage <= kRingLds &&
+         p.ts * p.ts <= 2 * kRingRed;
+  // ≈ 2 chunks per CU, whole stages
+  int64_t chl = (numel + 511) / 512;
+  const int64_t minl = int64_t(p.S) * 8;
+  if (chl < minl) chl = minl;
+  p.chl = (chl + p.S - 1) / p.S * p.S;
+  p.max_chunks = numel / p.chl + nseg + 1;
+  return p;
+}
+
+typedef __attribute__((address_space(3))) float lfloat_t;
+
+// 16-B LDS-DMA of one wave: lane l's 16 bytes at sbase + voff land at LDS
+// byte address lds_addr + 16·l.  Inline asm on purpose: issued through the
+// builtin, the DMA is a pending LDS write the compiler guards with
+// vmcnt(0) before every later ds_read — which would drain the ring's
+// in-flight stages every step.  The ring counts its DMAs itself.
+__device__ __forceinline__ void glds16(const float *sbase, uint32_t voff,
+                                       uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds_addr)
+      : "memory");
+}
+
+template <int TS, int RW>
+__global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
+    const float *const *__restrict__ tab, int64_t ss, int n, RingPlan pl,
+    const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
+    int nseg, const int *__restrict__ prefix, float *__restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) float lds[kRingLds];
+  const int c = blockIdx.x;
+  if (c >= prefix[nseg]) return;
+  int lo = 0, hi = nseg;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (prefix[mid] <= c) lo = mid;
+    else hi = mid;
+  }
+  const int s = lo;
+  const int64_t start = seg_lo[s] + int64_t(c - prefix[s]) * pl.chl;
+  int64_t end = start + pl.chl;
+  if (end > seg_end[s]) end = seg_end[s];
+  const float *const *__restrict__ rows = tab + int64_t(s) * ss;
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int lane = tid & (kWave - 1);
+  const int qs = pl.qs, S = pl.S;
+  const bool active = tid < pl.ntp * qs;
+  const int tp = active ? tid / qs : 0;
+  const int q = tid - tp * qs;
+  int ti = 0, tj = 0;
+  tp_to_tiles(tp, pl.nt, ti, tj);
+
+  // 16-B DMA needs 16-B aligned sources: the chunk start and every row
+  bool vec = (start & 3) == 0;
+  for (int r = 0; r < n; ++r)
+    vec = vec && (reinterpret_cast<uintptr_t>(rows[r]) & 15u) == 0;
+  const int64_t end4 = vec ? start + ((end - start) & ~int64_t(3)) : start;
+  const int nstage = int((end4 - start + S - 1) / S);
+
+  float acc[TS][TS];
+#pragma unroll
+  for (int u = 0; u < TS; ++u)
+#pragma unroll
+    for (int v = 0; v < TS; ++v) acc[u][v] = 0.0f;
+
+  // this wave's DMA rows (slots wave + 8k; slots past the tile rows repeat
+  // row n-1 and are never read)
+  const float *rp[RW];
+#pragma unroll
+  for (int k = 0; k < RW; ++k)
+    rp[k] = rows[min(wave + kRingWaves * k, n - 1)];
+
+  const uint32_t lds_base = uint32_t(uintptr_t((lfloat_t *)lds));
+  auto issue = [&](int st) {
+    const int64_t cs = start + int64_t(st) * S;
+    const int nq = int(min(int64_t(S), end4 - cs) >> 2);
+    const uint32_t slot =
+        lds_base + 4u * uint32_t((st % kRingBufs) * pl.stage);
+    if (lane < qs) {
+      // lanes past the stage's quads re-read its first quad into columns
+      // nobody reads
+      const uint32_t voff = 16u * uint32_t(lane < nq ? lane : 0);
+#pragma unroll
+      for (int k = 0; k < RW; ++k)
+        glds16(rp[k] + cs, voff,
+               slot + 4u * uint32_t((wave + kRingWaves * k) * S));
+    }
+  };
+
+  if (nstage > 0) issue(0);
+  if (nstage > 1) issue(1);
+  for (int st = 0; st < nstage; ++st) {
+    if (st + 1 < nstage)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RW) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (st + 2 < nstage) issue(st + 2);
+    const int64_t cs = start + int64_t(st) * S;
+    const int nq = int(min(int64_t(S), end4 - cs) >> 2);
+    if (active && q < nq) {
+      const float *slot = lds + (st % kRingBufs) * pl.stage + 4 * q;
+      float4 a[TS], b[TS];
+#pragma unroll
+      for (int u = 0; u < TS; ++u)
+        a[u] = *reinterpret_cast<const float4 *>(slot + (ti * TS + u) * S);
+#pragma unroll
+      for (int v = 0; v < TS; ++v)
+        b[v] = *reinterpret_cast<const float4 *>(slot + (tj * TS + v) * S);
+#pragma unroll
+      for (int u = 0; u < TS; ++u)
+#pragma unroll
+        for (int v = 0; v < TS; ++v) {
+          float d = a[u].x - b[v].x;
+          acc[u][v] = __builtin_fmaf(d, d, acc[u][v]);
+          d = a[u].y - b[v].y;
+          acc[u][v] = __builtin_fmaf(d, d, acc[u][v]);
+          d = a[u].z - b[v].z;
+          acc[u][v] = __builtin_fmaf(d, d, acc[u][v]);
+          d = a[u].w - b[v].w;
+          acc[u][v] = __builtin_fmaf(d, d, acc[u][v]);
+        }
+    }
+  }
+  // coordinates past the last whole quad (or a misaligned chunk): straight
+  // from the rows, by the q = 0 lane of each tile pair
+  if (active && q == 0) {
+    for (int64_t p = end4; p < end; ++p) {
+      float a[TS], b[TS];
+#pragma unroll
+      for (int u = 0; u < TS; ++u) a[u] = gld(rows[min(ti * TS + u, n - 1)] + p);
+#pragma unroll
+      for (int v = 0; v < TS; ++v) b[v] = gld(rows[min(tj * TS + v, n - 1)] + p);
+#pragma unroll
+      for (int u = 0; u < TS; ++u)
+#pragma unroll
+        for (int v = 0; v < TS; ++v) {
+          const float d = a[u] - b[v];
+          acc[u][v] = __builtin_fmaf(d, d, acc[u][v]);
+        }
+    }
+  }
+  __syncthreads();  // every stage read: the ring becomes the reduction buffer
+
+  // Σ over the q-slices of each tile pair, in slice order
+  constexpr int kE = TS * TS;
+#pragma unroll
+  for (int e0 = 0; e0 < kE; e0 += kRingRed) {
+    constexpr int R = kRingRed;
+    const int ne = kE - e0 < R ? kE - e0 : R;
+    if (active) {
+      float *slot = lds + tid * R;
+#pragma unroll
+      for (int e = e0; e < e0 + R && e < kE; ++e) slot[e - e0] = acc[e / TS][e % TS];
+    }
+    __syncthreads();
+    for (int o = tid; o < pl.ntp * ne; o += kRingThreads) {
+      const int t = o / ne, e = o - t * ne;
+      float sum = 0.0f;
+      for (int k = 0; k < qs; ++k) sum += lds[(t * qs + k) * R + e];
+      partial[(int64_t(c) * pl.ntp + t) * kE + e0 + e] = sum;
+    }
+    __syncthreads();
+  }
+}
+
 // Σ over a segment's chunks in fp64 for every pair of the tile layout, in a
 // fixed order (deterministic, no atomics).  Block = (segment, 64 partial
 // columns); its 16 waves take every 16th chunk each (consecutive lanes read
@@ -554,14 +770,35 @@ extern "C" int fsagg_rows_sqnorm_f32(const fsagg_rows *rows,
   return check_launch("fsagg_rows_sqnorm_f32");
 }
 
+// chunks of the partial buffer: the larger of the two plans
+static int64_t pairdist_max_chunks(int n, int64_t numel, int nseg) {
+  const PairPlan pl = make_plan(n, numel, nseg);
+  const RingPlan rp = make_ring_plan(n, numel, nseg);
+  return pl.max_chunks > rp.max_chunks ? pl.max_chunks : rp.max_chunks;
+}
+
+static size_t partial_bytes(int n, int64_t numel, int nseg) {
+  const PairPlan pl = make_plan(n, numel, nseg);
+  return align256(sizeof(float) * size_t(pairdist_max_chunks(n, numel, nseg)) *
+                  size_t(pl.ntp) * size_t(pl.ts * pl.ts));
+}
+
 extern "C" size_t fsagg_pairdist_workspace_bytes(int n, int64_t numel,
                                                  int nseg) {
   if (n < 1 || nseg < 1) return 0;
-  const PairPlan pl = make_plan(n, numel, nseg);
   return align256(sizeof(int) * size_t(nseg + 1)) +
-         align256(sizeof(float) * size_t(pl.max_chunks) * size_t(pl.ntp) *
-                  size_t(pl.ts * pl.ts)) +
+         partial_bytes(n, numel, nseg) +
          align256(sizeof(double) * size_t(nseg) * size_t(n) * size_t(n));
+}
+
+// FSAGG_PAIRDIST=flat forces the register-staged kernel (A/B runs)
+static bool ring_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char *e = getenv("FSAGG_PAIRDIST");
+    on = !(e && strcmp(e, "flat") == 0);
+  }
+  return on == 1;
 }
 
 // Enqueue the chunk and per-segment kernels; segsq receives [nseg][n][n].
@@ -574,6 +811,34 @@ static int pairdist_segsq_impl(const float *const *tab, int64_t ss, int n,
   int *prefix = static_cast<int *>(workspace);
   float *partial = reinterpret_cast<float *>(
       static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)));
+  const RingPlan rp = make_ring_plan(n, numel, nseg);
+  if (rp.ok && ring_enabled() && numel > 0) {
+    hipLaunchKernelGGL(chunk_prefix_kernel, dim3(1), dim3(1), 0, s, seg_lo,
+                       seg_end, nseg, rp.chl, prefix);
+    const dim3 grid(unsigned(rp.max_chunks));
+#define FSAGG_RING(TS, RW)                                                  \
+  hipLaunchKernelGGL((pairdist_ring_kernel<TS, RW>), grid,                  \
+                     dim3(kRingThreads), 0, s, tab, ss, n, rp, seg_lo,      \
+                     seg_end, nseg, prefix, partial)
+    const bool t10 = rp.ts == 10;
+    switch (rp.rw) {
+      case 1: if (t10) FSAGG_RING(10, 1); else FSAGG_RING(8, 1); break;
+      case 2: if (t10) FSAGG_RING(10, 2); else FSAGG_RING(8, 2); break;
+      case 3: if (t10) FSAGG_RING(10, 3); else FSAGG_RING(8, 3); break;
+      case 4: if (t10) FSAGG_RING(10, 4); else FSAGG_RING(8, 4); break;
+      case 5: if (t10) FSAGG_RING(10, 5); else FSAGG_RING(8, 5); break;
+      case 6: if (t10) FSAGG_RING(10, 6); else FSAGG_RING(8, 6); break;
+      case 7: if (t10) FSAGG_RING(10, 7); else FSAGG_RING(8, 7); break;
+      default: if (t10) FSAGG_RING(10, 8); else FSAGG_RING(8, 8); break;
+    }
+#undef FSAGG_RING
+    const int per_seg = pl.ntp * pl.ts * pl.ts;
+    hipLaunchKernelGGL(pairdist_segsq_kernel,
+                       dim3(unsigned(nseg), unsigned((per_seg + kWave - 1) / kWave)),
+                       dim3(kSegBlock), 0, s, partial, n, pl, nseg, prefix,
+                       segsq);
+    return FSAGG_OK;
+  }
   hipLaunchKernelGGL(chunk_prefix_kernel, dim3(1), dim3(1), 0, s, seg_lo,
                      seg_end, nseg, pl.chl, prefix);
   if (numel > 0) {
@@ -614,8 +879,7 @@ extern "C" int fsagg_pairdist_f32(const float *const *rows, int n,
   const PairPlan pl = make_plan(n, numel, nseg);
   double *segsq = reinterpret_cast<double *>(
       static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)) +
-      align256(sizeof(float) * size_t(pl.max_chunks) * size_t(pl.ntp) *
-               size_t(pl.ts * pl.ts)));
+      partial_bytes(n, numel, nseg));
   pairdist_segsq_impl(rows, 0, n, numel, seg_off, seg_off + 1, nseg, segsq,
                       workspace, s);
   hipLaunchKernelGGL(pairdist_finish_kernel,
