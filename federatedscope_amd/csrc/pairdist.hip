@@ -339,19 +339,32 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
 // tile pair are summed through LDS in slice order → partial[chunk][pair].
 constexpr int kRingThreads = 512;
 constexpr int kRingWaves = kRingThreads / kWave;
-constexpr int kRingBufs = 3;
 constexpr int kRingLds = 38912;  // floats: 152 KiB, one workgroup per CU
 constexpr int kRingRed = kRingLds / kRingThreads;  // accumulators per pass
 
 struct RingPlan {
   int ts, nt, ntp;
-  int qs;     // coordinate quads per stage (lanes per tile pair)
+  int qs;     // coordinate quads per stage (lanes per tile pair, <= 64:
+              // one DMA wave-instruction per row)
   int S;      // coordinates per stage
   int rw;     // DMA rows per wave per stage
   int stage;  // floats per stage slot (rw·8 rows × S)
+  int nbuf;   // ring slots (nbuf − 1 stages in flight)
+  int mode;   // experiments only (FSAGG_RING_MODE): 1 = no compute,
+              // 2 = no DMA; 0 = the kernel
   int64_t chl, max_chunks;
   int ok;
 };
+
+static int ring_bufs_env() {
+  static int nb = -1;
+  if (nb < 0) {
+    const char *e = getenv("FSAGG_RING_BUFS");
+    nb = e ? atoi(e) : 4;
+    if (nb < 3 || nb > 4) nb = 4;
+  }
+  return nb;
+}
 
 RingPlan make_ring_plan(int n, int64_t numel, int nseg) {
   const PairPlan pp = make_plan(n, numel, nseg);
@@ -360,11 +373,19 @@ RingPlan make_ring_plan(int n, int64_t numel, int nseg) {
   p.nt = pp.nt;
   p.ntp = pp.ntp;
   p.qs = kRingThreads / p.ntp;
+  if (p.qs > kWave) p.qs = kWave;
   p.S = 4 * p.qs;
   p.rw = (p.nt * p.ts + kRingWaves - 1) / kRingWaves;
   p.stage = p.rw * kRingWaves * p.S;
-  p.ok = p.qs >= 2 && p.rw <= 8 && kRingBufs * p.stage <= kRingLds &&
-         p.ts * p.ts <= 2 * kRingRed;
+  p.nbuf = ring_bufs_env();
+  {
+    const char *e = getenv("FSAGG_RING_MODE");
+    p.mode = e ? atoi(e) : 0;
+  }
+  while (p.nbuf > 3 && p.nbuf * p.stage > kRingLds) --p.nbuf;
+  // most lanes busy (small n leaves tile pairs × 64 quads < 3/4 of them)
+  p.ok = p.qs >= 2 && p.ntp * p.qs * 4 >= kRingThreads * 3 && p.rw <= 8 &&
+         p.nbuf * p.stage <= kRingLds && p.ts * p.ts <= 2 * kRingRed;
   // ≈ 2 chunks per CU, whole stages
   int64_t chl = (numel + 511) / 512;
   const int64_t minl = int64_t(p.S) * 8;
@@ -395,7 +416,7 @@ __device__ __forceinline__ void glds16(const float *sbase, uint32_t voff,
       : "memory");
 }
 
-template <int TS, int RW>
+template <int TS, int RW, int NB>
 __global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n, RingPlan pl,
     const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
@@ -447,10 +468,10 @@ __global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
 
   const uint32_t lds_base = uint32_t(uintptr_t((lfloat_t *)lds));
   auto issue = [&](int st) {
+    if (pl.mode == 2) return;
     const int64_t cs = start + int64_t(st) * S;
     const int nq = int(min(int64_t(S), end4 - cs) >> 2);
-    const uint32_t slot =
-        lds_base + 4u * uint32_t((st % kRingBufs) * pl.stage);
+    const uint32_t slot = lds_base + 4u * uint32_t((st % NB) * pl.stage);
     if (lane < qs) {
       // lanes past the stage's quads re-read its first quad into columns
       // nobody reads
@@ -462,19 +483,26 @@ __global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
     }
   };
 
-  if (nstage > 0) issue(0);
-  if (nstage > 1) issue(1);
+  // NB − 1 stages in flight; stage st + NB − 1 goes into the slot stage
+  // st − 1 vacated (every wave is past it: the barrier)
+#pragma unroll
+  for (int k = 0; k < NB - 1; ++k)
+    if (k < nstage) issue(k);
   for (int st = 0; st < nstage; ++st) {
-    if (st + 1 < nstage)
+    // this wave's DMAs of stage st have landed (later ones may fly)
+    const int later = min(nstage - 1 - st, NB - 2);
+    if (later >= 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * RW) : "memory");
+    else if (later == 1)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RW) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (st + 2 < nstage) issue(st + 2);
+    if (st + NB - 1 < nstage) issue(st + NB - 1);
     const int64_t cs = start + int64_t(st) * S;
     const int nq = int(min(int64_t(S), end4 - cs) >> 2);
-    if (active && q < nq) {
-      const float *slot = lds + (st % kRingBufs) * pl.stage + 4 * q;
+    if (active && q < nq && pl.mode != 1) {
+      const float *slot = lds + (st % NB) * pl.stage + 4 * q;
       float4 a[TS], b[TS];
 #pragma unroll
       for (int u = 0; u < TS; ++u)
@@ -817,9 +845,16 @@ static int pairdist_segsq_impl(const float *const *tab, int64_t ss, int n,
                        seg_end, nseg, rp.chl, prefix);
     const dim3 grid(unsigned(rp.max_chunks));
 #define FSAGG_RING(TS, RW)                                                  \
-  hipLaunchKernelGGL((pairdist_ring_kernel<TS, RW>), grid,                  \
-                     dim3(kRingThreads), 0, s, tab, ss, n, rp, seg_lo,      \
-                     seg_end, nseg, prefix, partial)
+  do {                                                                      \
+    if (rp.nbuf == 4)                                                       \
+      hipLaunchKernelGGL((pairdist_ring_kernel<TS, RW, 4>), grid,           \
+                         dim3(kRingThreads), 0, s, tab, ss, n, rp, seg_lo,  \
+                         seg_end, nseg, prefix, partial);                   \
+    else                                                                    \
+      hipLaunchKernelGGL((pairdist_ring_kernel<TS, RW, 3>), grid,           \
+                         dim3(kRingThreads), 0, s, tab, ss, n, rp, seg_lo,  \
+                         seg_end, nseg, prefix, partial);                   \
+  } while (0)
     const bool t10 = rp.ts == 10;
     switch (rp.rw) {
       case 1: if (t10) FSAGG_RING(10, 1); else FSAGG_RING(8, 1); break;
@@ -876,7 +911,6 @@ extern "C" int fsagg_pairdist_f32(const float *const *rows, int n,
     return FSAGG_ESPACE;
   }
   hipStream_t s = as_stream(stream);
-  const PairPlan pl = make_plan(n, numel, nseg);
   double *segsq = reinterpret_cast<double *>(
       static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)) +
       partial_bytes(n, numel, nseg));
