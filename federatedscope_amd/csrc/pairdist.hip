@@ -374,6 +374,7 @@ RingPlan make_ring_plan(int n, int64_t numel, int nseg) {
   p.ntp = pp.ntp;
   p.qs = kRingThreads / p.ntp;
   if (p.qs > kWave) p.qs = kWave;
+  if (p.qs < 1) p.qs = 1;  // more tile pairs than lanes: not ok (below)
   p.S = 4 * p.qs;
   p.rw = (p.nt * p.ts + kRingWaves - 1) / kRingWaves;
   p.stage = p.rw * kRingWaves * p.S;
@@ -525,10 +526,11 @@ __global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
         }
     }
   }
-  // coordinates past the last whole quad (or a misaligned chunk): straight
-  // from the rows, by the q = 0 lane of each tile pair
-  if (active && q == 0) {
-    for (int64_t p = end4; p < end; ++p) {
+  // coordinates past the last whole quad (or all of a misaligned chunk):
+  // straight from the rows, the q-lanes of each tile pair taking every
+  // qs-th coordinate
+  if (active) {
+    for (int64_t p = end4 + q; p < end; p += qs) {
       float a[TS], b[TS];
 #pragma unroll
       for (int u = 0; u < TS; ++u) a[u] = gld(rows[min(ti * TS + u, n - 1)] + p);
