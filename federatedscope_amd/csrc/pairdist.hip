@@ -47,6 +47,14 @@ constexpr int kLdsFloats = kBlock * kRedPitch;  // 16640 floats = 65 KiB
 // registers) and stage fewer coordinates per pass
 constexpr int stage_items(int ts) { return ts == 10 ? 3 : 4; }
 typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// accumulator of pair (u, v) in the row-pair packed form acc[u/2][v]
+template <int TS>
+__device__ __forceinline__ float pair_acc(const f2 (&acc)[TS / 2][TS], int u,
+                                          int v) {
+  return (u & 1) ? acc[u >> 1][v].y : acc[u >> 1][v].x;
+}
 
 // Client tiles of side ts (8 or 10: the one with fewer pair slots
 // ntp·ts²; at n = 50, 15 × 100 = 1500 against 28 × 64 = 1792); each lane
@@ -152,7 +160,9 @@ __device__ __forceinline__ void read_tile(const float *col, int t,
   }
 }
 
-template <int TS>
+// PK: the row-pair packed form (v_pk_add_f32 / v_pk_fma_f32, two pairs per
+// instruction); else scalar v_sub_f32 / v_fma_f32 on the same accumulators
+template <int TS, bool PK>
 __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n,
     PairPlan pl, const int64_t *__restrict__ seg_lo,
@@ -200,11 +210,16 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   for (int r = 0; r < n; ++r)
     vec = vec && (reinterpret_cast<uintptr_t>(rows[r]) & 15u) == 0;
 
-  float acc[TS][TS];
+  // acc[h][v] = (pair (2h, v), pair (2h+1, v)) of the tile pair: tile
+  // ti's rows 2h, 2h+1 are adjacent in a staged coordinate row, so one
+  // ds_read_b64 gives both and each v_pk_add_f32 / v_pk_fma_f32 works two
+  // pairs with tile tj's value broadcast (op_sel) — no operand moves
+  static_assert(TS % 2 == 0, "row pairs");
+  f2 acc[TS / 2][TS];
 #pragma unroll
-  for (int u = 0; u < TS; ++u)
+  for (int h = 0; h < TS / 2; ++h)
 #pragma unroll
-    for (int v = 0; v < TS; ++v) acc[u][v] = 0.0f;
+    for (int v = 0; v < TS; ++v) acc[h][v] = f2{0.0f, 0.0f};
 
   constexpr int kStageItems = stage_items(TS);
   // 8×8 tiles have the registers to unroll two coordinates (the LDS
@@ -282,16 +297,32 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
 #pragma unroll kUnroll
       for (int cc = ksl; cc < len; cc += pl.ks) {
         const float *col = lds + cc * pl.ldsp;
-        float a[TS], b[TS];
-        read_tile<TS>(col, ti, a);
+        float b[TS];
         read_tile<TS>(col, tj, b);
+        if constexpr (PK) {
+          const f2 *ap = reinterpret_cast<const f2 *>(col + ti * TS);
+          f2 a[TS / 2];
 #pragma unroll
-        for (int u = 0; u < TS; ++u)
+          for (int h = 0; h < TS / 2; ++h) a[h] = ap[h];
 #pragma unroll
-          for (int v = 0; v < TS; ++v) {
-            const float d = a[u] - b[v];
-            acc[u][v] = __builtin_fmaf(d, d, acc[u][v]);
-          }
+          for (int v = 0; v < TS; ++v)
+#pragma unroll
+            for (int h = 0; h < TS / 2; ++h) {
+              const f2 d = a[h] - f2{b[v], b[v]};
+              acc[h][v] = __builtin_elementwise_fma(d, d, acc[h][v]);
+            }
+        } else {
+          float a[TS];
+          read_tile<TS>(col, ti, a);
+#pragma unroll
+          for (int u = 0; u < TS; ++u)
+#pragma unroll
+            for (int v = 0; v < TS; ++v) {
+              const float d = a[u] - b[v];
+              acc[u >> 1][v][u & 1] =
+                  __builtin_fmaf(d, d, acc[u >> 1][v][u & 1]);
+            }
+        }
       }
     }
     __syncthreads();
@@ -306,7 +337,7 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
       float *slot = lds + (ksl * pl.tpg + tpl) * kRedPitch;
 #pragma unroll
       for (int e = e0; e < e0 + 64 && e < kE; ++e)
-        slot[e - e0] = acc[e / TS][e % TS];
+        slot[e - e0] = pair_acc<TS>(acc, e / TS, e % TS);
     }
     __syncthreads();
     const int ne = kE - e0 < 64 ? kE - e0 : 64;
@@ -351,7 +382,7 @@ struct RingPlan {
   int stage;  // floats per stage slot (rw·8 rows × S)
   int nbuf;   // ring slots (nbuf − 1 stages in flight)
   int mode;   // experiments only (FSAGG_RING_MODE): 1 = no compute,
-              // 2 = no DMA; 0 = the kernel
+              // 2 = no DMA, 3 = no DMA and no barrier; 0 = the kernel
   int64_t chl, max_chunks;
   int ok;
 };
@@ -417,6 +448,20 @@ __device__ __forceinline__ void glds16(const float *sbase, uint32_t voff,
       : "memory");
 }
 
+// acc[v] += (x − b[v].c)² for one coordinate c, x = the coordinate of two
+// tile rows: one v_pk_add_f32 (b's value broadcast) and one v_pk_fma_f32
+// per v
+template <int TS, typename Pick>
+__device__ __forceinline__ void pair_step(f2 (&acc)[TS], f2 x,
+                                          const float4 (&b)[TS], Pick pick) {
+#pragma unroll
+  for (int v = 0; v < TS; ++v) {
+    const float y = pick(b[v]);
+    const f2 d = x - f2{y, y};
+    acc[v] = __builtin_elementwise_fma(d, d, acc[v]);
+  }
+}
+
 template <int TS, int RW, int NB>
 __global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n, RingPlan pl,
@@ -454,11 +499,11 @@ __global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
   const int64_t end4 = vec ? start + ((end - start) & ~int64_t(3)) : start;
   const int nstage = int((end4 - start + S - 1) / S);
 
-  float acc[TS][TS];
+  f2 acc[TS / 2][TS];  // row-pair packed, as pairdist_chunk_kernel
 #pragma unroll
-  for (int u = 0; u < TS; ++u)
+  for (int h = 0; h < TS / 2; ++h)
 #pragma unroll
-    for (int v = 0; v < TS; ++v) acc[u][v] = 0.0f;
+    for (int v = 0; v < TS; ++v) acc[h][v] = f2{0.0f, 0.0f};
 
   // this wave's DMA rows (slots wave + 8k; slots past the tile rows repeat
   // row n-1 and are never read)
@@ -469,7 +514,7 @@ __global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
 
   const uint32_t lds_base = uint32_t(uintptr_t((lfloat_t *)lds));
   auto issue = [&](int st) {
-    if (pl.mode == 2) return;
+    if (pl.mode >= 2) return;
     const int64_t cs = start + int64_t(st) * S;
     const int nq = int(min(int64_t(S), end4 - cs) >> 2);
     const uint32_t slot = lds_base + 4u * uint32_t((st % NB) * pl.stage);
@@ -498,32 +543,30 @@ __global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RW) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (pl.mode != 3) __builtin_amdgcn_s_barrier();
     if (st + NB - 1 < nstage) issue(st + NB - 1);
     const int64_t cs = start + int64_t(st) * S;
     const int nq = int(min(int64_t(S), end4 - cs) >> 2);
     if (active && q < nq && pl.mode != 1) {
       const float *slot = lds + (st % NB) * pl.stage + 4 * q;
-      float4 a[TS], b[TS];
-#pragma unroll
-      for (int u = 0; u < TS; ++u)
-        a[u] = *reinterpret_cast<const float4 *>(slot + (ti * TS + u) * S);
+      float4 b[TS];
 #pragma unroll
       for (int v = 0; v < TS; ++v)
         b[v] = *reinterpret_cast<const float4 *>(slot + (tj * TS + v) * S);
 #pragma unroll
-      for (int u = 0; u < TS; ++u)
-#pragma unroll
-        for (int v = 0; v < TS; ++v) {
-          float d = a[u].x - b[v].x;
-          acc[u][v] = __builtin_fmaf(d, d, acc[u][v]);
-          d = a[u].y - b[v].y;
-          acc[u][v] = __builtin_fmaf(d, d, acc[u][v]);
-          d = a[u].z - b[v].z;
-          acc[u][v] = __builtin_fmaf(d, d, acc[u][v]);
-          d = a[u].w - b[v].w;
-          acc[u][v] = __builtin_fmaf(d, d, acc[u][v]);
-        }
+      for (int h = 0; h < TS / 2; ++h) {
+        const float4 a0 =
+            *reinterpret_cast<const float4 *>(slot + (ti * TS + 2 * h) * S);
+        const float4 a1 = *reinterpret_cast<const float4 *>(
+            slot + (ti * TS + 2 * h + 1) * S);
+        // rows are [row][coordinate] here: the two rows' values are paired
+        // by moves; coordinate-major, so the four updates of one
+        // accumulator are TS packed ops apart
+        pair_step(acc[h], f2{a0.x, a1.x}, b, [](const float4 &t) { return t.x; });
+        pair_step(acc[h], f2{a0.y, a1.y}, b, [](const float4 &t) { return t.y; });
+        pair_step(acc[h], f2{a0.z, a1.z}, b, [](const float4 &t) { return t.z; });
+        pair_step(acc[h], f2{a0.w, a1.w}, b, [](const float4 &t) { return t.w; });
+      }
     }
   }
   // coordinates past the last whole quad (or all of a misaligned chunk):
@@ -537,11 +580,11 @@ __global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
 #pragma unroll
       for (int v = 0; v < TS; ++v) b[v] = gld(rows[min(tj * TS + v, n - 1)] + p);
 #pragma unroll
-      for (int u = 0; u < TS; ++u)
+      for (int h = 0; h < TS / 2; ++h)
 #pragma unroll
         for (int v = 0; v < TS; ++v) {
-          const float d = a[u] - b[v];
-          acc[u][v] = __builtin_fmaf(d, d, acc[u][v]);
+          const f2 d = f2{a[2 * h], a[2 * h + 1]} - f2{b[v], b[v]};
+          acc[h][v] = __builtin_elementwise_fma(d, d, acc[h][v]);
         }
     }
   }
@@ -556,7 +599,8 @@ __global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
     if (active) {
       float *slot = lds + tid * R;
 #pragma unroll
-      for (int e = e0; e < e0 + R && e < kE; ++e) slot[e - e0] = acc[e / TS][e % TS];
+      for (int e = e0; e < e0 + R && e < kE; ++e)
+        slot[e - e0] = pair_acc<TS>(acc, e / TS, e % TS);
     }
     __syncthreads();
     for (int o = tid; o < pl.ntp * ne; o += kRingThreads) {
@@ -821,12 +865,24 @@ extern "C" size_t fsagg_pairdist_workspace_bytes(int n, int64_t numel,
          align256(sizeof(double) * size_t(nseg) * size_t(n) * size_t(n));
 }
 
-// FSAGG_PAIRDIST=flat forces the register-staged kernel (A/B runs)
+// FSAGG_PAIR_FORM=scalar selects the scalar form of the register-staged
+// kernel (A/B runs)
+static bool packed_form() {
+  static int on = -1;
+  if (on < 0) {
+    const char *e = getenv("FSAGG_PAIR_FORM");
+    on = !(e && strcmp(e, "scalar") == 0);
+  }
+  return on == 1;
+}
+
+// FSAGG_PAIRDIST=ring selects the LDS-DMA ring kernel (A/B runs; the
+// register-staged kernel measured faster at C4)
 static bool ring_enabled() {
   static int on = -1;
   if (on < 0) {
     const char *e = getenv("FSAGG_PAIRDIST");
-    on = !(e && strcmp(e, "flat") == 0);
+    on = e && strcmp(e, "ring") == 0;
   }
   return on == 1;
 }
@@ -880,14 +936,16 @@ static int pairdist_segsq_impl(const float *const *tab, int64_t ss, int n,
                      seg_end, nseg, pl.chl, prefix);
   if (numel > 0) {
     const dim3 grid(unsigned(pl.max_chunks), unsigned(pl.groups));
-    if (pl.ts == 10)
-      hipLaunchKernelGGL(pairdist_chunk_kernel<10>, grid, dim3(kBlock), 0, s,
-                         tab, ss, n, pl, seg_lo, seg_end, nseg, prefix,
-                         partial);
-    else
-      hipLaunchKernelGGL(pairdist_chunk_kernel<8>, grid, dim3(kBlock), 0, s,
-                         tab, ss, n, pl, seg_lo, seg_end, nseg, prefix,
-                         partial);
+#define FSAGG_FLAT(TS, PK)                                                    \
+  hipLaunchKernelGGL((pairdist_chunk_kernel<TS, PK>), grid, dim3(kBlock), 0, \
+                     s, tab, ss, n, pl, seg_lo, seg_end, nseg, prefix, partial)
+    const bool pk = packed_form();
+    if (pl.ts == 10) {
+      if (pk) FSAGG_FLAT(10, true); else FSAGG_FLAT(10, false);
+    } else {
+      if (pk) FSAGG_FLAT(8, true); else FSAGG_FLAT(8, false);
+    }
+#undef FSAGG_FLAT
   }
   const int per_seg = pl.ntp * pl.ts * pl.ts;
   hipLaunchKernelGGL(pairdist_segsq_kernel,
