@@ -12,9 +12,15 @@ namespace os {
 
 // Non-temporal global load at a 32-bit element offset from a row base (each
 // column value is read once).
+// The byte offset is formed in 32 bits and zero-extended, so the load takes
+// the SGPR-base + 32-bit VGPR-offset form (global_load_dword v, v_off, s[b])
+// with no per-row 64-bit address add.  Callers keep off < 2^30.
 typedef __attribute__((address_space(1))) const float gfloat;
+typedef __attribute__((address_space(1))) const char gchar;
 __device__ __forceinline__ float ld_nt(const float *row, uint32_t off) {
-  return __builtin_nontemporal_load((gfloat *)(row) + off);
+  const uint32_t boff = off * 4u;
+  return __builtin_nontemporal_load(
+      (gfloat *)((gchar *)(row) + boff));
 }
 
 

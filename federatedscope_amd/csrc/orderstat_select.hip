@@ -117,32 +117,68 @@ __device__ __forceinline__ uint32_t hist_bin(int w, uint32_t x, int before,
   return uint32_t(w) * 4u + byte;
 }
 
-// One pass over W histogram words (from H) for rank ra (and rb if TWO):
-// the number of words whose inclusive prefix count is <= r is the word
-// holding r, and the last such prefix is the count before it.
+// Rank ra (and rb if TWO) in W histogram words (from H), in two levels:
+// the W / 4 groups of four words first (the word byte sums chained through
+// v_sad_u8's accumulator), then the four words of the group holding the
+// rank.  At either level the number of entries whose inclusive prefix count
+// is <= r is the one holding r, and the last such prefix is the count
+// before it.
+template <bool TWO, int W>
+__device__ __forceinline__ void group_find(const uint32_t *H, int ra, int rb,
+                                           int &ga, int &fa, int &gb,
+                                           int &fb) {
+  int cum = 0, na = 0, ba = 0, nb = 0, bb = 0;
+#pragma unroll
+  for (int q = 0; q < W / 4; ++q) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      cum = int(__builtin_amdgcn_sad_u8(H[(4 * q + i) * kWave], 0u,
+                                        uint32_t(cum)));
+    const bool ta = cum <= ra;
+    na += ta;
+    ba = ta ? cum : ba;
+    if (TWO) {
+      const bool tb = cum <= rb;
+      nb += tb;
+      bb = tb ? cum : bb;
+    }
+  }
+  ga = min(na, W / 4 - 1);
+  fa = ba;
+  gb = min(nb, W / 4 - 1);
+  fb = bb;
+}
+
+__device__ __forceinline__ uint32_t word_find(const uint32_t *H, int g,
+                                              int before, int r, int &below,
+                                              int &count) {
+  const uint32_t *G = H + 4 * g * kWave;
+  uint32_t x[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) x[i] = G[i * kWave];
+  int cum = before, n = 0, f = before;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    cum = int(__builtin_amdgcn_sad_u8(x[i], 0u, uint32_t(cum)));
+    const bool t = cum <= r;
+    n += t;
+    f = t ? cum : f;
+  }
+  n = min(n, 3);
+  uint32_t w = x[0];
+#pragma unroll
+  for (int i = 1; i < 4; ++i) w = n == i ? x[i] : w;
+  return hist_bin(4 * g + n, w, f, r, below, count);
+}
+
 template <bool TWO, int W = 64>
 __device__ __forceinline__ void hist_scan(const uint32_t *H, int ra, int rb,
                                           uint32_t &da, int &ba, int &ca,
                                           uint32_t &db, int &bb, int &cb) {
-  int cum = 0, na = 0, fa = 0, nb = 0, fb = 0;
-#pragma unroll 16
-  for (int w = 0; w < W; ++w) {
-    cum += int(__builtin_amdgcn_sad_u8(H[w * kWave], 0u, 0u));
-    const bool ta = cum <= ra;
-    na += ta;
-    fa = ta ? cum : fa;
-    if (TWO) {
-      const bool tb = cum <= rb;
-      nb += tb;
-      fb = tb ? cum : fb;
-    }
-  }
-  na = min(na, W - 1);
-  da = hist_bin(na, H[na * kWave], fa, ra, ba, ca);
-  if (TWO) {
-    nb = min(nb, W - 1);
-    db = hist_bin(nb, H[nb * kWave], fb, rb, bb, cb);
-  }
+  int ga, fa, gb, fb;
+  group_find<TWO, W>(H, ra, rb, ga, fa, gb, fb);
+  da = word_find(H, ga, fa, ra, ba, ca);
+  if (TWO) db = word_find(H, gb, fb, rb, bb, cb);
 }
 
 // Refinement: the next 7-bit digit of the keys of BOTH ranks' bins in one
@@ -324,8 +360,9 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
   const uint32_t lo1 = s1.P, hi1 = s1.P | ~bin_mask(s1.lvl);
   const uint32_t lo2 = s2.P, hi2 = s2.P | ~bin_mask(s2.lvl);
   double mid = 0.0;
+  // (no per-key test of "any list" — that compiles to a branch per key; a
+  // lane with no list writes slots nobody reads: stored == 0 below)
   if (__any(list1 || list2) || MODE == kTrimmed) {
-    const bool any = list1 || list2;
     int c = 0;
     if constexpr (MODE == kMedian) {
       // ranks r1, r1 + 1 are adjacent: no key lies between the two bins, so
@@ -336,7 +373,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
       for (int j = 0; j < N; ++j) {
         if (j >= N - kSelStep && j >= n) continue;
         const uint32_t key = k[j];
-        const bool m = any && key - lo <= span;
+        const bool m = key - lo <= span;
         H[min(c, kList) * kWave] = key;  // a miss: overwritten by next hit
         c += m;
       }
@@ -352,8 +389,10 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
       for (int j = 0; j < N; ++j) {
         if (j >= N - kSelStep && j >= n) continue;
         const uint32_t key = k[j];
-        const bool m = any && (key - l1 <= span1 || key - l2 <= span2);
-        mid += key - mlo < mspan ? double(key2f(key)) : 0.0;
+        const bool m = key - l1 <= span1 || key - l2 <= span2;
+        // select in fp32, then widen: one v_cndmask, not a 64-bit pair
+        const float x = key - mlo < mspan ? key2f(key) : 0.0f;
+        mid += double(x);
         H[min(c, kList) * kWave] = key;  // a miss: overwritten by next hit
         c += m;
       }
@@ -380,10 +419,15 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
   }
   uint32_t va = 0, vb = 0;
   double lsum = 0.0;
+  // the smallest network that holds every lane's list
   if (__any(stored > 32))
     list_select<kList, SUM>(H, stored, rr1, pb, lo, hi, va, vb, lsum);
-  else if (__any(stored > 0))
+  else if (__any(stored > 16))
     list_select<32, SUM>(H, stored, rr1, pb, lo, hi, va, vb, lsum);
+  else if (__any(stored > 8))
+    list_select<16, SUM>(H, stored, rr1, pb, lo, hi, va, vb, lsum);
+  else if (__any(stored > 0))
+    list_select<8, SUM>(H, stored, rr1, pb, lo, hi, va, vb, lsum);
   const uint32_t v1 = list1 ? va : s1.P;
   const uint32_t v2 = (shared ? list1 : list2) ? vb : s2.P;
   const double sum1 = lsum + fixed, sum2 = 0.0;

@@ -2,9 +2,9 @@
 # krum) and the per-kernel average from a kernel trace, per variant.
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 set -e
-# KRUM_VARIANTS: '|'-separated, each a space-separated list of VAR=value
+# KAB_VARIANTS: '|'-separated, each a space-separated list of VAR=value
 i=0
-IFS='|' read -ra VARIANTS <<< "${KRUM_VARIANTS:-FSAGG_PAIRDIST=flat|FSAGG_PAIRDIST=ring|FSAGG_PAIRDIST=ring FSAGG_RING_MODE=2}"
+IFS='|' read -ra VARIANTS <<< "${KAB_VARIANTS:-FSAGG_PAIRDIST=flat|FSAGG_PAIRDIST=ring|FSAGG_PAIRDIST=ring FSAGG_RING_MODE=2}"
 for v in "${VARIANTS[@]}"; do
   i=$((i+1))
   echo "== $v"
