@@ -1,34 +1,34 @@
-// Range-adaptive radix select with LDS compaction for the coordinate-wise
+// Octave-digit radix select with LDS compaction for the coordinate-wise
 // median (median_aggregator.py:43-52) and trimmed mean
 // (trimmedmean_aggregator.py:44-57), for SEL_N - kSelStep < n <= SEL_N.
 // Compiled once per SEL_N (Makefile) so the register-heavy instantiations
 // build in parallel.
 //
-// Keys stay in registers (one lane = one coordinate).  Per lane:
-//  1. kmin/kmax of the column give the common key prefix; the first 8-bit
-//     digit is the 8 bits just below it, so the first histogram splits the
-//     column's actual value range (clustered deltas included), not the
-//     sign/exponent byte.
-//  2. One private 256-bin histogram of byte counters in LDS (ds_add_u32 of
-//     1 << 8·(d & 3) into word d / 4; n <= 255 keeps every byte from
-//     overflowing) places both needed ranks in their bins; one pass over its
-//     64 words finds both.  While the keys of the two bins would overflow
-//     the 64-slot list, the bins are refined by their next 7-bit digits,
-//     both in one pass over the keys (rank 1's bins in histogram words
-//     [0, 32), rank 2's in [32, 64)).
-//  3. One compaction pass writes the keys of both bins to one per-lane LDS
-//     list (bin 1 before bin 2 in key order, so the sorted list holds both
-//     ranks) and, for the trimmed mean, sums every key strictly between the
-//     bins in fp64.  The list is sorted in registers with the compile-time
-//     bitonic network (32 or 64 keys) and the ranks read off.
-// Histogram words and list slots are laid out [slot][lane], so the 64 lanes
-// of a wave always hit 64 distinct banks.  The compaction stores every key
-// at the list's current end (branch-free); a key outside both bins is
-// overwritten by the next one inside, and word 64 catches the stores made
-// once the list is full.
-//
-// Register budget: SEL_N keys + ~40 must stay within 256 VGPRs (2 waves per
-// SIMD); SEL_N moves in steps of kSelStep so no more than 7 are padding.
+// One lane owns one coordinate; its n values stay in registers as raw float
+// bits (so the trimmed mean's middle sum needs no key-to-float decode).
+//  1. Load pass: the column's largest magnitude |x|max (one and + half a
+//     max3 per value) — it also flags NaN/inf.
+//  2. One histogram of an *octave digit* places both needed ranks: a value's
+//     magnitude code m = 8 exponent bits + 3 mantissa bits (8 codes per
+//     octave) relative to |x|max's code, clamped to the 128 codes (16
+//     octaves) below it, on the value's sign side — digits 0..127 negative
+//     (large magnitudes first), 128..255 positive.  Monotone in the value,
+//     so each rank's digit is a key interval.  Unlike a digit of raw key
+//     bits, whose top byte spans two octaves per bin, the octave digit splits
+//     the bulk of a column finely whatever its signs: at C5 (N(0,1) with 10 %
+//     ×100 outliers) the rank bins hold ~2-10 values where the top byte's
+//     held ~50.  Byte counters, 256 bins in 64 words of LDS per lane
+//     ([word][lane], 64 distinct banks per wave).
+//  3. If the two rank bins hold more than the 64-slot list, the larger bin is
+//     refined by a linear digit of its key interval (the fallback for columns
+//     spanning more than 16 octaves, e.g. exact zeros or huge outliers);
+//     every round shrinks a bin ≥ 2^6-fold, so 10 rounds always suffice.
+//  4. One compaction pass writes the keys of both bins to one per-lane LDS
+//     list (bin 1 before bin 2 in key order) and, for the trimmed mean, sums
+//     every value strictly between the bins in fp64.  The list is sorted with
+//     the smallest bitonic network that holds every lane's list and the ranks
+//     (and the kept partial sums) read off.
+// Register budget: SEL_N values + ~40 within 256 VGPRs (2 waves per SIMD).
 #include "orderstat.h"
 
 #ifndef SEL_N
@@ -42,62 +42,79 @@ namespace {
 constexpr int kSelWords = 65;                    // 64 hist/list words + dump
 constexpr int kSelWaves = kBlock / kWave;
 constexpr int kSelLds = kSelWords * kWave * kSelWaves;  // 66.5 KiB per block
-constexpr int kList = 64;  // LDS list slots per lane (slot 64: dump)
-constexpr uint32_t kKeyPosInf = 0xFF800000u;  // f2key(+inf)
-constexpr uint32_t kKeyNegInf = 0x007FFFFFu;  // f2key(-inf)
+constexpr int kList = 64;      // LDS list slots per lane (slot 64: dump)
+constexpr int kMagShift = 20;  // magnitude code: bits [30:20] of |x|
+constexpr int kCodes = 128;    // codes per sign side (16 octaves)
+constexpr uint32_t kKeyPosInf = 0xFF800000u;  // ukey(+inf)
+constexpr uint32_t kKeyNegInf = 0x007FFFFFu;  // ukey(-inf)
 
-// Selection state of one rank.  Its bin is the keys whose bits >= lvl equal
-// P's (P's lower bits are zero); `below` keys sort before the bin and `cnt`
-// are in it.  lvl == 0: all 32 bits resolved, the bin is `cnt` copies of P.
+// float bits -> order-preserving key (-0 < +0), 3 ops
+__device__ __forceinline__ uint32_t ukey(uint32_t u) {
+  return u ^ (uint32_t(int32_t(u) >> 31) | 0x80000000u);
+}
+
+// Selection state of one rank: its bin is the key interval [lo, hi] holding
+// `cnt` keys, `below` keys sort before it.  lo == hi: resolved (cnt copies).
 struct RankSel {
-  uint32_t P;
-  int lvl, below, cnt;
+  uint32_t lo, hi;
+  int below, cnt;
 };
 
-__device__ __forceinline__ uint32_t bin_mask(int lvl) {
-  return lvl >= 32 ? 0u : (0xFFFFFFFFu << lvl);
-}
-// shift of the next digit of `width` bits
-__device__ __forceinline__ int digit_shift(const RankSel &s, int width = 8) {
-  return s.lvl > width ? s.lvl - width : 0;
-}
-
-__device__ __forceinline__ RankSel rank_init(uint32_t kmin, uint32_t kmax,
-                                             int n) {
-  RankSel s;
-  s.below = 0;
-  s.cnt = n;
-  s.lvl = kmin == kmax ? 0 : 32 - __builtin_clz(kmin ^ kmax);
-  s.P = kmin & bin_mask(s.lvl);
-  return s;
-}
-
-__device__ __forceinline__ void hist_clear(uint32_t *H) {
-#pragma unroll
-  for (int w = 0; w < 64; ++w) H[w * kWave] = 0u;
-}
-
-// Histogram address of digit d = (key >> sh) & 255: byte d & 3 of word d / 4.
-// (v_bfe_u32 + v_lshl_add_u32 for the address; the shift amount of the
-// value uses only its low 5 bits, so ((key >> sh) << 3) needs no mask.)
-__device__ __forceinline__ uint32_t *hist_word(uint32_t *H, uint32_t key,
-                                               int sh) {
-  return H + __builtin_amdgcn_ubfe(key, uint32_t(sh + 2), 6u) * kWave;
-}
-__device__ __forceinline__ uint32_t hist_one(uint32_t key, int sh) {
-  return 1u << (((key >> sh) << 3) & 31u);
-}
-
-// First digit: every real key of the lane (all share the common prefix).
+// Opaque copy barrier: keeps the compiler from hoisting per-pass key math
+// (ukey of every value) out of a pass and holding N more registers live.
 template <int N>
-__device__ __forceinline__ void hist_add_all(uint32_t *H,
-                                             const uint32_t (&k)[N], int n,
-                                             int sh) {
+__device__ __forceinline__ void fence_regs(uint32_t (&u)[N]) {
 #pragma unroll
-  for (int j = 0; j < N; ++j) {
-    if (j >= N - kSelStep && j >= n) continue;  // pads
-    atomicAdd(hist_word(H, k[j], sh), hist_one(k[j], sh));
+  for (int j = 0; j < N; ++j) asm volatile("" : "+v"(u[j]));
+}
+
+__device__ __forceinline__ bool resolved(const RankSel &s) {
+  return s.lo == s.hi;
+}
+__device__ __forceinline__ bool same_bin(const RankSel &a, const RankSel &b) {
+  return a.lo == b.lo && a.hi == b.hi;
+}
+
+// Octave digit of float bits u (monotone in the value):
+//   t = clamp(m(u) - base, 0, 127); digit = negative ? 127 - t : 128 + t
+// ((t ^ sign) + 128 with sign = -1 or 0: v_xad_u32).
+__device__ __forceinline__ uint32_t octave_digit(uint32_t u, int base) {
+  const int m = int(__builtin_amdgcn_ubfe(u, uint32_t(kMagShift), 11u));
+  const int t = min(max(m - base, 0), kCodes - 1);
+  return (uint32_t(t) ^ uint32_t(int32_t(u) >> 31)) + 128u;
+}
+
+// The key interval of octave digit d (given the launch's base).
+__device__ __forceinline__ void octave_bin(uint32_t d, int base, uint32_t &lo,
+                                           uint32_t &hi) {
+  const bool pos = d >= 128u;
+  const int t = pos ? int(d) - 128 : 127 - int(d);
+  const int mlo = t == 0 ? 0 : base + t;
+  const int mhi = t == kCodes - 1 ? 2047 : base + t;
+  // |x| bits [mlo << 20, (mhi << 20) | 0xFFFFF] (a selected bin is never
+  // empty, so 0 <= mlo <= mhi)
+  const uint32_t alo = uint32_t(max(mlo, 0)) << kMagShift;
+  const uint32_t ahi = (uint32_t(max(mhi, 0)) << kMagShift) | 0xFFFFFu;
+  // the top bins stop at ±inf, so no band [lo1, hi2] spans all 2^32 keys
+  // (NaN keys lie outside every bin; a NaN column's result is NaN anyway)
+  if (pos) {
+    lo = alo | 0x80000000u;
+    hi = min(ahi | 0x80000000u, kKeyPosInf);
+  } else {
+    lo = max(~(ahi | 0x80000000u), kKeyNegInf);
+    hi = ~(alo | 0x80000000u);
   }
+}
+
+__device__ __forceinline__ void hist_clear(uint32_t *H, int words) {
+#pragma unroll
+  for (int w = 0; w < 64; ++w)
+    if (w < words) H[w * kWave] = 0u;
+}
+
+// byte counter of digit d: byte d & 3 of word d / 4
+__device__ __forceinline__ void hist_inc(uint32_t *H, uint32_t d) {
+  atomicAdd(&H[(d >> 2) * kWave], 1u << ((d << 3) & 31u));
 }
 
 // Locate rank r in the histogram given the word that holds it (w, x) and
@@ -171,7 +188,7 @@ __device__ __forceinline__ uint32_t word_find(const uint32_t *H, int g,
   return hist_bin(4 * g + n, w, f, r, below, count);
 }
 
-template <bool TWO, int W = 64>
+template <bool TWO, int W>
 __device__ __forceinline__ void hist_scan(const uint32_t *H, int ra, int rb,
                                           uint32_t &da, int &ba, int &ca,
                                           uint32_t &db, int &bb, int &cb) {
@@ -181,65 +198,42 @@ __device__ __forceinline__ void hist_scan(const uint32_t *H, int ra, int rb,
   if (TWO) db = word_find(H, gb, fb, rb, bb, cb);
 }
 
-// Refinement: the next 7-bit digit of the keys of BOTH ranks' bins in one
-// pass — rank 1's bin counts into histogram words [0, 32), rank 2's into
-// [32, 64) (the bins are disjoint unless shared, and then only rank 1's is
-// counted); other keys and lanes add zeros.
-template <int N>
-__device__ __forceinline__ void hist_add_dual(uint32_t *H,
-                                              const uint32_t (&k)[N], int n,
-                                              const RankSel &s1, bool on1,
-                                              const RankSel &s2, bool on2) {
-  const int sh1 = digit_shift(s1, 7), sh2 = digit_shift(s2, 7);
-  const uint32_t M1 = bin_mask(s1.lvl), M2 = bin_mask(s2.lvl);
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-    if (j >= N - kSelStep && j >= n) continue;
-    const uint32_t key = k[j];
-    const bool m1 = on1 && (key & M1) == s1.P;
-    const bool m2 = on2 && (key & M2) == s2.P;
-    const uint32_t d = __builtin_amdgcn_ubfe(key, uint32_t(m2 ? sh2 : sh1),
-                                             7u) | (m2 ? 128u : 0u);
-    atomicAdd(&H[(d >> 2) * kWave],
-              (m1 || m2) ? 1u << ((d & 3u) * 8u) : 0u);
-  }
+// Linear refinement digit of a key interval [lo, lo + lim - 1]: rel =
+// min(key - lo, lim) (keys below lo wrap, so every key outside maps to lim),
+// digit = (rel + pad) >> sh with pad making lim + pad a multiple of 2^sh —
+// the bin's keys take digits [pad >> sh, (lim - 1 + pad) >> sh] <= 127 and
+// every key outside the bin the single digit above them (<= 128, word 32),
+// which a scan for a rank inside the bin never reaches.
+struct Refine {
+  uint32_t lo, lim, pad;
+  int sh;
+};
+
+__device__ __forceinline__ Refine refine_plan(const RankSel &s) {
+  Refine f;
+  f.lo = s.lo;
+  f.lim = s.hi - s.lo + 1u;  // <= 2^31: a bin never crosses the sign
+  int sh = max(0, 32 - __builtin_clz(f.lim | 1u) - 7);
+  if (((f.lim + (1u << sh) - 1u) >> sh) > 127u) ++sh;
+  f.sh = sh;
+  f.pad = (0u - f.lim) & ((1u << sh) - 1u);
+  return f;
 }
 
-// Refinement of rank 1's bin alone (the common case: the median's two
-// ranks share a bin): the key's offset from the bin base, shifted to the
-// next 7-bit digit and clamped to 128, is the digit for keys in the bin; a
-// key outside it lands in bin 128 (word 32, outside the 32-word scan) or,
-// when the bin has fewer than 128 digits, in a digit above the bin's own —
-// after every key of the bin, so the scan for a rank inside the bin never
-// reaches it.  No compare/select per key.  (Lanes whose rank needs no
-// refinement count garbage and ignore the result; <= 255 keys per lane
-// keep every byte counter in range.)
-template <int N>
-__device__ __forceinline__ void hist_add_one(uint32_t *H,
-                                             const uint32_t (&k)[N], int n,
-                                             const RankSel &s) {
-  const int sh = digit_shift(s, 7);
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-    if (j >= N - kSelStep && j >= n) continue;
-    const uint32_t d = min((k[j] - s.P) >> sh, 128u);
-    atomicAdd(&H[(d >> 2) * kWave], 1u << ((d << 3) & 31u));
-  }
-}
-
-// Narrow s to digit bin d (count b below it, c in it), if on.
-__device__ __forceinline__ void rank_apply(RankSel &s, bool on, uint32_t d,
-                                           int b, int c, int width = 8) {
+// Narrow s to refinement digit d (count b below it, c in it).
+__device__ __forceinline__ void refine_apply(RankSel &s, const Refine &f,
+                                             bool on, uint32_t d, int b,
+                                             int c) {
   if (!on) return;
-  const int sh = digit_shift(s, width);
+  const uint32_t span = f.lim - 1u;
+  const uint32_t r0 = d << f.sh;
+  const uint32_t rlo = r0 > f.pad ? r0 - f.pad : 0u;
+  const uint32_t r1 = ((d + 1u) << f.sh) - 1u - f.pad;
+  const uint32_t rhi = r1 < span ? r1 : span;
   s.below += b;
   s.cnt = c;
-  s.P |= d << sh;
-  s.lvl = sh;
-}
-
-__device__ __forceinline__ bool same_bin(const RankSel &a, const RankSel &b) {
-  return a.lvl == b.lvl && a.P == b.P;
+  s.hi = f.lo + rhi;
+  s.lo = f.lo + rlo;
 }
 
 // Sort the lane's list of `cnt` keys at LDS slots [0, cnt) and read list
@@ -281,141 +275,133 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
   const int64_t p = br.lo + threadIdx.x;
   const bool live = int(threadIdx.x) < br.len;
   __builtin_assume(n > N - kSelStep && n <= N);  // dispatch
-  uint32_t k[N];
+  // 1. the column as raw float bits; |x|max.  Rows past n (pads) re-read
+  // row n - 1: harmless for the max, skipped by every counting pass.
+  uint32_t u[N];
+  uint32_t amax = 0u;
   {
     // coordinates < 2^30 (launch); dead lanes re-read the chunk's first
     const uint32_t off = uint32_t(live ? p : br.lo);
 #pragma unroll
     for (int j = 0; j < N; ++j)
-      k[j] = __float_as_uint(ld_nt(rows[j < n ? j : n - 1], off));
+      u[j] = __float_as_uint(ld_nt(rows[j < n ? j : n - 1], off));
+#pragma unroll
+    for (int j = 0; j < N; ++j) amax = max(amax, u[j] & 0x7FFFFFFFu);
+  }
+  const bool nan = amax > 0x7F800000u;
+  const bool nonfinite = amax >= 0x7F800000u;
+  const int obase = int(amax >> kMagShift) - (kCodes - 1);
+  const int r1 = MODE == kMedian ? (n - 1) / 2 : kk;
+  const int r2 = MODE == kMedian ? n / 2 : n - kk - 1;
+
+  // 2. octave-digit histogram: both ranks' bins
+  RankSel s1, s2;
+  {
+    hist_clear(H, 64);
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-      const uint32_t key = f2key(__uint_as_float(k[j]));
-      k[j] = (j < N - kSelStep || j < n) ? key : kPad;
+      if (j >= N - kSelStep && j >= n) continue;  // pads
+      hist_inc(H, octave_digit(u[j], obase));
     }
+    uint32_t d1, d2;
+    int b1, c1, b2, c2;
+    hist_scan<true, 64>(H, r1, r2, d1, b1, c1, d2, b2, c2);
+    octave_bin(d1, obase, s1.lo, s1.hi);
+    octave_bin(d2, obase, s2.lo, s2.hi);
+    s1.below = b1;
+    s1.cnt = c1;
+    s2.below = b2;
+    s2.cnt = c2;
   }
-  bool nan, nonfinite;
-  RankSel s1;
-  {
-    uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;
+
+  // 3. refine while the two bins would overflow the list (rare)
+  bool shared = same_bin(s1, s2);
+#pragma unroll 1
+  for (int round = 0; round < 10; ++round) {
+    const bool list1 = !resolved(s1), list2 = !shared && !resolved(s2);
+    const int stored = (list1 ? s1.cnt : 0) + (list2 ? s2.cnt : 0);
+    const bool need = stored > kList;
+    if (!__any(need)) break;
+    // the larger listed bin (a shared bin carries both ranks)
+    const bool pick2 = list2 && (!list1 || s2.cnt > s1.cnt);
+    fence_regs<N>(u);
+    const Refine f = refine_plan(pick2 ? s2 : s1);
+    hist_clear(H, 33);
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       if (j >= N - kSelStep && j >= n) continue;
-      kmin = min(kmin, k[j]);
-      kmax = max(kmax, k[j]);
+      const uint32_t rel = min(ukey(u[j]) - f.lo, f.lim);
+      hist_inc(H, (rel + f.pad) >> f.sh);
     }
-    nan = kmax > kKeyPosInf || kmin < kKeyNegInf;
-    nonfinite = kmax >= kKeyPosInf || kmin <= kKeyNegInf;
-    s1 = rank_init(kmin, kmax, n);
-  }
-  const int r1 = MODE == kMedian ? (n - 1) / 2 : kk;
-  const int r2 = MODE == kMedian ? n / 2 : n - kk - 1;
-  // first digit: one histogram places both ranks
-  RankSel s2 = s1;
-  if (__any(s1.lvl > 0)) {
-    const bool on = s1.lvl > 0;
-    hist_clear(H);
-    hist_add_all<N>(H, k, n, digit_shift(s1));
-    uint32_t d1, d2;
-    int b1, c1, b2, c2;
-    hist_scan<true>(H, r1, r2, d1, b1, c1, d2, b2, c2);
-    rank_apply(s1, on, d1, b1, c1);
-    rank_apply(s2, on, d2, b2, c2);
-  }
-  // The keys of both rank bins go to one LDS list of at most kList keys
-  // (bin 1 then bin 2 in key order).  Refine a bin with more than
-  // kList / 2 keys while the list would overflow.
-  bool shared = same_bin(s1, s2);
-#pragma unroll 1
-  for (int round = 0; round < 4; ++round) {  // 7-bit digits: lvl 24 → 0
-    const bool list1 = s1.lvl > 0, list2 = !shared && s2.lvl > 0;
-    const int stored = (list1 ? s1.cnt : 0) + (list2 ? s2.cnt : 0);
-    const bool need1 =
-        list1 && stored > kList && (shared || s1.cnt > kList / 2);
-    const bool need2 = list2 && stored > kList && s2.cnt > kList / 2;
-    if (!__any(need1 || need2)) break;
-    hist_clear(H);
-    if (__any(need2))
-      hist_add_dual<N>(H, k, n, s1, need1, s2, need2);
-    else
-      hist_add_one<N>(H, k, n, s1);
-    uint32_t d1, d2, d3 = 0;
-    int b1, c1, b2, c2, b3 = 0, c3 = 0;
-    // rank 1 (and rank 2 where it shares rank 1's bin) in words [0, 32)
-    hist_scan<true, 32>(H, r1 - s1.below, r2 - s2.below, d1, b1, c1, d2, b2,
-                        c2);
-    // rank 2 in its own bin: words [32, 64)
-    if (__any(need2))
-      hist_scan<false, 32>(H + 32 * kWave, r2 - s2.below, 0, d3, b3, c3, d3,
-                           b3, c3);
-    rank_apply(s2, need1 && shared, d2, b2, c2, 7);
-    rank_apply(s2, need2, d3, b3, c3, 7);
-    rank_apply(s1, need1, d1, b1, c1, 7);
+    uint32_t da, db;
+    int ba, ca, bb, cb;
+    const int ra = pick2 ? r2 - s2.below : r1 - s1.below;
+    hist_scan<true, 32>(H, ra, r2 - s2.below, da, ba, ca, db, bb, cb);
+    refine_apply(s2, f, need && shared, db, bb, cb);
+    refine_apply(s2, f, need && pick2, da, ba, ca);
+    refine_apply(s1, f, need && !pick2, da, ba, ca);
     shared = same_bin(s1, s2);
   }
 
-  // compaction: the keys of the listed bins, in row order
-  const bool list1 = s1.lvl > 0;
-  const bool list2 = !shared && s2.lvl > 0;
-  const uint32_t lo1 = s1.P, hi1 = s1.P | ~bin_mask(s1.lvl);
-  const uint32_t lo2 = s2.P, hi2 = s2.P | ~bin_mask(s2.lvl);
+  // 4. compaction: the keys of the listed bins, in row order (at most kList,
+  // so the running slot c never passes the dump slot kList)
+  const bool list1 = !resolved(s1);
+  const bool list2 = !shared && !resolved(s2);
   double mid = 0.0;
-  // (no per-key test of "any list" — that compiles to a branch per key; a
-  // lane with no list writes slots nobody reads: stored == 0 below)
+  fence_regs<N>(u);
   if (__any(list1 || list2) || MODE == kTrimmed) {
     int c = 0;
     if constexpr (MODE == kMedian) {
       // ranks r1, r1 + 1 are adjacent: no key lies between the two bins, so
-      // one key range covers both lists
-      const uint32_t lo = list1 ? lo1 : lo2;
-      const uint32_t span = (list2 ? hi2 : hi1) - lo;
+      // one key range [lo, lo + w) covers both lists
+      const uint32_t lo = list1 ? s1.lo : s2.lo;
+      const uint32_t w =
+          (list1 || list2) ? (list2 ? s2.hi : s1.hi) - lo + 1u : 0u;
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         if (j >= N - kSelStep && j >= n) continue;
-        const uint32_t key = k[j];
-        const bool m = key - lo <= span;
-        H[min(c, kList) * kWave] = key;  // a miss: overwritten by next hit
-        c += m;
+        const uint32_t key = ukey(u[j]);
+        H[c * kWave] = key;  // a miss: overwritten by the next hit
+        c += (key - lo) < w;
       }
     } else {
-      const uint32_t span1 = list1 ? hi1 - lo1 : 0u;
-      const uint32_t l1 = list1 ? lo1 : 0xFFFFFFFFu;
-      const uint32_t span2 = list2 ? hi2 - lo2 : 0u;
-      const uint32_t l2 = list2 ? lo2 : 0xFFFFFFFFu;
-      // strictly between the bins: (hi1, lo2)
-      const uint32_t mlo = hi1 + 1u;
-      const uint32_t mspan = shared ? 0u : lo2 - mlo;
+      // the band from bin 1 to bin 2 relative to A: [0, w1) bin 1 listed,
+      // [w1, w1 + wm) strictly between the bins (summed), then bin 2 listed
+      // up to wb
+      const uint32_t A = list1 ? s1.lo : s1.hi + 1u;
+      const uint32_t w1 = list1 ? s1.hi - s1.lo + 1u : 0u;
+      const uint32_t wm = shared ? 0u : s2.lo - (s1.hi + 1u);
+      const uint32_t wb = w1 + wm + (list2 ? s2.hi - s2.lo + 1u : 0u);
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         if (j >= N - kSelStep && j >= n) continue;
-        const uint32_t key = k[j];
-        const bool m = key - l1 <= span1 || key - l2 <= span2;
+        const uint32_t rel = ukey(u[j]) - A;
+        const bool inm = rel - w1 < wm;
         // select in fp32, then widen: one v_cndmask, not a 64-bit pair
-        const float x = key - mlo < mspan ? key2f(key) : 0.0f;
-        mid += double(x);
-        H[min(c, kList) * kWave] = key;  // a miss: overwritten by next hit
-        c += m;
+        mid += double(inm ? __uint_as_float(u[j]) : 0.0f);
+        H[c * kWave] = rel + A;  // a miss: overwritten by the next hit
+        c += (rel < wb) && !inm;
       }
     }
   }
 
-  // read the ranks (and the kept sum) off the sorted list
+  // 5. read the ranks (and the kept sum) off the sorted list
   constexpr bool SUM = MODE == kTrimmed;
   const int rr1 = r1 - s1.below, rr2 = r2 - s2.below;
   const int c1off = list1 ? s1.cnt : 0;
   const int stored = c1off + (list2 ? s2.cnt : 0);
   const int pb = shared ? rr2 : c1off + rr2;
   int lo, hi;
-  double fixed = 0.0;  // kept copies of fully resolved (unlisted) bins
+  double fixed = 0.0;  // kept copies of resolved (unlisted) bins
   if (shared) {
     lo = list1 ? rr1 : 0;
     hi = list1 ? rr2 : -1;
-    if (!list1) fixed = double(key2f(s1.P)) * double(rr2 - rr1 + 1);
+    if (!list1) fixed = double(key2f(s1.lo)) * double(rr2 - rr1 + 1);
   } else {
     lo = list1 ? rr1 : 0;
     hi = list2 ? c1off + rr2 : c1off - 1;
-    if (!list1) fixed += double(key2f(s1.P)) * double(s1.cnt - rr1);
-    if (!list2) fixed += double(key2f(s2.P)) * double(rr2 + 1);
+    if (!list1) fixed += double(key2f(s1.lo)) * double(s1.cnt - rr1);
+    if (!list2) fixed += double(key2f(s2.lo)) * double(rr2 + 1);
   }
   uint32_t va = 0, vb = 0;
   double lsum = 0.0;
@@ -428,9 +414,8 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
     list_select<16, SUM>(H, stored, rr1, pb, lo, hi, va, vb, lsum);
   else if (__any(stored > 0))
     list_select<8, SUM>(H, stored, rr1, pb, lo, hi, va, vb, lsum);
-  const uint32_t v1 = list1 ? va : s1.P;
-  const uint32_t v2 = (shared ? list1 : list2) ? vb : s2.P;
-  const double sum1 = lsum + fixed, sum2 = 0.0;
+  const uint32_t v1 = list1 ? va : s1.lo;
+  const uint32_t v2 = (shared ? list1 : list2) ? vb : s2.lo;
   if (!live) return;
   float r;
   if constexpr (MODE == kMedian) {
@@ -441,7 +426,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
     // Σall − Σtop − Σbottom in fp32: with k >= 1 an infinity is always
     // among the excluded values, so inf - inf (or a NaN) gives NaN; with
     // k == 0 it is Σall itself, summed in row order (rare: re-read).
-    float s = float(sum1 + mid + sum2);
+    float s = float(lsum + fixed + mid);
     if (nonfinite) {
       s = __builtin_nanf("");
       if (kk == 0 && !nan) {

@@ -1,16 +1,22 @@
 # PMC passes (one counter group per rocprofv3 run) over tools/bench_robust.py
-# <what>; csv under gpurun_out/pmc_<what>_<tag>_<pass>/.
-# Usage: bash tools/pmc.sh <what> <tag>
+# <what>; per-kernel means summarised into gpurun_out/pmc_<what>_<tag>.json
+# (tools/pmc_summary.py) and the raw per-dispatch CSVs removed (they exceed
+# gpurun's copy-back limit).  Usage: bash tools/pmc.sh <what> <tag>
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
 what=${1:-orderstat}; tag=${2:-base}
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT"
-P2="SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH"
+P2="SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_ACTIVE_INST_LDS"
 P3="FETCH_SIZE"
 P4="WRITE_SIZE"
 i=0
+dirs=""
 for P in "$P1" "$P2" "$P3" "$P4"; do
   i=$((i+1))
+  d=gpurun_out/pmc_${what}_${tag}_$i
   timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv \
-    -d gpurun_out/pmc_${what}_${tag}_$i -o run -- python3 tools/bench_robust.py $what \
-    > gpurun_out/pmc_${what}_${tag}_$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
+    -d $d -o run -- python3 tools/bench_robust.py $what \
+    > $d.log 2>&1 || { echo "pass $i failed"; exit 1; }
+  dirs="$dirs $d"
 done
+python3 tools/pmc_summary.py gpurun_out/pmc_${what}_${tag}.json $dirs && rm -rf $dirs
