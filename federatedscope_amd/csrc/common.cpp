@@ -23,6 +23,20 @@ int check_launch(const char *what) {
   return FSAGG_OK;
 }
 
+int device_cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
+                              dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    cached[dev] = cus;
+  }
+  return cached[dev];
+}
+
 }  // namespace fsagg
 
 extern "C" int fsagg_version(void) { return FSAGG_VERSION; }

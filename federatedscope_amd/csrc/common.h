@@ -25,6 +25,10 @@ inline bool aligned16(const void *p) {
 // Check the launch status once, after the kernel is enqueued.
 int check_launch(const char *what);
 
+// Compute units of the current device (cached per device; 256 if the query
+// fails) — grid size of the persistent kernels.
+int device_cu_count();
+
 constexpr int kWave = 64;
 
 // fp32 loads through a pointer read from a device table: the address space

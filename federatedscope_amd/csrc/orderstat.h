@@ -23,6 +23,15 @@ __device__ __forceinline__ float ld_nt(const float *row, uint32_t off) {
       (gfloat *)((gchar *)(row) + boff));
 }
 
+// Row pointer j of a device row table, read through the constant address
+// space: the table is never written while a kernel runs, so the load stays a
+// scalar s_load even in a loop that also stores to global memory (a plain
+// load there becomes a vector load + v_readfirstlane per row).
+typedef const float *const __attribute__((address_space(4))) const_row_t;
+__device__ __forceinline__ const float *row_at(const float *const *tab,
+                                               int j) {
+  return ((const_row_t *)(tab))[j];
+}
 
 constexpr int kBlock = 256;
 constexpr uint32_t kPad = 0xFFFFFFFFu;

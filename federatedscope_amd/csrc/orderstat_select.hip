@@ -39,10 +39,10 @@ namespace fsagg {
 namespace os {
 namespace {
 
-constexpr int kSelWords = 65;                    // 64 hist/list words + dump
+constexpr int kSelWords = 64;  // hist/list words per lane (list: 63 + dump)
 constexpr int kSelWaves = kBlock / kWave;
-constexpr int kSelLds = kSelWords * kWave * kSelWaves;  // 66.5 KiB per block
-constexpr int kList = 64;      // LDS list slots per lane (slot 64: dump)
+constexpr int kSelLds = kSelWords * kWave * kSelWaves;  // 64 KiB per block
+constexpr int kList = 63;      // LDS list slots per lane (slot 63: dump)
 constexpr int kMagShift = 20;  // magnitude code: bits [30:20] of |x|
 constexpr int kCodes = 128;    // codes per sign side (16 octaves)
 constexpr uint32_t kKeyPosInf = 0xFF800000u;  // ukey(+inf)
@@ -59,6 +59,13 @@ struct RankSel {
   uint32_t lo, hi;
   int below, cnt;
 };
+
+// a < b as the borrow of a - b (v_sub_co_u32 + v_addc_co_u32 when added to
+// a counter, instead of v_cmp + v_cndmask + v_add)
+__device__ __forceinline__ uint32_t below(uint32_t a, uint32_t b) {
+  uint32_t d;
+  return __builtin_sub_overflow(a, b, &d) ? 1u : 0u;
+}
 
 // Opaque copy barrier: keeps the compiler from hoisting per-pass key math
 // (ukey of every value) out of a pass and holding N more registers live.
@@ -112,9 +119,20 @@ __device__ __forceinline__ void hist_clear(uint32_t *H, int words) {
     if (w < words) H[w * kWave] = 0u;
 }
 
+// The lane's LDS words by byte address: word w at hb | (w << 8) ([word][lane]
+// layout: a wave's 64 lanes hit 64 distinct banks).  hb = wave·16 KiB +
+// lane·4 has bits 8..13 clear (the kernel's only LDS array starts at 0,
+// checked at entry), so a word address is one v_and_or / v_lshl_or.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ lds_u32 *lds_at(uint32_t byte) {
+  return (lds_u32 *)(uintptr_t)byte;
+}
+
 // byte counter of digit d: byte d & 3 of word d / 4
-__device__ __forceinline__ void hist_inc(uint32_t *H, uint32_t d) {
-  atomicAdd(&H[(d >> 2) * kWave], 1u << ((d << 3) & 31u));
+__device__ __forceinline__ void hist_inc(uint32_t hb, uint32_t d) {
+  __hip_atomic_fetch_add(lds_at(hb | ((d << 6) & 0x3F00u)),
+                         1u << ((d << 3) & 31u), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // Locate rank r in the histogram given the word that holds it (w, x) and
@@ -236,8 +254,9 @@ __device__ __forceinline__ void refine_apply(RankSel &s, const Refine &f,
   s.lo = f.lo + rlo;
 }
 
-// Sort the lane's list of `cnt` keys at LDS slots [0, cnt) and read list
-// positions pa and pb off it; Σ key2f over positions [lo, hi] in fp64.
+// Sort the lane's list of `cnt` values (float bits) at LDS slots [0, cnt) by
+// key and read list positions pa and pb off it (as keys); Σ over positions
+// [lo, hi] in fp64.
 template <int S, bool SUM>
 __device__ __forceinline__ void list_select(const uint32_t *H, int cnt,
                                             int pa, int pb, int lo, int hi,
@@ -246,7 +265,7 @@ __device__ __forceinline__ void list_select(const uint32_t *H, int cnt,
   uint32_t a[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) {
-    const uint32_t x = H[i * kWave];
+    const uint32_t x = ukey(H[i * kWave]);
     a[i] = i < cnt ? x : kPad;
   }
   bitonic_sort<S>(a);
@@ -269,6 +288,8 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
   __shared__ uint32_t lds[kSelLds];
   uint32_t *H = lds + (threadIdx.x / kWave) * kSelWords * kWave +
                 (threadIdx.x & (kWave - 1));
+  const uint32_t hb = uint32_t(uintptr_t((lds_u32 *)H));
+  if (uint32_t(uintptr_t((lds_u32 *)lds)) & 0x3FFFu) __builtin_trap();
   const BlockRows br = block_rows(rs, blockIdx.x);
   const float *const *__restrict__ rows = br.rows;
   const float *__restrict__ base = br.base;
@@ -284,7 +305,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
     const uint32_t off = uint32_t(live ? p : br.lo);
 #pragma unroll
     for (int j = 0; j < N; ++j)
-      u[j] = __float_as_uint(ld_nt(rows[j < n ? j : n - 1], off));
+      u[j] = __float_as_uint(ld_nt(row_at(rows, j < n ? j : n - 1), off));
 #pragma unroll
     for (int j = 0; j < N; ++j) amax = max(amax, u[j] & 0x7FFFFFFFu);
   }
@@ -301,7 +322,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       if (j >= N - kSelStep && j >= n) continue;  // pads
-      hist_inc(H, octave_digit(u[j], obase));
+      hist_inc(hb, octave_digit(u[j], obase));
     }
     uint32_t d1, d2;
     int b1, c1, b2, c2;
@@ -331,7 +352,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
     for (int j = 0; j < N; ++j) {
       if (j >= N - kSelStep && j >= n) continue;
       const uint32_t rel = min(ukey(u[j]) - f.lo, f.lim);
-      hist_inc(H, (rel + f.pad) >> f.sh);
+      hist_inc(hb, (rel + f.pad) >> f.sh);
     }
     uint32_t da, db;
     int ba, ca, bb, cb;
@@ -343,8 +364,8 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
     shared = same_bin(s1, s2);
   }
 
-  // 4. compaction: the keys of the listed bins, in row order (at most kList,
-  // so the running slot c never passes the dump slot kList)
+  // 4. compaction: the values of the listed bins, in row order (at most
+  // kList, so the running slot c never passes the dump slot kList)
   const bool list1 = !resolved(s1);
   const bool list2 = !shared && !resolved(s2);
   double mid = 0.0;
@@ -353,16 +374,29 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
     int c = 0;
     if constexpr (MODE == kMedian) {
       // ranks r1, r1 + 1 are adjacent: no key lies between the two bins, so
-      // one key range [lo, lo + w) covers both lists
+      // one key range [lo, lo + w) covers both lists.  When it lies on one
+      // side of zero (every lane of the wave), it is one interval of the
+      // float bits themselves, [ulo, ulo + w): no key transform per value.
       const uint32_t lo = list1 ? s1.lo : s2.lo;
       const uint32_t w =
           (list1 || list2) ? (list2 ? s2.hi : s1.hi) - lo + 1u : 0u;
+      const uint32_t hi = lo + (w - 1u);
+      const bool pos = lo >= 0x80000000u, neg = hi < 0x80000000u;
+      if (!__any(w != 0u && !pos && !neg)) {
+        const uint32_t ulo = pos ? lo - 0x80000000u : ~hi;
 #pragma unroll
-      for (int j = 0; j < N; ++j) {
-        if (j >= N - kSelStep && j >= n) continue;
-        const uint32_t key = ukey(u[j]);
-        H[c * kWave] = key;  // a miss: overwritten by the next hit
-        c += (key - lo) < w;
+        for (int j = 0; j < N; ++j) {
+          if (j >= N - kSelStep && j >= n) continue;
+          *lds_at(hb | (uint32_t(c) << 8)) = u[j];  // a miss: overwritten
+          c += below(u[j] - ulo, w);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          if (j >= N - kSelStep && j >= n) continue;
+          *lds_at(hb | (uint32_t(c) << 8)) = u[j];  // a miss: overwritten
+          c += below(ukey(u[j]) - lo, w);
+        }
       }
     } else {
       // the band from bin 1 to bin 2 relative to A: [0, w1) bin 1 listed,
@@ -377,9 +411,12 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
         if (j >= N - kSelStep && j >= n) continue;
         const uint32_t rel = ukey(u[j]) - A;
         const bool inm = rel - w1 < wm;
-        // select in fp32, then widen: one v_cndmask, not a 64-bit pair
-        mid += double(inm ? __uint_as_float(u[j]) : 0.0f);
-        H[c * kWave] = rel + A;  // a miss: overwritten by the next hit
+        // select in fp32, then widen: one v_cndmask, not a 64-bit pair (the
+        // empty asm keeps the compiler from sinking the select past the cvt)
+        float x = inm ? __uint_as_float(u[j]) : 0.0f;
+        asm("" : "+v"(x));
+        mid += double(x);
+        *lds_at(hb | (uint32_t(c) << 8)) = u[j];  // a miss: overwritten
         c += (rel < wb) && !inm;
       }
     }
@@ -407,7 +444,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
   double lsum = 0.0;
   // the smallest network that holds every lane's list
   if (__any(stored > 32))
-    list_select<kList, SUM>(H, stored, rr1, pb, lo, hi, va, vb, lsum);
+    list_select<64, SUM>(H, stored, rr1, pb, lo, hi, va, vb, lsum);
   else if (__any(stored > 16))
     list_select<32, SUM>(H, stored, rr1, pb, lo, hi, va, vb, lsum);
   else if (__any(stored > 8))

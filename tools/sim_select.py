@@ -72,7 +72,7 @@ def select(col, n, kk, median):
         l1 = s1[0] != s1[1]
         l2 = not shared and s2[0] != s2[1]
         stored = (s1[3] if l1 else 0) + (s2[3] if l2 else 0)
-        if stored <= 64:
+        if stored <= 32:
             break
         pick2 = l2 and (not l1 or s2[3] > s1[3])
         s = s2 if pick2 else s1
