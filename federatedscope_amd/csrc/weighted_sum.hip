@@ -205,21 +205,31 @@ void launch_wsum_v(const float *const *rows, const float *w, const float *pre,
                      base, out);
 }
 
+// V of the streaming kernels for nvec float4 columns of n clients: the
+// largest V that leaves >= min_tiles one-tile workgroups.  1000 (two rounds
+// of the 2 × 256 resident workgroups) below 150 clients; with n >= 150 a
+// tile runs long enough that ~400 workgroups keep HBM busy and the wider V
+// wins: 200 × 6.6M, V = 16 (403 tiles) 0.79 ms against V = 4 (1612) 0.83 ms
+// and V = 24 (269) 1.06 ms (profiles/r02_tune_wsum_200x6p6M.txt).
+inline int wsum_width(int64_t nvec, int n) {
+  const int64_t min_tiles = n >= 150 ? 400 : 1000;
+  auto tiles = [&](int v) { return (nvec + 256 * v - 1) / (256 * v); };
+  for (int v : {24, 16, 8, 4})
+    if (tiles(v) >= min_tiles) return v;
+  return 1;
+}
+
 template <bool PRE, bool BASE>
 void launch_wsum(const float *const *rows, const float *w, const float *pre,
                  int n, int64_t nvec, const float *base, float *out,
                  hipStream_t s) {
-  auto tiles = [&](int v) { return (nvec + 256 * v - 1) / (256 * v); };
-  if (tiles(24) >= 1000)
-    launch_wsum_v<PRE, BASE, 24>(rows, w, pre, n, nvec, base, out, s);
-  else if (tiles(16) >= 1000)
-    launch_wsum_v<PRE, BASE, 16>(rows, w, pre, n, nvec, base, out, s);
-  else if (tiles(8) >= 1000)
-    launch_wsum_v<PRE, BASE, 8>(rows, w, pre, n, nvec, base, out, s);
-  else if (tiles(4) >= 1000)
-    launch_wsum_v<PRE, BASE, 4>(rows, w, pre, n, nvec, base, out, s);
-  else
-    launch_wsum_v<PRE, BASE, 1>(rows, w, pre, n, nvec, base, out, s);
+  switch (wsum_width(nvec, n)) {
+    case 24: launch_wsum_v<PRE, BASE, 24>(rows, w, pre, n, nvec, base, out, s); break;
+    case 16: launch_wsum_v<PRE, BASE, 16>(rows, w, pre, n, nvec, base, out, s); break;
+    case 8: launch_wsum_v<PRE, BASE, 8>(rows, w, pre, n, nvec, base, out, s); break;
+    case 4: launch_wsum_v<PRE, BASE, 4>(rows, w, pre, n, nvec, base, out, s); break;
+    default: launch_wsum_v<PRE, BASE, 1>(rows, w, pre, n, nvec, base, out, s);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -331,15 +341,8 @@ __global__ __launch_bounds__(kBlock) void wsum_rows_kernel(
 }
 
 // V of the flat launcher (launch_wsum) for a bucket of `numel` coordinates
-int wsum_vec_width(int64_t numel) {
-  const int64_t nvec = numel / 4;
-  auto tiles = [&](int v) { return (nvec + 256 * v - 1) / (256 * v); };
-  if (tiles(24) >= 1000) return 24;
-  if (tiles(16) >= 1000) return 16;
-  if (tiles(8) >= 1000) return 8;
-  if (tiles(4) >= 1000) return 4;
-  return 1;
-}
+// of n clients
+int wsum_vec_width(int64_t numel, int n) { return wsum_width(numel / 4, n); }
 
 template <int V, bool PRE, bool BASE>
 void launch_wsum_rows(const fsagg_rows &rs, const fsagg_chunk *chunks,
@@ -613,7 +616,11 @@ extern "C" int fsagg_weighted_sum_f32(const float *const *rows,
 }
 
 extern "C" int64_t fsagg_wsum_chunk_elems(int64_t numel) {
-  return int64_t(1024) * wsum_vec_width(numel < 0 ? 0 : numel);
+  return int64_t(1024) * wsum_vec_width(numel < 0 ? 0 : numel, 0);
+}
+
+extern "C" int64_t fsagg_wsum_chunk_elems_n(int64_t numel, int n) {
+  return int64_t(1024) * wsum_vec_width(numel < 0 ? 0 : numel, n);
 }
 
 extern "C" int fsagg_weighted_sum_rows_f32(const fsagg_rows *rows,

@@ -741,7 +741,7 @@ def weighted_sum_rows(rs, weights, out, prescale=None, base=None, lo=0,
                          'tensors')
     _rows_out(rs, out, ALIGN_BYTES)
     lib = L.load()
-    unit = lib.fsagg_wsum_chunk_elems(rs.layout.numel)
+    unit = lib.fsagg_wsum_chunk_elems_n(rs.layout.numel, rs.n)
     chunks, nchunk = rs.layout.row_chunks(unit, rs.device, lo, hi)
     if nchunk == 0:
         return out
