@@ -383,7 +383,8 @@ class DeviceEngine:
                     raise KeyError('client %d lacks key %r' %
                                    (i, layout.keys[s]))
                 return StagedSet(layout, ops.RowSet.from_pointers(
-                    layout, ptrs, self.compute_device, keepalive=(dicts, )))
+                    layout, ptrs, self.compute_device, keepalive=(dicts, ),
+                    missing=int(gone.sum())))
         # staged through a device stack
         layout = self._layout(d0, as_float=as_float)
         present = [[k in d for k in layout.keys] for d in dicts]

@@ -51,6 +51,9 @@ __global__ __launch_bounds__(kBlock) void orderstat_reg_kernel(
   const float *__restrict__ base = br.base;
   uint32_t k[N];
   bool nan = false, nonfinite = false;
+  // the init coordinate with the column, not after the sort (its latency
+  // would be exposed at the end of every wave)
+  const float bval = base ? gld_nt(base + p) : 0.0f;
   load_column<N>(br.rows, n, p, k, nan, nonfinite);
   bitonic_sort<N>(k);
   using Seq = std::make_integer_sequence<int, N>;
@@ -70,7 +73,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_reg_kernel(
     }
     r = __fdiv_rn(s, divisor);
   }
-  if (base) r = add_rn(gld(base + p), r);
+  if (base) r = add_rn(bval, r);
   out[p] = r;
 }
 

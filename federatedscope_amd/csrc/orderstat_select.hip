@@ -300,12 +300,16 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
   // row n - 1: harmless for the max, skipped by every counting pass.
   uint32_t u[N];
   uint32_t amax = 0u;
+  float bval = 0.0f;  // the init model's coordinate (init + update)
   {
     // coordinates < 2^30 (launch); dead lanes re-read the chunk's first
     const uint32_t off = uint32_t(live ? p : br.lo);
 #pragma unroll
     for (int j = 0; j < N; ++j)
       u[j] = __float_as_uint(ld_nt(row_at(rows, j < n ? j : n - 1), off));
+    // with the rows, not at the end: a load issued as the wave's last act
+    // exposes one full HBM round trip per wave (0.14 ms at C5)
+    if (base) bval = ld_nt(base, off);
 #pragma unroll
     for (int j = 0; j < N; ++j) amax = max(amax, u[j] & 0x7FFFFFFFu);
   }
@@ -474,7 +478,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
     }
     r = __fdiv_rn(s, divisor);
   }
-  if (base) r = add_rn(gld(base + p), r);
+  if (base) r = add_rn(bval, r);
   out[p] = r;
 }
 

@@ -15,31 +15,82 @@ from . import _lib as L
 ALIGN_BYTES = 16
 
 
+class _PinnedRing:
+    """Reusable pinned staging for the small host tables every call uploads
+    (row pointers, weights, chunk lists): NSLOT slots of SLOT bytes, used
+    round robin; a slot is refilled only after the copy that last read it
+    has run (its event).  torch's pin_memory() per table cost ~10-20 µs of
+    host time per upload in the drop-in path."""
+    SLOT = 1 << 16
+    NSLOT = 64
+
+    def __init__(self):
+        self.buf = None
+        self.events = [None] * self.NSLOT
+        self.i = 0
+
+    def upload(self, arr, device):
+        """numpy array -> device tensor of its dtype and shape (async)."""
+        import numpy as np
+        arr = np.ascontiguousarray(arr)
+        raw = arr.reshape(-1).view(np.uint8)
+        nb = raw.size
+        if nb == 0 or nb > self.SLOT:
+            host = torch.from_numpy(raw.copy())
+            return host.pin_memory().to(device, non_blocking=True).view(
+                _TORCH_OF[arr.dtype.str]).reshape(arr.shape)
+        if self.buf is None:
+            self.buf = torch.empty(self.SLOT * self.NSLOT, dtype=torch.uint8,
+                                   pin_memory=True)
+            self.np = self.buf.numpy()
+        k = self.i
+        self.i = (k + 1) % self.NSLOT
+        ev = self.events[k]
+        if ev is not None:
+            ev.synchronize()            # the copy that last read slot k
+        lo = k * self.SLOT
+        self.np[lo:lo + nb] = raw
+        dev = torch.empty(nb, dtype=torch.uint8, device=device)
+        dev.copy_(self.buf[lo:lo + nb], non_blocking=True)
+        if ev is None:
+            ev = self.events[k] = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        return dev.view(_TORCH_OF[arr.dtype.str]).reshape(arr.shape)
+
+
+_TORCH_OF = {'<i8': torch.int64, '<i4': torch.int32, '<i2': torch.int16,
+             '|i1': torch.int8, '<f4': torch.float32, '<f8': torch.float64,
+             '<f2': torch.float16, '|u1': torch.uint8, '|b1': torch.bool}
+_NP_OF = {}
+_RING = _PinnedRing()
+
+
 def _h2d(values, dtype, device):
     """A small host table (row pointers, weights, offsets) on ``device``:
     staged through pinned memory and copied asynchronously on the current
-    stream, so a call never blocks the host on the GPU's queue (torch's
-    host allocator keeps the pinned block until the copy has run)."""
-    host = torch.tensor(values, dtype=dtype)
+    stream, so a call never blocks the host on the GPU's queue."""
+    import numpy as np
     device = torch.device(device)
     if device.type != 'cuda':
-        return host.to(device)
-    return host.pin_memory().to(device, non_blocking=True)
+        return torch.tensor(values, dtype=dtype).to(device)
+    npt = _NP_OF.get(dtype)
+    if npt is None:
+        npt = _NP_OF[dtype] = torch.empty(0, dtype=dtype).numpy().dtype
+    return _RING.upload(np.asarray(values, dtype=npt), device)
 
 
 def _h2d_bytes(arr, device):
     """A numpy record array as a uint8 device tensor (pinned, async)."""
     import numpy as np
-    host = torch.from_numpy(
-        np.ascontiguousarray(arr).view(np.uint8).reshape(-1).copy())
-    return host.pin_memory().to(torch.device(device), non_blocking=True)
+    return _RING.upload(np.ascontiguousarray(arr).view(np.uint8).reshape(-1),
+                        torch.device(device))
 
 
 def _h2d_np(arr, device):
-    """A numpy array as a device tensor of its dtype (pinned, async)."""
+    """A numpy array as a flat device tensor of its dtype (pinned, async)."""
     import numpy as np
-    host = torch.from_numpy(np.ascontiguousarray(arr).reshape(-1).copy())
-    return host.pin_memory().to(torch.device(device), non_blocking=True)
+    return _RING.upload(np.ascontiguousarray(arr).reshape(-1),
+                        torch.device(device))
 
 
 def _stream(device):
@@ -627,7 +678,8 @@ class RowSet:
     coordinates).  0 = the client lacks the key.  ``table`` is the host
     copy ([n][1] for a stack without absent keys, else [n][nseg])."""
 
-    def __init__(self, layout, table, device, keepalive=(), aligned16=True):
+    def __init__(self, layout, table, device, keepalive=(), aligned16=True,
+                 missing=None):
         table = _np.ascontiguousarray(table, dtype=_np.int64)
         if table.ndim != 2 or table.shape[0] < 1:
             raise ValueError('row table must be [n][1] or [n][nseg]')
@@ -647,7 +699,8 @@ class RowSet:
                              (table.shape[1], self.nseg))
         self.device = _cuda_index(device)
         self.aligned16 = bool(aligned16)
-        self.missing = int(absent(layout, table).sum())
+        self.missing = int(absent(layout, table).sum()) if missing is None \
+            else int(missing)
         self.tab = _h2d_np(table.T, self.device)
         self.struct = L.Rows(self.tab.data_ptr(), self.ss, self.n,
                              self.nseg)
@@ -671,15 +724,18 @@ class RowSet:
 
     @classmethod
     def from_pointers(cls, layout, ptrs, device, keepalive=(),
-                      aligned16=True):
+                      aligned16=True, missing=None):
         """[n][nseg] real data pointers of the clients' key tensors (0:
-        absent), in layout key order."""
+        absent), in layout key order (``missing``: the count of absent
+        non-empty keys, when the caller has it)."""
         ptrs = _np.asarray(ptrs, dtype=_np.int64)
-        offs = _np.array([layout.offsets[k] for k in layout.keys],
-                         dtype=_np.int64)
-        virt = _np.where(ptrs != 0, ptrs - 4 * offs[None, :], 0)
+        offs = layout.__dict__.get('_offs4')
+        if offs is None:
+            offs = layout.__dict__['_offs4'] = 4 * _np.array(
+                [layout.offsets[k] for k in layout.keys], dtype=_np.int64)
+        virt = _np.where(ptrs != 0, ptrs - offs[None, :], 0)
         return cls(layout, virt, device, keepalive=keepalive,
-                   aligned16=aligned16)
+                   aligned16=aligned16, missing=missing)
 
     def subset(self, sel):
         """The clients ``sel`` (indices, in the new reduction order)."""
