@@ -73,7 +73,7 @@ struct PairPlan {
   int64_t max_chunks;
 };
 
-PairPlan make_plan(int n, int64_t numel, int nseg) {
+PairPlan make_plan(int n, int64_t numel, int nseg, bool dbuf = false) {
   PairPlan pl;
   const int nt8 = (n + 7) / 8, nt10 = (n + 9) / 10;
   pl.ts = int64_t(nt10) * (nt10 + 1) / 2 * 100 < int64_t(nt8) * (nt8 + 1) / 2 * 64
@@ -92,7 +92,8 @@ PairPlan make_plan(int n, int64_t numel, int nseg) {
   // most what the LDS holds and, when the stage can be register-prefetched
   // (stage_items(ts) float4 quads per thread), what the registers hold.
   const int unit = std::lcm(4, pl.ks);
-  const int lds_cap = kLdsFloats / pl.ldsp;
+  // double-buffered stages (dbuf): two stage buffers share the LDS
+  const int lds_cap = kLdsFloats / (dbuf ? 2 : 1) / pl.ldsp;
   const int quads = (pl.nt * pl.ts + 3) / 4;
   const int reg_cap = stage_items(pl.ts) * kBlock / quads * 4;
   const int limit = reg_cap >= unit && reg_cap < lds_cap ? reg_cap : lds_cap;
@@ -162,7 +163,7 @@ __device__ __forceinline__ void read_tile(const float *col, int t,
 
 // PK: the row-pair packed form (v_pk_add_f32 / v_pk_fma_f32, two pairs per
 // instruction); else scalar v_sub_f32 / v_fma_f32 on the same accumulators
-template <int TS, bool PK>
+template <int TS, bool PK, bool DB>
 __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n,
     PairPlan pl, const int64_t *__restrict__ seg_lo,
@@ -245,13 +246,13 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
       }
     }
   };
-  auto stage_from_regs = [&]() {
+  auto stage_from_regs = [&](float *buf) {
 #pragma unroll
     for (int k = 0; k < kStageItems; ++k) {
       const int it = tid + k * kBlock;
       if (it < items) {
         const int qd = it / groups, g = it - qd * groups;
-        float *dst = lds + (4 * g) * pl.ldsp + qd * 4;
+        float *dst = buf + (4 * g) * pl.ldsp + qd * 4;
         *reinterpret_cast<float4 *>(dst) =
             make_float4(pre[k][0].x, pre[k][1].x, pre[k][2].x, pre[k][3].x);
         *reinterpret_cast<float4 *>(dst + pl.ldsp) =
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     }
   };
   // partial or unaligned stage: guarded 4-B loads straight to LDS
-  auto stage_scalar = [&](int64_t cs, int len) {
+  auto stage_scalar = [&](float *buf, int64_t cs, int len) {
     const int wave = tid / kWave, lane = tid & (kWave - 1);
     for (int qd = wave; qd < quads; qd += kBlock / kWave) {
       const int r0 = qd * 4;
@@ -273,7 +274,7 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
       const float *p2 = rows[min(r0 + 2, n - 1)] + cs;
       const float *p3 = rows[min(r0 + 3, n - 1)] + cs;
       for (int cc = lane; cc < len; cc += kWave)
-        *reinterpret_cast<float4 *>(lds + cc * pl.ldsp + r0) =
+        *reinterpret_cast<float4 *>(buf + cc * pl.ldsp + r0) =
             make_float4(gld(p0 + cc), gld(p1 + cc), gld(p2 + cc), gld(p3 + cc));
     }
   };
@@ -284,48 +285,80 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     for (int r = tid; r < n; r += kBlock) rowp[r] = rows[r];
     __syncthreads();
   }
-  if (prefetch && end - start >= pl.sub) fetch(start);
-  for (int64_t cs = start; cs < end; cs += pl.sub) {
-    const int len = int(end - cs < pl.sub ? end - cs : pl.sub);
-    const bool full = prefetch && len == pl.sub;
-    if (full) stage_from_regs();
-    else stage_scalar(cs, len);
-    __syncthreads();
-    // next full stage's loads fly while this one is computed
-    if (prefetch && end - (cs + pl.sub) >= pl.sub) fetch(cs + pl.sub);
-    if (active) {
+  // one stage's distance updates from the staged rows in buf
+  auto compute = [&](const float *buf, int len) {
+    if (!active) return;
 #pragma unroll kUnroll
-      for (int cc = ksl; cc < len; cc += pl.ks) {
-        const float *col = lds + cc * pl.ldsp;
-        float b[TS];
-        read_tile<TS>(col, tj, b);
-        if constexpr (PK) {
-          const f2 *ap = reinterpret_cast<const f2 *>(col + ti * TS);
-          f2 a[TS / 2];
+    for (int cc = ksl; cc < len; cc += pl.ks) {
+      const float *col = buf + cc * pl.ldsp;
+      float b[TS];
+      read_tile<TS>(col, tj, b);
+      if constexpr (PK) {
+        const f2 *ap = reinterpret_cast<const f2 *>(col + ti * TS);
+        f2 a[TS / 2];
 #pragma unroll
-          for (int h = 0; h < TS / 2; ++h) a[h] = ap[h];
+        for (int h = 0; h < TS / 2; ++h) a[h] = ap[h];
 #pragma unroll
-          for (int v = 0; v < TS; ++v)
+        for (int v = 0; v < TS; ++v)
 #pragma unroll
-            for (int h = 0; h < TS / 2; ++h) {
-              const f2 d = a[h] - f2{b[v], b[v]};
-              acc[h][v] = __builtin_elementwise_fma(d, d, acc[h][v]);
-            }
-        } else {
-          float a[TS];
-          read_tile<TS>(col, ti, a);
+          for (int h = 0; h < TS / 2; ++h) {
+            const f2 d = a[h] - f2{b[v], b[v]};
+            acc[h][v] = __builtin_elementwise_fma(d, d, acc[h][v]);
+          }
+      } else {
+        float a[TS];
+        read_tile<TS>(col, ti, a);
 #pragma unroll
-          for (int u = 0; u < TS; ++u)
+        for (int u = 0; u < TS; ++u)
 #pragma unroll
-            for (int v = 0; v < TS; ++v) {
-              const float d = a[u] - b[v];
-              acc[u >> 1][v][u & 1] =
-                  __builtin_fmaf(d, d, acc[u >> 1][v][u & 1]);
-            }
-        }
+          for (int v = 0; v < TS; ++v) {
+            const float d = a[u] - b[v];
+            acc[u >> 1][v][u & 1] =
+                __builtin_fmaf(d, d, acc[u >> 1][v][u & 1]);
+          }
       }
     }
+  };
+  auto stage_len = [&](int64_t cs) {
+    return int(end - cs < pl.sub ? end - cs : pl.sub);
+  };
+
+  if (prefetch && end - start >= pl.sub) fetch(start);
+  if constexpr (!DB) {
+    for (int64_t cs = start; cs < end; cs += pl.sub) {
+      const int len = stage_len(cs);
+      if (prefetch && len == pl.sub) stage_from_regs(lds);
+      else stage_scalar(lds, cs, len);
+      __syncthreads();
+      // next full stage's loads fly while this one is computed
+      if (prefetch && end - (cs + pl.sub) >= pl.sub) fetch(cs + pl.sub);
+      compute(lds, len);
+      __syncthreads();
+    }
+  } else {
+    // two stage buffers, one barrier per stage: stage s + 1 is written into
+    // the buffer stage s - 1 was read from (every wave has passed the
+    // barrier after it) while stage s is computed from the other
+    auto buf_of = [&](int b) { return b ? lds + kLdsFloats / 2 : lds; };
+    if (start < end) {
+      const int len = stage_len(start);
+      if (prefetch && len == pl.sub) stage_from_regs(lds);
+      else stage_scalar(lds, start, len);
+    }
     __syncthreads();
+    if (prefetch && end - (start + pl.sub) >= pl.sub) fetch(start + pl.sub);
+    int st = 0;
+    for (int64_t cs = start; cs < end; cs += pl.sub, st ^= 1) {
+      const int64_t ncs = cs + pl.sub;
+      if (ncs < end) {
+        const int nlen = stage_len(ncs);
+        if (prefetch && nlen == pl.sub) stage_from_regs(buf_of(st ^ 1));
+        else stage_scalar(buf_of(st ^ 1), ncs, nlen);
+        if (prefetch && end - (ncs + pl.sub) >= pl.sub) fetch(ncs + pl.sub);
+      }
+      compute(buf_of(st), stage_len(cs));
+      __syncthreads();
+    }
   }
 
   // sum the k-slices of each tile pair in slice order, ≤ 64 accumulators
@@ -878,6 +911,19 @@ static bool packed_form() {
 
 // FSAGG_PAIRDIST=ring selects the LDS-DMA ring kernel (A/B runs; the
 // register-staged kernel measured faster at C4)
+// The double-buffered stage loop (one barrier per stage, half-size stages)
+// is the default: 0.556 against 0.567–0.571 ms for the single-buffered loop
+// (two barriers per stage) at C4 in interleaved A/B; FSAGG_PAIRDIST=flat
+// selects the latter.
+static bool dbuf_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char *e = getenv("FSAGG_PAIRDIST");
+    on = !(e && (strcmp(e, "flat") == 0 || strcmp(e, "ring") == 0));
+  }
+  return on == 1;
+}
+
 static bool ring_enabled() {
   static int on = -1;
   if (on < 0) {
@@ -893,7 +939,8 @@ static int pairdist_segsq_impl(const float *const *tab, int64_t ss, int n,
                                const int64_t *seg_lo, const int64_t *seg_end,
                                int nseg, double *segsq, void *workspace,
                                hipStream_t s) {
-  const PairPlan pl = make_plan(n, numel, nseg);
+  const bool db = dbuf_enabled();
+  const PairPlan pl = make_plan(n, numel, nseg, db);
   int *prefix = static_cast<int *>(workspace);
   float *partial = reinterpret_cast<float *>(
       static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)));
@@ -937,8 +984,16 @@ static int pairdist_segsq_impl(const float *const *tab, int64_t ss, int n,
   if (numel > 0) {
     const dim3 grid(unsigned(pl.max_chunks), unsigned(pl.groups));
 #define FSAGG_FLAT(TS, PK)                                                    \
-  hipLaunchKernelGGL((pairdist_chunk_kernel<TS, PK>), grid, dim3(kBlock), 0, \
-                     s, tab, ss, n, pl, seg_lo, seg_end, nseg, prefix, partial)
+  do {                                                                        \
+    if (db)                                                                   \
+      hipLaunchKernelGGL((pairdist_chunk_kernel<TS, PK, true>), grid,         \
+                         dim3(kBlock), 0, s, tab, ss, n, pl, seg_lo, seg_end, \
+                         nseg, prefix, partial);                              \
+    else                                                                      \
+      hipLaunchKernelGGL((pairdist_chunk_kernel<TS, PK, false>), grid,        \
+                         dim3(kBlock), 0, s, tab, ss, n, pl, seg_lo, seg_end, \
+                         nseg, prefix, partial);                              \
+  } while (0)
     const bool pk = packed_form();
     if (pl.ts == 10) {
       if (pk) FSAGG_FLAT(10, true); else FSAGG_FLAT(10, false);

@@ -43,7 +43,15 @@ def log(*a):
     print('[robust]', *a, file=sys.stderr, flush=True)
 
 
-def timed(fn, reps=5):
+def timed(fn, reps=15, warm_s=0.05):
+    # untimed calls for warm_s seconds first: the GPU clocks ramp up from
+    # idle over the first milliseconds of load (the first timed calls of a
+    # cold process read up to 15 % slow)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < warm_s:
+        fn()
+        torch.cuda.synchronize()
     ts = []
     for _ in range(reps + 1):
         e0 = torch.cuda.Event(enable_timing=True)
@@ -230,9 +238,13 @@ def dropin_rules(dev):
     for name, n, agg in rules:
         fb = c50 if n == 50 else c200
         info = {'client_feedback': fb, 'recover_fun': None}
-        agg.aggregate(info)
+        torch.cuda.synchronize()
+        w0 = time.perf_counter()
+        while time.perf_counter() - w0 < 0.05:   # clocks up (see timed)
+            agg.aggregate(info)
+            torch.cuda.synchronize()
         ts = []
-        for _ in range(10):
+        for _ in range(20):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             agg.aggregate(info)
