@@ -121,8 +121,8 @@ __device__ __forceinline__ void hist_clear(uint32_t *H, int words) {
 
 // The lane's LDS words by byte address: word w at hb | (w << 8) ([word][lane]
 // layout: a wave's 64 lanes hit 64 distinct banks).  hb = wave·16 KiB +
-// lane·4 has bits 8..13 clear (the kernel's only LDS array starts at 0,
-// checked at entry), so a word address is one v_and_or / v_lshl_or.
+// lane·4 has bits 8..13 clear (the LDS array is 16 KiB-aligned), so a word
+// address is one v_and_or / v_lshl_or.
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 __device__ __forceinline__ lds_u32 *lds_at(uint32_t byte) {
   return (lds_u32 *)(uintptr_t)byte;
@@ -285,11 +285,11 @@ __device__ __forceinline__ void list_select(const uint32_t *H, int cnt,
 template <int N, int MODE>
 __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
     RowSrc rs, int n, int kk, float divisor, float *__restrict__ out) {
-  __shared__ uint32_t lds[kSelLds];
+  // 16 KiB-aligned: a lane's word addresses are hb | (w << 8)
+  __shared__ __attribute__((aligned(16384))) uint32_t lds[kSelLds];
   uint32_t *H = lds + (threadIdx.x / kWave) * kSelWords * kWave +
                 (threadIdx.x & (kWave - 1));
   const uint32_t hb = uint32_t(uintptr_t((lds_u32 *)H));
-  if (uint32_t(uintptr_t((lds_u32 *)lds)) & 0x3FFFu) __builtin_trap();
   const BlockRows br = block_rows(rs, blockIdx.x);
   const float *const *__restrict__ rows = br.rows;
   const float *__restrict__ base = br.base;
