@@ -60,11 +60,18 @@ struct RankSel {
   int below, cnt;
 };
 
-// a < b as the borrow of a - b (v_sub_co_u32 + v_addc_co_u32 when added to
-// a counter, instead of v_cmp + v_cndmask + v_add)
-__device__ __forceinline__ uint32_t below(uint32_t a, uint32_t b) {
-  uint32_t d;
-  return __builtin_sub_overflow(a, b, &d) ? 1u : 0u;
+// c + (a < b): the borrow of a − b carried straight into the counter
+// (v_sub_co_u32 + v_addc_co_u32, a VCC carry chain with no wait states).
+// The compiler's own form is v_cmp + s_nop 1 + v_cndmask_b32_e64 + v_add —
+// the wait states guard the e64 cndmask's read of VCC — one per value.
+__device__ __forceinline__ int add_below(int c, uint32_t a, uint32_t b) {
+  uint32_t t;
+  asm("v_sub_co_u32 %1, vcc, %2, %3\n\t"
+      "v_addc_co_u32 %0, vcc, 0, %0, vcc"
+      : "+v"(c), "=&v"(t)
+      : "v"(a), "v"(b)
+      : "vcc");
+  return c;
 }
 
 // Opaque copy barrier: keeps the compiler from hoisting per-pass key math
@@ -392,14 +399,14 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
         for (int j = 0; j < N; ++j) {
           if (j >= N - kSelStep && j >= n) continue;
           *lds_at(hb | (uint32_t(c) << 8)) = u[j];  // a miss: overwritten
-          c += below(u[j] - ulo, w);
+          c = add_below(c, u[j] - ulo, w);
         }
       } else {
 #pragma unroll
         for (int j = 0; j < N; ++j) {
           if (j >= N - kSelStep && j >= n) continue;
           *lds_at(hb | (uint32_t(c) << 8)) = u[j];  // a miss: overwritten
-          c += below(ukey(u[j]) - lo, w);
+          c = add_below(c, ukey(u[j]) - lo, w);
         }
       }
     } else {

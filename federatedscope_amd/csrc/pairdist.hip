@@ -299,12 +299,16 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
 #pragma unroll
         for (int h = 0; h < TS / 2; ++h) a[h] = ap[h];
 #pragma unroll
-        for (int v = 0; v < TS; ++v)
+        for (int v = 0; v < TS; ++v) {
+          // all TS/2 differences first, then the fmas: a packed fma that
+          // reads the packed add just before it needs a wait state (s_nop)
+          f2 d[TS / 2];
 #pragma unroll
-          for (int h = 0; h < TS / 2; ++h) {
-            const f2 d = a[h] - f2{b[v], b[v]};
-            acc[h][v] = __builtin_elementwise_fma(d, d, acc[h][v]);
-          }
+          for (int h = 0; h < TS / 2; ++h) d[h] = a[h] - f2{b[v], b[v]};
+#pragma unroll
+          for (int h = 0; h < TS / 2; ++h)
+            acc[h][v] = __builtin_elementwise_fma(d[h], d[h], acc[h][v]);
+        }
       } else {
         float a[TS];
         read_tile<TS>(col, ti, a);
