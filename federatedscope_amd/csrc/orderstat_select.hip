@@ -261,6 +261,25 @@ __device__ __forceinline__ void refine_apply(RankSel &s, const Refine &f,
   s.lo = f.lo + rlo;
 }
 
+// a[idx] for a per-lane idx without dynamic register indexing: a binary
+// select tree, one lane mask per bit of idx (S − 1 v_cndmask and log2 S
+// compares, where comparing idx with every position costs S of each plus a
+// wait state per position)
+template <int S>
+__device__ __forceinline__ uint32_t tree_pick(const uint32_t (&a)[S],
+                                              int idx) {
+  uint32_t t[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) t[i] = a[i];
+#pragma unroll
+  for (int w = S / 2, b = 0; w >= 1; w /= 2, ++b) {
+    const bool up = (idx >> b) & 1;
+#pragma unroll
+    for (int k = 0; k < w; ++k) t[k] = up ? t[2 * k + 1] : t[2 * k];
+  }
+  return t[0];
+}
+
 // Sort the lane's list of `cnt` values (float bits) at LDS slots [0, cnt) by
 // key and read list positions pa and pb off it (as keys); Σ over positions
 // [lo, hi] in fp64.
@@ -276,16 +295,23 @@ __device__ __forceinline__ void list_select(const uint32_t *H, int cnt,
     a[i] = i < cnt ? x : kPad;
   }
   bitonic_sort<S>(a);
-  uint32_t xa = 0, xb = 0;
   double acc = 0.0;
+  if (SUM) {
+    // [lo, hi] as one unsigned range test; an empty range (hi < lo) moves
+    // lo far above every position so that no i passes
+    const bool empty = hi < lo;
+    const int lo1 = empty ? (1 << 30) : lo;
+    const uint32_t span = empty ? 0u : uint32_t(hi - lo);
 #pragma unroll
-  for (int i = 0; i < S; ++i) {
-    xa = i == pa ? a[i] : xa;
-    xb = i == pb ? a[i] : xb;
-    if (SUM) acc += (i >= lo && i <= hi) ? double(key2f(a[i])) : 0.0;
+    for (int i = 0; i < S; ++i) {
+      // select in fp32, then widen (one v_cndmask, not a 64-bit pair)
+      float x = uint32_t(i - lo1) <= span ? key2f(a[i]) : 0.0f;
+      asm("" : "+v"(x));
+      acc += double(x);
+    }
   }
-  va = xa;
-  vb = xb;
+  va = tree_pick<S>(a, pa);
+  vb = tree_pick<S>(a, pb);
   sum = acc;
 }
 
