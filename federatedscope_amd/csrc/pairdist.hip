@@ -29,6 +29,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
+#include <type_traits>
 
 #include "common.h"
 
@@ -48,6 +49,11 @@ constexpr int kLdsFloats = kBlock * kRedPitch;  // 16640 floats = 65 KiB
 constexpr int stage_items(int ts) { return ts == 10 ? 3 : 4; }
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef float f2 __attribute__((ext_vector_type(2)));
+
+// 8×8 tiles have the registers to unroll two coordinates (the LDS latency
+// of one hides behind the FMAs of the other); 10×10 do not
+template <int TS>
+constexpr int kCoordUnroll = TS == 8 ? 2 : 1;
 
 // accumulator of pair (u, v) in the row-pair packed form acc[u/2][v]
 template <int TS>
@@ -71,7 +77,36 @@ struct PairPlan {
   int sub;      // coordinates per stage
   int64_t chl;  // coordinates per chunk
   int64_t max_chunks;
+  // split-role form (split = 1): the first `wo` waves own the ro
+  // off-diagonal tile pairs (kso k-slices each), the other waves the rd
+  // diagonal roles — tiles 2d and 2d+1, the two upper triangles packed into
+  // one TS×TS accumulator set (kso/ksd k-slices); no slot is spent on a
+  // diagonal tile's lower half
+  int split, wo, ro, kso, rd, ksd;
+  int mode;  // experiments only (FSAGG_PAIR_MODE): 1 = no distance updates
 };
+
+// FSAGG_PAIRDIST=nosplit keeps the whole-tile form (A/B runs); the split
+// form is packed only (FSAGG_PAIR_FORM=scalar turns it off too)
+static bool split_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char *e = getenv("FSAGG_PAIRDIST");
+    const char *f = getenv("FSAGG_PAIR_FORM");
+    on = !(e && strcmp(e, "nosplit") == 0) && !(f && strcmp(f, "scalar") == 0);
+  }
+  return on == 1;
+}
+
+// The LDS pitch of a staged coordinate row: ≥ the client slots, ≡ 4 (mod
+// 8) words — with the blocked item order of stage_item() (8 lanes = 2
+// coordinate groups × 4 client quads) every ds_write_b128 lane group then
+// hits 8 distinct 4-bank sets
+inline int stage_pitch(int quads) {
+  int p = quads * 4;
+  while (p % 8 != 4) p += 4;
+  return p;
+}
 
 PairPlan make_plan(int n, int64_t numel, int nseg, bool dbuf = false) {
   PairPlan pl;
@@ -83,6 +118,12 @@ PairPlan make_plan(int n, int64_t numel, int nseg, bool dbuf = false) {
   pl.groups = (pl.ntp + kBlock - 1) / kBlock;
   pl.tpg = (pl.ntp + pl.groups - 1) / pl.groups;
   pl.ks = kBlock / pl.tpg;
+  pl.split = 0;
+  pl.wo = pl.ro = pl.kso = pl.rd = pl.ksd = 0;
+  {
+    const char *e = getenv("FSAGG_PAIR_MODE");
+    pl.mode = e ? atoi(e) : 0;
+  }
   // pitch ≡ 28 (mod 32) words: conflict-free b128 staging writes and reads
   pl.ldsp = (pl.nt * pl.ts + 3) / 4 * 4 + 4;
   while (pl.ldsp % 32 != 28) pl.ldsp += 4;
@@ -93,15 +134,50 @@ PairPlan make_plan(int n, int64_t numel, int nseg, bool dbuf = false) {
   // (stage_items(ts) float4 quads per thread), what the registers hold.
   const int unit = std::lcm(4, pl.ks);
   // double-buffered stages (dbuf): two stage buffers share the LDS
-  const int lds_cap = kLdsFloats / (dbuf ? 2 : 1) / pl.ldsp;
+  // (one row of each buffer region stays free for the kernel's zero row)
+  const int lds_cap = kLdsFloats / (dbuf ? 2 : 1) / pl.ldsp - 1;
   const int quads = (pl.nt * pl.ts + 3) / 4;
   const int reg_cap = stage_items(pl.ts) * kBlock / quads * 4;
   const int limit = reg_cap >= unit && reg_cap < lds_cap ? reg_cap : lds_cap;
   pl.sub = limit / unit * unit;
   if (pl.sub < unit) pl.sub = limit >= 4 ? limit / 4 * 4 : limit;  // huge n
+  // Split-role form, when it covers more coordinates per unit of lane time:
+  // a stage costs max(⌈sub/kso⌉, ⌈sub/ksd⌉) coordinate steps of TS² packed
+  // ops against ⌈sub/ks⌉ for the whole-tile form (at n = 50: 152 / 8 = 19
+  // coordinates per step against 136 / 8 = 17)
+  if (dbuf && split_enabled() && pl.groups == 1 && pl.nt >= 2) {
+    const int ro = pl.nt * (pl.nt - 1) / 2, rd = (pl.nt + 1) / 2;
+    const int ldsp = stage_pitch(quads);
+    const int lcap = kLdsFloats / 2 / ldsp - 1;
+    double best = double(pl.sub) / ((pl.sub + pl.ks - 1) / pl.ks) * 1.03;
+    for (int wo = 1; wo < kBlock / kWave; ++wo) {
+      const int kso = kWave * wo / ro, ksd = kWave * (kBlock / kWave - wo) / rd;
+      if (kso < 1 || ksd < 1) continue;
+      const int u = std::lcm(8, kso);  // whole float4 rows, even groups
+      const int rcap = 2 * kBlock / quads * 4;  // two items per thread
+      const int lim = rcap < lcap ? rcap : lcap;
+      const int sub = lim / u * u;
+      if (sub < u) continue;
+      const int steps = std::max((sub + kso - 1) / kso, (sub + ksd - 1) / ksd);
+      const double eff = double(sub) / steps;
+      if (eff > best) {
+        best = eff;
+        pl.split = 1;
+        pl.wo = wo;
+        pl.ro = ro;
+        pl.kso = kso;
+        pl.rd = rd;
+        pl.ksd = ksd;
+        pl.ldsp = ldsp;
+        pl.sub = sub;
+      }
+    }
+  }
   // ≈ 1000 chunks (two rounds of the 2 × 256 resident workgroups), whole
   // stages (16-B aligned whenever the chunk start is)
-  const int64_t target = 1024 - nseg > 256 ? 1024 - nseg : 256;
+  int64_t rounds = 1024;
+  if (const char *e = getenv("FSAGG_PAIR_CHUNKS")) rounds = atoi(e);
+  const int64_t target = rounds - nseg > 256 ? rounds - nseg : 256;
   int64_t chl = (numel + target - 1) / target;
   if (chl < 2048) chl = 2048;
   pl.chl = (chl + pl.sub - 1) / pl.sub * pl.sub;
@@ -136,6 +212,46 @@ __device__ __forceinline__ void tp_to_tiles(int tp, int nt, int &ti, int &tj) {
   tj = r + (tp - base);
 }
 
+// off-diagonal tile pair r (ti < tj, row-major) → tiles
+__device__ __forceinline__ void od_to_tiles(int r, int nt, int &ti, int &tj) {
+  int t = 0, base = 0;
+  while (r >= base + (nt - 1 - t)) {
+    base += nt - 1 - t;
+    ++t;
+  }
+  ti = t;
+  tj = t + 1 + (r - base);
+}
+
+// tiles (ti <= tj) → tile-pair index of tp_to_tiles
+__device__ __forceinline__ int tiles_to_tp(int ti, int tj, int nt) {
+  return ti * nt - ti * (ti - 1) / 2 + (tj - ti);
+}
+
+// Stage item `it` → (client quad qd, coordinate group g).  Blocks of 8
+// items = 4 consecutive quads × 2 consecutive groups, so the 8 lanes of a
+// ds_write_b128 group land on 8 distinct 4-bank sets (pitch ≡ 4 mod 8) and
+// each 16-B row load of a wave still covers 16 consecutive groups of 4 rows;
+// the quads past the last whole block of 4 (or every quad, for an odd
+// group count) in plain order.
+__device__ __forceinline__ void stage_item(int it, int quads, int groups,
+                                           int &qd, int &g) {
+  const int q4 = (groups & 1) ? 0 : quads / 4;
+  const int blocked = q4 * 4 * groups;
+  if (it < blocked) {
+    const int half = groups >> 1;
+    const int b = it >> 3, w = it & 7;
+    const int qb = b / half;
+    qd = 4 * qb + (w & 3);
+    g = 2 * (b - qb * half) + (w >> 2);
+  } else {
+    const int r = it - blocked;
+    const int q = r / groups;
+    qd = 4 * q4 + q;
+    g = r - q * groups;
+  }
+}
+
 // TS values of tile t at one staged coordinate row
 template <int TS>
 __device__ __forceinline__ void read_tile(const float *col, int t,
@@ -162,8 +278,9 @@ __device__ __forceinline__ void read_tile(const float *col, int t,
 }
 
 // PK: the row-pair packed form (v_pk_add_f32 / v_pk_fma_f32, two pairs per
-// instruction); else scalar v_sub_f32 / v_fma_f32 on the same accumulators
-template <int TS, bool PK, bool DB>
+// instruction); else scalar v_sub_f32 / v_fma_f32 on the same accumulators.
+// SPLIT (with PK and DB): the split-role form of PairPlan.
+template <int TS, bool PK, bool DB, bool SPLIT>
 __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n,
     PairPlan pl, const int64_t *__restrict__ seg_lo,
@@ -192,13 +309,37 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   // client r's row of this key segment: rows[r] (a virtual base)
   const float *const *__restrict__ rows = tab + int64_t(s) * ss;
 
+  static_assert(!SPLIT || (PK && DB), "split form: packed, double-buffered");
   const int tid = threadIdx.x;
-  const int tpl = tid % pl.tpg;
-  const int ksl = tid / pl.tpg;
-  const int tp = blockIdx.y * pl.tpg + tpl;
-  const bool active = ksl < pl.ks && tpl < pl.tpg && tp < pl.ntp;
+  int tpl = 0, ksl, kstep;
+  bool active, diag = false;
   int ti = 0, tj = 0;
-  if (active) tp_to_tiles(tp, pl.nt, ti, tj);
+  if constexpr (SPLIT) {
+    // wave-uniform role: off-diagonal tile pairs, or diagonal tile pairs
+    // (2d, 2d+1) whose two upper triangles share one accumulator set
+    const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+    diag = wave >= pl.wo;
+    if (!diag) {
+      ksl = tid / pl.ro;
+      kstep = pl.kso;
+      active = ksl < pl.kso;
+      od_to_tiles(tid - ksl * pl.ro, pl.nt, ti, tj);
+    } else {
+      const int l = tid - kWave * pl.wo;
+      ksl = l / pl.rd;
+      kstep = pl.ksd;
+      active = ksl < pl.ksd;
+      ti = 2 * (l - ksl * pl.rd);
+      tj = ti + 1 < pl.nt ? ti + 1 : ti;  // odd tile count: a repeat, unused
+    }
+  } else {
+    tpl = tid % pl.tpg;
+    ksl = tid / pl.tpg;
+    kstep = pl.ks;
+    const int tp = blockIdx.y * pl.tpg + tpl;
+    active = ksl < pl.ks && tpl < pl.tpg && tp < pl.ntp;
+    if (active) tp_to_tiles(tp, pl.nt, ti, tj);
+  }
 
   // client slots (rows >= n repeat row n-1), rounded to whole quads
   const int quads = (pl.nt * TS + 3) / 4;
@@ -222,20 +363,31 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
 #pragma unroll
     for (int v = 0; v < TS; ++v) acc[h][v] = f2{0.0f, 0.0f};
 
-  constexpr int kStageItems = stage_items(TS);
-  // 8×8 tiles have the registers to unroll two coordinates (the LDS
-  // latency of one hides behind the FMAs of the other); 10×10 do not
-  constexpr int kUnroll = TS == 8 ? 2 : 1;
-  f4v pre[kStageItems][4];
+  // the split form keeps two stages in flight in registers (two sets of two
+  // items: 64 VGPRs), the whole-tile form one stage (stage_items(TS) items)
+  constexpr int kStageItems = SPLIT ? 2 : stage_items(TS);
+  f4v pre[kStageItems][4], pre1[kStageItems][4];
   // global (not flat) loads: a flat load also counts in lgkmcnt, so the
   // compute loop's first LDS-read wait would wait for the whole prefetch
   typedef __attribute__((address_space(1))) const f4v gf4v;
-  auto fetch = [&](int64_t cs) {
+  // this thread's stage items, placed once (qd < 0: none)
+  // (the split form's loads are issued by every lane, a lane without item k
+  // re-reading the last item: no branch around a load, so the compiler's
+  // vmcnt bookkeeping stays exact and a stage waits only for its own set)
+  int item_qd[kStageItems], item_g[kStageItems];
+  bool item_ok[kStageItems];
+#pragma unroll
+  for (int k = 0; k < kStageItems; ++k) {
+    const int it = tid + k * kBlock;
+    item_ok[k] = it < items;
+    stage_item(it < items ? it : items - 1, quads, groups, item_qd[k],
+               item_g[k]);
+  }
+  auto fetch = [&](int64_t cs, f4v (&pre)[kStageItems][4]) {
 #pragma unroll
     for (int k = 0; k < kStageItems; ++k) {
-      const int it = tid + k * kBlock;
-      if (it < items) {
-        const int qd = it / groups, g = it - qd * groups;
+      if (SPLIT || item_ok[k]) {
+        const int qd = item_qd[k], g = item_g[k];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = min(qd * 4 + e, n - 1);
@@ -246,12 +398,11 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
       }
     }
   };
-  auto stage_from_regs = [&](float *buf) {
+  auto stage_from_regs = [&](float *buf, const f4v (&pre)[kStageItems][4]) {
 #pragma unroll
     for (int k = 0; k < kStageItems; ++k) {
-      const int it = tid + k * kBlock;
-      if (it < items) {
-        const int qd = it / groups, g = it - qd * groups;
+      if (item_ok[k]) {
+        const int qd = item_qd[k], g = item_g[k];
         float *dst = buf + (4 * g) * pl.ldsp + qd * 4;
         *reinterpret_cast<float4 *>(dst) =
             make_float4(pre[k][0].x, pre[k][1].x, pre[k][2].x, pre[k][3].x);
@@ -281,16 +432,84 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
 
   const bool prefetch =
       vec && items <= kStageItems * kBlock && n <= kPtrSlots;
+  // a zero row past the last stage row of buffer 0 (the plan keeps it
+  // free): lanes past their last coordinate of a stage read it
+  float *const zrow = lds + (DB ? kLdsFloats / 2 : kLdsFloats) - pl.ldsp;
+  for (int i = tid; i < pl.ldsp; i += kBlock) zrow[i] = 0.0f;
   if (n <= kPtrSlots) {
     for (int r = tid; r < n; r += kBlock) rowp[r] = rows[r];
-    __syncthreads();
   }
+  __syncthreads();
   // one stage's distance updates from the staged rows in buf
-  auto compute = [&](const float *buf, int len) {
-    if (!active) return;
-#pragma unroll kUnroll
-    for (int cc = ksl; cc < len; cc += pl.ks) {
-      const float *col = buf + cc * pl.ldsp;
+  // role: std::true_type for the diagonal roles of the split form
+  // A wave-uniform trip count (len and kstep are): a lane past its last
+  // coordinate, or an idle lane, reads the zero row and adds (0 - 0)^2 — no
+  // divergent loop, so the accumulators stay in place across stages.
+  auto compute = [&](const float *buf, int len, auto role) {
+    if (pl.mode == 1) return;
+    const int steps = (len + kstep - 1) / kstep;
+    auto col_of = [&](int s) {
+      const int cc = ksl + s * kstep;
+      return active && cc < len ? buf + cc * pl.ldsp : zrow;
+    };
+    if constexpr (SPLIT) {
+      auto load = [&](int s, f2 (&A)[TS / 2], f2 (&B)[TS / 2]) {
+        const float *col = col_of(s);
+        const f2 *pa = reinterpret_cast<const f2 *>(col + ti * TS);
+        const f2 *pb = reinterpret_cast<const f2 *>(col + tj * TS);
+#pragma unroll
+        for (int h = 0; h < TS / 2; ++h) {
+          A[h] = pa[h];
+          B[h] = pb[h];
+        }
+      };
+      auto step = [&](const f2 (&A)[TS / 2], const f2 (&B)[TS / 2]) {
+        if constexpr (decltype(role)::value) {
+          // diagonal roles — tile A = ti: pair (u, v), u < v, in
+          // acc[u/2][v] (slots 2h < v); tile B = tj: its slot (h, v)
+          // mirrored to acc[TS/2-1-h][TS-1-v] (exactly the slots 2h >= v)
+#pragma unroll
+          for (int v = 1; v < TS; ++v) {
+            const float av = (v & 1) ? A[v >> 1].y : A[v >> 1].x;
+            const float bv = (v & 1) ? B[v >> 1].y : B[v >> 1].x;
+            f2 da[TS / 2], db[TS / 2];
+#pragma unroll
+            for (int h = 0; 2 * h < v; ++h) {
+              da[h] = A[h] - f2{av, av};
+              db[h] = B[h] - f2{bv, bv};
+            }
+#pragma unroll
+            for (int h = 0; 2 * h < v; ++h) {
+              acc[h][v] = __builtin_elementwise_fma(da[h], da[h], acc[h][v]);
+              f2 &m = acc[TS / 2 - 1 - h][TS - 1 - v];
+              m = __builtin_elementwise_fma(db[h], db[h], m);
+            }
+          }
+        } else {
+          // off-diagonal tile pair (ti, tj): every slot
+#pragma unroll
+          for (int v = 0; v < TS; ++v) {
+            const float bv = (v & 1) ? B[v >> 1].y : B[v >> 1].x;
+            f2 d[TS / 2];
+#pragma unroll
+            for (int h = 0; h < TS / 2; ++h) d[h] = A[h] - f2{bv, bv};
+#pragma unroll
+            for (int h = 0; h < TS / 2; ++h)
+              acc[h][v] = __builtin_elementwise_fma(d[h], d[h], acc[h][v]);
+          }
+        }
+      };
+      int s = 0;
+      do {  // len >= 1: at least one step
+        f2 A[TS / 2], B[TS / 2];
+        load(s, A, B);
+        step(A, B);
+      } while (++s < steps);
+      return;
+    }
+#pragma unroll kCoordUnroll<TS>
+    for (int s = 0; s < steps; ++s) {
+      const float *col = col_of(s);
       float b[TS];
       read_tile<TS>(col, tj, b);
       if constexpr (PK) {
@@ -327,16 +546,70 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     return int(end - cs < pl.sub ? end - cs : pl.sub);
   };
 
-  if (prefetch && end - start >= pl.sub) fetch(start);
+  // the stage loop, instantiated per role (a wave-uniform branch around
+  // whole loops: the accumulators merge once, after the chunk)
+  auto run = [&](auto role) {
+  if constexpr (SPLIT) {
+    // Two stages in flight: the rows of stage s + 2 are loaded into the
+    // register set stage s + 1 was just staged from, so each load has two
+    // stages of distance updates to land.  Unrolled by two: sets pre (even
+    // stages) and pre1 (odd) are fixed registers.  Every trip issues its
+    // loads (clamped to the chunk's last whole stage near its end).
+    float *const buf0 = lds, *const buf1 = lds + kLdsFloats / 2;
+    if (prefetch && end - start >= pl.sub) {
+      const int64_t last = start + ((end - pl.sub - start) & ~int64_t(3));
+      auto fetch_at = [&](int64_t cs, f4v (&p)[kStageItems][4]) {
+        fetch(cs < last ? cs : last, p);
+      };
+      auto put = [&](float *buf, int64_t cs,
+                     const f4v (&p)[kStageItems][4]) {
+        if (end - cs >= pl.sub) stage_from_regs(buf, p);
+        else stage_scalar(buf, cs, stage_len(cs));
+      };
+      fetch_at(start, pre);
+      fetch_at(start + pl.sub, pre1);
+      put(buf0, start, pre);
+      fetch_at(start + 2 * pl.sub, pre);
+      __syncthreads();
+      for (int64_t cs = start; cs < end;) {
+        int64_t ncs = cs + pl.sub;
+        if (ncs < end) put(buf1, ncs, pre1);
+        fetch_at(ncs + 2 * pl.sub, pre1);
+        compute(buf0, stage_len(cs), role);
+        __syncthreads();
+        cs = ncs;
+        if (cs >= end) break;
+        ncs = cs + pl.sub;
+        if (ncs < end) put(buf0, ncs, pre);
+        fetch_at(ncs + 2 * pl.sub, pre);
+        compute(buf1, stage_len(cs), role);
+        __syncthreads();
+        cs = ncs;
+      }
+    } else {
+      // unaligned rows or a chunk shorter than a stage: scalar staging
+      int st = 0;
+      if (start < end) stage_scalar(buf0, start, stage_len(start));
+      __syncthreads();
+      for (int64_t cs = start; cs < end; cs += pl.sub, st ^= 1) {
+        const int64_t ncs = cs + pl.sub;
+        if (ncs < end) stage_scalar(st ? buf0 : buf1, ncs, stage_len(ncs));
+        compute(st ? buf1 : buf0, stage_len(cs), role);
+        __syncthreads();
+      }
+    }
+    return;
+  }
+  if (prefetch && end - start >= pl.sub) fetch(start, pre);
   if constexpr (!DB) {
     for (int64_t cs = start; cs < end; cs += pl.sub) {
       const int len = stage_len(cs);
-      if (prefetch && len == pl.sub) stage_from_regs(lds);
+      if (prefetch && len == pl.sub) stage_from_regs(lds, pre);
       else stage_scalar(lds, cs, len);
       __syncthreads();
       // next full stage's loads fly while this one is computed
-      if (prefetch && end - (cs + pl.sub) >= pl.sub) fetch(cs + pl.sub);
-      compute(lds, len);
+      if (prefetch && end - (cs + pl.sub) >= pl.sub) fetch(cs + pl.sub, pre);
+      compute(lds, len, role);
       __syncthreads();
     }
   } else {
@@ -346,28 +619,81 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     auto buf_of = [&](int b) { return b ? lds + kLdsFloats / 2 : lds; };
     if (start < end) {
       const int len = stage_len(start);
-      if (prefetch && len == pl.sub) stage_from_regs(lds);
+      if (prefetch && len == pl.sub) stage_from_regs(lds, pre);
       else stage_scalar(lds, start, len);
     }
     __syncthreads();
-    if (prefetch && end - (start + pl.sub) >= pl.sub) fetch(start + pl.sub);
+    if (prefetch && end - (start + pl.sub) >= pl.sub) fetch(start + pl.sub, pre);
     int st = 0;
     for (int64_t cs = start; cs < end; cs += pl.sub, st ^= 1) {
       const int64_t ncs = cs + pl.sub;
       if (ncs < end) {
         const int nlen = stage_len(ncs);
-        if (prefetch && nlen == pl.sub) stage_from_regs(buf_of(st ^ 1));
+        if (prefetch && nlen == pl.sub) stage_from_regs(buf_of(st ^ 1), pre);
         else stage_scalar(buf_of(st ^ 1), ncs, nlen);
-        if (prefetch && end - (ncs + pl.sub) >= pl.sub) fetch(ncs + pl.sub);
+        if (prefetch && end - (ncs + pl.sub) >= pl.sub) fetch(ncs + pl.sub, pre);
       }
-      compute(buf_of(st), stage_len(cs));
+      compute(buf_of(st), stage_len(cs), role);
       __syncthreads();
     }
   }
+  };
+  if (SPLIT && diag) run(std::true_type{});
+  else run(std::false_type{});
 
   // sum the k-slices of each tile pair in slice order, ≤ 64 accumulators
   // at a time through LDS
   constexpr int kE = TS * TS;
+  if constexpr (SPLIT) {
+    // lane tid's accumulators at slot tid; role l's k-slices are lanes
+    // k·ro + l (off-diagonal) or 64·wo + k·rd + d (diagonal)
+#pragma unroll
+    for (int e0 = 0; e0 < kE; e0 += 64) {
+      const int ne = kE - e0 < 64 ? kE - e0 : 64;
+      if (active) {
+        float *slot = lds + tid * kRedPitch;
+#pragma unroll
+        for (int e = e0; e < e0 + 64 && e < kE; ++e)
+          slot[e - e0] = pair_acc<TS>(acc, e / TS, e % TS);
+      }
+      __syncthreads();
+      const int nod = pl.ro * ne;
+      const int outs = nod + pl.rd * ne;
+      for (int o = tid; o < outs; o += kBlock) {
+        float sum = 0.0f;
+        int tp, idx;
+        bool valid = true;
+        if (o < nod) {
+          const int l = o / ne, e = o - l * ne;
+          for (int k = 0; k < pl.kso; ++k)
+            sum += lds[(k * pl.ro + l) * kRedPitch + e];
+          int a, b;
+          od_to_tiles(l, pl.nt, a, b);
+          tp = tiles_to_tp(a, b, pl.nt);
+          idx = e0 + e;
+        } else {
+          const int o2 = o - nod;
+          const int d = o2 / ne, e = o2 - d * ne;
+          for (int k = 0; k < pl.ksd; ++k)
+            sum += lds[(kWave * pl.wo + k * pl.rd + d) * kRedPitch + e];
+          const int u = (e0 + e) / TS, v = (e0 + e) % TS;
+          const int h = u >> 1, half = u & 1;
+          int t = 2 * d, uu = u, vv = v;
+          if (2 * h >= v) {  // tile B's mirrored slot
+            t = 2 * d + 1;
+            uu = 2 * (TS / 2 - 1 - h) + half;
+            vv = TS - 1 - v;
+          }
+          valid = uu < vv && t < pl.nt;
+          tp = tiles_to_tp(t, t, pl.nt);
+          idx = uu * TS + vv;
+        }
+        if (valid) partial[(int64_t(c) * pl.ntp + tp) * kE + idx] = sum;
+      }
+      __syncthreads();
+    }
+    return;
+  }
 #pragma unroll
   for (int e0 = 0; e0 < kE; e0 += 64) {
     if (ksl < pl.ks) {
@@ -668,8 +994,17 @@ __global__ __launch_bounds__(kSegBlock) void pairdist_segsq_kernel(
   const int per_seg = pl.ntp * ee;
   const int lane = threadIdx.x & (kWave - 1), slice = threadIdx.x / kWave;
   const int r = blockIdx.y * kWave + lane;
-  double sq = 0.0;
+  int i = n, j = n;  // the pair of slot r (only i < j < n is ever written)
   if (r < per_seg) {
+    const int tp = r / ee, e = r % ee;
+    int ti, tj;
+    tp_to_tiles(tp, pl.nt, ti, tj);
+    i = ti * pl.ts + e / pl.ts;
+    j = tj * pl.ts + e % pl.ts;
+  }
+  const bool want = i < j && j < n;
+  double sq = 0.0;
+  if (want) {
 #pragma unroll 4
     for (int c = prefix[s] + slice; c < prefix[s + 1]; c += kSegSlices)
       sq += double(partial[int64_t(c) * per_seg + r]);
@@ -680,16 +1015,12 @@ __global__ __launch_bounds__(kSegBlock) void pairdist_segsq_kernel(
   double t = 0.0;
 #pragma unroll
   for (int k = 0; k < kSegSlices; ++k) t += red[k][lane];
-  const int tp = r / ee, e = r % ee;
-  int ti, tj;
-  tp_to_tiles(tp, pl.nt, ti, tj);
-  const int i = ti * pl.ts + e / pl.ts, j = tj * pl.ts + e % pl.ts;
   double *m = segsq + int64_t(s) * n * n;
   if (i == 0 && j == 1) {
     // the diagonal of this segment (one writer per segment)
     for (int d = 0; d < n; ++d) m[int64_t(d) * n + d] = 0.0;
   }
-  if (i >= n || j >= n || i >= j) return;
+  if (!want) return;
   m[int64_t(i) * n + j] = t;
   m[int64_t(j) * n + i] = t;
 }
@@ -990,16 +1321,25 @@ static int pairdist_segsq_impl(const float *const *tab, int64_t ss, int n,
 #define FSAGG_FLAT(TS, PK)                                                    \
   do {                                                                        \
     if (db)                                                                   \
-      hipLaunchKernelGGL((pairdist_chunk_kernel<TS, PK, true>), grid,         \
+      hipLaunchKernelGGL((pairdist_chunk_kernel<TS, PK, true, false>), grid,  \
                          dim3(kBlock), 0, s, tab, ss, n, pl, seg_lo, seg_end, \
                          nseg, prefix, partial);                              \
     else                                                                      \
-      hipLaunchKernelGGL((pairdist_chunk_kernel<TS, PK, false>), grid,        \
+      hipLaunchKernelGGL((pairdist_chunk_kernel<TS, PK, false, false>), grid, \
                          dim3(kBlock), 0, s, tab, ss, n, pl, seg_lo, seg_end, \
                          nseg, prefix, partial);                              \
   } while (0)
     const bool pk = packed_form();
-    if (pl.ts == 10) {
+    if (pl.split) {
+      if (pl.ts == 10)
+        hipLaunchKernelGGL((pairdist_chunk_kernel<10, true, true, true>), grid,
+                           dim3(kBlock), 0, s, tab, ss, n, pl, seg_lo, seg_end,
+                           nseg, prefix, partial);
+      else
+        hipLaunchKernelGGL((pairdist_chunk_kernel<8, true, true, true>), grid,
+                           dim3(kBlock), 0, s, tab, ss, n, pl, seg_lo, seg_end,
+                           nseg, prefix, partial);
+    } else if (pl.ts == 10) {
       if (pk) FSAGG_FLAT(10, true); else FSAGG_FLAT(10, false);
     } else {
       if (pk) FSAGG_FLAT(8, true); else FSAGG_FLAT(8, false);
