@@ -19,8 +19,12 @@
 //   * the clients are cut into tiles of TS = 8 or 10 (whichever gives fewer
 //     pair slots: at n = 50, 15 × 100 = 1500 vs 28 × 64 = 1792); each lane
 //     owns one TS×TS tile pair of the upper triangle (TS² fp32 accumulators)
-//     and a k-slice of the stage's coordinates; at the end of the chunk the
-//     k-slices are summed through LDS in a fixed order → partial[chunk][pair];
+//     and a k-slice of the stage's coordinates; in the split-role form (the
+//     default when it fits) whole waves own the off-diagonal tile pairs and
+//     the others pairs of diagonal tiles, whose two upper triangles fill one
+//     TS² accumulator set (n = 50: 1300 pair slots instead of 1500); at the
+//     end of the chunk the k-slices are summed through LDS in a fixed order
+//     → partial[chunk][pair];
 //   * a 1024-thread kernel sums each key's chunks in fp64 (fixed order), and
 //     a final kernel takes the per-key sqrt, rounds to fp32 and accumulates
 //     the keys in fp32 in key order (the reference's
@@ -277,6 +281,76 @@ __device__ __forceinline__ void read_tile(const float *col, int t,
   }
 }
 
+// One coordinate's distance updates of a lane, from its two tiles' values
+// at that coordinate as row pairs (A[h] = rows 2h, 2h+1 of tile ti; B the
+// same of tile tj).  Off-diagonal (DIAG false): every slot, acc[h][v] +=
+// (A[h] − B_v)².  Diagonal roles (the split form's tiles ti and tj = ti+1):
+// tile ti's pairs (u, v), u < v, in acc[u/2][v] (the slots 2h < v) and tile
+// tj's slot (h, v) mirrored to acc[TS/2−1−h][TS−1−v] (exactly the slots
+// 2h ≥ v).  All differences of a v first, then the fmas: a packed fma that
+// reads the packed add just before it needs a wait state (s_nop).
+template <int TS, bool DIAG>
+__device__ __forceinline__ void pair_update(f2 (&acc)[TS / 2][TS],
+                                            const f2 (&A)[TS / 2],
+                                            const f2 (&B)[TS / 2]) {
+  if constexpr (DIAG) {
+#pragma unroll
+    for (int v = 1; v < TS; ++v) {
+      const float av = (v & 1) ? A[v >> 1].y : A[v >> 1].x;
+      const float bv = (v & 1) ? B[v >> 1].y : B[v >> 1].x;
+      f2 da[TS / 2], db[TS / 2];
+#pragma unroll
+      for (int h = 0; 2 * h < v; ++h) {
+        da[h] = A[h] - f2{av, av};
+        db[h] = B[h] - f2{bv, bv};
+      }
+#pragma unroll
+      for (int h = 0; 2 * h < v; ++h) {
+        acc[h][v] = __builtin_elementwise_fma(da[h], da[h], acc[h][v]);
+        f2 &m = acc[TS / 2 - 1 - h][TS - 1 - v];
+        m = __builtin_elementwise_fma(db[h], db[h], m);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int v = 0; v < TS; ++v) {
+      const float bv = (v & 1) ? B[v >> 1].y : B[v >> 1].x;
+      f2 d[TS / 2];
+#pragma unroll
+      for (int h = 0; h < TS / 2; ++h) d[h] = A[h] - f2{bv, bv};
+#pragma unroll
+      for (int h = 0; h < TS / 2; ++h)
+        acc[h][v] = __builtin_elementwise_fma(d[h], d[h], acc[h][v]);
+    }
+  }
+}
+
+// Partial slot of a split-form accumulator: element idx = u·TS + v of a
+// lane of role `l` (off-diagonal pair l, or diagonal role l = tiles 2l,
+// 2l+1) → tile pair tp and element within it; false for a slot no pair
+// owns (a diagonal tile's repeated half, or a tile past the last).
+__device__ __forceinline__ bool split_slot(bool diag, int l, int idx, int ts,
+                                           int nt, int &tp, int &e) {
+  const int u = idx / ts, v = idx % ts;
+  if (!diag) {
+    int a, b;
+    od_to_tiles(l, nt, a, b);
+    tp = tiles_to_tp(a, b, nt);
+    e = idx;
+    return true;
+  }
+  const int h = u >> 1, half = u & 1;
+  int t = 2 * l, uu = u, vv = v;
+  if (2 * h >= v) {  // tile B's mirrored slot
+    t = 2 * l + 1;
+    uu = 2 * (ts / 2 - 1 - h) + half;
+    vv = ts - 1 - v;
+  }
+  tp = tiles_to_tp(t, t, nt);
+  e = uu * ts + vv;
+  return uu < vv && t < nt;
+}
+
 // PK: the row-pair packed form (v_pk_add_f32 / v_pk_fma_f32, two pairs per
 // instruction); else scalar v_sub_f32 / v_fma_f32 on the same accumulators.
 // SPLIT (with PK and DB): the split-role form of PairPlan.
@@ -463,47 +537,11 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
           B[h] = pb[h];
         }
       };
-      auto step = [&](const f2 (&A)[TS / 2], const f2 (&B)[TS / 2]) {
-        if constexpr (decltype(role)::value) {
-          // diagonal roles — tile A = ti: pair (u, v), u < v, in
-          // acc[u/2][v] (slots 2h < v); tile B = tj: its slot (h, v)
-          // mirrored to acc[TS/2-1-h][TS-1-v] (exactly the slots 2h >= v)
-#pragma unroll
-          for (int v = 1; v < TS; ++v) {
-            const float av = (v & 1) ? A[v >> 1].y : A[v >> 1].x;
-            const float bv = (v & 1) ? B[v >> 1].y : B[v >> 1].x;
-            f2 da[TS / 2], db[TS / 2];
-#pragma unroll
-            for (int h = 0; 2 * h < v; ++h) {
-              da[h] = A[h] - f2{av, av};
-              db[h] = B[h] - f2{bv, bv};
-            }
-#pragma unroll
-            for (int h = 0; 2 * h < v; ++h) {
-              acc[h][v] = __builtin_elementwise_fma(da[h], da[h], acc[h][v]);
-              f2 &m = acc[TS / 2 - 1 - h][TS - 1 - v];
-              m = __builtin_elementwise_fma(db[h], db[h], m);
-            }
-          }
-        } else {
-          // off-diagonal tile pair (ti, tj): every slot
-#pragma unroll
-          for (int v = 0; v < TS; ++v) {
-            const float bv = (v & 1) ? B[v >> 1].y : B[v >> 1].x;
-            f2 d[TS / 2];
-#pragma unroll
-            for (int h = 0; h < TS / 2; ++h) d[h] = A[h] - f2{bv, bv};
-#pragma unroll
-            for (int h = 0; h < TS / 2; ++h)
-              acc[h][v] = __builtin_elementwise_fma(d[h], d[h], acc[h][v]);
-          }
-        }
-      };
       int s = 0;
       do {  // len >= 1: at least one step
         f2 A[TS / 2], B[TS / 2];
         load(s, A, B);
-        step(A, B);
+        pair_update<TS, decltype(role)::value>(acc, A, B);
       } while (++s < steps);
       return;
     }
@@ -662,31 +700,18 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
       for (int o = tid; o < outs; o += kBlock) {
         float sum = 0.0f;
         int tp, idx;
-        bool valid = true;
+        bool valid;
         if (o < nod) {
           const int l = o / ne, e = o - l * ne;
           for (int k = 0; k < pl.kso; ++k)
             sum += lds[(k * pl.ro + l) * kRedPitch + e];
-          int a, b;
-          od_to_tiles(l, pl.nt, a, b);
-          tp = tiles_to_tp(a, b, pl.nt);
-          idx = e0 + e;
+          valid = split_slot(false, l, e0 + e, TS, pl.nt, tp, idx);
         } else {
           const int o2 = o - nod;
           const int d = o2 / ne, e = o2 - d * ne;
           for (int k = 0; k < pl.ksd; ++k)
             sum += lds[(kWave * pl.wo + k * pl.rd + d) * kRedPitch + e];
-          const int u = (e0 + e) / TS, v = (e0 + e) % TS;
-          const int h = u >> 1, half = u & 1;
-          int t = 2 * d, uu = u, vv = v;
-          if (2 * h >= v) {  // tile B's mirrored slot
-            t = 2 * d + 1;
-            uu = 2 * (TS / 2 - 1 - h) + half;
-            vv = TS - 1 - v;
-          }
-          valid = uu < vv && t < pl.nt;
-          tp = tiles_to_tp(t, t, pl.nt);
-          idx = uu * TS + vv;
+          valid = split_slot(true, d, e0 + e, TS, pl.nt, tp, idx);
         }
         if (valid) partial[(int64_t(c) * pl.ntp + tp) * kE + idx] = sum;
       }
@@ -719,74 +744,89 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   }
 }
 
-// ---- ring form: LDS-DMA stages, quad-coordinate lanes ---------------------
-// One 512-thread workgroup per CU (152 KiB of LDS).  A chunk streams
-// through a 3-slot ring of stages; a stage is every client row's next S
-// coordinates, written to LDS by 16-byte LDS-DMA (global_load_lds_dwordx4:
-// no VGPR round trip, no staging writes) in the rows' own layout
-// [row][coordinate].  Lane (tp, q) owns tile pair tp and coordinate quad q
-// of every stage: 2·TS ds_read_b128 give it its two tiles' rows at 4
-// coordinates (lanes of one tile pair read consecutive quads of one row:
-// conflict-free), then 4 × TS² packed sub/fma.  One raw barrier per stage:
-// stage st+2 is issued into the slot stage st−1 vacated, while stage st+1
-// stays in flight (counted vmcnt).  At the chunk end the q-slices of each
-// tile pair are summed through LDS in slice order → partial[chunk][pair].
+// ---- ring form: LDS-DMA stages, split roles --------------------------------
+// One 512-thread workgroup per CU (152 KiB of LDS): a chunk streams through
+// a 3-slot ring of stages written by 16-byte LDS-DMA
+// (global_load_lds_dwordx4: no VGPR round trip, no staging stores, no
+// prefetch registers) in the rows' own layout [row][coordinate] with a row
+// pitch P of 64·P64 floats.  Two stages are in flight while one is computed;
+// one raw barrier per stage (stage st+2 goes into the slot stage st−1
+// vacated; each wave counts its own DMAs with vmcnt).
+// Lanes take the split-form roles of PairPlan (the first wo waves the
+// off-diagonal tile pairs, the rest the paired diagonal tiles), k-slices
+// fastest: the lanes of a role read consecutive coordinates of a row (one
+// LDS bank each).  A lane's row pair (2h, 2h+1) of a tile at one coordinate
+// is one ds_read2st64_b32 (row offsets 2h·P64 and (2h+1)·P64 in units of
+// 64 dwords), so the packed updates need no operand moves.  Columns [S, P)
+// stay zero: a lane past the stage's coordinates reads them and adds 0.
 constexpr int kRingThreads = 512;
 constexpr int kRingWaves = kRingThreads / kWave;
 constexpr int kRingLds = 38912;  // floats: 152 KiB, one workgroup per CU
 constexpr int kRingRed = kRingLds / kRingThreads;  // accumulators per pass
+constexpr int kRingSlots = 3;
 
 struct RingPlan {
-  int ts, nt, ntp;
-  int qs;     // coordinate quads per stage (lanes per tile pair, <= 64:
-              // one DMA wave-instruction per row)
-  int S;      // coordinates per stage
-  int rw;     // DMA rows per wave per stage
-  int stage;  // floats per stage slot (rw·8 rows × S)
-  int nbuf;   // ring slots (nbuf − 1 stages in flight)
-  int mode;   // experiments only (FSAGG_RING_MODE): 1 = no compute,
-              // 2 = no DMA, 3 = no DMA and no barrier; 0 = the kernel
+  int ts, nt, ntp;  // tile layout (PairPlan's; partial[] has its layout)
+  int rw;           // DMA rows per wave per stage (staged rows rw·8; rows
+                    // past the tiles repeat row n − 1 and are never read)
+  int p64;          // row pitch / 64 floats
+  int S;            // coordinates per stage (multiple of 4, <= 256)
+  int slot;         // floats per ring slot (rw·8 rows × pitch)
+  int wo, ro, ko, rd, kd;  // split roles (as PairPlan's wo, ro, kso, ...)
+  int mo, md;       // coordinate steps per stage of the two role kinds
   int64_t chl, max_chunks;
   int ok;
 };
 
-static int ring_bufs_env() {
-  static int nb = -1;
-  if (nb < 0) {
-    const char *e = getenv("FSAGG_RING_BUFS");
-    nb = e ? atoi(e) : 4;
-    if (nb < 3 || nb > 4) nb = 4;
-  }
-  return nb;
-}
-
 RingPlan make_ring_plan(int n, int64_t numel, int nseg) {
   const PairPlan pp = make_plan(n, numel, nseg);
-  RingPlan p;
+  RingPlan p{};
   p.ts = pp.ts;
   p.nt = pp.nt;
   p.ntp = pp.ntp;
-  p.qs = kRingThreads / p.ntp;
-  if (p.qs > kWave) p.qs = kWave;
-  if (p.qs < 1) p.qs = 1;  // more tile pairs than lanes: not ok (below)
-  p.S = 4 * p.qs;
   p.rw = (p.nt * p.ts + kRingWaves - 1) / kRingWaves;
-  p.stage = p.rw * kRingWaves * p.S;
-  p.nbuf = ring_bufs_env();
-  {
-    const char *e = getenv("FSAGG_RING_MODE");
-    p.mode = e ? atoi(e) : 0;
+  p.ok = 0;
+  p.S = 4;
+  const int ro = p.nt * (p.nt - 1) / 2, rd = (p.nt + 1) / 2;
+  double best = 0.0;
+  if (p.nt >= 2 && p.rw <= 8) {
+    for (int wo = 1; wo < kRingWaves; ++wo) {
+      const int ko = kWave * wo / ro, kd = kWave * (kRingWaves - wo) / rd;
+      if (ko < 1 || kd < 1) continue;
+      for (int S = 4; S <= 4 * kWave; S += 4) {
+        const int mo = (S + ko - 1) / ko, md = (S + kd - 1) / kd;
+        // highest column read + 1: the zero column S included
+        const int reach = std::max(std::max(mo * ko, md * kd), S + 1);
+        const int p64 = (reach + 63) / 64;
+        if (p64 > 4) break;
+        const int slot = p.rw * kRingWaves * 64 * p64;
+        if (kRingSlots * slot > kRingLds) break;
+        const double eff = double(S) / std::max(mo, md);
+        if (eff > best || (eff == best && S > p.S)) {
+          best = eff;
+          p.ok = 1;
+          p.wo = wo;
+          p.ro = ro;
+          p.ko = ko;
+          p.rd = rd;
+          p.kd = kd;
+          p.mo = mo;
+          p.md = md;
+          p.S = S;
+          p.p64 = p64;
+          p.slot = slot;
+        }
+      }
+    }
   }
-  while (p.nbuf > 3 && p.nbuf * p.stage > kRingLds) --p.nbuf;
-  // most lanes busy (small n leaves tile pairs × 64 quads < 3/4 of them)
-  p.ok = p.qs >= 2 && p.ntp * p.qs * 4 >= kRingThreads * 3 && p.rw <= 8 &&
-         p.nbuf * p.stage <= kRingLds && p.ts * p.ts <= 2 * kRingRed;
-  // ≈ 2 chunks per CU, whole stages
-  int64_t chl = (numel + 511) / 512;
+  p.ok = p.ok && p.ts * p.ts <= 2 * kRingRed;
+  // ≈ 4 rounds of the 256 resident workgroups, whole stages
+  const int64_t target = 1024 - nseg > 256 ? 1024 - nseg : 256;
+  int64_t chl = (numel + target - 1) / target;
   const int64_t minl = int64_t(p.S) * 8;
   if (chl < minl) chl = minl;
   p.chl = (chl + p.S - 1) / p.S * p.S;
-  p.max_chunks = numel / p.chl + nseg + 1;
+  p.max_chunks = numel / chl + nseg + 1;
   return p;
 }
 
@@ -811,25 +851,25 @@ __device__ __forceinline__ void glds16(const float *sbase, uint32_t voff,
       : "memory");
 }
 
-// acc[v] += (x − b[v].c)² for one coordinate c, x = the coordinate of two
-// tile rows: one v_pk_add_f32 (b's value broadcast) and one v_pk_fma_f32
-// per v
-template <int TS, typename Pick>
-__device__ __forceinline__ void pair_step(f2 (&acc)[TS], f2 x,
-                                          const float4 (&b)[TS], Pick pick) {
-#pragma unroll
-  for (int v = 0; v < TS; ++v) {
-    const float y = pick(b[v]);
-    const f2 d = x - f2{y, y};
-    acc[v] = __builtin_elementwise_fma(d, d, acc[v]);
+// s_waitcnt vmcnt(k) for a wave-uniform k in [0, 16]
+__device__ __forceinline__ void wait_vmcnt(int k) {
+  switch (k) {
+#define FSAGG_VM(K) \
+  case K: asm volatile("s_waitcnt vmcnt(" #K ")" ::: "memory"); break;
+    FSAGG_VM(0) FSAGG_VM(1) FSAGG_VM(2) FSAGG_VM(3) FSAGG_VM(4) FSAGG_VM(5)
+    FSAGG_VM(6) FSAGG_VM(7) FSAGG_VM(8) FSAGG_VM(9) FSAGG_VM(10) FSAGG_VM(11)
+    FSAGG_VM(12) FSAGG_VM(13) FSAGG_VM(14) FSAGG_VM(15)
+#undef FSAGG_VM
+    default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
   }
 }
 
-template <int TS, int RW, int NB>
+template <int TS, int P64>
 __global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n, RingPlan pl,
     const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
     int nseg, const int *__restrict__ prefix, float *__restrict__ partial) {
+  constexpr int P = 64 * P64;
   __shared__ __attribute__((aligned(16))) float lds[kRingLds];
   const int c = blockIdx.x;
   if (c >= prefix[nseg]) return;
@@ -848,112 +888,127 @@ __global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int lane = tid & (kWave - 1);
-  const int qs = pl.qs, S = pl.S;
-  const bool active = tid < pl.ntp * qs;
-  const int tp = active ? tid / qs : 0;
-  const int q = tid - tp * qs;
+  const bool diag = wave >= pl.wo;  // wave-uniform role kind
+  int role, k, K;
+  bool active;
   int ti = 0, tj = 0;
-  tp_to_tiles(tp, pl.nt, ti, tj);
+  if (!diag) {
+    role = tid / pl.ko;
+    k = tid - role * pl.ko;
+    K = pl.ko;
+    active = role < pl.ro;
+    od_to_tiles(active ? role : 0, pl.nt, ti, tj);
+  } else {
+    const int l = tid - kWave * pl.wo;
+    role = l / pl.kd;
+    k = l - role * pl.kd;
+    K = pl.kd;
+    active = role < pl.rd;
+    ti = 2 * (active ? role : 0);
+    tj = ti + 1 < pl.nt ? ti + 1 : ti;  // odd tile count: a repeat, unused
+  }
 
   // 16-B DMA needs 16-B aligned sources: the chunk start and every row
   bool vec = (start & 3) == 0;
   for (int r = 0; r < n; ++r)
     vec = vec && (reinterpret_cast<uintptr_t>(rows[r]) & 15u) == 0;
   const int64_t end4 = vec ? start + ((end - start) & ~int64_t(3)) : start;
-  const int nstage = int((end4 - start + S - 1) / S);
+  const int nstage = int((end4 - start + pl.S - 1) / pl.S);
 
-  f2 acc[TS / 2][TS];  // row-pair packed, as pairdist_chunk_kernel
+  f2 acc[TS / 2][TS];
 #pragma unroll
   for (int h = 0; h < TS / 2; ++h)
 #pragma unroll
     for (int v = 0; v < TS; ++v) acc[h][v] = f2{0.0f, 0.0f};
 
-  // this wave's DMA rows (slots wave + 8k; slots past the tile rows repeat
-  // row n-1 and are never read)
-  const float *rp[RW];
-#pragma unroll
-  for (int k = 0; k < RW; ++k)
-    rp[k] = rows[min(wave + kRingWaves * k, n - 1)];
+  // zero columns [S, P) of every staged row of every slot (never DMA'd)
+  {
+    const int zc = P - pl.S, nrow = kRingSlots * pl.rw * kRingWaves;
+    for (int i = tid; i < nrow * zc; i += kRingThreads) {
+      const int r = i / zc;
+      lds[r * P + pl.S + (i - r * zc)] = 0.0f;
+    }
+  }
+  __syncthreads();
 
+  // this wave's DMA rows (wave + 8j, j < rw), pointers loaded once
+  const float *rp[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) rp[j] = rows[min(wave + kRingWaves * j, n - 1)];
   const uint32_t lds_base = uint32_t(uintptr_t((lfloat_t *)lds));
   auto issue = [&](int st) {
-    if (pl.mode >= 2) return;
-    const int64_t cs = start + int64_t(st) * S;
-    const int nq = int(min(int64_t(S), end4 - cs) >> 2);
-    const uint32_t slot = lds_base + 4u * uint32_t((st % NB) * pl.stage);
-    if (lane < qs) {
-      // lanes past the stage's quads re-read its first quad into columns
-      // nobody reads
+    const int64_t cs = start + int64_t(st) * pl.S;
+    const int nq = int(min(int64_t(pl.S), end4 - cs) >> 2);
+    const uint32_t slot = lds_base + 4u * uint32_t((st % kRingSlots) * pl.slot);
+    if (lane < (pl.S >> 2)) {
+      // lanes past the stage's quads (its last, partial stage) re-read its
+      // first quad into columns no lane reads (c >= len maps to column S)
       const uint32_t voff = 16u * uint32_t(lane < nq ? lane : 0);
 #pragma unroll
-      for (int k = 0; k < RW; ++k)
-        glds16(rp[k] + cs, voff,
-               slot + 4u * uint32_t((wave + kRingWaves * k) * S));
+      for (int j = 0; j < 8; ++j)
+        if (j < pl.rw)
+          glds16(rp[j] + cs, voff,
+                 slot + 4u * uint32_t((wave + kRingWaves * j) * P));
     }
   };
-
-  // NB − 1 stages in flight; stage st + NB − 1 goes into the slot stage
-  // st − 1 vacated (every wave is past it: the barrier)
+  // the lane's row pairs of tiles ti, tj at column cc of a slot
+  auto load = [&](const float *sb, int cc, f2 (&A)[TS / 2],
+                  f2 (&B)[TS / 2]) {
+    const float *pa = sb + ti * TS * P + cc;
+    const float *pb = sb + tj * TS * P + cc;
 #pragma unroll
-  for (int k = 0; k < NB - 1; ++k)
-    if (k < nstage) issue(k);
-  for (int st = 0; st < nstage; ++st) {
-    // this wave's DMAs of stage st have landed (later ones may fly)
-    const int later = min(nstage - 1 - st, NB - 2);
-    if (later >= 2)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * RW) : "memory");
-    else if (later == 1)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RW) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (pl.mode != 3) __builtin_amdgcn_s_barrier();
-    if (st + NB - 1 < nstage) issue(st + NB - 1);
-    const int64_t cs = start + int64_t(st) * S;
-    const int nq = int(min(int64_t(S), end4 - cs) >> 2);
-    if (active && q < nq && pl.mode != 1) {
-      const float *slot = lds + (st % NB) * pl.stage + 4 * q;
-      float4 b[TS];
-#pragma unroll
-      for (int v = 0; v < TS; ++v)
-        b[v] = *reinterpret_cast<const float4 *>(slot + (tj * TS + v) * S);
-#pragma unroll
-      for (int h = 0; h < TS / 2; ++h) {
-        const float4 a0 =
-            *reinterpret_cast<const float4 *>(slot + (ti * TS + 2 * h) * S);
-        const float4 a1 = *reinterpret_cast<const float4 *>(
-            slot + (ti * TS + 2 * h + 1) * S);
-        // rows are [row][coordinate] here: the two rows' values are paired
-        // by moves; coordinate-major, so the four updates of one
-        // accumulator are TS packed ops apart
-        pair_step(acc[h], f2{a0.x, a1.x}, b, [](const float4 &t) { return t.x; });
-        pair_step(acc[h], f2{a0.y, a1.y}, b, [](const float4 &t) { return t.y; });
-        pair_step(acc[h], f2{a0.z, a1.z}, b, [](const float4 &t) { return t.z; });
-        pair_step(acc[h], f2{a0.w, a1.w}, b, [](const float4 &t) { return t.w; });
+    for (int h = 0; h < TS / 2; ++h) {
+      A[h] = f2{pa[2 * h * P], pa[(2 * h + 1) * P]};
+      B[h] = f2{pb[2 * h * P], pb[(2 * h + 1) * P]};
+    }
+  };
+  auto run = [&](auto is_diag) {
+    constexpr bool D = decltype(is_diag)::value;
+    const int M = D ? pl.md : pl.mo;
+    // one stage's updates from slot sb (len coordinates; past them the
+    // zero column)
+    auto compute = [&](const float *sb, int len) {
+      for (int m = 0; m < M; ++m) {
+        const int cc0 = k + m * K;
+        const int cc = active && cc0 < len ? cc0 : pl.S;
+        f2 A[TS / 2], B[TS / 2];
+        load(sb, cc, A, B);
+        pair_update<TS, D>(acc, A, B);
       }
+    };
+#pragma unroll
+    for (int q = 0; q < kRingSlots - 1; ++q)
+      if (q < nstage) issue(q);
+    for (int st = 0; st < nstage; ++st) {
+      // this wave's DMAs of stage st have landed (later ones may fly)
+      const int later = min(nstage - 1 - st, kRingSlots - 2);
+      wait_vmcnt(later * pl.rw);
+      __builtin_amdgcn_s_barrier();
+      if (st + kRingSlots - 1 < nstage) issue(st + kRingSlots - 1);
+      const int64_t cs = start + int64_t(st) * pl.S;
+      compute(lds + (st % kRingSlots) * pl.slot,
+              int(min(int64_t(pl.S), end4 - cs)));
     }
-  }
-  // coordinates past the last whole quad (or all of a misaligned chunk):
-  // straight from the rows, the q-lanes of each tile pair taking every
-  // qs-th coordinate
-  if (active) {
-    for (int64_t p = end4 + q; p < end; p += qs) {
-      float a[TS], b[TS];
-#pragma unroll
-      for (int u = 0; u < TS; ++u) a[u] = gld(rows[min(ti * TS + u, n - 1)] + p);
-#pragma unroll
-      for (int v = 0; v < TS; ++v) b[v] = gld(rows[min(tj * TS + v, n - 1)] + p);
-#pragma unroll
-      for (int h = 0; h < TS / 2; ++h)
-#pragma unroll
-        for (int v = 0; v < TS; ++v) {
-          const f2 d = f2{a[2 * h], a[2 * h + 1]} - f2{b[v], b[v]};
-          acc[h][v] = __builtin_elementwise_fma(d, d, acc[h][v]);
-        }
+    // [end4, end): the sub-quad tail, or the whole chunk when a row is not
+    // 16-B aligned — staged by 4-B loads into slot 0
+    const int nrows = pl.nt * TS;
+    for (int64_t cs = end4; cs < end; cs += pl.S) {
+      const int len = int(min(int64_t(pl.S), end - cs));
+      __syncthreads();  // every wave is done with the slots
+      for (int i = tid; i < nrows * len; i += kRingThreads) {
+        const int r = i / len, col = i - r * len;
+        lds[r * P + col] = gld(rows[min(r, n - 1)] + cs + col);
+      }
+      __syncthreads();
+      compute(lds, len);
     }
-  }
+  };
+  if (diag) run(std::true_type{});
+  else run(std::false_type{});
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // every stage read: the ring becomes the reduction buffer
 
-  // Σ over the q-slices of each tile pair, in slice order
+  // Σ over the k-slices of each role, in slice order
   constexpr int kE = TS * TS;
 #pragma unroll
   for (int e0 = 0; e0 < kE; e0 += kRingRed) {
@@ -966,11 +1021,18 @@ __global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
         slot[e - e0] = pair_acc<TS>(acc, e / TS, e % TS);
     }
     __syncthreads();
-    for (int o = tid; o < pl.ntp * ne; o += kRingThreads) {
-      const int t = o / ne, e = o - t * ne;
+    const int nod = pl.ro * ne, outs = nod + pl.rd * ne;
+    for (int o = tid; o < outs; o += kRingThreads) {
+      const bool dg = o >= nod;
+      const int o2 = dg ? o - nod : o;
+      const int l = o2 / ne, e = o2 - l * ne;
+      const int base = dg ? kWave * pl.wo + l * pl.kd : l * pl.ko;
+      const int kk = dg ? pl.kd : pl.ko;
       float sum = 0.0f;
-      for (int k = 0; k < qs; ++k) sum += lds[(t * qs + k) * R + e];
-      partial[(int64_t(c) * pl.ntp + t) * kE + e0 + e] = sum;
+      for (int q = 0; q < kk; ++q) sum += lds[(base + q) * R + e];
+      int tp, idx;
+      if (split_slot(dg, l, e0 + e, TS, pl.nt, tp, idx))
+        partial[(int64_t(c) * pl.ntp + tp) * kE + idx] = sum;
     }
     __syncthreads();
   }
@@ -1244,12 +1306,13 @@ static bool packed_form() {
   return on == 1;
 }
 
-// FSAGG_PAIRDIST=ring selects the LDS-DMA ring kernel (A/B runs; the
-// register-staged kernel measured faster at C4)
+// FSAGG_PAIRDIST=ring selects the LDS-DMA ring kernel (A/B runs; at C4 the
+// register-staged split-role kernel measured 0.49 ms against the ring's
+// 0.51, and 0.56 with the ring's LDS reads software-pipelined).
 // The double-buffered stage loop (one barrier per stage, half-size stages)
 // is the default: 0.556 against 0.567–0.571 ms for the single-buffered loop
-// (two barriers per stage) at C4 in interleaved A/B; FSAGG_PAIRDIST=flat
-// selects the latter.
+// (two barriers per stage) at C4 in interleaved A/B, before the split form;
+// FSAGG_PAIRDIST=flat selects the latter.
 static bool dbuf_enabled() {
   static int on = -1;
   if (on < 0) {
@@ -1284,27 +1347,16 @@ static int pairdist_segsq_impl(const float *const *tab, int64_t ss, int n,
     hipLaunchKernelGGL(chunk_prefix_kernel, dim3(1), dim3(1), 0, s, seg_lo,
                        seg_end, nseg, rp.chl, prefix);
     const dim3 grid(unsigned(rp.max_chunks));
-#define FSAGG_RING(TS, RW)                                                  \
-  do {                                                                      \
-    if (rp.nbuf == 4)                                                       \
-      hipLaunchKernelGGL((pairdist_ring_kernel<TS, RW, 4>), grid,           \
-                         dim3(kRingThreads), 0, s, tab, ss, n, rp, seg_lo,  \
-                         seg_end, nseg, prefix, partial);                   \
-    else                                                                    \
-      hipLaunchKernelGGL((pairdist_ring_kernel<TS, RW, 3>), grid,           \
-                         dim3(kRingThreads), 0, s, tab, ss, n, rp, seg_lo,  \
-                         seg_end, nseg, prefix, partial);                   \
-  } while (0)
+#define FSAGG_RING(TS, P64)                                                 \
+  hipLaunchKernelGGL((pairdist_ring_kernel<TS, P64>), grid,                 \
+                     dim3(kRingThreads), 0, s, tab, ss, n, rp, seg_lo,      \
+                     seg_end, nseg, prefix, partial)
     const bool t10 = rp.ts == 10;
-    switch (rp.rw) {
+    switch (rp.p64) {
       case 1: if (t10) FSAGG_RING(10, 1); else FSAGG_RING(8, 1); break;
       case 2: if (t10) FSAGG_RING(10, 2); else FSAGG_RING(8, 2); break;
       case 3: if (t10) FSAGG_RING(10, 3); else FSAGG_RING(8, 3); break;
-      case 4: if (t10) FSAGG_RING(10, 4); else FSAGG_RING(8, 4); break;
-      case 5: if (t10) FSAGG_RING(10, 5); else FSAGG_RING(8, 5); break;
-      case 6: if (t10) FSAGG_RING(10, 6); else FSAGG_RING(8, 6); break;
-      case 7: if (t10) FSAGG_RING(10, 7); else FSAGG_RING(8, 7); break;
-      default: if (t10) FSAGG_RING(10, 8); else FSAGG_RING(8, 8); break;
+      default: if (t10) FSAGG_RING(10, 4); else FSAGG_RING(8, 4); break;
     }
 #undef FSAGG_RING
     const int per_seg = pl.ntp * pl.ts * pl.ts;

@@ -38,8 +38,17 @@ def _run2(args, timeout=110):
     p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True,
                        timeout=timeout, env=env)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
-    return [json.loads(l) for l in p.stdout.splitlines()
-            if l.startswith('{')]
+    # every JSON object in the output (the two ranks' lines can interleave)
+    dec, out, i = json.JSONDecoder(), [], p.stdout.find('{')
+    while i >= 0:
+        try:
+            obj, j = dec.raw_decode(p.stdout, i)
+        except json.JSONDecodeError:
+            j = i + 1
+        else:
+            out.append(obj)
+        i = p.stdout.find('{', j)
+    return out
 
 
 def test_bench_strong_scaling_world2():
