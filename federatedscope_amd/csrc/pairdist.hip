@@ -325,6 +325,104 @@ __device__ __forceinline__ void pair_update(f2 (&acc)[TS / 2][TS],
   }
 }
 
+// The same step with its operand reads as separate ds_read_b64 (LDSR = 1):
+// the compiler merges the row-pair reads into ds_read2_b64, which the LDS
+// serves as 4 × 16-lane groups on 32 banks (8 cycles for 16 B per lane, 2-way
+// conflicted between k-slices of the staged pitch), where two ds_read_b64 take
+// 2 cycles each on 64 banks.  The reads are issued in the order the updates
+// consume them and each group of updates waits only for its own (counted
+// lgkmcnt; the wait names the registers it releases, so no use of them moves
+// above it).  ``ca``/``cb``: LDS byte addresses of the two tiles' rows.
+#define FSAGG_DSR(dst, addr, off) \
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "n"(off))
+#define FSAGG_LGKM(N, a, b) \
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N))
+#define FSAGG_LGKM3(N, a, b, c) \
+  asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(a), "+v"(b), "+v"(c) : "n"(N))
+template <int TS, bool DIAG>
+__device__ __forceinline__ void pair_step_dsr(f2 (&acc)[TS / 2][TS],
+                                              uint32_t ca, uint32_t cb) {
+  static_assert(TS == 10, "the counted waits are written for 10-row tiles");
+  f2 A[TS / 2], B[TS / 2];
+  if constexpr (DIAG) {
+    // A0 B0 A1 B1 ...: updates of v ∈ {2k, 2k+1} need row pairs ≤ k
+    FSAGG_DSR(A[0], ca, 0);  FSAGG_DSR(B[0], cb, 0);
+    FSAGG_DSR(A[1], ca, 8);  FSAGG_DSR(B[1], cb, 8);
+    FSAGG_DSR(A[2], ca, 16); FSAGG_DSR(B[2], cb, 16);
+    FSAGG_DSR(A[3], ca, 24); FSAGG_DSR(B[3], cb, 24);
+    FSAGG_DSR(A[4], ca, 32); FSAGG_DSR(B[4], cb, 32);
+  } else {
+    // A0..A4 B0..B4: every update needs all of A and B[v/2]
+    FSAGG_DSR(A[0], ca, 0);  FSAGG_DSR(A[1], ca, 8);
+    FSAGG_DSR(A[2], ca, 16); FSAGG_DSR(A[3], ca, 24);
+    FSAGG_DSR(A[4], ca, 32);
+    FSAGG_DSR(B[0], cb, 0);  FSAGG_DSR(B[1], cb, 8);
+    FSAGG_DSR(B[2], cb, 16); FSAGG_DSR(B[3], cb, 24);
+    FSAGG_DSR(B[4], cb, 32);
+  }
+  // group k's wait also names an accumulator the previous group just
+  // updated, so the scheduler keeps that group's updates above the wait
+  auto wait_for = [&](int k) {
+    // row pairs <= k of both tiles have landed
+    f2 &prev = acc[0][k > 0 ? 2 * k - 1 : 0];
+    if constexpr (DIAG) {
+      switch (k) {
+        case 0: FSAGG_LGKM(8, A[0], B[0]); break;
+        case 1: FSAGG_LGKM3(6, A[1], B[1], prev); break;
+        case 2: FSAGG_LGKM3(4, A[2], B[2], prev); break;
+        case 3: FSAGG_LGKM3(2, A[3], B[3], prev); break;
+        default: FSAGG_LGKM3(0, A[4], B[4], prev); break;
+      }
+    } else {
+      switch (k) {
+        case 0:
+          FSAGG_LGKM(4, A[4], B[0]);
+          asm volatile("" : "+v"(A[0]), "+v"(A[1]), "+v"(A[2]), "+v"(A[3]));
+          break;
+        case 1: FSAGG_LGKM(3, B[1], prev); break;
+        case 2: FSAGG_LGKM(2, B[2], prev); break;
+        case 3: FSAGG_LGKM(1, B[3], prev); break;
+        default: FSAGG_LGKM(0, B[4], prev); break;
+      }
+    }
+  };
+  if constexpr (DIAG) {
+#pragma unroll
+    for (int v = 1; v < TS; ++v) {
+      if (v == 1 || (v & 1) == 0) wait_for(v >> 1);
+      const float av = (v & 1) ? A[v >> 1].y : A[v >> 1].x;
+      const float bv = (v & 1) ? B[v >> 1].y : B[v >> 1].x;
+      f2 da[TS / 2], db[TS / 2];
+#pragma unroll
+      for (int h = 0; 2 * h < v; ++h) {
+        da[h] = A[h] - f2{av, av};
+        db[h] = B[h] - f2{bv, bv};
+      }
+#pragma unroll
+      for (int h = 0; 2 * h < v; ++h) {
+        acc[h][v] = __builtin_elementwise_fma(da[h], da[h], acc[h][v]);
+        f2 &m = acc[TS / 2 - 1 - h][TS - 1 - v];
+        m = __builtin_elementwise_fma(db[h], db[h], m);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int v = 0; v < TS; ++v) {
+      if ((v & 1) == 0) wait_for(v >> 1);
+      const float bv = (v & 1) ? B[v >> 1].y : B[v >> 1].x;
+      f2 d[TS / 2];
+#pragma unroll
+      for (int h = 0; h < TS / 2; ++h) d[h] = A[h] - f2{bv, bv};
+#pragma unroll
+      for (int h = 0; h < TS / 2; ++h)
+        acc[h][v] = __builtin_elementwise_fma(d[h], d[h], acc[h][v]);
+    }
+  }
+}
+#undef FSAGG_DSR
+#undef FSAGG_LGKM
+#undef FSAGG_LGKM3
+
 // Partial slot of a split-form accumulator: element idx = u·TS + v of a
 // lane of role `l` (off-diagonal pair l, or diagonal role l = tiles 2l,
 // 2l+1) → tile pair tp and element within it; false for a slot no pair
@@ -353,8 +451,9 @@ __device__ __forceinline__ bool split_slot(bool diag, int l, int idx, int ts,
 
 // PK: the row-pair packed form (v_pk_add_f32 / v_pk_fma_f32, two pairs per
 // instruction); else scalar v_sub_f32 / v_fma_f32 on the same accumulators.
-// SPLIT (with PK and DB): the split-role form of PairPlan.
-template <int TS, bool PK, bool DB, bool SPLIT>
+// SPLIT (with PK and DB): the split-role form of PairPlan; LDSR = 1 reads
+// its operands with pair_step_dsr.
+template <int TS, bool PK, bool DB, bool SPLIT, int LDSR = 0>
 __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n,
     PairPlan pl, const int64_t *__restrict__ seg_lo,
@@ -538,6 +637,16 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
         }
       };
       int s = 0;
+      if constexpr (LDSR == 1) {
+        typedef __attribute__((address_space(3))) const float lds_f;
+        do {
+          const float *col = col_of(s);
+          const uint32_t ca = uint32_t(uintptr_t((lds_f *)(col + ti * TS)));
+          const uint32_t cb = uint32_t(uintptr_t((lds_f *)(col + tj * TS)));
+          pair_step_dsr<TS, decltype(role)::value>(acc, ca, cb);
+        } while (++s < steps);
+        return;
+      }
       do {  // len >= 1: at least one step
         f2 A[TS / 2], B[TS / 2];
         load(s, A, B);
@@ -1322,6 +1431,17 @@ static bool dbuf_enabled() {
   return on == 1;
 }
 
+// FSAGG_PAIR_LDS=dsr: the split form's operand reads as counted ds_read_b64
+// (pair_step_dsr) instead of the compiler's merged ds_read2_b64 (A/B runs)
+static int lds_read_form() {
+  static int form = -1;
+  if (form < 0) {
+    const char *e = getenv("FSAGG_PAIR_LDS");
+    form = e && strcmp(e, "dsr") == 0 ? 1 : 0;
+  }
+  return form;
+}
+
 static bool ring_enabled() {
   static int on = -1;
   if (on < 0) {
@@ -1383,7 +1503,11 @@ static int pairdist_segsq_impl(const float *const *tab, int64_t ss, int n,
   } while (0)
     const bool pk = packed_form();
     if (pl.split) {
-      if (pl.ts == 10)
+      if (pl.ts == 10 && lds_read_form() == 1)
+        hipLaunchKernelGGL((pairdist_chunk_kernel<10, true, true, true, 1>),
+                           grid, dim3(kBlock), 0, s, tab, ss, n, pl, seg_lo,
+                           seg_end, nseg, prefix, partial);
+      else if (pl.ts == 10)
         hipLaunchKernelGGL((pairdist_chunk_kernel<10, true, true, true>), grid,
                            dim3(kBlock), 0, s, tab, ss, n, pl, seg_lo, seg_end,
                            nseg, prefix, partial);

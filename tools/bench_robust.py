@@ -125,9 +125,10 @@ def krum_c4(dev, n=50, f=10):
     }
 
 
-def orderstat_c5(dev, n=200, ratio=0.2):
-    lay = layout()
-    P = lay.numel
+def orderstat_c5(dev, n=200, ratio=0.2, P=None, tag='C5'):
+    """``P`` given: a flat P-coordinate bucket instead of the C5 layout (the
+    n > 255 sweep: the bit-by-bit select that re-reads columns from L2)."""
+    P = layout().numel if P is None else int(P)
     g = torch.Generator(device=dev).manual_seed(2)
     slab = torch.randn((n, P), device=dev, generator=g)
     out_idx = torch.randperm(n, generator=torch.Generator().manual_seed(2))
@@ -165,8 +166,8 @@ def orderstat_c5(dev, n=200, ratio=0.2):
         res.append({
             'kernel': 'fsagg_%s_f32' % ('coord_median' if name == 'median'
                                         else name), 'config':
-            'C5 %s n=%d P=%d k=%d' % (name, n, P, k if name != 'median' else
-                                      0), 'ms_median': med, 'ms_min': mn,
+            '%s %s n=%d P=%d k=%d' % (tag, name, n, P, k if name != 'median'
+                                      else 0), 'ms_median': med, 'ms_min': mn,
             'GBps': 4.0 * n * P / med / 1e6,
             'hbm_frac': nbytes / med / 1e6 / PEAK,
             'parity_sampled_4096_cols': ok, 'max_abs_err': err})
@@ -272,6 +273,13 @@ def main():
         for r in orderstat_c5(dev):
             print(json.dumps(r), flush=True)
         torch.cuda.empty_cache()
+    if 'orderstat_large' in which:
+        # n > 255 at the C5 byte count (4nP = 5.28 GB)
+        for n in (300, 500):
+            for r in orderstat_c5(dev, n=n, P=(200 * 6603904 // n) // 64 * 64,
+                                  tag='n>255'):
+                print(json.dumps(r), flush=True)
+            torch.cuda.empty_cache()
     if 'dropin' in which:
         for r in dropin_rules(dev):
             print(json.dumps(r), flush=True)
