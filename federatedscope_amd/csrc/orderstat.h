@@ -161,5 +161,11 @@ template <int N, int MODE>
 void launch_select(const RowSrc &rs, unsigned grid, int n, int kk,
                    float divisor, float *out, hipStream_t s);
 
+// Launch the streaming select kernel for 255 < n <= 65535
+// (orderstat_stream.hip).
+template <int MODE>
+void launch_stream(const RowSrc &rs, unsigned grid, int n, int kk,
+                   float divisor, float *out, hipStream_t s);
+
 }  // namespace os
 }  // namespace fsagg

@@ -11,8 +11,10 @@
 //    sort last).
 //  - 64 < n <= 255: range-adaptive radix select + LDS compaction
 //    (orderstat_select.hip, one translation unit per register-array size).
-//  - n > 255 (or more than 2^30 columns): bit-by-bit radix select that
-//    re-reads the column from L2.
+//  - 255 < n <= 65535: the same select streaming the column from memory in
+//    each pass (orderstat_stream.hip).
+//  - more than 65535 clients or 2^30 columns: bit-by-bit radix select that
+//    re-reads the column 64 times.
 //
 // Algorithmic bytes per coordinate: 4·n read + 4 (base) read + 4 written.
 #include "orderstat.h"
@@ -191,6 +193,8 @@ int launch(const RowSrc &rs, int nchunk, int n, int kk, float divisor,
     case 248: FSAGG_RX(248); break;
     case 256: FSAGG_RX(256); break;
     }
+  } else if (n <= 65535 && rs.numel <= (int64_t(1) << 30)) {
+    launch_stream<MODE>(rs, grid, n, kk, divisor, out, s);
   } else {
     hipLaunchKernelGGL((orderstat_generic_kernel<MODE>), dim3(grid),
                        dim3(kBlock), 0, s, rs, n, kk, divisor, out);

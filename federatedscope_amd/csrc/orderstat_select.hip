@@ -29,7 +29,7 @@
 //     the smallest bitonic network that holds every lane's list and the ranks
 //     (and the kept partial sums) read off.
 // Register budget: SEL_N values + ~40 within 256 VGPRs (2 waves per SIMD).
-#include "orderstat.h"
+#include "orderstat_sel.h"
 
 #ifndef SEL_N
 #error "compile with -DSEL_N=<keys per lane>"
@@ -38,282 +38,6 @@
 namespace fsagg {
 namespace os {
 namespace {
-
-constexpr int kSelWords = 64;  // hist/list words per lane (list: 63 + dump)
-constexpr int kSelWaves = kBlock / kWave;
-constexpr int kSelLds = kSelWords * kWave * kSelWaves;  // 64 KiB per block
-constexpr int kList = 63;      // LDS list slots per lane (slot 63: dump)
-constexpr int kMagShift = 20;  // magnitude code: bits [30:20] of |x|
-constexpr int kCodes = 128;    // codes per sign side (16 octaves)
-constexpr uint32_t kKeyPosInf = 0xFF800000u;  // ukey(+inf)
-constexpr uint32_t kKeyNegInf = 0x007FFFFFu;  // ukey(-inf)
-
-// float bits -> order-preserving key (-0 < +0), 3 ops
-__device__ __forceinline__ uint32_t ukey(uint32_t u) {
-  return u ^ (uint32_t(int32_t(u) >> 31) | 0x80000000u);
-}
-
-// Selection state of one rank: its bin is the key interval [lo, hi] holding
-// `cnt` keys, `below` keys sort before it.  lo == hi: resolved (cnt copies).
-struct RankSel {
-  uint32_t lo, hi;
-  int below, cnt;
-};
-
-// c + (a < b): the borrow of a − b carried straight into the counter
-// (v_sub_co_u32 + v_addc_co_u32, a VCC carry chain with no wait states).
-// The compiler's own form is v_cmp + s_nop 1 + v_cndmask_b32_e64 + v_add —
-// the wait states guard the e64 cndmask's read of VCC — one per value.
-__device__ __forceinline__ int add_below(int c, uint32_t a, uint32_t b) {
-  uint32_t t;
-  asm("v_sub_co_u32 %1, vcc, %2, %3\n\t"
-      "v_addc_co_u32 %0, vcc, 0, %0, vcc"
-      : "+v"(c), "=&v"(t)
-      : "v"(a), "v"(b)
-      : "vcc");
-  return c;
-}
-
-// Opaque copy barrier: keeps the compiler from hoisting per-pass key math
-// (ukey of every value) out of a pass and holding N more registers live.
-template <int N>
-__device__ __forceinline__ void fence_regs(uint32_t (&u)[N]) {
-#pragma unroll
-  for (int j = 0; j < N; ++j) asm volatile("" : "+v"(u[j]));
-}
-
-__device__ __forceinline__ bool resolved(const RankSel &s) {
-  return s.lo == s.hi;
-}
-__device__ __forceinline__ bool same_bin(const RankSel &a, const RankSel &b) {
-  return a.lo == b.lo && a.hi == b.hi;
-}
-
-// Octave digit of float bits u (monotone in the value):
-//   t = clamp(m(u) - base, 0, 127); digit = negative ? 127 - t : 128 + t
-// ((t ^ sign) + 128 with sign = -1 or 0: v_xad_u32).
-__device__ __forceinline__ uint32_t octave_digit(uint32_t u, int base) {
-  const int m = int(__builtin_amdgcn_ubfe(u, uint32_t(kMagShift), 11u));
-  const int t = min(max(m - base, 0), kCodes - 1);
-  return (uint32_t(t) ^ uint32_t(int32_t(u) >> 31)) + 128u;
-}
-
-// The key interval of octave digit d (given the launch's base).
-__device__ __forceinline__ void octave_bin(uint32_t d, int base, uint32_t &lo,
-                                           uint32_t &hi) {
-  const bool pos = d >= 128u;
-  const int t = pos ? int(d) - 128 : 127 - int(d);
-  const int mlo = t == 0 ? 0 : base + t;
-  const int mhi = t == kCodes - 1 ? 2047 : base + t;
-  // |x| bits [mlo << 20, (mhi << 20) | 0xFFFFF] (a selected bin is never
-  // empty, so 0 <= mlo <= mhi)
-  const uint32_t alo = uint32_t(max(mlo, 0)) << kMagShift;
-  const uint32_t ahi = (uint32_t(max(mhi, 0)) << kMagShift) | 0xFFFFFu;
-  // the top bins stop at ±inf, so no band [lo1, hi2] spans all 2^32 keys
-  // (NaN keys lie outside every bin; a NaN column's result is NaN anyway)
-  if (pos) {
-    lo = alo | 0x80000000u;
-    hi = min(ahi | 0x80000000u, kKeyPosInf);
-  } else {
-    lo = max(~(ahi | 0x80000000u), kKeyNegInf);
-    hi = ~(alo | 0x80000000u);
-  }
-}
-
-__device__ __forceinline__ void hist_clear(uint32_t *H, int words) {
-#pragma unroll
-  for (int w = 0; w < 64; ++w)
-    if (w < words) H[w * kWave] = 0u;
-}
-
-// The lane's LDS words by byte address: word w at hb | (w << 8) ([word][lane]
-// layout: a wave's 64 lanes hit 64 distinct banks).  hb = wave·16 KiB +
-// lane·4 has bits 8..13 clear (the LDS array is 16 KiB-aligned), so a word
-// address is one v_and_or / v_lshl_or.
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-__device__ __forceinline__ lds_u32 *lds_at(uint32_t byte) {
-  return (lds_u32 *)(uintptr_t)byte;
-}
-
-// byte counter of digit d: byte d & 3 of word d / 4
-__device__ __forceinline__ void hist_inc(uint32_t hb, uint32_t d) {
-  __hip_atomic_fetch_add(lds_at(hb | ((d << 6) & 0x3F00u)),
-                         1u << ((d << 3) & 31u), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// Locate rank r in the histogram given the word that holds it (w, x) and
-// the count before that word: returns the bin, the count below and in it.
-__device__ __forceinline__ uint32_t hist_bin(int w, uint32_t x, int before,
-                                            int r, int &below, int &count) {
-  uint32_t byte = 3;
-#pragma unroll
-  for (int b = 0; b < 3; ++b) {
-    const int c = int((x >> (8 * b)) & 255u);
-    const bool stop = byte == 3 && before + c > r;
-    byte = stop ? uint32_t(b) : byte;
-    before += (byte == 3) ? c : 0;
-  }
-  below = before;
-  count = int((x >> (8 * byte)) & 255u);
-  return uint32_t(w) * 4u + byte;
-}
-
-// Rank ra (and rb if TWO) in W histogram words (from H), in two levels:
-// the W / 4 groups of four words first (the word byte sums chained through
-// v_sad_u8's accumulator), then the four words of the group holding the
-// rank.  At either level the number of entries whose inclusive prefix count
-// is <= r is the one holding r, and the last such prefix is the count
-// before it.
-template <bool TWO, int W>
-__device__ __forceinline__ void group_find(const uint32_t *H, int ra, int rb,
-                                           int &ga, int &fa, int &gb,
-                                           int &fb) {
-  int cum = 0, na = 0, ba = 0, nb = 0, bb = 0;
-#pragma unroll
-  for (int q = 0; q < W / 4; ++q) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      cum = int(__builtin_amdgcn_sad_u8(H[(4 * q + i) * kWave], 0u,
-                                        uint32_t(cum)));
-    const bool ta = cum <= ra;
-    na += ta;
-    ba = ta ? cum : ba;
-    if (TWO) {
-      const bool tb = cum <= rb;
-      nb += tb;
-      bb = tb ? cum : bb;
-    }
-  }
-  ga = min(na, W / 4 - 1);
-  fa = ba;
-  gb = min(nb, W / 4 - 1);
-  fb = bb;
-}
-
-__device__ __forceinline__ uint32_t word_find(const uint32_t *H, int g,
-                                              int before, int r, int &below,
-                                              int &count) {
-  const uint32_t *G = H + 4 * g * kWave;
-  uint32_t x[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) x[i] = G[i * kWave];
-  int cum = before, n = 0, f = before;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    cum = int(__builtin_amdgcn_sad_u8(x[i], 0u, uint32_t(cum)));
-    const bool t = cum <= r;
-    n += t;
-    f = t ? cum : f;
-  }
-  n = min(n, 3);
-  uint32_t w = x[0];
-#pragma unroll
-  for (int i = 1; i < 4; ++i) w = n == i ? x[i] : w;
-  return hist_bin(4 * g + n, w, f, r, below, count);
-}
-
-template <bool TWO, int W>
-__device__ __forceinline__ void hist_scan(const uint32_t *H, int ra, int rb,
-                                          uint32_t &da, int &ba, int &ca,
-                                          uint32_t &db, int &bb, int &cb) {
-  int ga, fa, gb, fb;
-  group_find<TWO, W>(H, ra, rb, ga, fa, gb, fb);
-  da = word_find(H, ga, fa, ra, ba, ca);
-  if (TWO) db = word_find(H, gb, fb, rb, bb, cb);
-}
-
-// Linear refinement digit of a key interval [lo, lo + lim - 1]: rel =
-// min(key - lo, lim) (keys below lo wrap, so every key outside maps to lim),
-// digit = (rel + pad) >> sh with pad making lim + pad a multiple of 2^sh —
-// the bin's keys take digits [pad >> sh, (lim - 1 + pad) >> sh] <= 127 and
-// every key outside the bin the single digit above them (<= 128, word 32),
-// which a scan for a rank inside the bin never reaches.
-struct Refine {
-  uint32_t lo, lim, pad;
-  int sh;
-};
-
-__device__ __forceinline__ Refine refine_plan(const RankSel &s) {
-  Refine f;
-  f.lo = s.lo;
-  f.lim = s.hi - s.lo + 1u;  // <= 2^31: a bin never crosses the sign
-  int sh = max(0, 32 - __builtin_clz(f.lim | 1u) - 7);
-  if (((f.lim + (1u << sh) - 1u) >> sh) > 127u) ++sh;
-  f.sh = sh;
-  f.pad = (0u - f.lim) & ((1u << sh) - 1u);
-  return f;
-}
-
-// Narrow s to refinement digit d (count b below it, c in it).
-__device__ __forceinline__ void refine_apply(RankSel &s, const Refine &f,
-                                             bool on, uint32_t d, int b,
-                                             int c) {
-  if (!on) return;
-  const uint32_t span = f.lim - 1u;
-  const uint32_t r0 = d << f.sh;
-  const uint32_t rlo = r0 > f.pad ? r0 - f.pad : 0u;
-  const uint32_t r1 = ((d + 1u) << f.sh) - 1u - f.pad;
-  const uint32_t rhi = r1 < span ? r1 : span;
-  s.below += b;
-  s.cnt = c;
-  s.hi = f.lo + rhi;
-  s.lo = f.lo + rlo;
-}
-
-// a[idx] for a per-lane idx without dynamic register indexing: a binary
-// select tree, one lane mask per bit of idx (S − 1 v_cndmask and log2 S
-// compares, where comparing idx with every position costs S of each plus a
-// wait state per position)
-template <int S>
-__device__ __forceinline__ uint32_t tree_pick(const uint32_t (&a)[S],
-                                              int idx) {
-  uint32_t t[S];
-#pragma unroll
-  for (int i = 0; i < S; ++i) t[i] = a[i];
-#pragma unroll
-  for (int w = S / 2, b = 0; w >= 1; w /= 2, ++b) {
-    const bool up = (idx >> b) & 1;
-#pragma unroll
-    for (int k = 0; k < w; ++k) t[k] = up ? t[2 * k + 1] : t[2 * k];
-  }
-  return t[0];
-}
-
-// Sort the lane's list of `cnt` values (float bits) at LDS slots [0, cnt) by
-// key and read list positions pa and pb off it (as keys); Σ over positions
-// [lo, hi] in fp64.
-template <int S, bool SUM>
-__device__ __forceinline__ void list_select(const uint32_t *H, int cnt,
-                                            int pa, int pb, int lo, int hi,
-                                            uint32_t &va, uint32_t &vb,
-                                            double &sum) {
-  uint32_t a[S];
-#pragma unroll
-  for (int i = 0; i < S; ++i) {
-    const uint32_t x = ukey(H[i * kWave]);
-    a[i] = i < cnt ? x : kPad;
-  }
-  bitonic_sort<S>(a);
-  double acc = 0.0;
-  if (SUM) {
-    // [lo, hi] as one unsigned range test; an empty range (hi < lo) moves
-    // lo far above every position so that no i passes
-    const bool empty = hi < lo;
-    const int lo1 = empty ? (1 << 30) : lo;
-    const uint32_t span = empty ? 0u : uint32_t(hi - lo);
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-      // select in fp32, then widen (one v_cndmask, not a 64-bit pair)
-      float x = uint32_t(i - lo1) <= span ? key2f(a[i]) : 0.0f;
-      asm("" : "+v"(x));
-      acc += double(x);
-    }
-  }
-  va = tree_pick<S>(a, pa);
-  vb = tree_pick<S>(a, pb);
-  sum = acc;
-}
 
 template <int N, int MODE>
 __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(

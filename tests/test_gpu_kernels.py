@@ -99,8 +99,13 @@ def test_weighted_sum_row_order_is_reduction_order():
 
 
 @pytest.mark.parametrize('n', [1, 2, 3, 4, 7, 8, 31, 64, 65, 72, 73, 100,
-                               127, 200, 233, 250, 255, 256, 300])
+                               127, 200, 233, 250, 255, 256, 257, 300, 511,
+                               1000, 2049])
 def test_median_trimmed_all_kernels(n):
+    """Every order-statistic kernel (register network n <= 64, register
+    select 64 < n <= 255, streaming select n > 255) against the oracle on
+    ties, signed zeros and columns spanning > 16 octaves (the refinement
+    rounds)."""
     from federatedscope_amd import ops
     P = 3001
     rng = np.random.default_rng(n)
@@ -214,10 +219,10 @@ def test_typed_weighted_sum(dt):
         assert got.numpy().tobytes() == np.asarray(want).tobytes()
 
 
-@pytest.mark.parametrize('n', [9, 65, 100, 200, 255, 300])
+@pytest.mark.parametrize('n', [9, 65, 100, 200, 255, 300, 1000])
 def test_orderstat_nonfinite_columns_all_kernels(n):
     """±inf / NaN columns through every order-statistic kernel (the
-    register network, the select kernels and the generic n > 255 path)."""
+    register network, the select kernels and the streaming n > 255 path)."""
     from federatedscope_amd import ops
     P = 8
     X = np.ones((n, P), np.float32)
