@@ -487,6 +487,7 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   int tpl = 0, ksl, kstep;
   bool active, diag = false;
   int ti = 0, tj = 0;
+  bool swapped = false;  // diagonal role with its two tiles read swapped
   if constexpr (SPLIT) {
     // wave-uniform role: off-diagonal tile pairs, or diagonal tile pairs
     // (2d, 2d+1) whose two upper triangles share one accumulator set
@@ -504,6 +505,21 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
       active = ksl < pl.ksd;
       ti = 2 * (l - ksl * pl.rd);
       tj = ti + 1 < pl.nt ? ti + 1 : ti;  // odd tile count: a repeat, unused
+      // Every diagonal lane's tile ti starts at a multiple of 4 words of a
+      // staged row (ti even, TS = 10, pitch ≡ 0 mod 4), so the 32 lanes of
+      // a ds_read_b64 group meet only 16 bank pairs (2-way conflicts).  Lanes
+      // of odd k-slices read the tiles the other way round (tile tj's rows at
+      // ≡ 2 mod 4 words in the same instruction) and swap the two triangles'
+      // accumulators back after the chunk (pair_update's two halves are
+      // symmetric: acc[h][v] <-> acc[TS/2-1-h][TS-1-v]).
+      if constexpr (LDSR == 1) {
+        if (ksl & 1) {
+          const int t = ti;
+          ti = tj;
+          tj = t;
+          swapped = true;
+        }
+      }
     }
   } else {
     tpl = tid % pl.tpg;
@@ -787,6 +803,17 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   };
   if (SPLIT && diag) run(std::true_type{});
   else run(std::false_type{});
+  if constexpr (SPLIT && LDSR == 1) {
+    // the swapped diagonal lanes' triangles back into place
+#pragma unroll
+    for (int h = 0; h < TS / 2; ++h)
+#pragma unroll
+      for (int v = 2 * h + 1; v < TS; ++v) {
+        const f2 a = acc[h][v], b = acc[TS / 2 - 1 - h][TS - 1 - v];
+        acc[h][v] = swapped ? b : a;
+        acc[TS / 2 - 1 - h][TS - 1 - v] = swapped ? a : b;
+      }
+  }
 
   // sum the k-slices of each tile pair in slice order, ≤ 64 accumulators
   // at a time through LDS
