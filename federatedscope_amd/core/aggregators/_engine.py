@@ -220,27 +220,33 @@ class DeviceEngine:
         layout.pack_device(src, flat)
         return flat
 
-    def _key_table(self, layout, dicts):
-        """(ptrs [n][nseg], aligned16) when every present layout key of
-        every dict is a contiguous fp32 tensor of the layout's shape on the
-        compute device (the C++ walk of csrc/host/keytable.cpp), else
-        None."""
+    def _key_table(self, layout, dicts, virtual=False):
+        """(ptrs [n][nseg], aligned16, missing) when every present layout
+        key of every dict is a contiguous fp32 tensor of the layout's shape
+        on the compute device (the C++ walk of csrc/host/keytable.cpp), else
+        None.  ``virtual``: the device row table instead — [nseg][n]
+        virtual bases (ptr − 4·offset, 0 where absent)."""
         import numpy as np
         from ... import _lib
         dev = self.compute_device
         kl = layout.__dict__.get('_key_list')
         if kl is None:
             kl = layout.__dict__['_key_list'] = (
-                list(layout.keys), [layout.shapes[k] for k in layout.keys])
+                list(layout.keys), [layout.shapes[k] for k in layout.keys],
+                [4 * layout.offsets[k] for k in layout.keys])
         if not kl[0] or not all(isinstance(d, dict) for d in dicts):
             return None
-        res = _lib.host().key_table(dicts, kl[0], kl[1], dev.index)
+        if virtual:
+            res = _lib.host().key_table(dicts, kl[0], kl[1], dev.index, kl[2])
+        else:
+            res = _lib.host().key_table(dicts, kl[0], kl[1], dev.index)
         if res is None:
             return None
-        raw, _, aligned = res
-        return (np.frombuffer(raw, dtype=np.int64).reshape(len(dicts),
-                                                           len(kl[0])),
-                aligned)
+        raw, missing, aligned = res
+        shape = (len(kl[0]), len(dicts)) if virtual else (len(dicts),
+                                                            len(kl[0]))
+        return np.frombuffer(raw, dtype=np.int64).reshape(shape), aligned, \
+            missing
 
     def _base(self, layout, model, as_float=False):
         """The server model as the kernels' ``base`` operand: its own device
@@ -374,17 +380,20 @@ class DeviceEngine:
             layout = self._layout(d0, as_float=as_float)
             self._fast_layouts[fk] = layout
         if not layout.other:
-            kt = self._key_table(layout, dicts)
+            kt = self._key_table(layout, dicts, virtual=True)
             if kt is not None and kt[1]:
-                ptrs = kt[0]
-                gone = ops.absent(layout, ptrs)
-                if require_all and gone.any():
-                    i, s = [int(x[0]) for x in gone.nonzero()]
-                    raise KeyError('client %d lacks key %r' %
-                                   (i, layout.keys[s]))
-                return StagedSet(layout, ops.RowSet.from_pointers(
-                    layout, ptrs, self.compute_device, keepalive=(dicts, ),
-                    missing=int(gone.sum())))
+                virt, _, nmiss = kt
+                gone = 0
+                if nmiss:        # absent keys (an empty key never counts)
+                    absent = ops.absent(layout, virt.T)
+                    if require_all and absent.any():
+                        i, s = [int(x[0]) for x in absent.nonzero()]
+                        raise KeyError('client %d lacks key %r' %
+                                       (i, layout.keys[s]))
+                    gone = int(absent.sum())
+                return StagedSet(layout, ops.RowSet.from_virtual(
+                    layout, virt, self.compute_device, keepalive=(dicts, ),
+                    missing=gone))
         # staged through a device stack
         layout = self._layout(d0, as_float=as_float)
         present = [[k in d for k in layout.keys] for d in dicts]

@@ -10,15 +10,19 @@
 // the walk in Python costs ~1 us per tensor (five attribute reads each);
 // here it is one dict lookup and a few inline TensorImpl reads per tensor.
 //
-// key_table(dicts, keys, shapes, device_index)
+// key_table(dicts, keys, shapes, device_index[, offs4])
 //   dicts  list of dict (client state_dicts; OrderedDict is a dict)
 //   keys   list of str (the layout's fp32 keys, in bucket order)
 //   shapes list of tuple[int] (each key's shape, as client 0 holds it)
+//   offs4  optional list of int: each key's bucket offset in bytes
 // returns (bytes ptrs, int missing, bool aligned16) — ptrs is n*len(keys)
 // native int64 data pointers, 0 where a client lacks the key — or None when
 // any present value is not a contiguous float32 tensor of that shape on
 // cuda:device_index, or an element of dicts is not a dict.  None is not an
 // error: the caller then stages the dicts instead.
+// With offs4 the table is the device row table itself (include/fsagg.h
+// fsagg_rows): segment-major [key][client] virtual bases ptr - offs4[key]
+// (0 stays 0), so the caller uploads it as is.
 #include <Python.h>
 #include <torch/csrc/autograd/python_variable.h>
 
@@ -29,16 +33,26 @@
 namespace {
 
 PyObject *key_table(PyObject *, PyObject *args) {
-  PyObject *dicts, *keys, *shapes;
+  PyObject *dicts, *keys, *shapes, *offs = nullptr;
   int device_index;
-  if (!PyArg_ParseTuple(args, "O!O!O!i", &PyList_Type, &dicts, &PyList_Type,
-                        &keys, &PyList_Type, &shapes, &device_index))
+  if (!PyArg_ParseTuple(args, "O!O!O!i|O!", &PyList_Type, &dicts,
+                        &PyList_Type, &keys, &PyList_Type, &shapes,
+                        &device_index, &PyList_Type, &offs))
     return nullptr;
   const Py_ssize_t n = PyList_GET_SIZE(dicts);
   const Py_ssize_t nk = PyList_GET_SIZE(keys);
-  if (PyList_GET_SIZE(shapes) != nk) {
-    PyErr_SetString(PyExc_ValueError, "keys and shapes differ in length");
+  if (PyList_GET_SIZE(shapes) != nk ||
+      (offs && PyList_GET_SIZE(offs) != nk)) {
+    PyErr_SetString(PyExc_ValueError,
+                    "keys, shapes and offsets differ in length");
     return nullptr;
+  }
+  std::vector<int64_t> off4(nk, 0);
+  if (offs) {
+    for (Py_ssize_t s = 0; s < nk; ++s) {
+      off4[s] = PyLong_AsLongLong(PyList_GET_ITEM(offs, s));
+      if (off4[s] == -1 && PyErr_Occurred()) return nullptr;
+    }
   }
   std::vector<std::vector<int64_t>> shp(nk);
   for (Py_ssize_t s = 0; s < nk; ++s) {
@@ -65,9 +79,11 @@ PyObject *key_table(PyObject *, PyObject *args) {
     if (!PyDict_Check(d)) Py_RETURN_NONE;
     for (Py_ssize_t s = 0; s < nk; ++s) {
       PyObject *v = PyDict_GetItemWithError(d, PyList_GET_ITEM(keys, s));
+      // [client][key], or segment-major [key][client] with offsets
+      int64_t &slot = offs ? out[s * n + i] : out[i * nk + s];
       if (!v) {
         if (PyErr_Occurred()) return nullptr;
-        out[i * nk + s] = 0;
+        slot = 0;
         ++missing;
         continue;
       }
@@ -83,7 +99,7 @@ PyObject *key_table(PyObject *, PyObject *args) {
       const auto p = reinterpret_cast<uintptr_t>(t.data_ptr());
       if (p == 0 && t.numel() > 0) Py_RETURN_NONE;
       aligned = aligned && (p & 15u) == 0;
-      out[i * nk + s] = int64_t(p);
+      slot = p ? int64_t(p) - off4[s] : 0;
     }
   }
   PyObject *bytes = PyBytes_FromStringAndSize(buf.data(), Py_ssize_t(buf.size()));
@@ -93,8 +109,8 @@ PyObject *key_table(PyObject *, PyObject *args) {
 
 PyMethodDef kMethods[] = {
     {"key_table", key_table, METH_VARARGS,
-     "key_table(dicts, keys, shapes, device_index) -> (bytes, missing, "
-     "aligned16) or None"},
+     "key_table(dicts, keys, shapes, device_index[, offs4]) -> (bytes, "
+     "missing, aligned16) or None"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_fsagg_host",

@@ -171,12 +171,29 @@ class BucketLayout:
         return out_row
 
     def unpack(self, flat, keys=None):
-        """Views of the flat bucket, one per fp32 key, in the given order."""
-        out = OrderedDict()
-        for k in (self.keys if keys is None else keys):
-            o, m = self.offsets[k], self.numels[k]
-            out[k] = flat[o:o + m].view(self.shapes[k])
-        return out
+        """Views of the flat bucket, one per fp32 key, in the given order
+        (one as_strided per key: a third of slice + view's host time, which
+        the drop-in's result emission pays per key every call)."""
+        if flat.dim() != 1 or not flat.is_contiguous() or \
+                flat.numel() < self.numel:
+            raise ValueError('unpack needs a flat contiguous bucket of %d '
+                             'elements' % self.numel)
+        spec = self.__dict__.get('_view_spec')
+        if spec is None:
+            spec = {}
+            for k in self.keys:
+                shp = tuple(self.shapes[k])
+                st, acc = [], 1
+                for d in reversed(shp):
+                    st.append(acc)
+                    acc *= d
+                spec[k] = (shp, tuple(reversed(st)), self.offsets[k])
+            self.__dict__['_view_spec'] = spec
+        view = flat.as_strided
+        base = flat.storage_offset()
+        return OrderedDict([(k, view(spec[k][0], spec[k][1],
+                                     base + spec[k][2]))
+                            for k in (self.keys if keys is None else keys)])
 
 
 # Pinned staging buffers are shared by every HostStager of the process, so

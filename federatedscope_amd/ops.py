@@ -679,8 +679,14 @@ class RowSet:
     copy ([n][1] for a stack without absent keys, else [n][nseg])."""
 
     def __init__(self, layout, table, device, keepalive=(), aligned16=True,
-                 missing=None):
-        table = _np.ascontiguousarray(table, dtype=_np.int64)
+                 missing=None, segmajor=None):
+        if segmajor is not None:
+            # the device layout built by the caller ([nseg][n]); the host
+            # copy is its transposed view
+            segmajor = _np.ascontiguousarray(segmajor, dtype=_np.int64)
+            table = segmajor.T
+        else:
+            table = _np.ascontiguousarray(table, dtype=_np.int64)
         if table.ndim != 2 or table.shape[0] < 1:
             raise ValueError('row table must be [n][1] or [n][nseg]')
         self.layout = layout
@@ -701,7 +707,8 @@ class RowSet:
         self.aligned16 = bool(aligned16)
         self.missing = int(absent(layout, table).sum()) if missing is None \
             else int(missing)
-        self.tab = _h2d_np(table.T, self.device)
+        self.tab = _h2d_np(table.T if segmajor is None else segmajor,
+                           self.device)
         self.struct = L.Rows(self.tab.data_ptr(), self.ss, self.n,
                              self.nseg)
         self._keep = tuple(keepalive)
@@ -736,6 +743,14 @@ class RowSet:
         virt = _np.where(ptrs != 0, ptrs - offs[None, :], 0)
         return cls(layout, virt, device, keepalive=keepalive,
                    aligned16=aligned16, missing=missing)
+
+    @classmethod
+    def from_virtual(cls, layout, segmajor, device, keepalive=(),
+                     aligned16=True, missing=None):
+        """[nseg][n] virtual bases (0: absent), i.e. the device table as
+        csrc/host/keytable.cpp builds it with offsets."""
+        return cls(layout, None, device, keepalive=keepalive,
+                   aligned16=aligned16, missing=missing, segmajor=segmajor)
 
     def subset(self, sel):
         """The clients ``sel`` (indices, in the new reduction order)."""

@@ -29,16 +29,20 @@ def main():
                              for k, s in layout) for _ in range(n)]
         keys = [k for k, _ in layout]
         shapes = [s for _, s in layout]
-        ts = []
-        for _ in range(20):
-            t0 = time.perf_counter()
-            host.key_table(dicts, keys, shapes, dev.index)
-            ts.append(time.perf_counter() - t0)
-        t = min(ts)
-        print(json.dumps({'layout': name, 'clients': n, 'keys': len(keys),
-                          'us_per_call': round(t * 1e6, 1),
-                          'ns_per_tensor': round(t * 1e9 / (n * len(keys)),
-                                                 1)}), flush=True)
+        offs = [0] * len(keys)
+        for form, args in (('pointers', ()), ('virtual', (offs, ))):
+            ts = []
+            for _ in range(20):
+                t0 = time.perf_counter()
+                host.key_table(dicts, keys, shapes, dev.index, *args)
+                ts.append(time.perf_counter() - t0)
+            t = min(ts)
+            print(json.dumps({'layout': name, 'clients': n,
+                              'keys': len(keys), 'form': form,
+                              'us_per_call': round(t * 1e6, 1),
+                              'ns_per_tensor': round(
+                                  t * 1e9 / (n * len(keys)), 1)}),
+                  flush=True)
 
 
 if __name__ == '__main__':
