@@ -6,23 +6,28 @@
 // One lane owns one coordinate.  A column of n > 255 values no longer fits a
 // lane's registers, and the register kernel's byte counters would overflow,
 // so each pass re-reads the column (coalesced: one 256-B row segment per
-// wave-instruction, 16 rows in flight per lane; plain loads, so the later
+// wave-instruction, 32 rows in flight per lane; plain loads, so the later
 // passes hit the caches where the workgroup's rows are still resident):
-//  1. |x|max of the column (flags NaN/inf) and the init coordinate;
+//  1. the largest finite |x| of the first 64 rows (the digit's base: any
+//     base gives exact bins, the sample only sets how finely they split the
+//     bulk) and the init coordinate;
 //  2. a histogram of a 128-bin octave digit (4 codes per octave, 16 octaves
-//     below |x|max's, per sign side) in 16-bit LDS counters — the same 64
+//     below the base, per sign side) in 16-bit LDS counters — the same 64
 //     LDS words per lane as the register kernel's 256 byte counters —
-//     places both ranks;
+//     places both ranks (and flags NaN/inf);
 //  3. while the two rank bins would overflow the 63-slot list, the larger
 //     is refined by a 64-bin linear digit of its key interval (every round
 //     shrinks it 64-fold; rare);
 //  4. one compaction pass lists both bins' values (and, for the trimmed
 //     mean, sums every value strictly between them in fp64); the list is
 //     sorted and the ranks read off, as in the register kernel.
-// Three column reads in the common case, against the 2·32 of the bit-by-bit
-// select it replaces (orderstat.hip orderstat_generic_kernel, kept for
-// n > 65535).  Algorithmic bytes per coordinate: 4·n + 4 read, 4 written.
+// Two column reads (and 64 rows) in the common case, against the 2·32 of
+// the bit-by-bit select it replaces (orderstat.hip
+// orderstat_generic_kernel, kept for n > 65535).  Algorithmic bytes per coordinate: 4·n + 4 read, 4 written.
+#include <cstdlib>
+
 #include "orderstat_sel.h"
+
 
 namespace fsagg {
 namespace os {
@@ -31,7 +36,7 @@ namespace {
 constexpr int kStMagShift = 21;  // magnitude code: bits [30:21] of |x|
 constexpr int kStCodes = 64;     // codes per sign side (16 octaves)
 constexpr int kStRefineBins = 64;
-constexpr int kStUnroll = 16;    // rows in flight per lane
+constexpr int kStSample = 64;    // rows that set the digit's base
 
 __device__ __forceinline__ uint32_t st_digit(uint32_t u, int base) {
   const int m = int(__builtin_amdgcn_ubfe(u, uint32_t(kStMagShift), 10u));
@@ -126,27 +131,39 @@ __device__ __forceinline__ Refine st_refine_plan(const RankSel &s) {
   return f;
 }
 
-// f(u) for the lane's n column values (raw float bits) in row order
-template <typename F>
-__device__ __forceinline__ void stream_column(const float *const *rows, int n,
-                                              uint32_t off, F &&f) {
-  typedef __attribute__((address_space(1))) const uint32_t gu32;
-  int j = 0;
-#pragma unroll 1
-  for (; j + kStUnroll <= n; j += kStUnroll) {
-    uint32_t u[kStUnroll];
-#pragma unroll
-    for (int i = 0; i < kStUnroll; ++i)
-      u[i] = *(gu32 *)((gchar *)row_at(rows, j + i) + off * 4u);
-#pragma unroll
-    for (int i = 0; i < kStUnroll; ++i) f(u[i]);
-  }
-#pragma unroll 1
-  for (; j < n; ++j)
-    f(*(gu32 *)((gchar *)row_at(rows, j) + off * 4u));
+// f(u) for the lane's n column values (raw float bits) in row order.
+// U loads in flight per lane (the kernel's LDS caps it at 2 waves
+// per SIMD, so the bytes in flight per CU come from this depth); the last
+// partial batch re-reads row n - 1 in its unused slots and skips them.
+typedef __attribute__((address_space(1))) const uint32_t gu32;
+__device__ __forceinline__ uint32_t col_at(const float *const *rows, int j,
+                                           uint32_t off) {
+  return *(gu32 *)((gchar *)row_at(rows, j) + off * 4u);
 }
 
-template <int MODE>
+template <int U, typename F>
+__device__ __forceinline__ void stream_column(const float *const *rows, int n,
+                                              uint32_t off, F &&f) {
+  int j = 0;
+#pragma unroll 1
+  for (; j + U <= n; j += U) {
+    uint32_t u[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) u[i] = col_at(rows, j + i, off);
+#pragma unroll
+    for (int i = 0; i < U; ++i) f(u[i]);
+  }
+  if (j < n) {
+    uint32_t u[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) u[i] = col_at(rows, min(j + i, n - 1), off);
+#pragma unroll
+    for (int i = 0; i < U; ++i)
+      if (j + i < n) f(u[i]);
+  }
+}
+
+template <int MODE, int U>
 __global__ __launch_bounds__(kBlock) void orderstat_stream_kernel(
     RowSrc rs, int n, int kk, float divisor, float *__restrict__ out) {
   __shared__ __attribute__((aligned(16384))) uint32_t lds[kSelLds];
@@ -160,23 +177,29 @@ __global__ __launch_bounds__(kBlock) void orderstat_stream_kernel(
   // coordinates < 2^30 (launch); dead lanes re-read the chunk's first
   const uint32_t off = uint32_t(live ? p : br.lo);
 
-  // 1. |x|max (and NaN/inf)
-  uint32_t amax = 0u;
+  // 1. the digit's reference magnitude: the largest finite |x| of the
+  // first kStSample rows.  Any base gives exact bins (the top digit runs
+  // up to +-inf, the bottom one down to 0), the sample only sets how finely
+  // the bulk is split; values above it land in the top bins.
+  uint32_t smax = 0u;
   const float bval = br.base ? ld_nt(br.base, off) : 0.0f;
-  stream_column(rows, n, off,
-                [&](uint32_t u) { amax = max(amax, u & 0x7FFFFFFFu); });
-  const bool nan = amax > 0x7F800000u;
-  const bool nonfinite = amax >= 0x7F800000u;
-  const int obase = int(amax >> kStMagShift) - (kStCodes - 1);
+  stream_column<U>(rows, min(n, kStSample), off, [&](uint32_t u) {
+    const uint32_t a = u & 0x7FFFFFFFu;
+    smax = a < 0x7F800000u ? max(smax, a) : smax;
+  });
+  const int obase = int(smax >> kStMagShift) - (kStCodes - 1);
   const int r1 = MODE == kMedian ? (n - 1) / 2 : kk;
   const int r2 = MODE == kMedian ? n / 2 : n - kk - 1;
 
-  // 2. octave-digit histogram: both ranks' bins
+  // 2. octave-digit histogram: both ranks' bins (and NaN/inf over all rows)
   RankSel s1, s2;
+  uint32_t amax = 0u;
   {
     hist_clear(H, 64);
-    stream_column(rows, n, off,
-                  [&](uint32_t u) { hist16_inc(hb, st_digit(u, obase)); });
+    stream_column<U>(rows, n, off, [&](uint32_t u) {
+      amax = max(amax, u & 0x7FFFFFFFu);
+      hist16_inc(hb, st_digit(u, obase));
+    });
     uint32_t d1, d2;
     int b1, c1, b2, c2;
     hist16_find2(H, r1, r2, d1, b1, c1, d2, b2, c2);
@@ -187,6 +210,8 @@ __global__ __launch_bounds__(kBlock) void orderstat_stream_kernel(
     s2.below = b2;
     s2.cnt = c2;
   }
+  const bool nan = amax > 0x7F800000u;
+  const bool nonfinite = amax >= 0x7F800000u;
 
   // 3. refine while the two bins would overflow the list
   bool shared = same_bin(s1, s2);
@@ -199,7 +224,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_stream_kernel(
     const bool pick2 = list2 && (!list1 || s2.cnt > s1.cnt);
     const Refine f = st_refine_plan(pick2 ? s2 : s1);
     hist_clear(H, 33);
-    stream_column(rows, n, off, [&](uint32_t u) {
+    stream_column<U>(rows, n, off, [&](uint32_t u) {
       const uint32_t rel = min(ukey(u) - f.lo, f.lim);
       hist16_inc(hb, (rel + f.pad) >> f.sh);
     });
@@ -225,7 +250,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_stream_kernel(
       const uint32_t lo = list1 ? s1.lo : s2.lo;
       const uint32_t w =
           (list1 || list2) ? (list2 ? s2.hi : s1.hi) - lo + 1u : 0u;
-      stream_column(rows, n, off, [&](uint32_t u) {
+      stream_column<U>(rows, n, off, [&](uint32_t u) {
         *lds_at(hb | (uint32_t(c) << 8)) = u;  // a miss: overwritten
         c = add_below(c, ukey(u) - lo, w);
       });
@@ -234,7 +259,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_stream_kernel(
       const uint32_t w1 = list1 ? s1.hi - s1.lo + 1u : 0u;
       const uint32_t wm = shared ? 0u : s2.lo - (s1.hi + 1u);
       const uint32_t wb = w1 + wm + (list2 ? s2.hi - s2.lo + 1u : 0u);
-      stream_column(rows, n, off, [&](uint32_t u) {
+      stream_column<U>(rows, n, off, [&](uint32_t u) {
         const uint32_t rel = ukey(u) - A;
         const bool inm = rel - w1 < wm;
         float x = inm ? __uint_as_float(u) : 0.0f;
@@ -299,11 +324,29 @@ __global__ __launch_bounds__(kBlock) void orderstat_stream_kernel(
 
 }  // namespace
 
+// rows in flight per lane: 32 (FSAGG_OS_UNROLL=16|64 for A/B runs)
+static int stream_unroll() {
+  static int u = -1;
+  if (u < 0) {
+    const char *e = getenv("FSAGG_OS_UNROLL");
+    u = e ? atoi(e) : 32;
+    if (u != 16 && u != 64) u = 32;
+  }
+  return u;
+}
+
 template <int MODE>
 void launch_stream(const RowSrc &rs, unsigned grid, int n, int kk,
                    float divisor, float *out, hipStream_t s) {
-  hipLaunchKernelGGL((orderstat_stream_kernel<MODE>), dim3(grid),
-                     dim3(kBlock), 0, s, rs, n, kk, divisor, out);
+#define FSAGG_ST(U)                                                         \
+  hipLaunchKernelGGL((orderstat_stream_kernel<MODE, U>), dim3(grid),       \
+                     dim3(kBlock), 0, s, rs, n, kk, divisor, out)
+  switch (stream_unroll()) {
+    case 16: FSAGG_ST(16); break;
+    case 64: FSAGG_ST(64); break;
+    default: FSAGG_ST(32); break;
+  }
+#undef FSAGG_ST
 }
 
 template void launch_stream<kMedian>(const RowSrc &, unsigned, int, int,

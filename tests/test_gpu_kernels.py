@@ -114,6 +114,10 @@ def test_median_trimmed_all_kernels(n):
     X[:, 6] = np.float32(rng.integers(0, 3, n))  # heavy ties
     X[:, 7] = -0.0
     X[: max(1, n // 10), 8] *= 1e30
+    # large values only past the first 64 rows (the streaming kernel's
+    # base sample) and a column whose magnitudes grow down the rows
+    X[n - max(1, n // 5):, 9] *= 1e6
+    X[:, 10] = np.float32(np.linspace(-1, 1, n) * np.logspace(0, 20, n))
     slab = torch.from_numpy(X).cuda()
     rows = ops.RowTable.from_slab(slab)
     out = torch.empty(P, device='cuda')
@@ -124,7 +128,7 @@ def test_median_trimmed_all_kernels(n):
     # -0/+0 ties may pick either zero; compare values, and bits elsewhere
     assert np.array_equal(got, want)
     assert got[np.arange(P) != 7].tobytes() == \
-        want[np.arange(P) != 7].tobytes()
+        want[np.arange(P) != 7].tobytes(), n
     for ratio in (0.0, 0.1, 0.2, 0.45):
         k = int(n * ratio)
         if 2 * k >= n:
