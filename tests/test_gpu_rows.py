@@ -112,7 +112,7 @@ def test_weighted_sum_rows_missing_keys_one_launch():
         ops.coord_median_rows(rs, out)
 
 
-@pytest.mark.parametrize('n', [7, 64, 100, 200])
+@pytest.mark.parametrize('n', [7, 64, 100, 200, 300])
 def test_order_statistics_rows_match_flat(n):
     from federatedscope_amd import ops
     sizes = [1, 1023, 5, 70_001, 3, 257]
