@@ -655,12 +655,28 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
       int s = 0;
       if constexpr (LDSR == 1) {
         typedef __attribute__((address_space(3))) const float lds_f;
-        do {
+        auto at = [](const float *p) {
+          return uint32_t(uintptr_t((lds_f *)p));
+        };
+        // every coordinate ksl + s·kstep of the first len / kstep steps
+        // lies inside the stage: those steps take no zero-row select, only
+        // an address increment (idle lanes read the zero row throughout)
+        const int plain = len / kstep;  // wave-uniform
+        if (plain > 0) {
+          const float *col = active ? buf + ksl * pl.ldsp : zrow;
+          uint32_t ca = at(col + ti * TS), cb = at(col + tj * TS);
+          const uint32_t inc = active ? uint32_t(kstep * pl.ldsp * 4) : 0u;
+          do {
+            pair_step_dsr<TS, decltype(role)::value>(acc, ca, cb);
+            ca += inc;
+            cb += inc;
+          } while (++s < plain);
+        }
+        for (; s < steps; ++s) {
           const float *col = col_of(s);
-          const uint32_t ca = uint32_t(uintptr_t((lds_f *)(col + ti * TS)));
-          const uint32_t cb = uint32_t(uintptr_t((lds_f *)(col + tj * TS)));
-          pair_step_dsr<TS, decltype(role)::value>(acc, ca, cb);
-        } while (++s < steps);
+          pair_step_dsr<TS, decltype(role)::value>(acc, at(col + ti * TS),
+                                                   at(col + tj * TS));
+        }
         return;
       }
       do {  // len >= 1: at least one step
