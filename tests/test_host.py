@@ -74,6 +74,32 @@ def test_host_extension_key_table_without_gpu():
     assert raw == b'' and missing == 0 and aligned
     with pytest.raises(ValueError):
         h.key_table(d, ['a'], [], 0)
+    # the device-table form (per-key byte offsets): same checks
+    assert h.key_table(d, ['a', 'b'], [(3, ), (2, 2)], 0, [0, 64]) is None
+    raw, missing, aligned = h.key_table(d, [], [], 0, [])
+    assert raw == b'' and missing == 0 and aligned
+    with pytest.raises(ValueError):
+        h.key_table(d, ['a', 'b'], [(3, ), (2, 2)], 0, [0])
+
+
+def test_unpack_views_of_a_row():
+    """BucketLayout.unpack on a slab row (a view with a storage offset):
+    each key's view starts at the row's own offset, and a bucket shorter
+    than the layout is refused."""
+    from federatedscope_amd.layout import BucketLayout
+    tmpl = OrderedDict([('a', torch.zeros(3)), ('b', torch.zeros(5, 7)),
+                        ('s', torch.zeros(()))])
+    lay = BucketLayout(tmpl)
+    slab = torch.arange(3 * lay.numel, dtype=torch.float32).view(3, -1)
+    row = slab[1]
+    v = lay.unpack(row)
+    for k in lay.keys:
+        o, m = lay.offsets[k], lay.numels[k]
+        assert v[k].shape == tmpl[k].shape
+        assert torch.equal(v[k].reshape(-1), row[o:o + m])
+    assert v['b'].data_ptr() == row[lay.offsets['b']:].data_ptr()
+    with pytest.raises(ValueError):
+        lay.unpack(row[:lay.numel - 1])
 
 
 def test_bucket_layout_alignment_and_dtypes():
