@@ -1,4 +1,5 @@
-"""Multi-rank sharding logic on CPU (gloo, world_size 2).
+"""Multi-rank sharding logic on CPU (gloo, world_size 2; the pipelined
+assembly also at 4 and 8 ranks).
 
 The per-rank compute here is the CPU oracle (test infrastructure standing in
 for the rank's GPU kernel); what is under test is the product's sharding
@@ -153,12 +154,14 @@ def _assembly_worker(rank, world, port, q, P, chunks):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('P,chunks', [(1000, 3), (37, 4), (4096, 1)])
-def test_pipelined_assembly_world2(P, chunks):
+@pytest.mark.parametrize('world,P,chunks', [(2, 1000, 3), (2, 37, 4),
+                                            (2, 4096, 1), (4, 1000, 3),
+                                            (8, 5003, 4), (8, 37, 2)])
+def test_pipelined_assembly_world2(world, P, chunks):
     """Block-cyclic pieces + in-place all-gather per round reproduce the
     single-device FedAvg bit for bit, ragged tails and empty pieces
-    included; every coordinate is computed by exactly one rank."""
-    world = 2
+    included; every coordinate is computed by exactly one rank (world 2, and
+    the 4- and 8-rank plans the driver's multi-GPU runs use)."""
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
