@@ -247,6 +247,10 @@ def main():
     ap.add_argument('--chunks', type=int, default=0,
                     help='pipeline rounds of the assembly (0: 1 on one GPU, '
                          '4 otherwise)')
+    ap.add_argument('--streams', type=int, default=0,
+                    help='side streams the pipeline pieces round-robin over '
+                         '(0: by piece size, core/sharding.py SMALL_PIECE; '
+                         '1: all on the current stream)')
     ap.add_argument('--cpu-clients', type=int, default=20,
                     help='clients (full width) timed on the CPU baseline')
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -271,14 +275,14 @@ def main():
     world, rank, dev = D.world, D.rank, D.dev
     n, P = args.clients, args.params
     chunks = args.chunks or (1 if world == 1 else 4)
-    pa = PipelinedAssembly(P, chunks=chunks)
+    pa = PipelinedAssembly(P, chunks=chunks, streams=args.streams or None)
     sizes = sample_sizes(n)
     weights = fedavg_weights(sizes)
     w_dev = torch.tensor(weights, dtype=torch.float32, device=dev)
     log('rank %d/%d on %s: %d clients x %d params, %d round(s) of %d-param '
-        'pieces (%.2f GB per rank)' %
+        'pieces on %d stream(s) (%.2f GB per rank)' %
         (rank, world, torch.cuda.get_device_name(dev), n, P, chunks, pa.pc,
-         4.0 * n * pa.local_numel() / 1e9))
+         pa.streams, 4.0 * n * pa.local_numel() / 1e9))
 
     # this rank's pieces of every client: global coordinates [lo, hi) of
     # the same counter-hash model at every N
@@ -290,7 +294,6 @@ def main():
         pieces.append((slab, ops.RowTable.from_slab(slab,
                                                     numel=max(hi - lo, 1))))
     out = torch.empty(pa.padded, dtype=torch.float32, device=dev)
-    stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize()
 
     # per-launch HIP events on the launch stream (the roofline's kernel time)
@@ -299,11 +302,14 @@ def main():
 
     def compute(j, lo, hi, view):
         if record[0]:
+            # on the stream the piece is launched on (a side stream when the
+            # pipeline uses them)
+            st = torch.cuda.current_stream(dev)
             a = torch.cuda.Event(enable_timing=True)
             b = torch.cuda.Event(enable_timing=True)
-            a.record(stream)
+            a.record(st)
             ops.weighted_sum(pieces[j][1], w_dev, view)
-            b.record(stream)
+            b.record(st)
             events.append((a, b, hi - lo))
         else:
             ops.weighted_sum(pieces[j][1], w_dev, view)
@@ -435,7 +441,8 @@ def main():
                 'clients': n,
                 'params': P,
                 'parallelism': ('param-range x%d, %d pipelined all-gather '
-                                'rounds' % (world, chunks)) if world > 1
+                                'rounds on %d stream(s)' %
+                                (world, chunks, pa.streams)) if world > 1
                 else 'single GPU',
             },
             'roofline': {

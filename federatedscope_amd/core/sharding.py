@@ -16,6 +16,7 @@ exchanges are:
 Backend-agnostic: the collectives are plain torch.distributed calls, RCCL
 ("nccl") over xGMI on the GPU node, gloo in the CPU tests.
 """
+import contextlib
 import math
 
 import torch
@@ -24,6 +25,7 @@ import torch.distributed as dist
 from .. import ops
 
 ALIGN = 64  # elements (256 B): shard boundaries keep rows 16-B aligned
+_nullctx = contextlib.nullcontext
 
 
 def shard_ranges(numel, world, align=ALIGN):
@@ -165,9 +167,21 @@ class PipelinedAssembly:
     single-GPU reduction; the only traffic is the output itself (4·P bytes,
     ring all-gather over xGMI)."""
 
-    def __init__(self, numel, chunks=4, group=None, align=ALIGN, comm=None):
+    # Pieces below this many coordinates run on two side streams: piece j + 1
+    # starts while piece j's last workgroups drain.  One GPU's share of the
+    # 100 x 25M model at 8 GPUs (4 pieces of 781k): 0.239 against 0.279 ms;
+    # at 4 GPUs (1.56M pieces) one stream is faster (0.400 against 0.425 ms),
+    # and larger pieces only compete for the CUs.
+    SMALL_PIECE = 1 << 20
+
+    def __init__(self, numel, chunks=4, group=None, align=ALIGN, comm=None,
+                 streams=None):
         if chunks < 1:
             raise ValueError('chunks must be >= 1')
+        if streams is not None and streams < 1:
+            raise ValueError('streams must be >= 1')
+        self._streams = streams       # None: by piece size (SMALL_PIECE)
+        self._side = {}
         self.comm = comm if comm is not None else Comm(group)
         self.group = self.comm.group
         self.world = self.comm.world
@@ -178,6 +192,8 @@ class PipelinedAssembly:
         self.pc = int(math.ceil(self.numel / per / align)) * align \
             if self.numel else align
         self.padded = self.pc * per
+        self.streams = int(self._streams) if self._streams is not None else (
+            2 if self.chunks > 1 and self.pc < self.SMALL_PIECE else 1)
 
     def piece(self, j, r=None):
         """Global [lo, hi) of piece (j, r) (empty past numel)."""
@@ -204,17 +220,33 @@ class PipelinedAssembly:
                              (self.padded, out.numel()))
         works = []
         W, pc = self.world, self.pc
+        side = None
+        if self.streams > 1 and self.chunks > 1 and out.is_cuda:
+            side = self._side.get(out.device)
+            if side is None:
+                side = self._side[out.device] = [
+                    torch.cuda.Stream(out.device)
+                    for _ in range(self.streams)]
+            cur = torch.cuda.current_stream(out.device)
+            for st in side:
+                st.wait_stream(cur)
         for j in range(self.chunks):
             lo, hi = self.piece(j)
             slot = (j * W + self.rank) * pc
-            if hi > lo:
-                compute(j, lo, hi, out[slot:slot + (hi - lo)])
-            if W > 1:
-                w = self.comm.all_gather_into(
-                    out[j * W * pc:(j + 1) * W * pc], out[slot:slot + pc],
-                    async_op=True)
-                if w is not None:
-                    works.append(w)
+            with (torch.cuda.stream(side[j % len(side)]) if side
+                  else _nullctx()):
+                if hi > lo:
+                    compute(j, lo, hi, out[slot:slot + (hi - lo)])
+                if W > 1:
+                    # the collective waits for the piece's own stream
+                    w = self.comm.all_gather_into(
+                        out[j * W * pc:(j + 1) * W * pc],
+                        out[slot:slot + pc], async_op=True)
+                    if w is not None:
+                        works.append(w)
+        if side:
+            for st in side:
+                cur.wait_stream(st)
         for w in works:
             w.wait()
         return out[:self.numel]
