@@ -246,7 +246,7 @@ def main():
                          'over the GPUs')
     ap.add_argument('--chunks', type=int, default=0,
                     help='pipeline rounds of the assembly (0: 1 on one GPU, '
-                         '4 otherwise)')
+                         '8 on two, 4 otherwise)')
     ap.add_argument('--streams', type=int, default=0,
                     help='side streams the pipeline pieces round-robin over '
                          '(0: by piece size, core/sharding.py SMALL_PIECE; '
@@ -274,7 +274,11 @@ def main():
     D = Dist(args.gpus, args.backend)
     world, rank, dev = D.world, D.rank, D.dev
     n, P = args.clients, args.params
-    chunks = args.chunks or (1 if world == 1 else 4)
+    # rounds: the last round's gather is exposed.  Two GPUs share one
+    # xGMI link pair, so their gather is slowest: 8 rounds (pieces of 1.56M
+    # parameters still reduce at the one-launch rate); from 4 GPUs up the
+    # pieces would shrink below that, 4 rounds
+    chunks = args.chunks or (1 if world == 1 else 8 if world == 2 else 4)
     pa = PipelinedAssembly(P, chunks=chunks, streams=args.streams or None)
     sizes = sample_sizes(n)
     weights = fedavg_weights(sizes)
