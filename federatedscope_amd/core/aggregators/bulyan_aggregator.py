@@ -24,7 +24,10 @@ class BulyanAggregator(ClientsAvgAggregator):
         st = self._stage_all(models)
         layout = st.layout
         n = len(models)
-        D = self._pairdist(st).cpu()
+        D = self._pairdist(st)
+        # the init model's table is built while the distance kernels run
+        base = self._base(layout, self.model.state_dict(), as_float=True)
+        D = D.cpu()
         scores = krum_scores(D, self.byzantine_node_num)
         index_order = torch.sort(scores)[1].numpy()
         keep = n - int(2 * self.sample_client_rate * self.byzantine_node_num)
@@ -32,7 +35,6 @@ class BulyanAggregator(ClientsAvgAggregator):
         self.last_selection = sel
         k = int(self.sample_client_rate * self.byzantine_node_num)
         gamma = len(sel) - 2 * k
-        base = self._base(layout, self.model.state_dict(), as_float=True)
         out = self._run_pieces(st.subset(sel), lambda rs, o, lo, hi:
                                ops.trimmed_mean_rows(rs, k, o, divisor=gamma,
                                                      base=base, lo=lo, hi=hi))

@@ -160,9 +160,19 @@ class OnlineClientsAvgAggregator(ClientsAvgAggregator):
             if k in model_params and k not in self._m_other and \
                     param2tensor(model_params[k]).dtype == torch.float32:
                 fast.append(k)
-        if fast:
-            lay.pack_device(OrderedDict(
-                (k, param2tensor(model_params[k])) for k in fast), self._x)
+        dev = self._m.device
+        ups = {k: param2tensor(model_params[k]) for k in fast}
+        if fast and all(t.device == dev and t.is_contiguous() and
+                        t.data_ptr() % 16 == 0 for t in ups.values()):
+            # uploads already on the device: each key's running mean reads
+            # the upload in place (12 B per parameter, no packing copy)
+            for k in fast:
+                o, m = lay.offsets[k], lay.numels[k]
+                if m:            # an empty key's tensor may have no storage
+                    ops.online_inc(self._m[o:o + m], ups[k].reshape(-1),
+                                   self.cnt, sample_size)
+        elif fast:
+            lay.pack_device(OrderedDict((k, ups[k]) for k in fast), self._x)
             if len(fast) == len(lay.keys):
                 ops.online_inc(self._m, self._x, self.cnt, sample_size)
             else:

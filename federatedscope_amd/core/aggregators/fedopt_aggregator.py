@@ -125,7 +125,25 @@ class FedOptAggregator(ClientsAvgAggregator):
                 raise NotImplementedError(
                     'FedOpt on %s parameter %r' % (extra[k].dtype, k))
         dev = self.compute_device
-        if step_keys:
+        inplace = bool(step_keys) and all(
+            named[k].device == dev and named[k].dtype == torch.float32 and
+            named[k].is_contiguous() and named[k].data_ptr() % 16 == 0
+            for k in step_keys)
+        if inplace:
+            # parameters already on the compute device: the optimizer steps
+            # them in place (as torch.optim's step does), no bucket copy of
+            # the model in or out; the state stays bucket-shaped
+            st = self._states(self._state, layout.signature(), avg)
+            for k in step_keys:
+                o, m = layout.offsets[k], layout.numels[k]
+                for t in (avg, st[0]):
+                    _check_f32_cuda(t[o:o + m], 'FedOpt bucket')
+                self._step(lib.fsagg_server_opt_step_f32,
+                           named[k].data.view(-1), avg[o:o + m],
+                           [t[o:o + m] if t is not None else None
+                            for t in st[:3]] + [st[3]])
+            st[3] += 1
+        elif step_keys:
             param = self._bucket(layout, OrderedDict(
                 (k, named[k].detach() if k in named else torch.zeros(
                     layout.shapes[k])) for k in layout.keys))

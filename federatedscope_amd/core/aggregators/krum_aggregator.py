@@ -47,15 +47,19 @@ class KrumAggregator(ClientsAvgAggregator):
         return krum_scores(D, self.byzantine_node_num)
 
     def _krum_device(self, models, agg_num):
-        D, st = self.distance_matrix(models)
+        st = self._stage_all(models)
         layout = st.layout
+        D = self._pairdist(st)
+        # host work that does not need the selection runs while the
+        # distance kernels do (the .cpu() below waits for them)
+        base = self._base(layout, self.model.state_dict(), as_float=True)
+        D = D.cpu()
         scores = krum_scores(D, self.byzantine_node_num)
         index_order = torch.sort(scores)[1].numpy()
         sel = [int(i) for i in index_order[:agg_num]]
         self.last_selection = sel
         sizes = [models[i][0] for i in sel]
         weights = fedavg_weights(sizes, self.cfg.federate.ignore_weight)
-        base = self._base(layout, self.model.state_dict(), as_float=True)
         out = self._run_pieces(st.subset(sel), lambda rs, o, lo, hi:
                                ops.weighted_sum_rows(rs, weights, o,
                                                      base=base, lo=lo, hi=hi))

@@ -218,18 +218,21 @@ class ParamModel(torch.nn.Module):
             self.register_parameter(k, torch.nn.Parameter(to_torch(v, 'cpu')))
 
 
+@pytest.mark.parametrize('model_dev', ['cpu', 'cuda'])
 @pytest.mark.parametrize('opt', ['SGD', 'SGDm', 'Adam', 'AdamAms',
                                  'SGDm64', 'Adam64'])
-def test_fedopt_chain(opt):
+def test_fedopt_chain(opt, model_dev):
     """Three chained FedOpt rounds (optimizer state carried across rounds)
     against the reference (torch.optim on CPU): tolerance-pinned, the
-    reference's vectorised fmadd arithmetic being ISA-dependent."""
+    reference's vectorised fmadd arithmetic being ISA-dependent.  A model on
+    the GPU has its fp32 parameters stepped in place."""
     from federatedscope_amd.core.aggregators import FedOptAggregator
     metas = [load_case('fedopt_%s_%d' % (opt, r)) for r in range(3)]
     meta0, _, _, init, _ = metas[0]
     c = cfg()
     c.fedopt = SimpleNamespace(optimizer=dict(meta0['opt']), annealing=False)
-    agg = FedOptAggregator(config=c, model=ParamModel(init))
+    model = ParamModel(init).to(model_dev)
+    agg = FedOptAggregator(config=c, model=model)
     for r, (meta, clients, out, _, _) in enumerate(metas):
         got = agg.aggregate({'client_feedback': feedback(clients),
                              'recover_fun': None})
