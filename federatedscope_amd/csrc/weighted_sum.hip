@@ -43,6 +43,33 @@ __device__ __forceinline__ f4 ld4(const f4 *p) {
   }
 }
 
+// One client's chunk row as a raw buffer (wave-uniform base and byte count):
+// each 16-B load is buffer_load_dwordx4 v_off, s[rsrc], s_off nt — the lane
+// offset in one VGPR and the per-v displacement on the scalar side, where
+// global loads of a table-held row pointer need a 64-bit VALU add (and its
+// VCC carry) per load.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const float *p,
+                                                           int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p), short(0),
+                                           bytes, 0x00020000);
+}
+__device__ __forceinline__ f4 ld4_buf(__amdgpu_buffer_rsrc_t r, uint32_t voff,
+                                      uint32_t soff) {
+  // aux 2: non-temporal (streamed once)
+  return __builtin_bit_cast(
+      f4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 2));
+}
+// f4 column v of a chunk row: a whole chunk puts the displacement in the
+// scalar offset; a partial chunk (GUARD) keeps it in the vector offset, the
+// part of the address the range check covers, so columns past the chunk
+// read 0 instead of whatever follows it
+template <bool GUARD>
+__device__ __forceinline__ f4 ld4_rowv(__amdgpu_buffer_rsrc_t r,
+                                       uint32_t loff, int v) {
+  const uint32_t d = uint32_t(v) * uint32_t(kBlock) * 16u;
+  return GUARD ? ld4_buf(r, loff + d, 0u) : ld4_buf(r, loff, d);
+}
+
 __device__ __forceinline__ f4 mul4(f4 a, float s) {
   return f4{mul_rn(a.x, s), mul_rn(a.y, s), mul_rn(a.z, s), mul_rn(a.w, s)};
 }
@@ -258,13 +285,15 @@ __device__ __forceinline__ void wsum_rows_chunk(
   int i0 = 0;
   while (i0 < n && rows[i0] == nullptr) ++i0;
   f4 acc[V];
+  const uint32_t loff = uint32_t(threadIdx.x) * 16u;   // lane byte offset
+  const int cbytes = nvec * 16;                        // the chunk's f4s
   if (i0 < n) {
-    const f4 *r = reinterpret_cast<const f4 *>(rows[i0] + lo);
+    const __amdgpu_buffer_rsrc_t r = row_rsrc(rows[i0] + lo, cbytes);
     const float w0 = w[i0];
     const float s0 = PRE ? pre[i0] : 1.0f;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-      f4 x = ok[v] ? ld4<true>(r + idx[v]) : f4{0.0f, 0.0f, 0.0f, 0.0f};
+      f4 x = ld4_rowv<GUARD>(r, loff, v);
       if (PRE) x = mul4(x, s0);
       acc[v] = mul4(x, w0);
     }
@@ -275,11 +304,10 @@ __device__ __forceinline__ void wsum_rows_chunk(
   for (int i = i0 + 1; i < n; ++i) {
     const float *row = rows[i];
     if (row == nullptr) continue;
-    const f4 *r = reinterpret_cast<const f4 *>(row + lo);
+    const __amdgpu_buffer_rsrc_t r = row_rsrc(row + lo, cbytes);
     f4 x[V];
 #pragma unroll
-    for (int v = 0; v < V; ++v)
-      x[v] = ok[v] ? ld4<true>(r + idx[v]) : f4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int v = 0; v < V; ++v) x[v] = ld4_rowv<GUARD>(r, loff, v);
     const float wi = w[i];
     const float s = PRE ? pre[i] : 1.0f;
 #pragma unroll
