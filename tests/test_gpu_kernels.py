@@ -167,7 +167,7 @@ def test_orderstat_nonfinite_columns():
         np.isnan(t[3])
 
 
-@pytest.mark.parametrize('n', [2, 3, 9, 50, 64, 100, 200])
+@pytest.mark.parametrize('n', [2, 3, 9, 21, 25, 33, 45, 50, 64, 100, 200])
 def test_pairdist_vs_fp64(n):
     from federatedscope_amd import ops
     P = 20_011
