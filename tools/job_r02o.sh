@@ -2,7 +2,7 @@
 # row-set weighted sums, slab then separate rows
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_probe -o run -- python3 tools/probe_rows_alloc.py > gpurun_out/prof_probe.log 2>&1; echo rc=$?
+timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_probe -o run -- python3 tools/probe_rows_alloc.py > gpurun_out/prof_probe.log 2>&1; echo rc=$? order=${FSAGG_PROBE_ORDER:-forward}
 python3 - <<'PY'
 import csv, glob, statistics
 f = glob.glob('gpurun_out/prof_probe/**/*kernel_trace.csv', recursive=True)[0]
@@ -11,5 +11,6 @@ rows.sort(key=lambda r: int(r['Start_Timestamp']))
 for name in ('wsum_f32_vec_kernel', 'wsum_rows_kernel'):
     d = [(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6 for r in rows if name in r['Kernel_Name']]
     half = len(d) // 2
-    print(name, 'slab', round(statistics.median(d[1:half]), 4), 'separate', round(statistics.median(d[half + 1:]), 4), len(d))
+    first, second = statistics.median(d[1:half]), statistics.median(d[half + 1:])
+    print(name, 'first run', round(first, 4), 'second run', round(second, 4), len(d))
 PY

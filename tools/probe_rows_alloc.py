@@ -45,18 +45,26 @@ def main():
     out = torch.empty(P, device=dev)
     lay = BucketLayout(OrderedDict(w=torch.empty(P)))
     res = {}
-    res['flat_slab'] = timed(lambda: ops.weighted_sum(
-        ops.RowTable.from_slab(slab), w, out))
-    res['flat_separate'] = timed(lambda: ops.weighted_sum(
-        ops.RowTable([t.data_ptr() for t in sep], P, dev, keepalive=sep), w,
-        out))
     rs_slab = ops.RowSet.from_pointers(
         lay, [[slab[i].data_ptr()] for i in range(n)], dev, keepalive=(slab,))
     rs_sep = ops.RowSet.from_pointers(
         lay, [[t.data_ptr()] for t in sep], dev, keepalive=(sep,))
-    res['rows_slab'] = timed(lambda: ops.weighted_sum_rows(rs_slab, w, out))
-    res['rows_separate'] = timed(lambda: ops.weighted_sum_rows(rs_sep, w,
-                                                               out))
+    runs = {
+        'flat_slab': lambda: ops.weighted_sum(
+            ops.RowTable.from_slab(slab), w, out),
+        'flat_separate': lambda: ops.weighted_sum(
+            ops.RowTable([t.data_ptr() for t in sep], P, dev, keepalive=sep),
+            w, out),
+        'rows_slab': lambda: ops.weighted_sum_rows(rs_slab, w, out),
+        'rows_separate': lambda: ops.weighted_sum_rows(rs_sep, w, out),
+    }
+    # FSAGG_PROBE_ORDER=reverse runs them last to first (the clocks drift
+    # over a run: the order must not decide the comparison)
+    order = list(runs)
+    if os.environ.get('FSAGG_PROBE_ORDER') == 'reverse':
+        order.reverse()
+    for k in order:
+        res[k] = timed(runs[k])
     res['row_addr_mod_2MiB'] = sorted({t.data_ptr() % (1 << 21)
                                        for t in sep})[:4]
     print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v)
