@@ -61,10 +61,21 @@ def main():
     # FSAGG_PROBE_ORDER=reverse runs them last to first (the clocks drift
     # over a run: the order must not decide the comparison)
     order = list(runs)
-    if os.environ.get('FSAGG_PROBE_ORDER') == 'reverse':
+    mode = os.environ.get('FSAGG_PROBE_ORDER')
+    if mode == 'reverse':
         order.reverse()
-    for k in order:
-        res[k] = timed(runs[k])
+    if mode == 'interleave':
+        # one call of each case in turn, 12 rounds: every case sees the
+        # same drift
+        ts = {k: [] for k in order}
+        for _ in range(12):
+            for k in order:
+                ts[k].append(timed(runs[k], reps=1))
+        for k in order:
+            res[k] = statistics.median(ts[k][2:])
+    else:
+        for k in order:
+            res[k] = timed(runs[k])
     res['row_addr_mod_2MiB'] = sorted({t.data_ptr() % (1 << 21)
                                        for t in sep})[:4]
     print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v)
