@@ -184,6 +184,21 @@ def test_pipelined_assembly_world2(world, P, chunks):
     assert pos == P
 
 
+def test_pipelined_assembly_stream_choice():
+    """Pieces below SMALL_PIECE coordinates alternate over two side streams
+    (one GPU's share at 8 GPUs); larger pieces, a single round or an
+    explicit count keep what they are given."""
+    from federatedscope_amd.core.sharding import PipelinedAssembly
+    small = PipelinedAssembly(25_000_000 // 8, chunks=4)
+    assert small.pc < PipelinedAssembly.SMALL_PIECE and small.streams == 2
+    big = PipelinedAssembly(25_000_000 // 4, chunks=4)
+    assert big.pc >= PipelinedAssembly.SMALL_PIECE and big.streams == 1
+    assert PipelinedAssembly(1000, chunks=1).streams == 1
+    assert PipelinedAssembly(1000, chunks=4, streams=3).streams == 3
+    with pytest.raises(ValueError):
+        PipelinedAssembly(1000, chunks=4, streams=0)
+
+
 def test_pipelined_assembly_plan_world1():
     from federatedscope_amd.core.sharding import PipelinedAssembly
     pa = PipelinedAssembly(1000, chunks=3, align=64)
