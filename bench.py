@@ -217,6 +217,44 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+class _PeerPlan:
+    """core/sharding.PeerAssembly behind PipelinedAssembly's interface (one
+    round; compute(j, lo, hi, outs) gets the list of output addresses)."""
+
+    def __init__(self, P, dev):
+        from federatedscope_amd.core.sharding import PeerAssembly
+        self.pp = PeerAssembly(P, device=dev)
+        self.chunks = 1
+        self.pcs = [self.pp.pc]
+        self.padded = self.pp.padded
+        self.streams = 1
+        self.numel = P
+
+    def local_pieces(self):
+        return [self.pp.piece()]
+
+    def local_numel(self):
+        return self.pp.pc
+
+    def piece(self, j, r=None):
+        return self.pp.piece(r)
+
+    def run(self, compute, out=None):
+        return self.pp.run(lambda lo, hi, outs: compute(0, lo, hi, outs))
+
+    def check(self):
+        self.pp.check()
+
+    def close(self):
+        self.pp.close()
+
+
+def default_split(world):
+    """Rounds' relative sizes of the strong-scaling pipeline (None: equal
+    rounds).  DESIGN §7."""
+    return None
+
+
 def timed_steps(D, fn, steps, warmup):
     """W untimed steps, then K steps between barrier + synchronize pairs;
     returns the max-over-ranks seconds per step."""
@@ -251,6 +289,17 @@ def main():
                     help='side streams the pipeline pieces round-robin over '
                          '(0: by piece size, core/sharding.py SMALL_PIECE; '
                          '1: all on the current stream)')
+    ap.add_argument('--split', default='auto',
+                    help="rounds' relative sizes, e.g. 4/2/1/0.5 ('auto': "
+                         'by world size, DESIGN §7; "uniform": equal)')
+    ap.add_argument('--assembly', default='auto',
+                    choices=['auto', 'p2p', 'rccl'],
+                    help='how the result reaches every GPU (N > 1): p2p = '
+                         'the reducing kernel stores into every GPU\'s copy '
+                         'over xGMI + a flag barrier (core/sharding.py '
+                         'PeerAssembly); rccl = pipelined in-place '
+                         'all-gathers (PipelinedAssembly); auto = p2p on RCCL '
+                         'process groups')
     ap.add_argument('--cpu-clients', type=int, default=20,
                     help='clients (full width) timed on the CPU baseline')
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -279,20 +328,39 @@ def main():
     # parameters still reduce at the one-launch rate); from 4 GPUs up the
     # pieces would shrink below that, 4 rounds
     chunks = args.chunks or (1 if world == 1 else 8 if world == 2 else 4)
-    pa = PipelinedAssembly(P, chunks=chunks, streams=args.streams or None)
+    split = default_split(world) if args.split == 'auto' else (
+        None if args.split == 'uniform' else
+        [float(x) for x in args.split.split('/')])
+    if split is not None and args.chunks:
+        split = split[:args.chunks]
+    assembly = args.assembly
+    if assembly == 'auto':
+        assembly = 'p2p' if world > 1 and args.backend == 'nccl' else 'rccl'
+    pa = None
+    if assembly == 'p2p' and world > 1:
+        try:
+            pa = _PeerPlan(P, dev)
+        except Exception as e:          # no IPC / peer access: collective
+            log('peer assembly unavailable (%s: %s); using the pipelined '
+                'all-gather' % (type(e).__name__, e))
+            assembly = 'rccl'
+    if pa is None:
+        pa = PipelinedAssembly(P, chunks=chunks, streams=args.streams or None,
+                               split=split)
+    chunks = pa.chunks
     sizes = sample_sizes(n)
     weights = fedavg_weights(sizes)
     w_dev = torch.tensor(weights, dtype=torch.float32, device=dev)
-    log('rank %d/%d on %s: %d clients x %d params, %d round(s) of %d-param '
+    log('rank %d/%d on %s: %d clients x %d params, %d round(s) of %s-param '
         'pieces on %d stream(s) (%.2f GB per rank)' %
-        (rank, world, torch.cuda.get_device_name(dev), n, P, chunks, pa.pc,
+        (rank, world, torch.cuda.get_device_name(dev), n, P, chunks, pa.pcs,
          pa.streams, 4.0 * n * pa.local_numel() / 1e9))
 
     # this rank's pieces of every client: global coordinates [lo, hi) of
     # the same counter-hash model at every N
     pieces = []
     for j, (lo, hi) in enumerate(pa.local_pieces()):
-        slab = torch.empty((n, pa.pc), dtype=torch.float32, device=dev)
+        slab = torch.empty((n, pa.pcs[j]), dtype=torch.float32, device=dev)
         if hi > lo:
             ops.fill_uniform(slab, hi - lo, seed=SEED, index_offset=lo)
         pieces.append((slab, ops.RowTable.from_slab(slab,
@@ -312,14 +380,22 @@ def main():
             a = torch.cuda.Event(enable_timing=True)
             b = torch.cuda.Event(enable_timing=True)
             a.record(st)
-            ops.weighted_sum(pieces[j][1], w_dev, view)
+            reduce_piece(j, view)
             b.record(st)
             events.append((a, b, hi - lo))
         else:
+            reduce_piece(j, view)
+
+    def reduce_piece(j, view):
+        if isinstance(view, list):      # peer assembly: every GPU's copy
+            ops.weighted_sum_bcast(pieces[j][1], w_dev, view)
+        else:
             ops.weighted_sum(pieces[j][1], w_dev, view)
 
+    result = [out]
+
     def step():
-        pa.run(compute, out=out)
+        result[0] = pa.run(compute, out=out)
 
     def sharded_only():
         for j, (lo, hi) in enumerate(pa.local_pieces()):
@@ -340,6 +416,8 @@ def main():
     t_sharded = timed_steps(D, sharded_only, args.steps, args.warmup) \
         if world > 1 else t_step
 
+    out = result[0]
+    pa.check()
     # assembly check: columns of every rank's pieces (other ranks' too),
     # regenerated here and reduced by the same kernel, must equal what the
     # all-gather delivered, bit for bit
@@ -444,9 +522,14 @@ def main():
                             'GPU' % (n, P, world),
                 'clients': n,
                 'params': P,
-                'parallelism': ('param-range x%d, %d pipelined all-gather '
-                                'rounds on %d stream(s)' %
-                                (world, chunks, pa.streams)) if world > 1
+                'parallelism': (
+                    'param-range x%d, peer assembly: the reducing kernel '
+                    'stores every output tile into all %d GPUs\' copies over '
+                    'xGMI, then a flag barrier' % (world, world)
+                    if assembly == 'p2p' else
+                    'param-range x%d, %d pipelined all-gather rounds %s on '
+                    '%d stream(s)' % (world, chunks, pa.pcs, pa.streams))
+                if world > 1
                 else 'single GPU',
             },
             'roofline': {
@@ -471,6 +554,8 @@ def main():
         del pieces
         torch.cuda.empty_cache()
         e2e_leg(args, dev, weights, sizes)
+    if hasattr(pa, 'close'):
+        pa.close()
     D.close()
 
 

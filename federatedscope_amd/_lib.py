@@ -116,6 +116,21 @@ SIGNATURES['fsagg_rows_sqnorm_workspace_bytes'] = (_c_sz, [_c_i, _c_i])
 SIGNATURES['fsagg_rows_sqnorm_f32'] = (
     _c_i, [_rows_p, _c_p, _c_i, _c_p, _c_p, _c_sz, _c_p])
 
+FSAGG_MAX_PEERS = 8
+_c_u32 = ctypes.c_uint32
+SIGNATURES['fsagg_peer_handle_bytes'] = (_c_sz, [])
+SIGNATURES['fsagg_peer_alloc'] = (_c_i, [_c_i, _c_sz, ctypes.POINTER(_c_p)])
+SIGNATURES['fsagg_peer_free'] = (_c_i, [_c_i, _c_p])
+SIGNATURES['fsagg_peer_handle'] = (_c_i, [_c_p, _c_p])
+SIGNATURES['fsagg_peer_open'] = (_c_i, [_c_i, _c_p, ctypes.POINTER(_c_p)])
+SIGNATURES['fsagg_peer_close'] = (_c_i, [_c_i, _c_p])
+SIGNATURES['fsagg_weighted_sum_bcast_f32'] = (
+    _c_i, [_c_p, _c_p, _c_p, _c_i, _c_i64, _c_p, ctypes.POINTER(_c_p), _c_i,
+           _c_p])
+SIGNATURES['fsagg_peer_barrier'] = (
+    _c_i, [ctypes.POINTER(_c_p), _c_i, _c_i, _c_u32, ctypes.c_uint64, _c_p,
+           _c_p])
+
 _lib = None
 _host = None
 HOST_PATH = os.path.join(_HERE, 'lib', '_fsagg_host.so')

@@ -17,6 +17,7 @@ Backend-agnostic: the collectives are plain torch.distributed calls, RCCL
 ("nccl") over xGMI on the GPU node, gloo in the CPU tests.
 """
 import contextlib
+import ctypes
 import math
 
 import torch
@@ -74,6 +75,18 @@ class Comm:
         dist.all_gather(parts, ci, group=self.group)
         out.copy_(torch.cat(parts))
         return None
+
+    def all_gather_bytes(self, b):
+        """Every rank's ``b`` (small host bytes: IPC handles), rank order."""
+        if self.world == 1:
+            return [bytes(b)]
+        out = [None] * self.world
+        dist.all_gather_object(out, bytes(b), group=self.group)
+        return out
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier(group=self.group)
 
     def all_reduce_sum(self, t):
         if self.world == 1:
@@ -157,15 +170,20 @@ class PipelinedAssembly:
     """Strong-scaled aggregation whose full result is assembled on every
     rank, the gather overlapped with the compute.
 
-    The flat bucket is cut into ``chunks`` rounds of ``world`` equal pieces
-    (block-cyclic): piece (j, r) = [(j·world + r)·pc, … + pc).  Rank r owns
+    The flat bucket is cut into ``chunks`` rounds (block-cyclic); round j
+    holds ``world`` equal pieces of ``pcs[j]`` coordinates, contiguous in
+    the output: piece (j, r) = [off[j] + r·pcs[j], … + pcs[j]).  Rank r owns
     pieces (j, r) for every j.  Round j: the rank computes its piece
     straight into its slot of the output, then an asynchronous in-place
-    all-gather of round j's ``world`` pieces (contiguous in the output)
-    runs on the collective's stream while round j+1 computes.  Pieces are
-    disjoint coordinate ranges, so the result is bit-identical to the
-    single-GPU reduction; the only traffic is the output itself (4·P bytes,
-    ring all-gather over xGMI)."""
+    all-gather of round j's ``world`` pieces runs on the collective's stream
+    while round j+1 computes.  Pieces are disjoint coordinate ranges, so the
+    result is bit-identical to the single-GPU reduction; the only traffic is
+    the output itself (4·P bytes over xGMI).
+
+    ``split`` sets the rounds' relative sizes (default: equal).  Only the
+    last round's gather is exposed, so a plan that shrinks toward its end
+    (e.g. :func:`tapered_split`) exposes less of it while the early, large
+    pieces run at the one-launch rate."""
 
     # Pieces below this many coordinates run on two side streams: piece j + 1
     # starts while piece j's last workgroups drain.  One GPU's share of the
@@ -175,7 +193,12 @@ class PipelinedAssembly:
     SMALL_PIECE = 1 << 20
 
     def __init__(self, numel, chunks=4, group=None, align=ALIGN, comm=None,
-                 streams=None):
+                 streams=None, split=None):
+        if split is not None:
+            split = [float(f) for f in split]
+            if not split or min(split) <= 0:
+                raise ValueError('split needs positive round weights')
+            chunks = len(split)
         if chunks < 1:
             raise ValueError('chunks must be >= 1')
         if streams is not None and streams < 1:
@@ -188,38 +211,56 @@ class PipelinedAssembly:
         self.rank = self.comm.rank
         self.numel = int(numel)
         self.chunks = int(chunks)
-        per = self.world * self.chunks
-        self.pc = int(math.ceil(self.numel / per / align)) * align \
-            if self.numel else align
-        self.padded = self.pc * per
+        self.pcs = _round_lengths(self.numel, self.world, self.chunks,
+                                  split, align)
+        self.off = [0]
+        for pc in self.pcs:
+            self.off.append(self.off[-1] + self.world * pc)
+        self.padded = self.off[-1]
+        self.pc = max(self.pcs)
         self.streams = int(self._streams) if self._streams is not None else (
-            2 if self.chunks > 1 and self.pc < self.SMALL_PIECE else 1)
+            2 if self.chunks > 1 and min(self.pcs) < self.SMALL_PIECE else 1)
 
     def piece(self, j, r=None):
         """Global [lo, hi) of piece (j, r) (empty past numel)."""
         r = self.rank if r is None else r
-        lo = (j * self.world + r) * self.pc
-        return min(lo, self.numel), min(lo + self.pc, self.numel)
+        lo = self.off[j] + r * self.pcs[j]
+        return min(lo, self.numel), min(lo + self.pcs[j], self.numel)
+
+    def slot(self, j, r=None):
+        """Offset of piece (j, r) in the padded output."""
+        r = self.rank if r is None else r
+        return self.off[j] + r * self.pcs[j]
 
     def local_pieces(self):
         return [self.piece(j) for j in range(self.chunks)]
 
     def local_numel(self):
         """Columns of this rank's client slab: its pieces back to back, each
-        ``pc`` wide (so every piece starts 256-B aligned)."""
-        return self.chunks * self.pc
+        ``pcs[j]`` wide (so every piece starts 256-B aligned)."""
+        return sum(self.pcs)
+
+    def check(self):
+        """Nothing to verify (the collectives report their own errors)."""
 
     def run(self, compute, out=None, dtype=torch.float32, device=None):
         """compute(j, lo, hi, out_view) writes piece (j, rank) = global
         coordinates [lo, hi) into ``out_view`` (hi − lo elements).  Returns
-        the assembled [numel] result (every rank)."""
+        the assembled [numel] result (every rank).
+
+        Stream order: each piece runs on its side stream (or the current
+        one), which first waits for the current stream; the collective of
+        round j is issued under the piece's stream, so the backend orders it
+        after the piece (RCCL: its stream waits on the issuing stream); at
+        the end the current stream waits for every side stream and every
+        collective's work handle."""
         if out is None:
             out = torch.empty(self.padded, dtype=dtype, device=device)
         if out.numel() < self.padded:
             raise ValueError('out needs %d elements (padded), got %d' %
                              (self.padded, out.numel()))
         works = []
-        W, pc = self.world, self.pc
+        W = self.world
         side = None
         if self.streams > 1 and self.chunks > 1 and out.is_cuda:
             side = self._side.get(out.device)
@@ -232,7 +273,7 @@ class PipelinedAssembly:
                 st.wait_stream(cur)
         for j in range(self.chunks):
             lo, hi = self.piece(j)
-            slot = (j * W + self.rank) * pc
+            slot, pc = self.slot(j), self.pcs[j]
             with (torch.cuda.stream(side[j % len(side)]) if side
                   else _nullctx()):
                 if hi > lo:
@@ -240,7 +281,7 @@ class PipelinedAssembly:
                 if W > 1:
                     # the collective waits for the piece's own stream
                     w = self.comm.all_gather_into(
-                        out[j * W * pc:(j + 1) * W * pc],
+                        out[self.off[j]:self.off[j + 1]],
                         out[slot:slot + pc], async_op=True)
                     if w is not None:
                         works.append(w)
@@ -250,3 +291,190 @@ class PipelinedAssembly:
         for w in works:
             w.wait()
         return out[:self.numel]
+
+
+def tapered_split(chunks, ratio=0.5):
+    """Round weights that shrink geometrically (1, r, r², …): the early
+    rounds run at the one-launch rate, the exposed last gather is small."""
+    return [ratio ** j for j in range(chunks)]
+
+
+def _round_lengths(numel, world, chunks, split, align):
+    """Per-round piece lengths (aligned) covering ``numel`` coordinates in
+    ``chunks`` rounds of ``world`` pieces, in proportion to ``split``; the
+    last round takes the remainder (never negative, at least ``align``)."""
+    if split is None:
+        per = world * chunks
+        pc = int(math.ceil(numel / per / align)) * align if numel else align
+        return [pc] * chunks
+    tot = sum(split)
+    pcs = []
+    done = 0
+    for j in range(chunks - 1):
+        want = numel * split[j] / tot / world
+        pc = max(int(math.ceil(want / align)) * align, align)
+        pcs.append(pc)
+        done += world * pc
+    rest = max(numel - done, 0)
+    pcs.append(max(int(math.ceil(rest / world / align)) * align, align))
+    return pcs
+
+
+class PeerAssembly:
+    """Strong-scaled aggregation assembled by the producing kernel itself
+    (DESIGN §7).
+
+    Rank r owns piece r = [r·pc, (r+1)·pc) of the bucket, reduces it in ONE
+    launch and stores each output tile into every rank's copy of the
+    result: its own buffer and the peers' buffers, imported through IPC
+    handles and written over xGMI (ops.weighted_sum_bcast).  A flag barrier
+    on the same stream (fsagg_peer_barrier) then waits until every peer's
+    stores have landed.  No collective library call and no separate gather
+    pass: the 4·P output bytes cross the links while the 4·n·P input bytes
+    stream from HBM, every GPU pushing to all of its peers at once.
+
+    The output copies are double-buffered (round k writes buffer k mod 2): a
+    rank can be one round ahead, and the barrier of round k + 1 proves that
+    every rank has finished round k — so a rank never writes into a buffer a
+    peer is still reading.  Results of :meth:`run` stay valid until the next
+    call but one; callers that keep them longer copy them out.
+
+    Uploads stay where they are: each rank reads only its range of every
+    client (device-resident, as in the reference's multi-GPU mode where
+    uploads arrive on the ranks' GPUs, parallel_runner.py:243-302)."""
+
+    TIMEOUT_S = 10.0       # a lost peer ends the barrier with an error
+    CTRL_WORDS = 64        # flags [0, world), status word STATUS
+
+    STATUS = 32
+
+    def __init__(self, numel, comm=None, device=None, align=ALIGN,
+                 group=None, buffers=2):
+        from .. import _lib as L
+        self.comm = comm if comm is not None else Comm(group)
+        self.world = self.comm.world
+        self.rank = self.comm.rank
+        if self.world > L.FSAGG_MAX_PEERS:
+            raise ValueError('peer assembly supports up to %d GPUs' %
+                             L.FSAGG_MAX_PEERS)
+        self.device = torch.device(device) if device is not None else \
+            torch.device('cuda', torch.cuda.current_device())
+        self.numel = int(numel)
+        W = self.world
+        self.pc = max(int(math.ceil(self.numel / W / align)) * align, align)
+        self.padded = W * self.pc
+        self.epoch = 0
+        self._lib = L.load()
+        self._L = L
+        idx = self.device.index
+        self._own = []
+        self._opened = []
+        try:
+            nbytes = self.padded * 4
+            for _ in range(buffers):
+                self._own.append(self._alloc(nbytes))
+            self._own.append(self._alloc(self.CTRL_WORDS * 4))
+            hb = int(self._lib.fsagg_peer_handle_bytes())
+            mine = b''.join(self._handle(p, hb) for p in self._own)
+            every = self.comm.all_gather_bytes(mine)
+            # ptr[k] = rank k's allocations (buffers..., ctrl) as seen here
+            self._ptr = []
+            for k in range(W):
+                if k == self.rank:
+                    self._ptr.append(list(self._own))
+                    continue
+                if len(every[k]) != len(mine):
+                    raise RuntimeError('rank %d sent %d handle bytes, '
+                                       'expected %d' % (k, len(every[k]),
+                                                        len(mine)))
+                row = []
+                for a in range(len(self._own)):
+                    p = self._open(every[k][a * hb:(a + 1) * hb])
+                    self._opened.append(p)
+                    row.append(p)
+                self._ptr.append(row)
+        except Exception:
+            self._release()
+            raise
+        host = L.host()
+        self.buffers = [host.device_tensor(p, self.padded, 0, idx)
+                        for p in self._own[:-1]]
+        self.ctrl = host.device_tensor(self._own[-1], self.CTRL_WORDS, 1,
+                                       idx)
+        self._flags = (ctypes.c_void_p * W)(
+            *[self._ptr[k][-1] for k in range(W)])
+
+    # -- allocation plumbing ------------------------------------------------
+    def _alloc(self, nbytes):
+        p = ctypes.c_void_p()
+        self._L.check(self._lib.fsagg_peer_alloc(self.device.index, nbytes,
+                                                 ctypes.byref(p)),
+                      'fsagg_peer_alloc')
+        return int(p.value)
+
+    def _handle(self, ptr, hb):
+        buf = ctypes.create_string_buffer(hb)
+        self._L.check(self._lib.fsagg_peer_handle(ptr, buf),
+                      'fsagg_peer_handle')
+        return buf.raw
+
+    def _open(self, handle):
+        p = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(handle, len(handle))
+        self._L.check(self._lib.fsagg_peer_open(self.device.index, buf,
+                                                ctypes.byref(p)),
+                      'fsagg_peer_open')
+        return int(p.value)
+
+    def _release(self):
+        for p in self._opened:
+            self._lib.fsagg_peer_close(self.device.index, p)
+        for p in self._own:
+            self._lib.fsagg_peer_free(self.device.index, p)
+        self._opened, self._own = [], []
+
+    # -- the round ------------------------------------------------------------
+    def piece(self, r=None):
+        """Global [lo, hi) of rank r's piece (empty past numel)."""
+        r = self.rank if r is None else r
+        lo = r * self.pc
+        return min(lo, self.numel), min(lo + self.pc, self.numel)
+
+    def run(self, compute):
+        """compute(lo, hi, outs) launches, on the current stream, the
+        reduction of this rank's piece [lo, hi) into every address of
+        ``outs`` (own buffer first, then the peers'; hi − lo floats each).
+        Returns this GPU's assembled [numel] result (valid until the next
+        run() but one)."""
+        b = self.epoch % len(self.buffers)
+        self.epoch += 1
+        lo, hi = self.piece()
+        W = self.world
+        if hi > lo:
+            outs = [self._ptr[(self.rank + k) % W][b] + 4 * lo
+                    for k in range(W)]
+            compute(lo, hi, outs)
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        ticks = int(self.TIMEOUT_S * 1e8)
+        self._L.check(self._lib.fsagg_peer_barrier(
+            self._flags, W, self.rank, self.epoch & 0xFFFFFFFF, ticks,
+            self.ctrl.data_ptr() + 4 * self.STATUS, st or None),
+            'fsagg_peer_barrier')
+        return self.buffers[b][:self.numel]
+
+    def check(self):
+        """Raise if a barrier gave up waiting for a peer (synchronises)."""
+        v = int(self.ctrl[self.STATUS].item())
+        if v:
+            raise RuntimeError('peer barrier timed out waiting for rank %d'
+                               % (v - 1))
+
+    def close(self):
+        """Collective: unmap the peers' buffers and free this rank's."""
+        if not self._own:
+            return
+        torch.cuda.synchronize(self.device)
+        self.comm.barrier()
+        self.buffers, self.ctrl = [], None
+        self._release()
+        self.comm.barrier()

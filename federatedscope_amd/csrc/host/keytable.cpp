@@ -23,6 +23,7 @@
 // With offs4 the table is the device row table itself (include/fsagg.h
 // fsagg_rows): segment-major [key][client] virtual bases ptr - offs4[key]
 // (0 stays 0), so the caller uploads it as is.
+#include <ATen/ATen.h>
 #include <Python.h>
 #include <torch/csrc/autograd/python_variable.h>
 
@@ -107,7 +108,31 @@ PyObject *key_table(PyObject *, PyObject *args) {
   return Py_BuildValue("(NnO)", bytes, missing, aligned ? Py_True : Py_False);
 }
 
+// device_tensor(ptr, numel, kind, device_index) -> Tensor
+// A 1-D tensor over device memory torch does not own (the uncached peer
+// buffers fsagg_peer_alloc returns, include/fsagg.h): kind 0 = float32,
+// 1 = int32.  No deleter: the caller (core/sharding.PeerAssembly) keeps the
+// allocation alive for as long as the tensor is reachable.
+PyObject *device_tensor(PyObject *, PyObject *args) {
+  unsigned long long ptr;
+  long long numel;
+  int kind, device_index;
+  if (!PyArg_ParseTuple(args, "KLii", &ptr, &numel, &kind, &device_index))
+    return nullptr;
+  if (ptr == 0 || numel < 0 || kind < 0 || kind > 1 || device_index < 0) {
+    PyErr_SetString(PyExc_ValueError, "device_tensor: invalid argument");
+    return nullptr;
+  }
+  auto opts = at::TensorOptions()
+                  .dtype(kind == 0 ? at::kFloat : at::kInt)
+                  .device(at::Device(at::kCUDA, at::DeviceIndex(device_index)));
+  at::Tensor t = at::from_blob(reinterpret_cast<void *>(ptr), {numel}, opts);
+  return THPVariable_Wrap(t);
+}
+
 PyMethodDef kMethods[] = {
+    {"device_tensor", device_tensor, METH_VARARGS,
+     "device_tensor(ptr, numel, kind, device_index) -> Tensor (no ownership)"},
     {"key_table", key_table, METH_VARARGS,
      "key_table(dicts, keys, shapes, device_index[, offs4]) -> (bytes, "
      "missing, aligned16) or None"},

@@ -1,0 +1,152 @@
+// Peer assembly over xGMI (gfx950): the strong-scaled aggregation writes
+// its result straight into every GPU's copy of the output
+// (fsagg_weighted_sum_bcast_f32), then one tiny flag barrier tells each GPU
+// that every peer's stores have landed.  SURVEY §8(e): the cross-GPU step is
+// a concatenation of disjoint parameter ranges, never an arithmetic reduce.
+//
+// Memory: the output copies and the flag arrays are allocated uncached
+// (hipDeviceMallocUncached), so every GPU's stores and loads of them go to
+// the owning GPU's memory instead of a local L2 that a peer's xGMI stores
+// would not invalidate.  Buffers are exported with hipIpcGetMemHandle and
+// imported by the peer processes (one process per GPU).
+//
+// Replaces the reference's device-resident multi-GPU traffic: per-key
+// dist.send/recv of model tensors between the server rank and client ranks
+// (federatedscope/core/communication.py:61-76,
+// core/parallel/parallel_runner.py:22-24,243-302).
+#include "common.h"
+
+namespace fsagg {
+namespace {
+
+struct Flags {
+  uint32_t *p[FSAGG_MAX_PEERS];  // p[r] = rank r's flag array (world words)
+};
+
+// One workgroup.  Lane t < world stores `epoch` into rank t's flag word for
+// this rank, then waits until this rank's word for rank t reaches `epoch`.
+// The flag words are uncached; the stores are release and the loads acquire
+// at system scope.  The spin is bounded: after `timeout` ticks of the
+// 100 MHz constant clock the lane sets *status and gives up, so the grid
+// always drains (a lost peer becomes an error the host reads, not a hang).
+__global__ void peer_barrier_kernel(Flags f, int world, int rank,
+                                    uint32_t epoch, uint64_t timeout,
+                                    uint32_t *status) {
+  const int t = threadIdx.x;
+  if (t < world) {
+    __hip_atomic_store(f.p[t] + rank, epoch, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t *mine = f.p[rank] + t;
+    const uint64_t t0 = wall_clock64();
+    while (int32_t(__hip_atomic_load(mine, __ATOMIC_ACQUIRE,
+                                     __HIP_MEMORY_SCOPE_SYSTEM) -
+                   epoch) < 0) {
+      if (wall_clock64() - t0 > timeout) {
+        __hip_atomic_store(status, 1u + uint32_t(t), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+}
+
+int hip_fail(const char *what, hipError_t e) {
+  set_error("%s: %s", what, hipGetErrorString(e));
+  return FSAGG_EHIP;
+}
+
+}  // namespace
+}  // namespace fsagg
+
+using namespace fsagg;
+
+extern "C" size_t fsagg_peer_handle_bytes(void) {
+  return sizeof(hipIpcMemHandle_t);
+}
+
+extern "C" int fsagg_peer_alloc(int device, size_t bytes, void **ptr) {
+  if (!ptr || bytes == 0) {
+    set_error("fsagg_peer_alloc: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  *ptr = nullptr;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail("fsagg_peer_alloc: hipSetDevice", e);
+  e = hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess)
+    return hip_fail("fsagg_peer_alloc: hipExtMallocWithFlags", e);
+  e = hipMemset(*ptr, 0, bytes);
+  if (e != hipSuccess) return hip_fail("fsagg_peer_alloc: hipMemset", e);
+  e = hipDeviceSynchronize();
+  if (e != hipSuccess) return hip_fail("fsagg_peer_alloc: sync", e);
+  return FSAGG_OK;
+}
+
+extern "C" int fsagg_peer_free(int device, void *ptr) {
+  if (!ptr) return FSAGG_OK;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail("fsagg_peer_free: hipSetDevice", e);
+  e = hipFree(ptr);
+  if (e != hipSuccess) return hip_fail("fsagg_peer_free: hipFree", e);
+  return FSAGG_OK;
+}
+
+extern "C" int fsagg_peer_handle(void *ptr, void *handle) {
+  if (!ptr || !handle) {
+    set_error("fsagg_peer_handle: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  hipIpcMemHandle_t h;
+  hipError_t e = hipIpcGetMemHandle(&h, ptr);
+  if (e != hipSuccess) return hip_fail("fsagg_peer_handle", e);
+  std::memcpy(handle, &h, sizeof(h));
+  return FSAGG_OK;
+}
+
+extern "C" int fsagg_peer_open(int device, const void *handle, void **ptr) {
+  if (!handle || !ptr) {
+    set_error("fsagg_peer_open: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  *ptr = nullptr;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail("fsagg_peer_open: hipSetDevice", e);
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  e = hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+  if (e != hipSuccess) return hip_fail("fsagg_peer_open", e);
+  return FSAGG_OK;
+}
+
+extern "C" int fsagg_peer_close(int device, void *ptr) {
+  if (!ptr) return FSAGG_OK;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail("fsagg_peer_close: hipSetDevice", e);
+  e = hipIpcCloseMemHandle(ptr);
+  if (e != hipSuccess) return hip_fail("fsagg_peer_close", e);
+  return FSAGG_OK;
+}
+
+extern "C" int fsagg_peer_barrier(uint32_t *const *flags, int world, int rank,
+                                  uint32_t epoch, uint64_t timeout_ticks,
+                                  uint32_t *status, fsagg_stream_t stream) {
+  if (!flags || !status || world < 1 || world > FSAGG_MAX_PEERS || rank < 0 ||
+      rank >= world) {
+    set_error("fsagg_peer_barrier: invalid argument (world=%d rank=%d)",
+              world, rank);
+    return FSAGG_EINVAL;
+  }
+  Flags f{};
+  for (int r = 0; r < world; ++r) {
+    if (!flags[r]) {
+      set_error("fsagg_peer_barrier: flag array %d is NULL", r);
+      return FSAGG_EINVAL;
+    }
+    f.p[r] = flags[r];
+  }
+  hipLaunchKernelGGL(peer_barrier_kernel, dim3(1), dim3(kWave), 0,
+                     as_stream(stream), f, world, rank, epoch, timeout_ticks,
+                     status);
+  return check_launch("fsagg_peer_barrier");
+}

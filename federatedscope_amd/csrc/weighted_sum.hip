@@ -80,13 +80,29 @@ __device__ __forceinline__ f4 add4(f4 a, f4 b) {
 
 // One tile of V f4 columns per thread.  GUARD handles the ragged last
 // tile; all other tiles run unguarded.
-template <int U, int V, bool PRE, bool BASE, bool NT, bool GUARD>
+// Output of a tile: one bucket (float *), or the same coordinates of up to
+// kMaxPeers buckets — every GPU's copy of the assembled result, peers' over
+// xGMI (fsagg_weighted_sum_bcast_f32).
+struct Bcast {
+  float *p[FSAGG_MAX_PEERS];
+  int n;
+};
+__device__ __forceinline__ void put4(float *out, int64_t i, f4 a) {
+  reinterpret_cast<f4 *>(out)[i] = a;
+}
+__device__ __forceinline__ void put4(const Bcast &o, int64_t i, f4 a) {
+#pragma unroll
+  for (int k = 0; k < FSAGG_MAX_PEERS; ++k)
+    if (k < o.n) reinterpret_cast<f4 *>(o.p[k])[i] = a;
+}
+
+template <int U, int V, bool PRE, bool BASE, bool NT, bool GUARD, class O>
 __device__ __forceinline__ void wsum_tile(const float *const *__restrict__ rows,
                                           const float *__restrict__ w,
                                           const float *__restrict__ pre, int n,
                                           int64_t nvec, int64_t t0,
                                           const float *__restrict__ base,
-                                          float *__restrict__ out) {
+                                          const O &out) {
   int64_t idx[V];
   bool ok[V];
 #pragma unroll
@@ -145,15 +161,15 @@ __device__ __forceinline__ void wsum_tile(const float *const *__restrict__ rows,
     if (!ok[v]) continue;
     f4 a = acc[v];
     if (BASE) a = add4(reinterpret_cast<const f4 *>(base)[idx[v]], a);
-    reinterpret_cast<f4 *>(out)[idx[v]] = a;
+    put4(out, idx[v], a);
   }
 }
 
-template <int U, int V, bool PRE, bool BASE, bool NT>
+template <int U, int V, bool PRE, bool BASE, bool NT, class O = float *>
 __global__ __launch_bounds__(kBlock) void wsum_f32_vec_kernel(
     const float *const *__restrict__ rows, const float *__restrict__ w,
     const float *__restrict__ pre, int n, int64_t nvec,
-    const float *__restrict__ base, float *__restrict__ out) {
+    const float *__restrict__ base, O out) {
   constexpr int64_t tile = int64_t(kBlock) * V;
   const int64_t full = nvec / tile * tile;
   for (int64_t t0 = int64_t(blockIdx.x) * tile; t0 < nvec;
@@ -191,12 +207,18 @@ __global__ __launch_bounds__(kBlock) void wsum_f32_part_kernel(
 }
 
 // Scalar tail: elements [start, numel) (fewer than 4), one thread each.
+__device__ __forceinline__ void put1(float *out, int64_t p, float a) {
+  out[p] = a;
+}
+__device__ __forceinline__ void put1(const Bcast &o, int64_t p, float a) {
+  for (int k = 0; k < o.n; ++k) o.p[k][p] = a;
+}
+template <class O = float *>
 __global__ void wsum_f32_tail_kernel(const float *const *__restrict__ rows,
                                      const float *__restrict__ w,
                                      const float *__restrict__ pre, int n,
                                      int64_t start, int64_t numel,
-                                     const float *__restrict__ base,
-                                     float *__restrict__ out) {
+                                     const float *__restrict__ base, O out) {
   const int64_t p = start + threadIdx.x;
   if (p >= numel) return;
   float x = gld(rows[0] + p);
@@ -208,7 +230,7 @@ __global__ void wsum_f32_tail_kernel(const float *const *__restrict__ rows,
     acc = add_rn(acc, mul_rn(t, w[i]));
   }
   if (base) acc = add_rn(base[p], acc);
-  out[p] = acc;
+  put1(out, p, acc);
 }
 
 // Launch shape of the streaming kernel, from interleaved timing on MI355X
@@ -221,13 +243,13 @@ __global__ void wsum_f32_tail_kernel(const float *const *__restrict__ rows,
 // a ragged third round) loses 25 %.
 constexpr int kU = 1;
 
-template <bool PRE, bool BASE, int V>
+template <bool PRE, bool BASE, int V, class O>
 void launch_wsum_v(const float *const *rows, const float *w, const float *pre,
-                   int n, int64_t nvec, const float *base, float *out,
+                   int n, int64_t nvec, const float *base, O out,
                    hipStream_t s) {
   const int64_t tiles = (nvec + int64_t(kBlock) * V - 1) / (int64_t(kBlock) * V);
   const unsigned grid = stream_grid(tiles, 1, 256 * 16);
-  hipLaunchKernelGGL((wsum_f32_vec_kernel<kU, V, PRE, BASE, true>),
+  hipLaunchKernelGGL((wsum_f32_vec_kernel<kU, V, PRE, BASE, true, O>),
                      dim3(grid), dim3(kBlock), 0, s, rows, w, pre, n, nvec,
                      base, out);
 }
@@ -246,9 +268,9 @@ inline int wsum_width(int64_t nvec, int n) {
   return 1;
 }
 
-template <bool PRE, bool BASE>
+template <bool PRE, bool BASE, class O>
 void launch_wsum(const float *const *rows, const float *w, const float *pre,
-                 int n, int64_t nvec, const float *base, float *out,
+                 int n, int64_t nvec, const float *base, O out,
                  hipStream_t s) {
   switch (wsum_width(nvec, n)) {
     case 24: launch_wsum_v<PRE, BASE, 24>(rows, w, pre, n, nvec, base, out, s); break;
@@ -256,6 +278,26 @@ void launch_wsum(const float *const *rows, const float *w, const float *pre,
     case 8: launch_wsum_v<PRE, BASE, 8>(rows, w, pre, n, nvec, base, out, s); break;
     case 4: launch_wsum_v<PRE, BASE, 4>(rows, w, pre, n, nvec, base, out, s); break;
     default: launch_wsum_v<PRE, BASE, 1>(rows, w, pre, n, nvec, base, out, s);
+  }
+}
+
+template <class O>
+void launch_wsum_any(const float *const *rows, const float *weights,
+                     const float *prescale, int n, int64_t numel,
+                     const float *base, O out, hipStream_t s) {
+  const int64_t nvec = numel / 4;
+  if (nvec > 0) {
+    if (prescale) {
+      if (base) launch_wsum<true, true>(rows, weights, prescale, n, nvec, base, out, s);
+      else launch_wsum<true, false>(rows, weights, prescale, n, nvec, base, out, s);
+    } else {
+      if (base) launch_wsum<false, true>(rows, weights, prescale, n, nvec, base, out, s);
+      else launch_wsum<false, false>(rows, weights, prescale, n, nvec, base, out, s);
+    }
+  }
+  if (numel > nvec * 4) {
+    hipLaunchKernelGGL((wsum_f32_tail_kernel<O>), dim3(1), dim3(kWave), 0, s,
+                       rows, weights, prescale, n, nvec * 4, numel, base, out);
   }
 }
 
@@ -625,22 +667,41 @@ extern "C" int fsagg_weighted_sum_f32(const float *const *rows,
     return FSAGG_EINVAL;
   }
   if (numel == 0) return FSAGG_OK;
-  hipStream_t s = as_stream(stream);
-  const int64_t nvec = numel / 4;
-  if (nvec > 0) {
-    if (prescale) {
-      if (base) launch_wsum<true, true>(rows, weights, prescale, n, nvec, base, out, s);
-      else launch_wsum<true, false>(rows, weights, prescale, n, nvec, base, out, s);
-    } else {
-      if (base) launch_wsum<false, true>(rows, weights, prescale, n, nvec, base, out, s);
-      else launch_wsum<false, false>(rows, weights, prescale, n, nvec, base, out, s);
-    }
-  }
-  if (numel > nvec * 4) {
-    hipLaunchKernelGGL(wsum_f32_tail_kernel, dim3(1), dim3(kWave), 0, s, rows,
-                       weights, prescale, n, nvec * 4, numel, base, out);
-  }
+  launch_wsum_any(rows, weights, prescale, n, numel, base, out,
+                  as_stream(stream));
   return check_launch("fsagg_weighted_sum_f32");
+}
+
+extern "C" int fsagg_weighted_sum_bcast_f32(const float *const *rows,
+                                            const float *weights,
+                                            const float *prescale, int n,
+                                            int64_t numel, const float *base,
+                                            float *const *outs, int nout,
+                                            fsagg_stream_t stream) {
+  if (!rows || !weights || !outs || n < 1 || numel < 0 || nout < 1 ||
+      nout > FSAGG_MAX_PEERS) {
+    set_error("fsagg_weighted_sum_bcast_f32: invalid argument (n=%d "
+              "numel=%lld nout=%d)", n, (long long)numel, nout);
+    return FSAGG_EINVAL;
+  }
+  Bcast o{};
+  o.n = nout;
+  for (int k = 0; k < nout; ++k) {
+    if (!outs[k] || !aligned16(outs[k])) {
+      set_error("fsagg_weighted_sum_bcast_f32: out %d is NULL or not "
+                "16-byte aligned", k);
+      return FSAGG_EINVAL;
+    }
+    o.p[k] = outs[k];
+  }
+  if (base && !aligned16(base)) {
+    set_error("fsagg_weighted_sum_bcast_f32: base must be 16-byte aligned");
+    return FSAGG_EINVAL;
+  }
+  if (numel == 0) return FSAGG_OK;
+  launch_wsum_any(rows, weights, prescale, n, numel, base, o,
+                  as_stream(stream));
+  return check_launch("fsagg_weighted_sum_bcast_f32");
 }
 
 extern "C" int64_t fsagg_wsum_chunk_elems(int64_t numel) {

@@ -223,6 +223,41 @@ def weighted_sum(rows, weights, out, prescale=None, base=None, stream=None):
     return out
 
 
+def weighted_sum_bcast(rows, weights, outs, prescale=None, base=None,
+                       stream=None):
+    """weighted_sum whose result is written to every device address in
+    ``outs`` (this GPU's buffer and peers' imported buffers, each holding
+    ``rows.numel`` fp32, 16-byte aligned): the assembly epilogue of the
+    strong-scaled path (core/sharding.PeerAssembly)."""
+    if len(weights) != rows.n:
+        raise ValueError('%d weights for %d rows' % (len(weights), rows.n))
+    if not rows.aligned16:
+        raise ValueError('weighted_sum_bcast needs 16-byte aligned rows')
+    if not 1 <= len(outs) <= L.FSAGG_MAX_PEERS:
+        raise ValueError('1..%d outputs, got %d' % (L.FSAGG_MAX_PEERS,
+                                                    len(outs)))
+    for p in outs:
+        if not p or int(p) % ALIGN_BYTES:
+            raise ValueError('output address 0x%x not 16-byte aligned' %
+                             int(p or 0))
+    if base is not None:
+        _check_out(base, rows.numel, rows.device, 'base')
+    w = weights if isinstance(weights, torch.Tensor) else _fp32_dev(
+        weights, rows.device)
+    s = None
+    if prescale is not None:
+        if len(prescale) != rows.n:
+            raise ValueError('prescale length mismatch')
+        s = prescale if isinstance(prescale, torch.Tensor) else _fp32_dev(
+            prescale, rows.device)
+    arr = (ctypes.c_void_p * len(outs))(*[int(p) for p in outs])
+    st = stream if stream is not None else _stream(rows.device)
+    L.check(L.load().fsagg_weighted_sum_bcast_f32(
+        rows.ptr(), w.data_ptr(), s.data_ptr() if s is not None else None,
+        rows.n, rows.numel, base.data_ptr() if base is not None else None,
+        arr, len(outs), st), 'fsagg_weighted_sum_bcast_f32')
+
+
 _TYPED = {
     torch.float16: (L.FSAGG_F16, torch.float16),
     torch.bfloat16: (L.FSAGG_BF16, torch.bfloat16),

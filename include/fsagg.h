@@ -424,6 +424,55 @@ int fsagg_rows_sqnorm_f32(const fsagg_rows *rows, const fsagg_chunk *chunks,
                           size_t workspace_bytes, fsagg_stream_t stream);
 
 /*
+ * Peer assembly over xGMI (strong scaling across the GPUs of one node,
+ * SURVEY §8(e)).  Each GPU owns a parameter range of every client, reduces
+ * it and writes the result straight into every GPU's copy of the output
+ * (its own and its peers', imported through IPC handles) — the gather is
+ * the producing kernel's epilogue instead of a separate collective.  Stands
+ * in for the reference's device-resident multi-GPU transfer of model
+ * tensors (core/communication.py:61-76, core/parallel/parallel_runner.py:
+ * 22-24,243-302: per-key dist.send / dist.recv between ranks).
+ *
+ * fsagg_peer_alloc   `bytes` of zeroed, UNCACHED device memory on `device`
+ *                    (hipDeviceMallocUncached: peers' xGMI stores and local
+ *                    loads meet in memory, no stale L2 line) — the one
+ *                    allocation the library makes; free with
+ *                    fsagg_peer_free.
+ * fsagg_peer_handle  the allocation's IPC handle (fsagg_peer_handle_bytes()
+ *                    bytes) for the peer processes;
+ * fsagg_peer_open    a peer's handle mapped on `device` (peer access enabled
+ *                    lazily); fsagg_peer_close unmaps it.
+ * fsagg_weighted_sum_bcast_f32  fsagg_weighted_sum_f32 whose result goes to
+ *                    `nout` (<= FSAGG_MAX_PEERS) outputs: outs is a HOST
+ *                    array of device pointers (own and peer buffers, each
+ *                    16-byte aligned), every one receiving the same bits.
+ * fsagg_peer_barrier  after the bcast kernel, on the same stream: stores
+ *                    `epoch` into every rank's flag word for `rank`
+ *                    (flags[r] = rank r's array of `world` uint32, own and
+ *                    imported), then waits until every rank's word in this
+ *                    rank's array reached `epoch` (epochs increase by one
+ *                    per call; compared modulo 2^32).  A wait longer than
+ *                    `timeout_ticks` of the 100 MHz constant clock stores
+ *                    1 + the missing rank into *status (device) and ends
+ *                    instead of hanging.
+ */
+#define FSAGG_MAX_PEERS 8
+size_t fsagg_peer_handle_bytes(void);
+int fsagg_peer_alloc(int device, size_t bytes, void **ptr);
+int fsagg_peer_free(int device, void *ptr);
+int fsagg_peer_handle(void *ptr, void *handle);
+int fsagg_peer_open(int device, const void *handle, void **ptr);
+int fsagg_peer_close(int device, void *ptr);
+int fsagg_weighted_sum_bcast_f32(const float *const *rows,
+                                 const float *weights, const float *prescale,
+                                 int n, int64_t numel, const float *base,
+                                 float *const *outs, int nout,
+                                 fsagg_stream_t stream);
+int fsagg_peer_barrier(uint32_t *const *flags, int world, int rank,
+                       uint32_t epoch, uint64_t timeout_ticks,
+                       uint32_t *status, fsagg_stream_t stream);
+
+/*
  * Deterministic synthetic client updates (benchmarks / tests): fills the
  * [n][ld] slab X with u = hash(seed, client, index) mapped to [-1, 1),
  * index < numel; the same generator is restated on the host by the tests.

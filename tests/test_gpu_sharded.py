@@ -94,3 +94,56 @@ def test_pipelined_assembly_gpu_world1_bit_exact(chunks):
 
     got = pa.run(compute, device=dev)
     assert torch.equal(got, full)
+
+
+@pytest.mark.parametrize('world,rank,streams,split', [
+    (4, 0, 1, None), (4, 3, 2, None), (8, 5, 2, 'taper'), (8, 0, 1, 'taper'),
+    (2, 1, 2, (3, 1))])
+def test_pipelined_assembly_async_comm_ordering(world, rank, streams, split):
+    """PipelinedAssembly.run under a Comm whose all-gather returns a real
+    async work handle (tools/emu_comm.py: the gather runs on its own stream,
+    waits on the issuing stream and is delayed by a spin kernel, as RCCL's
+    in-place all_gather_into_tensor(async_op=True) does).  The code path only
+    RCCL reaches: works/w.wait() and the side-stream hand-off.  Every piece
+    the collective read must be the finished piece, and the assembled result
+    must be bit-exact once run() returns (read on the caller's stream)."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), 'tools'))
+    from emu_comm import EmuComm
+    from federatedscope_amd import ops
+    from federatedscope_amd.core.sharding import (PipelinedAssembly,
+                                                  tapered_split)
+    n, P = 11, 1_000_003
+    dev, slab, ld = _setup(n, P, seed=21)
+    w = O.fedavg_weights(list(range(5, n + 5)))
+    split = tapered_split(4) if split == 'taper' else split
+    probe = EmuComm(world, rank, dev)
+    pa = PipelinedAssembly(P, comm=probe, streams=streams, split=split)
+    expected = torch.zeros(pa.padded, device=dev)
+    ops.weighted_sum(ops.RowTable.from_slab(slab, numel=P), w,
+                     expected[:P])
+    out = torch.full((pa.padded, ), float('nan'), device=dev)
+    comm = EmuComm(world, rank, dev, expected=expected, base=out,
+                   delay_us=300.0)
+    pa = PipelinedAssembly(P, comm=comm, streams=streams, split=split)
+    assert pa.streams == streams
+
+    def compute(j, lo, hi, view):
+        # a slow piece: the spin makes a collective that does not wait for
+        # its piece read NaNs
+        torch.cuda._sleep(200_000)
+        ops.weighted_sum(ops.RowTable.from_slab(slab, col_offset=lo,
+                                                numel=hi - lo), w, view)
+
+    torch.cuda.synchronize()
+    got = pa.run(compute, out=out)
+    # read on the caller's stream right away (no synchronize before it)
+    res = got.clone()
+    assert comm.calls == pa.chunks
+    assert torch.equal(res, expected[:P])
+    for j, (own, snap) in enumerate(sorted(comm.sent, key=lambda s: s[0])):
+        lo, hi = pa.piece(j)
+        assert own == pa.slot(j)
+        assert torch.equal(snap[:hi - lo], expected[lo:hi])

@@ -30,9 +30,9 @@ def _port():
     return p
 
 
-def _run2(args, timeout=110):
+def _run2(args, timeout=110, nproc=2):
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes', '1',
-           '--nproc-per-node', '2', '--master-addr', '127.0.0.1',
+           '--nproc-per-node', str(nproc), '--master-addr', '127.0.0.1',
            '--master-port', str(_port())] + args
     env = dict(os.environ, OMP_NUM_THREADS='4')
     p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True,
@@ -60,6 +60,25 @@ def test_bench_strong_scaling_world2():
     assert r['n_gpus'] == 2 and r['scaling'] == 'strong'
     assert r['assembled_bit_exact'] is True
     assert r['config']['params'] == 1000003
+
+
+@pytest.mark.parametrize('world', [2, 4])
+def test_bench_peer_assembly(world):
+    """bench.py's peer assembly (core/sharding.PeerAssembly): each rank's
+    kernel stores its piece into every rank's uncached output buffer through
+    IPC-imported pointers, then the flag barrier — here 2 / 4 processes on
+    one GPU (same-device IPC), on the 8-GPU node the same code over xGMI.
+    Every rank's assembled result must be bit-exact, and the barrier must
+    not have timed out (bench.py calls PeerAssembly.check())."""
+    recs = _run2(['bench.py', '--gpus', str(world), '--backend', 'gloo',
+                  '--assembly', 'p2p', '--clients', '10', '--params',
+                  '1000003', '--steps', '5', '--warmup', '2',
+                  '--no-cpu-baseline', '--no-weak'], nproc=world)
+    assert len(recs) == 1
+    r = recs[0]
+    assert r['n_gpus'] == world
+    assert 'peer assembly' in r['config']['parallelism'], r['config']
+    assert r['assembled_bit_exact'] is True
 
 
 def test_sharded_aggregators_world2():

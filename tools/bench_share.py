@@ -1,0 +1,183 @@
+#!/usr/bin/env python3
+"""One GPU's share of the strong-scaled C3 FedAvg (bench.py --gpus N), on a
+one-GPU box: the rank's pieces of every round reduced by the same kernel on
+the same streams as PipelinedAssembly.run, with the RCCL all-gather replaced
+by tools/emu_comm.EmuComm (its own stream, a spin for the link time of the
+bytes the rank receives at an assumed per-GPU receive rate, plus a device
+copy of those bytes).  Prints one JSON line per (world, split, rate).
+
+    python tools/bench_share.py --world 8 --rates 0,350,450,550
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'tools'))
+
+import torch  # noqa: E402
+
+
+def parse_split(s):
+    if s == 'uniform4':
+        return None, 4
+    if s.startswith('uniform'):
+        return None, int(s[7:])
+    if s.startswith('taper'):
+        # taper<r>x<k>, e.g. taper0.5x4
+        r, k = s[5:].split('x')
+        from federatedscope_amd.core.sharding import tapered_split
+        return tapered_split(int(k), float(r)), int(k)
+    w = [float(x) for x in s.split('/')]
+    return w, len(w)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--world', type=int, default=8)
+    ap.add_argument('--rank', type=int, default=0)
+    ap.add_argument('--clients', type=int, default=100)
+    ap.add_argument('--params', type=int, default=25_000_000)
+    ap.add_argument('--splits', default='uniform4,taper0.5x4,taper0.7x4,'
+                    '4/3/2/1,1/3/3/1,uniform3,taper0.6x5')
+    ap.add_argument('--rates', default='0,350,450,550',
+                    help='emulated per-GPU receive GB/s (0: no gather)')
+    ap.add_argument('--streams', type=int, default=0)
+    ap.add_argument('--steps', type=int, default=30)
+    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--copy', type=int, default=1)
+    ap.add_argument('--p2p', action='store_true',
+                    help='time the peer-assembly share instead: one bcast '
+                         'launch over P/world writing `world` uncached local '
+                         'buffers (stand-ins for the peers) + the barrier')
+    args = ap.parse_args()
+    if args.p2p:
+        return p2p_share(args)
+
+    from bench import sample_sizes
+    from emu_comm import EmuComm, sleep_cycles_per_us
+    from federatedscope_amd import ops
+    from federatedscope_amd.core.aggregators._engine import fedavg_weights
+    from federatedscope_amd.core.sharding import PipelinedAssembly
+
+    dev = torch.device('cuda', 0)
+    n, P, W = args.clients, args.params, args.world
+    w = torch.tensor(fedavg_weights(sample_sizes(n)), dtype=torch.float32,
+                     device=dev)
+    cyc = sleep_cycles_per_us(dev)
+    print('[share] _sleep: %.1f cycles/us' % cyc, file=sys.stderr)
+    for spec in args.splits.split(','):
+        split, chunks = parse_split(spec)
+        for rate in [float(r) for r in args.rates.split(',')]:
+            comm = EmuComm(W, args.rank, dev, rate_gbps=rate or None,
+                           copy=bool(args.copy and rate), cyc_per_us=cyc)
+            pa = PipelinedAssembly(P, chunks=chunks, comm=comm, split=split,
+                                   streams=args.streams or None)
+            pieces = []
+            for j, (lo, hi) in enumerate(pa.local_pieces()):
+                slab = torch.empty((n, pa.pcs[j]), dtype=torch.float32,
+                                   device=dev)
+                if hi > lo:
+                    ops.fill_uniform(slab, hi - lo, seed=2026,
+                                     index_offset=lo)
+                pieces.append(ops.RowTable.from_slab(
+                    slab, numel=max(hi - lo, 1)))
+            out = torch.empty(pa.padded, dtype=torch.float32, device=dev)
+            ev = []
+            rec = [False]
+
+            def compute(j, lo, hi, view):
+                if rec[0]:
+                    st = torch.cuda.current_stream(dev)
+                    a = torch.cuda.Event(enable_timing=True)
+                    b = torch.cuda.Event(enable_timing=True)
+                    a.record(st)
+                    ops.weighted_sum(pieces[j], w, view)
+                    b.record(st)
+                    ev.append((a, b))
+                else:
+                    ops.weighted_sum(pieces[j], w, view)
+
+            for _ in range(args.warmup):
+                pa.run(compute, out=out)
+            torch.cuda.synchronize()
+            rec[0] = True
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                pa.run(compute, out=out)
+            torch.cuda.synchronize()
+            t = (time.perf_counter() - t0) / args.steps
+            kern = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+            print(json.dumps({
+                'world': W, 'split': spec, 'pcs': pa.pcs,
+                'streams': pa.streams, 'rate_GBps': rate,
+                'step_ms': round(t * 1e3, 4),
+                'kernel_ms_sum': round(kern, 4),
+                'speedup_vs_1458us': round(1.458 / (t * 1e3), 2)}),
+                flush=True)
+            del pieces, out
+            torch.cuda.empty_cache()
+
+
+def p2p_share(args):
+    """PeerAssembly's per-rank step on one GPU: the bcast kernel over this
+    rank's P/world coordinates storing into `world` uncached buffers (own +
+    stand-ins for the peers, all local here: on the node world-1 of them are
+    xGMI stores), then the flag barrier (world 1)."""
+    import ctypes
+    from bench import sample_sizes
+    from federatedscope_amd import _lib as L, ops
+    from federatedscope_amd.core.aggregators._engine import fedavg_weights
+    from federatedscope_amd.core.sharding import PeerAssembly
+    dev = torch.device('cuda', 0)
+    n, P, W = args.clients, args.params, args.world
+    w = torch.tensor(fedavg_weights(sample_sizes(n)), dtype=torch.float32,
+                     device=dev)
+    pp = PeerAssembly(P // W, device=dev)      # world 1: own buffers only
+    lib = L.load()
+    fake = []
+    for _ in range(W - 1):
+        p = ctypes.c_void_p()
+        L.check(lib.fsagg_peer_alloc(0, pp.padded * 4, ctypes.byref(p)))
+        fake.append(int(p.value))
+    slab = torch.empty((n, pp.pc), dtype=torch.float32, device=dev)
+    ops.fill_uniform(slab, pp.numel, seed=2026, index_offset=0)
+    rows = ops.RowTable.from_slab(slab, numel=pp.numel)
+    for ndst in sorted({1, W}):
+        ev = []
+
+        def compute(lo, hi, outs):
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record()
+            ops.weighted_sum_bcast(rows, w, (outs + fake)[:ndst])
+            b.record()
+            ev.append((a, b))
+
+        for _ in range(args.warmup):
+            pp.run(compute)
+        torch.cuda.synchronize()
+        ev.clear()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            pp.run(compute)
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / args.steps
+        pp.check()
+        kern = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+        print(json.dumps({
+            'mode': 'p2p-share', 'world': W, 'outputs': ndst,
+            'share_params': pp.numel, 'step_ms': round(t * 1e3, 4),
+            'kernel_ms': round(kern, 4),
+            'kernel_TBps_in': round(4.0 * n * pp.numel / kern / 1e9, 3),
+            'speedup_vs_1458us': round(1.458 / (t * 1e3), 2)}), flush=True)
+    for p in fake:
+        lib.fsagg_peer_free(0, p)
+    pp.close()
+
+
+if __name__ == '__main__':
+    main()
