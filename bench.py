@@ -422,7 +422,7 @@ def main():
     # regenerated here and reduced by the same kernel, must equal what the
     # all-gather delivered, bit for bit
     ok = True
-    probe = min(65536, pa.pc)
+    probe = min(65536, max(pa.pcs))
     for j in range(chunks):
         for r in range(world):
             lo, hi = pa.piece(j, r)

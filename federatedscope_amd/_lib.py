@@ -124,6 +124,8 @@ SIGNATURES['fsagg_peer_free'] = (_c_i, [_c_i, _c_p])
 SIGNATURES['fsagg_peer_handle'] = (_c_i, [_c_p, _c_p])
 SIGNATURES['fsagg_peer_open'] = (_c_i, [_c_i, _c_p, ctypes.POINTER(_c_p)])
 SIGNATURES['fsagg_peer_close'] = (_c_i, [_c_i, _c_p])
+SIGNATURES['fsagg_peer_pci_bus_id'] = (_c_i, [_c_i, ctypes.c_char_p, _c_i])
+SIGNATURES['fsagg_peer_can_access'] = (_c_i, [_c_i, ctypes.c_char_p])
 SIGNATURES['fsagg_weighted_sum_bcast_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i, _c_i64, _c_p, ctypes.POINTER(_c_p), _c_i,
            _c_p])

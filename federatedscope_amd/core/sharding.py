@@ -375,6 +375,18 @@ class PeerAssembly:
                 self._own.append(self._alloc(nbytes))
             self._own.append(self._alloc(self.CTRL_WORDS * 4))
             hb = int(self._lib.fsagg_peer_handle_bytes())
+            bus = ctypes.create_string_buffer(64)
+            self._L.check(self._lib.fsagg_peer_pci_bus_id(idx, bus, 64),
+                          'fsagg_peer_pci_bus_id')
+            buses = self.comm.all_gather_bytes(bus.value)
+            for k, b in enumerate(buses):
+                ok = self._lib.fsagg_peer_can_access(idx, b)
+                if ok < 0:
+                    self._L.check(ok, 'fsagg_peer_can_access')
+                if ok == 0:
+                    raise RuntimeError('GPU %s cannot access rank %d\'s GPU '
+                                       '%s' % (bus.value.decode(), k,
+                                               b.decode()))
             mine = b''.join(self._handle(p, hb) for p in self._own)
             every = self.comm.all_gather_bytes(mine)
             # ptr[k] = rank k's allocations (buffers..., ctrl) as seen here

@@ -87,20 +87,7 @@ struct PairPlan {
   // one TS×TS accumulator set (kso/ksd k-slices); no slot is spent on a
   // diagonal tile's lower half
   int split, wo, ro, kso, rd, ksd;
-  int mode;  // experiments only (FSAGG_PAIR_MODE): 1 = no distance updates
 };
-
-// FSAGG_PAIRDIST=nosplit keeps the whole-tile form (A/B runs); the split
-// form is packed only (FSAGG_PAIR_FORM=scalar turns it off too)
-static bool split_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char *e = getenv("FSAGG_PAIRDIST");
-    const char *f = getenv("FSAGG_PAIR_FORM");
-    on = !(e && strcmp(e, "nosplit") == 0) && !(f && strcmp(f, "scalar") == 0);
-  }
-  return on == 1;
-}
 
 // The LDS pitch of a staged coordinate row: ≥ the client slots, ≡ 4 (mod
 // 8) words — with the blocked item order of stage_item() (8 lanes = 2
@@ -112,7 +99,7 @@ inline int stage_pitch(int quads) {
   return p;
 }
 
-PairPlan make_plan(int n, int64_t numel, int nseg, bool dbuf = false) {
+PairPlan make_plan(int n, int64_t numel, int nseg) {
   PairPlan pl;
   const int nt8 = (n + 7) / 8, nt10 = (n + 9) / 10;
   pl.ts = int64_t(nt10) * (nt10 + 1) / 2 * 100 < int64_t(nt8) * (nt8 + 1) / 2 * 64
@@ -124,10 +111,6 @@ PairPlan make_plan(int n, int64_t numel, int nseg, bool dbuf = false) {
   pl.ks = kBlock / pl.tpg;
   pl.split = 0;
   pl.wo = pl.ro = pl.kso = pl.rd = pl.ksd = 0;
-  {
-    const char *e = getenv("FSAGG_PAIR_MODE");
-    pl.mode = e ? atoi(e) : 0;
-  }
   // pitch ≡ 28 (mod 32) words: conflict-free b128 staging writes and reads
   pl.ldsp = (pl.nt * pl.ts + 3) / 4 * 4 + 4;
   while (pl.ldsp % 32 != 28) pl.ldsp += 4;
@@ -137,9 +120,9 @@ PairPlan make_plan(int n, int64_t numel, int nseg, bool dbuf = false) {
   // most what the LDS holds and, when the stage can be register-prefetched
   // (stage_items(ts) float4 quads per thread), what the registers hold.
   const int unit = std::lcm(4, pl.ks);
-  // double-buffered stages (dbuf): two stage buffers share the LDS
-  // (one row of each buffer region stays free for the kernel's zero row)
-  const int lds_cap = kLdsFloats / (dbuf ? 2 : 1) / pl.ldsp - 1;
+  // double-buffered stages: two stage buffers share the LDS (one row of
+  // each buffer region stays free for the kernel's zero row)
+  const int lds_cap = kLdsFloats / 2 / pl.ldsp - 1;
   const int quads = (pl.nt * pl.ts + 3) / 4;
   const int reg_cap = stage_items(pl.ts) * kBlock / quads * 4;
   const int limit = reg_cap >= unit && reg_cap < lds_cap ? reg_cap : lds_cap;
@@ -149,7 +132,7 @@ PairPlan make_plan(int n, int64_t numel, int nseg, bool dbuf = false) {
   // a stage costs max(⌈sub/kso⌉, ⌈sub/ksd⌉) coordinate steps of TS² packed
   // ops against ⌈sub/ks⌉ for the whole-tile form (at n = 50: 152 / 8 = 19
   // coordinates per step against 136 / 8 = 17)
-  if (dbuf && split_enabled() && pl.groups == 1 && pl.nt >= 2) {
+  if (pl.groups == 1 && pl.nt >= 2) {
     const int ro = pl.nt * (pl.nt - 1) / 2, rd = (pl.nt + 1) / 2;
     const int ldsp = stage_pitch(quads);
     const int lcap = kLdsFloats / 2 / ldsp - 1;
@@ -179,8 +162,7 @@ PairPlan make_plan(int n, int64_t numel, int nseg, bool dbuf = false) {
   }
   // ≈ 1000 chunks (two rounds of the 2 × 256 resident workgroups), whole
   // stages (16-B aligned whenever the chunk start is)
-  int64_t rounds = 1024;
-  if (const char *e = getenv("FSAGG_PAIR_CHUNKS")) rounds = atoi(e);
+  const int64_t rounds = 1024;
   const int64_t target = rounds - nseg > 256 ? rounds - nseg : 256;
   int64_t chl = (numel + target - 1) / target;
   if (chl < 2048) chl = 2048;
@@ -449,11 +431,10 @@ __device__ __forceinline__ bool split_slot(bool diag, int l, int idx, int ts,
   return uu < vv && t < nt;
 }
 
-// PK: the row-pair packed form (v_pk_add_f32 / v_pk_fma_f32, two pairs per
-// instruction); else scalar v_sub_f32 / v_fma_f32 on the same accumulators.
-// SPLIT (with PK and DB): the split-role form of PairPlan; LDSR = 1 reads
-// its operands with pair_step_dsr.
-template <int TS, bool PK, bool DB, bool SPLIT, int LDSR = 0>
+// Row-pair packed updates (v_pk_add_f32 / v_pk_fma_f32, two pairs per
+// instruction) over double-buffered LDS stages.  SPLIT: the split-role form
+// of PairPlan; LDSR = 1 reads its operands with pair_step_dsr.
+template <int TS, bool SPLIT, int LDSR = 0>
 __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n,
     PairPlan pl, const int64_t *__restrict__ seg_lo,
@@ -482,7 +463,6 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   // client r's row of this key segment: rows[r] (a virtual base)
   const float *const *__restrict__ rows = tab + int64_t(s) * ss;
 
-  static_assert(!SPLIT || (PK && DB), "split form: packed, double-buffered");
   const int tid = threadIdx.x;
   int tpl = 0, ksl, kstep;
   bool active, diag = false;
@@ -623,7 +603,7 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
       vec && items <= kStageItems * kBlock && n <= kPtrSlots;
   // a zero row past the last stage row of buffer 0 (the plan keeps it
   // free): lanes past their last coordinate of a stage read it
-  float *const zrow = lds + (DB ? kLdsFloats / 2 : kLdsFloats) - pl.ldsp;
+  float *const zrow = lds + kLdsFloats / 2 - pl.ldsp;
   for (int i = tid; i < pl.ldsp; i += kBlock) zrow[i] = 0.0f;
   if (n <= kPtrSlots) {
     for (int r = tid; r < n; r += kBlock) rowp[r] = rows[r];
@@ -635,7 +615,6 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   // coordinate, or an idle lane, reads the zero row and adds (0 - 0)^2 — no
   // divergent loop, so the accumulators stay in place across stages.
   auto compute = [&](const float *buf, int len, auto role) {
-    if (pl.mode == 1) return;
     const int steps = (len + kstep - 1) / kstep;
     auto col_of = [&](int s) {
       const int cc = ksl + s * kstep;
@@ -691,33 +670,20 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
       const float *col = col_of(s);
       float b[TS];
       read_tile<TS>(col, tj, b);
-      if constexpr (PK) {
-        const f2 *ap = reinterpret_cast<const f2 *>(col + ti * TS);
-        f2 a[TS / 2];
+      const f2 *ap = reinterpret_cast<const f2 *>(col + ti * TS);
+      f2 a[TS / 2];
 #pragma unroll
-        for (int h = 0; h < TS / 2; ++h) a[h] = ap[h];
+      for (int h = 0; h < TS / 2; ++h) a[h] = ap[h];
 #pragma unroll
-        for (int v = 0; v < TS; ++v) {
-          // all TS/2 differences first, then the fmas: a packed fma that
-          // reads the packed add just before it needs a wait state (s_nop)
-          f2 d[TS / 2];
+      for (int v = 0; v < TS; ++v) {
+        // all TS/2 differences first, then the fmas: a packed fma that
+        // reads the packed add just before it needs a wait state (s_nop)
+        f2 d[TS / 2];
 #pragma unroll
-          for (int h = 0; h < TS / 2; ++h) d[h] = a[h] - f2{b[v], b[v]};
+        for (int h = 0; h < TS / 2; ++h) d[h] = a[h] - f2{b[v], b[v]};
 #pragma unroll
-          for (int h = 0; h < TS / 2; ++h)
-            acc[h][v] = __builtin_elementwise_fma(d[h], d[h], acc[h][v]);
-        }
-      } else {
-        float a[TS];
-        read_tile<TS>(col, ti, a);
-#pragma unroll
-        for (int u = 0; u < TS; ++u)
-#pragma unroll
-          for (int v = 0; v < TS; ++v) {
-            const float d = a[u] - b[v];
-            acc[u >> 1][v][u & 1] =
-                __builtin_fmaf(d, d, acc[u >> 1][v][u & 1]);
-          }
+        for (int h = 0; h < TS / 2; ++h)
+          acc[h][v] = __builtin_elementwise_fma(d[h], d[h], acc[h][v]);
       }
     }
   };
@@ -780,18 +746,7 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
     return;
   }
   if (prefetch && end - start >= pl.sub) fetch(start, pre);
-  if constexpr (!DB) {
-    for (int64_t cs = start; cs < end; cs += pl.sub) {
-      const int len = stage_len(cs);
-      if (prefetch && len == pl.sub) stage_from_regs(lds, pre);
-      else stage_scalar(lds, cs, len);
-      __syncthreads();
-      // next full stage's loads fly while this one is computed
-      if (prefetch && end - (cs + pl.sub) >= pl.sub) fetch(cs + pl.sub, pre);
-      compute(lds, len, role);
-      __syncthreads();
-    }
-  } else {
+  {
     // two stage buffers, one barrier per stage: stage s + 1 is written into
     // the buffer stage s - 1 was read from (every wave has passed the
     // barrier after it) while stage s is computed from the other
@@ -911,39 +866,42 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
 // is one ds_read2st64_b32 (row offsets 2h·P64 and (2h+1)·P64 in units of
 // 64 dwords), so the packed updates need no operand moves.  Columns [S, P)
 // stay zero: a lane past the stage's coordinates reads them and adds 0.
-constexpr int kRingThreads = 512;
-constexpr int kRingWaves = kRingThreads / kWave;
 constexpr int kRingLds = 38912;  // floats: 152 KiB, one workgroup per CU
-constexpr int kRingRed = kRingLds / kRingThreads;  // accumulators per pass
-constexpr int kRingSlots = 3;
 
 struct RingPlan {
   int ts, nt, ntp;  // tile layout (PairPlan's; partial[] has its layout)
-  int rw;           // DMA rows per wave per stage (staged rows rw·8; rows
-                    // past the tiles repeat row n − 1 and are never read)
+  int waves;        // workgroup waves (one workgroup per CU)
+  int slots;        // ring slots (slots - 1 stages in flight)
+  int rw;           // DMA rows per wave per stage (staged rows rw·waves;
+                    // rows past n are never loaded nor read)
   int p64;          // row pitch / 64 floats
   int S;            // coordinates per stage (multiple of 4, <= 256)
-  int slot;         // floats per ring slot (rw·8 rows × pitch)
+  int slot;         // floats per ring slot (rw·waves rows × pitch)
+  int red;          // reduction floats per thread (kRingLds / threads)
   int wo, ro, ko, rd, kd;  // split roles (as PairPlan's wo, ro, kso, ...)
   int mo, md;       // coordinate steps per stage of the two role kinds
   int64_t chl, max_chunks;
   int ok;
 };
 
-RingPlan make_ring_plan(int n, int64_t numel, int nseg) {
+RingPlan make_ring_plan(int n, int64_t numel, int nseg, int waves = 12,
+                        int slots = 3) {
   const PairPlan pp = make_plan(n, numel, nseg);
   RingPlan p{};
   p.ts = pp.ts;
   p.nt = pp.nt;
   p.ntp = pp.ntp;
-  p.rw = (p.nt * p.ts + kRingWaves - 1) / kRingWaves;
+  p.waves = waves;
+  p.slots = slots;
+  p.red = kRingLds / (waves * kWave);
+  p.rw = (p.nt * p.ts + waves - 1) / waves;
   p.ok = 0;
   p.S = 4;
   const int ro = p.nt * (p.nt - 1) / 2, rd = (p.nt + 1) / 2;
   double best = 0.0;
   if (p.nt >= 2 && p.rw <= 8) {
-    for (int wo = 1; wo < kRingWaves; ++wo) {
-      const int ko = kWave * wo / ro, kd = kWave * (kRingWaves - wo) / rd;
+    for (int wo = 1; wo < waves; ++wo) {
+      const int ko = kWave * wo / ro, kd = kWave * (waves - wo) / rd;
       if (ko < 1 || kd < 1) continue;
       for (int S = 4; S <= 4 * kWave; S += 4) {
         const int mo = (S + ko - 1) / ko, md = (S + kd - 1) / kd;
@@ -951,8 +909,8 @@ RingPlan make_ring_plan(int n, int64_t numel, int nseg) {
         const int reach = std::max(std::max(mo * ko, md * kd), S + 1);
         const int p64 = (reach + 63) / 64;
         if (p64 > 4) break;
-        const int slot = p.rw * kRingWaves * 64 * p64;
-        if (kRingSlots * slot > kRingLds) break;
+        const int slot = p.rw * waves * 64 * p64;
+        if (slots * slot > kRingLds) break;
         const double eff = double(S) / std::max(mo, md);
         if (eff > best || (eff == best && S > p.S)) {
           best = eff;
@@ -971,7 +929,7 @@ RingPlan make_ring_plan(int n, int64_t numel, int nseg) {
       }
     }
   }
-  p.ok = p.ok && p.ts * p.ts <= 2 * kRingRed;
+  p.ok = p.ok && p.ts * p.ts <= 2 * p.red;
   // ≈ 4 rounds of the 256 resident workgroups, whole stages
   const int64_t target = 1024 - nseg > 256 ? 1024 - nseg : 256;
   int64_t chl = (numel + target - 1) / target;
@@ -1016,12 +974,15 @@ __device__ __forceinline__ void wait_vmcnt(int k) {
   }
 }
 
-template <int TS, int P64>
-__global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
+template <int TS, int P64, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void pairdist_ring_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n, RingPlan pl,
     const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
     int nseg, const int *__restrict__ prefix, float *__restrict__ partial) {
   constexpr int P = 64 * P64;
+  constexpr int kRingThreads = WAVES * kWave;
+  constexpr int kRingWaves = WAVES;
+  const int kRingSlots = pl.slots;
   __shared__ __attribute__((aligned(16))) float lds[kRingLds];
   const int c = blockIdx.x;
   if (c >= prefix[nseg]) return;
@@ -1088,17 +1049,22 @@ __global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
 #pragma unroll
   for (int j = 0; j < 8; ++j) rp[j] = rows[min(wave + kRingWaves * j, n - 1)];
   const uint32_t lds_base = uint32_t(uintptr_t((lfloat_t *)lds));
+  // DMAs this wave issues per stage (its rows below n); a partial last
+  // stage issues as many (its lanes are masked, not its instructions)
+  int my_rows = 0;
+  for (int j = 0; j < pl.rw; ++j) my_rows += wave + kRingWaves * j < n;
   auto issue = [&](int st) {
     const int64_t cs = start + int64_t(st) * pl.S;
     const int nq = int(min(int64_t(pl.S), end4 - cs) >> 2);
     const uint32_t slot = lds_base + 4u * uint32_t((st % kRingSlots) * pl.slot);
-    if (lane < (pl.S >> 2)) {
-      // lanes past the stage's quads (its last, partial stage) re-read its
-      // first quad into columns no lane reads (c >= len maps to column S)
-      const uint32_t voff = 16u * uint32_t(lane < nq ? lane : 0);
+    // lanes past the stage's quads (its last, partial stage) load nothing:
+    // the columns they would fill are never read (c >= len maps to the
+    // zero column S); rows past the last client are never loaded
+    if (lane < nq) {
+      const uint32_t voff = 16u * uint32_t(lane);
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        if (j < pl.rw)
+        if (j < pl.rw && wave + kRingWaves * j < n)
           glds16(rp[j] + cs, voff,
                  slot + 4u * uint32_t((wave + kRingWaves * j) * P));
     }
@@ -1128,13 +1094,12 @@ __global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
         pair_update<TS, D>(acc, A, B);
       }
     };
-#pragma unroll
     for (int q = 0; q < kRingSlots - 1; ++q)
       if (q < nstage) issue(q);
     for (int st = 0; st < nstage; ++st) {
       // this wave's DMAs of stage st have landed (later ones may fly)
       const int later = min(nstage - 1 - st, kRingSlots - 2);
-      wait_vmcnt(later * pl.rw);
+      wait_vmcnt(later * my_rows);
       __builtin_amdgcn_s_barrier();
       if (st + kRingSlots - 1 < nstage) issue(st + kRingSlots - 1);
       const int64_t cs = start + int64_t(st) * pl.S;
@@ -1162,9 +1127,9 @@ __global__ __launch_bounds__(kRingThreads) void pairdist_ring_kernel(
 
   // Σ over the k-slices of each role, in slice order
   constexpr int kE = TS * TS;
+  constexpr int R = kRingLds / kRingThreads;
 #pragma unroll
-  for (int e0 = 0; e0 < kE; e0 += kRingRed) {
-    constexpr int R = kRingRed;
+  for (int e0 = 0; e0 < kE; e0 += R) {
     const int ne = kE - e0 < R ? kE - e0 : R;
     if (active) {
       float *slot = lds + tid * R;
@@ -1447,54 +1412,18 @@ extern "C" size_t fsagg_pairdist_workspace_bytes(int n, int64_t numel,
          align256(sizeof(double) * size_t(nseg) * size_t(n) * size_t(n));
 }
 
-// FSAGG_PAIR_FORM=scalar selects the scalar form of the register-staged
-// kernel (A/B runs)
-static bool packed_form() {
-  static int on = -1;
-  if (on < 0) {
-    const char *e = getenv("FSAGG_PAIR_FORM");
-    on = !(e && strcmp(e, "scalar") == 0);
-  }
-  return on == 1;
+// Experiment switches exist only in the probe build (tools/probe/Makefile,
+// -DFSAGG_PROBE); the product library always takes the defaults.
+#ifdef FSAGG_PROBE
+static int probe_int(const char *name, int dflt) {
+  const char *e = getenv(name);
+  return e ? atoi(e) : dflt;
 }
+#else
+static int probe_int(const char *, int dflt) { return dflt; }
+#endif
 
-// FSAGG_PAIRDIST=ring selects the LDS-DMA ring kernel (A/B runs; at C4 the
-// register-staged split-role kernel measured 0.49 ms against the ring's
-// 0.51, and 0.56 with the ring's LDS reads software-pipelined).
-// The double-buffered stage loop (one barrier per stage, half-size stages)
-// is the default: 0.556 against 0.567–0.571 ms for the single-buffered loop
-// (two barriers per stage) at C4 in interleaved A/B, before the split form;
-// FSAGG_PAIRDIST=flat selects the latter.
-static bool dbuf_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char *e = getenv("FSAGG_PAIRDIST");
-    on = !(e && (strcmp(e, "flat") == 0 || strcmp(e, "ring") == 0));
-  }
-  return on == 1;
-}
-
-// The split form's operand reads as counted ds_read_b64 (pair_step_dsr):
-// C4 chunk kernel 0.466-0.470 ms against 0.486-0.490 ms with the compiler's
-// merged ds_read2_b64 in interleaved A/B; FSAGG_PAIR_LDS=merged selects the
-// latter (A/B runs)
-static int lds_read_form() {
-  static int form = -1;
-  if (form < 0) {
-    const char *e = getenv("FSAGG_PAIR_LDS");
-    form = e && strcmp(e, "merged") == 0 ? 0 : 1;
-  }
-  return form;
-}
-
-static bool ring_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char *e = getenv("FSAGG_PAIRDIST");
-    on = e && strcmp(e, "ring") == 0;
-  }
-  return on == 1;
-}
+static bool ring_enabled() { return probe_int("FSAGG_PROBE_RING", 0) != 0; }
 
 // Enqueue the chunk and per-segment kernels; segsq receives [nseg][n][n].
 static int pairdist_segsq_impl(const float *const *tab, int64_t ss, int n,
@@ -1502,20 +1431,27 @@ static int pairdist_segsq_impl(const float *const *tab, int64_t ss, int n,
                                const int64_t *seg_lo, const int64_t *seg_end,
                                int nseg, double *segsq, void *workspace,
                                hipStream_t s) {
-  const bool db = dbuf_enabled();
-  const PairPlan pl = make_plan(n, numel, nseg, db);
+  const PairPlan pl = make_plan(n, numel, nseg);
   int *prefix = static_cast<int *>(workspace);
   float *partial = reinterpret_cast<float *>(
       static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)));
-  const RingPlan rp = make_ring_plan(n, numel, nseg);
+  const RingPlan rp = make_ring_plan(n, numel, nseg,
+                                     probe_int("FSAGG_PROBE_RING_WAVES", 12),
+                                     probe_int("FSAGG_PROBE_RING_SLOTS", 3));
   if (rp.ok && ring_enabled() && numel > 0) {
     hipLaunchKernelGGL(chunk_prefix_kernel, dim3(1), dim3(1), 0, s, seg_lo,
                        seg_end, nseg, rp.chl, prefix);
     const dim3 grid(unsigned(rp.max_chunks));
-#define FSAGG_RING(TS, P64)                                                 \
-  hipLaunchKernelGGL((pairdist_ring_kernel<TS, P64>), grid,                 \
-                     dim3(kRingThreads), 0, s, tab, ss, n, rp, seg_lo,      \
+#define FSAGG_RINGW(TS, P64, W)                                             \
+  hipLaunchKernelGGL((pairdist_ring_kernel<TS, P64, W>), grid,              \
+                     dim3(W * kWave), 0, s, tab, ss, n, rp, seg_lo,         \
                      seg_end, nseg, prefix, partial)
+#define FSAGG_RING(TS, P64)                                                 \
+  do {                                                                      \
+    if (rp.waves == 8) FSAGG_RINGW(TS, P64, 8);                             \
+    else if (rp.waves == 16) FSAGG_RINGW(TS, P64, 16);                      \
+    else FSAGG_RINGW(TS, P64, 12);                                          \
+  } while (0)
     const bool t10 = rp.ts == 10;
     switch (rp.p64) {
       case 1: if (t10) FSAGG_RING(10, 1); else FSAGG_RING(8, 1); break;
@@ -1524,6 +1460,7 @@ static int pairdist_segsq_impl(const float *const *tab, int64_t ss, int n,
       default: if (t10) FSAGG_RING(10, 4); else FSAGG_RING(8, 4); break;
     }
 #undef FSAGG_RING
+#undef FSAGG_RINGW
     const int per_seg = pl.ntp * pl.ts * pl.ts;
     hipLaunchKernelGGL(pairdist_segsq_kernel,
                        dim3(unsigned(nseg), unsigned((per_seg + kWave - 1) / kWave)),
@@ -1535,37 +1472,19 @@ static int pairdist_segsq_impl(const float *const *tab, int64_t ss, int n,
                      seg_end, nseg, pl.chl, prefix);
   if (numel > 0) {
     const dim3 grid(unsigned(pl.max_chunks), unsigned(pl.groups));
-#define FSAGG_FLAT(TS, PK)                                                    \
-  do {                                                                        \
-    if (db)                                                                   \
-      hipLaunchKernelGGL((pairdist_chunk_kernel<TS, PK, true, false>), grid,  \
-                         dim3(kBlock), 0, s, tab, ss, n, pl, seg_lo, seg_end, \
-                         nseg, prefix, partial);                              \
-    else                                                                      \
-      hipLaunchKernelGGL((pairdist_chunk_kernel<TS, PK, false, false>), grid, \
-                         dim3(kBlock), 0, s, tab, ss, n, pl, seg_lo, seg_end, \
-                         nseg, prefix, partial);                              \
-  } while (0)
-    const bool pk = packed_form();
+#define FSAGG_CHUNK(TS, SPLIT, LDSR)                                         \
+  hipLaunchKernelGGL((pairdist_chunk_kernel<TS, SPLIT, LDSR>), grid,        \
+                     dim3(kBlock), 0, s, tab, ss, n, pl, seg_lo, seg_end,   \
+                     nseg, prefix, partial)
     if (pl.split) {
-      if (pl.ts == 10 && lds_read_form() == 1)
-        hipLaunchKernelGGL((pairdist_chunk_kernel<10, true, true, true, 1>),
-                           grid, dim3(kBlock), 0, s, tab, ss, n, pl, seg_lo,
-                           seg_end, nseg, prefix, partial);
-      else if (pl.ts == 10)
-        hipLaunchKernelGGL((pairdist_chunk_kernel<10, true, true, true>), grid,
-                           dim3(kBlock), 0, s, tab, ss, n, pl, seg_lo, seg_end,
-                           nseg, prefix, partial);
-      else
-        hipLaunchKernelGGL((pairdist_chunk_kernel<8, true, true, true>), grid,
-                           dim3(kBlock), 0, s, tab, ss, n, pl, seg_lo, seg_end,
-                           nseg, prefix, partial);
+      if (pl.ts == 10) FSAGG_CHUNK(10, true, 1);
+      else FSAGG_CHUNK(8, true, 0);
     } else if (pl.ts == 10) {
-      if (pk) FSAGG_FLAT(10, true); else FSAGG_FLAT(10, false);
+      FSAGG_CHUNK(10, false, 0);
     } else {
-      if (pk) FSAGG_FLAT(8, true); else FSAGG_FLAT(8, false);
+      FSAGG_CHUNK(8, false, 0);
     }
-#undef FSAGG_FLAT
+#undef FSAGG_CHUNK
   }
   const int per_seg = pl.ntp * pl.ts * pl.ts;
   hipLaunchKernelGGL(pairdist_segsq_kernel,

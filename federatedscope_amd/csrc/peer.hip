@@ -128,6 +128,33 @@ extern "C" int fsagg_peer_close(int device, void *ptr) {
   return FSAGG_OK;
 }
 
+extern "C" int fsagg_peer_pci_bus_id(int device, char *buf, int len) {
+  if (!buf || len < 16) {
+    set_error("fsagg_peer_pci_bus_id: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  hipError_t e = hipDeviceGetPCIBusId(buf, len, device);
+  if (e != hipSuccess) return hip_fail("fsagg_peer_pci_bus_id", e);
+  return FSAGG_OK;
+}
+
+extern "C" int fsagg_peer_can_access(int device, const char *peer_bus_id) {
+  if (!peer_bus_id) {
+    set_error("fsagg_peer_can_access: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  int peer = -1;
+  if (hipDeviceGetByPCIBusId(&peer, peer_bus_id) != hipSuccess || peer < 0) {
+    (void)hipGetLastError();
+    return 2;  // the peer's GPU is not visible here: nothing to check
+  }
+  if (peer == device) return 1;
+  int ok = 0;
+  hipError_t e = hipDeviceCanAccessPeer(&ok, device, peer);
+  if (e != hipSuccess) return hip_fail("fsagg_peer_can_access", e);
+  return ok ? 1 : 0;
+}
+
 extern "C" int fsagg_peer_barrier(uint32_t *const *flags, int world, int rank,
                                   uint32_t epoch, uint64_t timeout_ticks,
                                   uint32_t *status, fsagg_stream_t stream) {

@@ -442,6 +442,11 @@ int fsagg_rows_sqnorm_f32(const fsagg_rows *rows, const fsagg_chunk *chunks,
  *                    bytes) for the peer processes;
  * fsagg_peer_open    a peer's handle mapped on `device` (peer access enabled
  *                    lazily); fsagg_peer_close unmaps it.
+ * fsagg_peer_pci_bus_id  `device`'s PCI bus id (buf of len >= 16 bytes);
+ * fsagg_peer_can_access  1 if `device` can access the GPU with that bus id
+ *                    (or it is `device`), 0 if it cannot, 2 if that GPU is
+ *                    not visible to this process (nothing to check), < 0 on
+ *                    error.
  * fsagg_weighted_sum_bcast_f32  fsagg_weighted_sum_f32 whose result goes to
  *                    `nout` (<= FSAGG_MAX_PEERS) outputs: outs is a HOST
  *                    array of device pointers (own and peer buffers, each
@@ -463,6 +468,8 @@ int fsagg_peer_free(int device, void *ptr);
 int fsagg_peer_handle(void *ptr, void *handle);
 int fsagg_peer_open(int device, const void *handle, void **ptr);
 int fsagg_peer_close(int device, void *ptr);
+int fsagg_peer_pci_bus_id(int device, char *buf, int len);
+int fsagg_peer_can_access(int device, const char *peer_bus_id);
 int fsagg_weighted_sum_bcast_f32(const float *const *rows,
                                  const float *weights, const float *prescale,
                                  int n, int64_t numel, const float *base,
