@@ -57,11 +57,13 @@ class OptParams(ctypes.Structure):
                 ('momentum', _c_d), ('dampening', _c_d),
                 ('weight_decay', _c_d), ('beta1', _c_d), ('beta2', _c_d),
                 ('eps', _c_d), ('step_size', _c_d),
-                ('bias_correction2_sqrt', _c_d)]
+                ('bias_correction2_sqrt', _c_d), ('alpha', _c_d),
+                ('clr', _c_d), ('decay_mul', _c_d)]
 
 
-FSAGG_OPT_SGD, FSAGG_OPT_ADAM = 0, 1
+FSAGG_OPT_SGD, FSAGG_OPT_ADAM, FSAGG_OPT_ADAGRAD, FSAGG_OPT_RMSPROP = range(4)
 FSAGG_OPT_NESTEROV, FSAGG_OPT_FIRST_STEP, FSAGG_OPT_AMSGRAD = 1, 2, 4
+FSAGG_OPT_DECOUPLED, FSAGG_OPT_MAXIMIZE, FSAGG_OPT_CENTERED = 8, 16, 32
 SIGNATURES['fsagg_server_opt_step_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, ctypes.POINTER(OptParams),
            _c_p])

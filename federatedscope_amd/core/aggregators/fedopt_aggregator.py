@@ -2,11 +2,13 @@
 fedopt_aggregator.py:7-44) with the server-optimizer step on the GPU.
 
 aggregate(): FedAvg of the clients into a device bucket (bit-exact, as
-ClientsAvgAggregator), then ONE fused pass fsagg_server_opt_step_f32 that
-forms g = model − avg and applies torch.optim's SGD (momentum, dampening,
-nesterov, weight decay) or Adam update to the server model's parameter
-bucket and the optimizer-state buckets, which stay resident in HBM across
-rounds.  The updated parameters are written back into ``self.model`` and
+ClientsAvgAggregator), then ONE fused pass fsagg_server_opt_step_f32 per
+parameter that forms g = model − avg and applies the torch.optim step of the
+configured optimizer — SGD (momentum, dampening, nesterov), Adam / AdamW
+(amsgrad), Adagrad (lr_decay, initial accumulator) or RMSprop (momentum,
+centered); weight decay and maximize for all — to the server model's
+parameters and the per-parameter optimizer state, which stays resident in
+HBM across rounds.  The updated parameters are written back into ``self.model`` and
 ``self.model.state_dict()`` is returned, as the reference does.
 
 Optimizer config: ``config.fedopt.optimizer`` = {type, lr, **kwargs} as in
@@ -23,7 +25,13 @@ from ...ops import _check_f32_cuda, _stream
 from ._engine import fedavg_weights
 from .clients_avg_aggregator import ClientsAvgAggregator
 
-_SUPPORTED = ('SGD', 'Adam')
+# torch.optim optimizers the device step implements (optimizer_builder.py:
+# 53-56 builds any torch.optim class by name; these are the ones with a
+# single-tensor elementwise step)
+_SUPPORTED = ('SGD', 'Adam', 'AdamW', 'Adagrad', 'RMSprop')
+# keyword arguments that do not change the arithmetic of a single-tensor CPU
+# step (the reference's optimizer runs on CPU tensors)
+_IGNORED = ('foreach', 'fused', 'capturable', 'differentiable')
 
 
 def _opt_cfg(optimizer_cfg):
@@ -47,28 +55,46 @@ class FedOptAggregator(ClientsAvgAggregator):
             raise NotImplementedError(
                 'FedOpt server optimizer %r is not on the device path '
                 '(supported: %s)' % (self.opt_type, ', '.join(_SUPPORTED)))
+        for k in _IGNORED:
+            opt.pop(k, None)
         self.kw = opt
-        if opt.get('maximize', False):
-            raise NotImplementedError('maximize=True')
-        if self.opt_type == 'SGD':
-            self.momentum = float(opt.get('momentum', 0.0))
-            self.dampening = float(opt.get('dampening', 0.0))
-            self.weight_decay = float(opt.get('weight_decay', 0.0))
-            self.nesterov = bool(opt.get('nesterov', False))
-            self.amsgrad = False
-        else:
-            betas = opt.get('betas', (0.9, 0.999))
+        self.maximize = bool(opt.pop('maximize', False))
+        t = self.opt_type
+        # torch.optim defaults per class
+        self.weight_decay = float(opt.pop('weight_decay',
+                                          1e-2 if t == 'AdamW' else 0.0))
+        self.amsgrad = False
+        if t == 'SGD':
+            self.momentum = float(opt.pop('momentum', 0.0))
+            self.dampening = float(opt.pop('dampening', 0.0))
+            self.nesterov = bool(opt.pop('nesterov', False))
+        elif t in ('Adam', 'AdamW'):
+            betas = opt.pop('betas', (0.9, 0.999))
             self.beta1, self.beta2 = float(betas[0]), float(betas[1])
-            self.eps = float(opt.get('eps', 1e-8))
-            self.weight_decay = float(opt.get('weight_decay', 0.0))
-            self.amsgrad = bool(opt.get('amsgrad', False))
+            self.eps = float(opt.pop('eps', 1e-8))
+            self.amsgrad = bool(opt.pop('amsgrad', False))
+            self.decoupled = t == 'AdamW' or bool(
+                opt.pop('decoupled_weight_decay', False))
+        elif t == 'Adagrad':
+            self.lr_decay = float(opt.pop('lr_decay', 0.0))
+            self.init_acc = float(opt.pop('initial_accumulator_value', 0.0))
+            self.eps = float(opt.pop('eps', 1e-10))
+        else:   # RMSprop
+            self.alpha = float(opt.pop('alpha', 0.99))
+            self.eps = float(opt.pop('eps', 1e-8))
+            self.momentum = float(opt.pop('momentum', 0.0))
+            self.centered = bool(opt.pop('centered', False))
+        if opt:
+            raise TypeError('%s got unexpected arguments %s' %
+                            (self.opt_type, sorted(opt)))
         fo = config.fedopt
         self._annealing = bool(getattr(fo, 'annealing', False))
         self._anneal_step = int(getattr(fo, 'annealing_step_size', 2000))
         self._anneal_gamma = float(getattr(fo, 'annealing_gamma', 0.5))
         self._rounds = 0
-        self._state = {}     # layout signature -> [s0, s1, s2, steps]
-        self._state64 = {}   # float64 parameter -> [s0, s1, s2, steps]
+        # optimizer state per parameter name, as torch.optim keeps it:
+        # name -> [state0, state1, state2, steps]
+        self._state = {}
 
     def _lr(self):
         if not self._annealing:
@@ -94,24 +120,35 @@ class FedOptAggregator(ClientsAvgAggregator):
         layout, avg, extra, _ = self._weighted_avg_device(models, weights)
         return layout, avg, extra
 
-    def _states(self, store, key, like):
-        st = store.get(key)
+    def _states(self, key, like):
+        """The optimizer state of parameter ``key`` (created on its first
+        step, shaped like ``like``: flat, on the compute device)."""
+        st = self._state.get(key)
         if st is None:
-            adam = self.opt_type == 'Adam'
-            st = store[key] = [
-                torch.zeros_like(like),
-                torch.zeros_like(like) if adam else None,
-                torch.zeros_like(like) if adam and self.amsgrad else None, 0]
+            t = self.opt_type
+            z = lambda: torch.zeros_like(like)  # noqa: E731
+            if t == 'SGD':
+                st = [z() if self.momentum != 0.0 else None, None, None]
+            elif t in ('Adam', 'AdamW'):
+                st = [z(), z(), z() if self.amsgrad else None]
+            elif t == 'Adagrad':
+                st = [torch.full_like(like, self.init_acc), None, None]
+            else:
+                st = [z(), z() if self.momentum > 0 else None,
+                      z() if self.centered else None]
+            st.append(0)
+            self._state[key] = st
         return st
 
     def _step(self, fn, param, avg, st):
         """One optimizer step of a contiguous device parameter range."""
         hp = self._params(first=(st[3] == 0), step=st[3] + 1)
-        L.check(fn(param.data_ptr(), avg.data_ptr(), st[0].data_ptr(),
-                   st[1].data_ptr() if st[1] is not None else None,
-                   st[2].data_ptr() if st[2] is not None else None,
+        L.check(fn(param.data_ptr(), avg.data_ptr(),
+                   *[t.data_ptr() if t is not None else None
+                     for t in st[:3]],
                    param.numel(), ctypes.byref(hp), _stream(param.device)),
                 'fedopt step')
+        st[3] += 1
 
     def aggregate(self, agg_info):
         layout, avg, extra = self._new_model(agg_info)
@@ -132,31 +169,23 @@ class FedOptAggregator(ClientsAvgAggregator):
         if inplace:
             # parameters already on the compute device: the optimizer steps
             # them in place (as torch.optim's step does), no bucket copy of
-            # the model in or out; the state stays bucket-shaped
-            st = self._states(self._state, layout.signature(), avg)
+            # the model in or out
             for k in step_keys:
                 o, m = layout.offsets[k], layout.numels[k]
-                for t in (avg, st[0]):
-                    _check_f32_cuda(t[o:o + m], 'FedOpt bucket')
+                _check_f32_cuda(avg[o:o + m], 'FedOpt bucket')
                 self._step(lib.fsagg_server_opt_step_f32,
                            named[k].data.view(-1), avg[o:o + m],
-                           [t[o:o + m] if t is not None else None
-                            for t in st[:3]] + [st[3]])
-            st[3] += 1
+                           self._states(k, avg[o:o + m]))
         elif step_keys:
             param = self._bucket(layout, OrderedDict(
                 (k, named[k].detach() if k in named else torch.zeros(
                     layout.shapes[k])) for k in layout.keys))
-            st = self._states(self._state, layout.signature(), param)
             for k in step_keys:      # per key: params the optimizer owns
                 o, m = layout.offsets[k], layout.numels[k]
-                for t in (param, avg, st[0]):
+                for t in (param, avg):
                     _check_f32_cuda(t[o:o + m], 'FedOpt bucket')
                 self._step(lib.fsagg_server_opt_step_f32, param[o:o + m],
-                           avg[o:o + m], [t[o:o + m] if t is not None
-                                          else None for t in st[:3]] +
-                           [st[3]])
-            st[3] += 1
+                           avg[o:o + m], self._states(k, avg[o:o + m]))
             views = layout.unpack(param)
             with torch.no_grad():
                 for k in step_keys:
@@ -166,9 +195,8 @@ class FedOptAggregator(ClientsAvgAggregator):
                 continue
             p64 = named[k].detach().to(dev, torch.float64).contiguous()
             a64 = extra[k].to(dev, torch.float64).contiguous()
-            st = self._states(self._state64, k, p64)
-            self._step(lib.fsagg_server_opt_step_f64, p64, a64, st)
-            st[3] += 1
+            self._step(lib.fsagg_server_opt_step_f64, p64, a64,
+                       self._states(k, p64.view(-1)))
             with torch.no_grad():
                 named[k].data.copy_(p64)
         self._rounds += 1
@@ -177,23 +205,36 @@ class FedOptAggregator(ClientsAvgAggregator):
     def _params(self, first, step):
         hp = L.OptParams()
         lr = self._lr()
+        t = self.opt_type
         hp.lr = lr
         hp.weight_decay = self.weight_decay
-        if self.opt_type == 'SGD':
+        flags = (L.FSAGG_OPT_FIRST_STEP if first else 0) | \
+            (L.FSAGG_OPT_MAXIMIZE if self.maximize else 0)
+        if t == 'SGD':
             hp.kind = L.FSAGG_OPT_SGD
             hp.momentum = self.momentum
             hp.dampening = self.dampening
-            hp.flags = (L.FSAGG_OPT_NESTEROV if self.nesterov else 0) | \
-                (L.FSAGG_OPT_FIRST_STEP if first else 0)
-        else:
+            flags |= L.FSAGG_OPT_NESTEROV if self.nesterov else 0
+        elif t in ('Adam', 'AdamW'):
             hp.kind = L.FSAGG_OPT_ADAM
             hp.beta1, hp.beta2, hp.eps = self.beta1, self.beta2, self.eps
             bc1 = 1 - self.beta1**step
             bc2 = 1 - self.beta2**step
             hp.step_size = lr / bc1
             hp.bias_correction2_sqrt = bc2**0.5
-            hp.flags = (L.FSAGG_OPT_FIRST_STEP if first else 0) | \
-                (L.FSAGG_OPT_AMSGRAD if self.amsgrad else 0)
+            hp.decay_mul = 1 - lr * self.weight_decay
+            flags |= (L.FSAGG_OPT_AMSGRAD if self.amsgrad else 0) | \
+                (L.FSAGG_OPT_DECOUPLED if self.decoupled else 0)
+        elif t == 'Adagrad':
+            hp.kind = L.FSAGG_OPT_ADAGRAD
+            hp.eps = self.eps
+            hp.clr = lr / (1 + (step - 1) * self.lr_decay)
+        else:
+            hp.kind = L.FSAGG_OPT_RMSPROP
+            hp.alpha, hp.eps, hp.momentum = self.alpha, self.eps, \
+                self.momentum
+            flags |= L.FSAGG_OPT_CENTERED if self.centered else 0
+        hp.flags = flags
         return hp
 
 

@@ -2,10 +2,12 @@
 //
 // FedOptAggregator.aggregate (federatedscope/core/aggregators/
 // fedopt_aggregator.py:26-44) forms the pseudo-gradient g = model - avg and
-// takes one torch.optim step on the server model.  Here the step is one
-// fused elementwise pass over the device buckets — param, FedAvg result and
-// the optimizer state are each read once and param/state written once
-// (SGD: 16 B/elem with momentum, Adam: 24 B/elem, +8 with amsgrad) —
+// takes one step of the torch.optim optimizer the config names
+// (core/auxiliaries/optimizer_builder.py:53-56: SGD, Adam, AdamW, Adagrad,
+// RMSprop) on the server model.  Here the step is one fused elementwise pass
+// over the device buckets — param, FedAvg result and the optimizer state are
+// each read once and param/state written once (SGD: 16 B/elem with
+// momentum, Adam: 24 B/elem, +8 with amsgrad, Adagrad 20 B, RMSprop 20-36) —
 // following the arithmetic of torch's single-tensor CPU kernels (the
 // reference runs the optimizer on CPU tensors): `add(alpha)` is a fused
 // multiply-add (Vectorized fmadd), `lerp` with weight < 0.5 is
@@ -37,6 +39,22 @@ __device__ __forceinline__ double div_t(double a, double b) { return __ddiv_rn(a
 __device__ __forceinline__ float sqrt_t(float a) { return __fsqrt_rn(a); }
 __device__ __forceinline__ double sqrt_t(double a) { return __dsqrt_rn(a); }
 
+// the pseudo-gradient: model - new_model (fedopt_aggregator.py:35), negated
+// for maximize (torch.optim: grad if not maximize else -grad)
+template <typename T>
+__device__ __forceinline__ T pseudo_grad(T x, T a, int flags) {
+  const T g = sub_t(x, a);
+  return (flags & FSAGG_OPT_MAXIMIZE) ? -g : g;
+}
+
+// torch.lerp(self, end, w) on CPU: self + w·(end − self) (an fma) for
+// |w| < 0.5, end − (end − self)·(1 − w) otherwise
+template <typename T>
+__device__ __forceinline__ T lerp_t(T self, T end, T w) {
+  return (w < T(0.5)) ? fma_t(w, sub_t(end, self), self)
+                      : sub_t(end, mul_t(sub_t(end, self), sub_t(T(1), w)));
+}
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void sgd_step_kernel(
     T *__restrict__ param, const T *__restrict__ avg, T *__restrict__ buf,
@@ -48,7 +66,7 @@ __global__ __launch_bounds__(kBlock) void sgd_step_kernel(
   for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < numel;
        p += int64_t(gridDim.x) * kBlock) {
     const T x = param[p];
-    T g = sub_t(x, avg[p]);  // grads = model - new_model  (fedopt_aggregator.py:35)
+    T g = pseudo_grad(x, avg[p], hp.flags);
     if (hp.weight_decay != 0.0) g = fma_t(x, wd, g);
     if (hp.momentum != 0.0) {
       T b;
@@ -74,15 +92,18 @@ __global__ __launch_bounds__(kBlock) void adam_step_kernel(
   const T w2 = T(1.0 - hp.beta2);  // addcmul value
   const T b2 = T(hp.beta2), wd = T(hp.weight_decay), eps = T(hp.eps);
   const T bc2 = T(hp.bias_correction2_sqrt), neg_step = T(-hp.step_size);
+  const bool decoupled = hp.flags & FSAGG_OPT_DECOUPLED;
+  const T dmul = T(hp.decay_mul);  // AdamW: param.mul_(1 - lr * wd)
   for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < numel;
        p += int64_t(gridDim.x) * kBlock) {
-    const T x = param[p];
-    T g = sub_t(x, avg[p]);
-    if (hp.weight_decay != 0.0) g = fma_t(x, wd, g);
-    T a = m1[p];
+    T x = param[p];
+    T g = pseudo_grad(x, avg[p], hp.flags);
+    if (hp.weight_decay != 0.0) {
+      if (decoupled) x = mul_t(x, dmul);
+      else g = fma_t(x, wd, g);
+    }
     // exp_avg.lerp_(grad, 1 - beta1)
-    a = (w1 < T(0.5)) ? fma_t(w1, sub_t(g, a), a)
-                      : sub_t(g, mul_t(sub_t(g, a), sub_t(T(1), w1)));
+    const T a = lerp_t(m1[p], g, w1);
     T v = mul_t(m2[p], b2);
     v = add_t(v, mul_t(mul_t(w2, g), g));  // addcmul_(g, g, 1 - beta2)
     m1[p] = a;
@@ -96,6 +117,67 @@ __global__ __launch_bounds__(kBlock) void adam_step_kernel(
     const T denom = add_t(div_t(sqrt_t(vd), bc2), eps);
     // param.addcdiv_(exp_avg, denom, value=-step_size)
     param[p] = add_t(x, div_t(mul_t(neg_step, a), denom));
+  }
+}
+
+// torch.optim Adagrad (_single_tensor_adagrad): state_sum.addcmul_(g, g,
+// value=1); std = sqrt(state_sum) + eps; param.addcdiv_(g, std,
+// value=-clr)
+template <typename T>
+__global__ __launch_bounds__(kBlock) void adagrad_step_kernel(
+    T *__restrict__ param, const T *__restrict__ avg, T *__restrict__ sum,
+    int64_t numel, fsagg_opt_params hp) {
+  const T wd = T(hp.weight_decay), eps = T(hp.eps), neg_clr = T(-hp.clr);
+  for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < numel;
+       p += int64_t(gridDim.x) * kBlock) {
+    const T x = param[p];
+    T g = pseudo_grad(x, avg[p], hp.flags);
+    if (hp.weight_decay != 0.0) g = fma_t(x, wd, g);
+    const T ss = add_t(sum[p], mul_t(g, g));  // (1·g)·g
+    sum[p] = ss;
+    const T sd = add_t(sqrt_t(ss), eps);
+    param[p] = add_t(x, div_t(mul_t(neg_clr, g), sd));
+  }
+}
+
+// torch.optim RMSprop (_single_tensor_rmsprop): square_avg.mul_(alpha)
+// .addcmul_(g, g, value=1-alpha); centered: grad_avg.lerp_(g, 1-alpha),
+// avg = sqrt(square_avg.addcmul(grad_avg, grad_avg, value=-1)); else
+// avg = sqrt(square_avg); avg += eps; momentum: buf.mul_(momentum)
+// .addcdiv_(g, avg), param.add_(buf, alpha=-lr); else param.addcdiv_(g,
+// avg, value=-lr)
+template <typename T, bool CENTERED, bool MOM>
+__global__ __launch_bounds__(kBlock) void rmsprop_step_kernel(
+    T *__restrict__ param, const T *__restrict__ avg, T *__restrict__ sq,
+    T *__restrict__ buf, T *__restrict__ gavg, int64_t numel,
+    fsagg_opt_params hp) {
+  const T wd = T(hp.weight_decay), eps = T(hp.eps), alpha = T(hp.alpha);
+  const T w = T(1.0 - hp.alpha), mom = T(hp.momentum), neg_lr = T(-hp.lr);
+  for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < numel;
+       p += int64_t(gridDim.x) * kBlock) {
+    const T x = param[p];
+    T g = pseudo_grad(x, avg[p], hp.flags);
+    if (hp.weight_decay != 0.0) g = fma_t(x, wd, g);
+    T v = mul_t(sq[p], alpha);
+    v = add_t(v, mul_t(mul_t(w, g), g));
+    sq[p] = v;
+    T d;
+    if (CENTERED) {
+      const T ga = lerp_t(gavg[p], g, w);
+      gavg[p] = ga;
+      d = sqrt_t(add_t(v, mul_t(mul_t(T(-1), ga), ga)));
+    } else {
+      d = sqrt_t(v);
+    }
+    d = add_t(d, eps);
+    if (MOM) {
+      T b = mul_t(buf[p], mom);
+      b = add_t(b, div_t(g, d));  // addcdiv value 1: (1·g)/avg
+      buf[p] = b;
+      param[p] = fma_t(b, neg_lr, x);
+    } else {
+      param[p] = add_t(x, div_t(mul_t(neg_lr, g), d));
+    }
   }
 }
 
@@ -134,6 +216,33 @@ int opt_step(T *param, const T *avg, T *state0, T *state1, T *state2,
                            dim3(kBlock), 0, s, param, avg, state0, state1,
                            state2, numel, *hp);
       break;
+    case FSAGG_OPT_ADAGRAD:
+      if (!state0) {
+        set_error("%s: Adagrad needs state0", what);
+        return FSAGG_EINVAL;
+      }
+      hipLaunchKernelGGL(adagrad_step_kernel<T>, dim3(grid), dim3(kBlock), 0,
+                         s, param, avg, state0, numel, *hp);
+      break;
+    case FSAGG_OPT_RMSPROP: {
+      const bool centered = hp->flags & FSAGG_OPT_CENTERED;
+      const bool mom = hp->momentum > 0.0;
+      if (!state0 || (mom && !state1) || (centered && !state2)) {
+        set_error("%s: RMSprop needs state0 (and state1 with momentum, "
+                  "state2 when centered)", what);
+        return FSAGG_EINVAL;
+      }
+#define FSAGG_RMS(C, M)                                                      \
+  hipLaunchKernelGGL((rmsprop_step_kernel<T, C, M>), dim3(grid), dim3(kBlock), \
+                     0, s, param, avg, state0, state1, state2, numel, *hp)
+      if (centered) {
+        if (mom) FSAGG_RMS(true, true); else FSAGG_RMS(true, false);
+      } else {
+        if (mom) FSAGG_RMS(false, true); else FSAGG_RMS(false, false);
+      }
+#undef FSAGG_RMS
+      break;
+    }
     default:
       set_error("%s: unknown optimizer kind %d", what, hp->kind);
       return FSAGG_EINVAL;

@@ -183,25 +183,39 @@ int fsagg_row_sqnorm_f32(const float *const *rows, int n, int64_t numel,
                          fsagg_stream_t stream);
 
 /*
- * FedOpt server step on the aggregated bucket (fedopt_aggregator.py:26-44):
- * per element g = param - avg, then one torch.optim step in place on param
- * and the optimizer state buckets (SGD: state0 = momentum buffer; Adam:
- * state0 = exp_avg, state1 = exp_avg_sq, state2 = max_exp_avg_sq with
- * amsgrad).  Scalars are the host's doubles; the kernels convert them to the
+ * FedOpt server step on the aggregated bucket (fedopt_aggregator.py:26-44,
+ * optimizer built by name, core/auxiliaries/optimizer_builder.py:53-56):
+ * per element g = param - avg (negated with FSAGG_OPT_MAXIMIZE), then one
+ * torch.optim single-tensor step in place on param and the optimizer state
+ * buckets:
+ *   SGD      state0 = momentum buffer;
+ *   Adam     state0 = exp_avg, state1 = exp_avg_sq, state2 = max_exp_avg_sq
+ *            (amsgrad); AdamW = Adam with FSAGG_OPT_DECOUPLED: param is
+ *            first scaled by decay_mul = 1 - lr·weight_decay;
+ *   Adagrad  state0 = state_sum; clr = lr / (1 + (step - 1)·lr_decay);
+ *   RMSprop  state0 = square_avg, state1 = momentum buffer (momentum > 0),
+ *            state2 = grad_avg (FSAGG_OPT_CENTERED); alpha the smoothing
+ *            constant.
+ * Scalars are the host's doubles; the kernels convert them to the
  * parameter type as ATen does (Adam's step_size = lr / (1 - beta1^t) and
  * bias_correction2_sqrt = (1 - beta2^t)^0.5 are computed on the host, as
  * torch does).  Tolerance-pinned: ATen's CPU optimizer arithmetic (fmadd
  * in the vectorised body) is ISA-dependent.  _f32 for float32 parameters,
  * _f64 for float64 ones.
  */
-enum fsagg_opt_kind { FSAGG_OPT_SGD = 0, FSAGG_OPT_ADAM = 1 };
+enum fsagg_opt_kind { FSAGG_OPT_SGD = 0, FSAGG_OPT_ADAM = 1,
+                      FSAGG_OPT_ADAGRAD = 2, FSAGG_OPT_RMSPROP = 3 };
 enum fsagg_opt_flags { FSAGG_OPT_NESTEROV = 1, FSAGG_OPT_FIRST_STEP = 2,
-                       FSAGG_OPT_AMSGRAD = 4 };
+                       FSAGG_OPT_AMSGRAD = 4, FSAGG_OPT_DECOUPLED = 8,
+                       FSAGG_OPT_MAXIMIZE = 16, FSAGG_OPT_CENTERED = 32 };
 typedef struct fsagg_opt_params {
   int kind;
   int flags;
   double lr, momentum, dampening, weight_decay;
   double beta1, beta2, eps, step_size, bias_correction2_sqrt;
+  double alpha;      /* RMSprop smoothing constant */
+  double clr;        /* Adagrad's decayed learning rate for this step */
+  double decay_mul;  /* AdamW: 1 - lr * weight_decay */
 } fsagg_opt_params;
 int fsagg_server_opt_step_f32(float *param, const float *avg, float *state0,
                               float *state1, float *state2, int64_t numel,

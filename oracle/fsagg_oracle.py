@@ -457,7 +457,7 @@ def interpolate_aggregate(models, global_model, beta):
 
 
 # ---------------------------------------------------------------------------
-# FedOpt  (fedopt_aggregator.py:26-44 + torch.optim single-tensor SGD/Adam)
+# FedOpt  (fedopt_aggregator.py:26-44 + torch.optim single-tensor steps)
 # ---------------------------------------------------------------------------
 def _fma32(a, b, c):
     """fp32 fused multiply-add, emulated in float64 (a·b is exact there)."""
@@ -466,10 +466,12 @@ def _fma32(a, b, c):
 
 
 class FedOptState:
-    """Server optimizer state carried across rounds (torch.optim semantics,
-    ATen's vectorised fmadd for add(alpha); tolerance-pinned).  float32
-    parameters use an exact fp32 fma; float64 ones plain float64 ops (numpy
-    has no fma: a few ulps apart, within the float64 tolerance)."""
+    """Server optimizer state carried across rounds (torch.optim
+    single-tensor semantics — SGD, Adam, AdamW, Adagrad, RMSprop — with
+    ATen's vectorised fmadd for add(alpha) and lerp; tolerance-pinned).
+    float32 parameters use an exact fp32 fma; float64 ones plain float64 ops
+    (numpy has no fma: a few ulps apart, within the float64 tolerance).
+    Follows torch/optim/{sgd,adam,adagrad,rmsprop}.py _single_tensor_*."""
 
     def __init__(self, params, opt):
         first = np.asarray(next(iter(params.values())))
@@ -481,26 +483,38 @@ class FedOptState:
         self.m = {}
         self.v = {}
         self.vmax = {}
-        self.t = 0
+        self.ga = {}
+        self.steps = {}
 
     def _fma(self, a, b, c):
         if self.dt == f32:
             return _fma32(a, b, c)
         return np.float64(a) * np.float64(b) + np.asarray(c, np.float64)
 
+    def _lerp(self, a, b, w):
+        """torch.lerp(a, b, w) on CPU (w < 0.5: a + w·(b − a) as an fma)."""
+        T = self.dt
+        if w < 0.5:
+            return self._fma(T(w), b - a, a)
+        return b - (b - a) * T(1 - w)
+
     def step(self, models):
         avg = para_weighted_avg(models)
         o = self.opt
         T = self.dt
-        self.t += 1
+        typ = o['type']
         for k, x in self.params.items():
             if k not in avg:
                 continue
+            t = self.steps[k] = self.steps.get(k, 0) + 1
             g = x - avg[k]
-            wd = o.get('weight_decay', 0.0)
-            if wd:
+            if o.get('maximize', False):
+                g = -g
+            wd = o.get('weight_decay', 1e-2 if typ == 'AdamW' else 0.0)
+            decoupled = typ == 'AdamW'
+            if wd and not decoupled:
                 g = self._fma(x, T(wd), g)
-            if o['type'] == 'SGD':
+            if typ == 'SGD':
                 mom = o.get('momentum', 0.0)
                 if mom:
                     if k not in self.buf:
@@ -512,15 +526,17 @@ class FedOptState:
                     g = self._fma(self.buf[k], T(mom), g) if o.get(
                         'nesterov', False) else self.buf[k]
                 self.params[k] = self._fma(g, T(-o['lr']), x)
-            else:
+            elif typ in ('Adam', 'AdamW'):
+                if wd and decoupled:
+                    x = x * T(1 - o['lr'] * wd)
                 b1, b2 = o.get('betas', (0.9, 0.999))
                 eps = o.get('eps', 1e-8)
                 m = self.m.get(k, np.zeros_like(x))
                 v = self.v.get(k, np.zeros_like(x))
-                m = self._fma(T(1 - b1), g - m, m)
+                m = self._lerp(m, g, 1 - b1)
                 v = v * T(b2) + (T(1 - b2) * g) * g
-                bc1 = 1 - b1**self.t
-                bc2 = 1 - b2**self.t
+                bc1 = 1 - b1**t
+                bc2 = 1 - b2**t
                 vd = v
                 if o.get('amsgrad', False):
                     vd = np.maximum(self.vmax.get(k, np.zeros_like(x)), v)
@@ -528,6 +544,38 @@ class FedOptState:
                 denom = np.sqrt(vd) / T(bc2**0.5) + T(eps)
                 self.params[k] = x + (T(-(o['lr'] / bc1)) * m) / denom
                 self.m[k], self.v[k] = m, v
+            elif typ == 'Adagrad':
+                ss = self.v.get(k, np.full_like(
+                    x, o.get('initial_accumulator_value', 0.0)))
+                ss = ss + g * g
+                self.v[k] = ss
+                clr = o['lr'] / (1 + (t - 1) * o.get('lr_decay', 0.0))
+                std = np.sqrt(ss) + T(o.get('eps', 1e-10))
+                self.params[k] = x + (T(-clr) * g) / std
+            elif typ == 'RMSprop':
+                alpha = o.get('alpha', 0.99)
+                eps = o.get('eps', 1e-8)
+                mom = o.get('momentum', 0.0)
+                v = self.v.get(k, np.zeros_like(x)) * T(alpha)
+                v = v + (T(1 - alpha) * g) * g
+                self.v[k] = v
+                if o.get('centered', False):
+                    ga = self._lerp(self.ga.get(k, np.zeros_like(x)), g,
+                                    1 - alpha)
+                    self.ga[k] = ga
+                    d = np.sqrt(v + (T(-1) * ga) * ga)
+                else:
+                    d = np.sqrt(v)
+                d = d + T(eps)
+                if mom > 0:
+                    b = self.buf.get(k, np.zeros_like(x)) * T(mom)
+                    b = b + g / d
+                    self.buf[k] = b
+                    self.params[k] = self._fma(b, T(-o['lr']), x)
+                else:
+                    self.params[k] = x + (T(-o['lr']) * g) / d
+            else:
+                raise NotImplementedError(typ)
         return OrderedDict((k, v.copy()) for k, v in self.params.items())
 
 

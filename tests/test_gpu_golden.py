@@ -19,6 +19,13 @@ from golden_io import case_names, load_case
 pytestmark = pytest.mark.gpu
 
 
+
+# FedOpt golden chains (tools/gen_golden.py): every torch.optim class the
+# device step implements, weight decay, maximize, float64, a dropped key
+FEDOPT_CHAINS = ['SGD', 'SGDm', 'Adam', 'AdamAms', 'SGDm64', 'Adam64',
+                 'AdamW', 'AdamWams', 'Adagrad', 'Adagradx', 'RMSprop',
+                 'RMSpropmc', 'SGDmax', 'RMSprop64', 'Adamdrop']
+
 def to_torch(a, device='cuda'):
     if isinstance(a, O.BF16):
         return torch.from_numpy(a.bits.view(np.int16).copy()).view(
@@ -219,8 +226,7 @@ class ParamModel(torch.nn.Module):
 
 
 @pytest.mark.parametrize('model_dev', ['cpu', 'cuda'])
-@pytest.mark.parametrize('opt', ['SGD', 'SGDm', 'Adam', 'AdamAms',
-                                 'SGDm64', 'Adam64'])
+@pytest.mark.parametrize('opt', FEDOPT_CHAINS)
 def test_fedopt_chain(opt, model_dev):
     """Three chained FedOpt rounds (optimizer state carried across rounds)
     against the reference (torch.optim on CPU): tolerance-pinned, the

@@ -504,11 +504,58 @@ def fedopt_more_cases(rng):
                       outs[r], init=init if r == 0 else None)
 
 
+def fedopt_round3_cases(rng):
+    """FedOpt with every torch.optim class the device step implements
+    (optimizer_builder.py:53-56 builds any by name): AdamW, Adagrad,
+    RMSprop (plain, momentum, centered), weight decay and maximize; one
+    float64 chain; and a chain whose clients drop a parameter in round 1
+    (torch.optim keeps per-parameter state and steps)."""
+    shapes = OrderedDict([('w', (5, 21)), ('b', (5, ))])
+    for tag, opt, dt, drop in (
+            ('AdamW', {'type': 'AdamW', 'lr': 0.01}, torch.float32, None),
+            ('AdamWams', {'type': 'AdamW', 'lr': 0.02, 'weight_decay': 0.1,
+                          'amsgrad': True}, torch.float32, None),
+            ('Adagrad', {'type': 'Adagrad', 'lr': 0.1}, torch.float32, None),
+            ('Adagradx', {'type': 'Adagrad', 'lr': 0.1, 'lr_decay': 0.05,
+                          'weight_decay': 0.01,
+                          'initial_accumulator_value': 0.1}, torch.float32,
+             None),
+            ('RMSprop', {'type': 'RMSprop', 'lr': 0.01}, torch.float32, None),
+            ('RMSpropmc', {'type': 'RMSprop', 'lr': 0.01, 'momentum': 0.9,
+                           'centered': True, 'weight_decay': 0.01},
+             torch.float32, None),
+            ('SGDmax', {'type': 'SGD', 'lr': 0.5, 'momentum': 0.9,
+                        'maximize': True}, torch.float32, None),
+            ('RMSprop64', {'type': 'RMSprop', 'lr': 0.01, 'momentum': 0.5},
+             torch.float64, None),
+            ('Adamdrop', {'type': 'Adam', 'lr': 0.01}, torch.float32, 'b')):
+        cfg = make_cfg(fedopt=opt)
+        init = OrderedDict((k, torch.from_numpy(
+            rng.standard_normal(s)).to(dt)) for k, s in shapes.items())
+        agg = FedOptAggregator(config=cfg, model=DictModel(init))
+        rounds, outs = [], []
+        for r in range(3):
+            clients = rand_clients(rng, 4, shapes, dtype=dt)
+            if drop and r == 1:
+                for _, d in clients:
+                    del d[drop]
+            rounds.append(clients)
+            outs.append(OrderedDict((k, v.detach().clone())
+                                    for k, v in run(agg, clients).items()))
+        for r in range(3):
+            save_case('fedopt_%s_%d' % (tag, r), {
+                'rule': 'fedopt', 'opt': opt, 'round': r}, rounds[r],
+                      outs[r], init=init if r == 0 else None)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(1)  # fed_runner.py:297-299
     if sys.argv[1:] == ['nonfinite']:  # added later: its own seed
         order_stat_nonfinite_cases(np.random.default_rng(20261016))
+        return 0
+    if sys.argv[1:] == ['round3']:     # round 3 cases: their own seed
+        fedopt_round3_cases(np.random.default_rng(20261018))
         return 0
     if sys.argv[1:] == ['round2']:     # round 2 cases: their own seed
         rng = np.random.default_rng(20261017)
