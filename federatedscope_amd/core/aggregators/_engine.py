@@ -236,10 +236,13 @@ class DeviceEngine:
                 [4 * layout.offsets[k] for k in layout.keys])
         if not kl[0] or not all(isinstance(d, dict) for d in dicts):
             return None
+        host = _host_ext()
+        if host is None:      # no _fsagg_host.so: stage the dicts instead
+            return None
         if virtual:
-            res = _lib.host().key_table(dicts, kl[0], kl[1], dev.index, kl[2])
+            res = host.key_table(dicts, kl[0], kl[1], dev.index, kl[2])
         else:
-            res = _lib.host().key_table(dicts, kl[0], kl[1], dev.index)
+            res = host.key_table(dicts, kl[0], kl[1], dev.index)
         if res is None:
             return None
         raw, missing, aligned = res
@@ -363,8 +366,11 @@ class DeviceEngine:
             ing.sync()
         if all(isinstance(d, StagedUpdate) for d in dicts):
             ing = dicts[0].ingress
+            # keys of other dtypes (typed side copies) are reduced per key
+            # by _weighted_avg_device; the robust rules cast every key to
+            # float and take the general path below
             if all(d.ingress is ing for d in dicts) and \
-                    not ing.layout.other:
+                    (not ing.layout.other or not as_float):
                 if require_all:
                     for i, d in enumerate(dicts):
                         if len(d) != len(ing.layout.keys):
@@ -414,6 +420,23 @@ class DeviceEngine:
     def _stage_all(self, models, as_float=True):
         """Pack every client (robust rules need all keys in all clients)."""
         return self._staged(models, as_float=as_float, require_all=True)
+
+
+_HOST = []
+
+
+def _host_ext():
+    """The _fsagg_host extension, or None when it was not built (looked up
+    once): the key-table fast path is then skipped and client dicts are
+    staged through a device stack — the kernels themselves still need
+    libfsagg.so."""
+    if not _HOST:
+        from ... import _lib
+        try:
+            _HOST.append(_lib.host())
+        except (_lib.FsaggError, ImportError, OSError):
+            _HOST.append(None)
+    return _HOST[0]
 
 
 class _NoRows:

@@ -29,13 +29,18 @@ class NormboundingAggregator(ClientsAvgAggregator):
         self.norm_bound = config.aggregator.BFT_args.normbounding_norm_bound
 
     def _rates(self, sq):
-        """fl32(bound / norm) per client whose norm exceeds the bound (else
-        None): norm = fl32(sqrt(Σ squares)) as torch.norm returns it."""
+        """The reference's ``self.norm_bound / torch.norm(param)`` per client
+        whose norm exceeds the bound (else None), with norm =
+        fl32(sqrt(Σ squares)) as torch.norm returns it.  A Python float over
+        a 0-dim tensor is Tensor.__rtruediv__ = reciprocal() * other:
+        fl32(fl32(1 / norm) · fl32(bound)), which differs from
+        fl32(bound / norm) in the last bit for ~16 % of norms."""
         bound32 = np.float32(self.norm_bound)
+        one = np.float32(1.0)
         out = []
         for v in sq:
             norm = np.float32(math.sqrt(float(v)))
-            out.append(float(np.float32(bound32 / norm))
+            out.append(float(np.float32(np.float32(one / norm) * bound32))
                        if norm > self.norm_bound else None)
         return out
 

@@ -20,14 +20,18 @@ from ..auxiliaries.utils import as_float_tensor, param2tensor
 
 class StagedUpdate(Mapping):
     """A client update resident in a ClientStack slot.  Behaves like the
-    read-only state_dict it came from (device views per key)."""
+    read-only state_dict it came from (device views per key).  Keys of
+    other dtypes (e.g. BatchNorm's int64 ``num_batches_tracked`` with
+    ``share_non_trainable_para``) are kept as device copies beside the
+    slot (``typed``), in their own dtype."""
 
-    def __init__(self, ingress, slot, keys):
+    def __init__(self, ingress, slot, keys, typed=None):
         self.ingress = ingress
         self.stack = ingress.stack
         self.slot = slot
         self._keys = list(keys)
         self._keyset = frozenset(self._keys)
+        self.typed = typed or {}
 
     def __contains__(self, k):
         # the aggregators test key membership n·K times per round; Mapping's
@@ -35,8 +39,10 @@ class StagedUpdate(Mapping):
         return k in self._keyset
 
     def __getitem__(self, k):
+        if k in self.typed:
+            return self.typed[k]
         lay = self.stack.layout
-        if k not in lay.offsets or k not in self._keys:
+        if k not in lay.offsets or k not in self._keyset:
             raise KeyError(k)
         o, m = lay.offsets[k], lay.numels[k]
         return self.stack.slab[self.slot, o:o + m].view(lay.shapes[k])
@@ -66,9 +72,6 @@ class DeviceIngress:
                 template = {k: torch.empty(param2tensor(v).shape)
                             for k, v in template.items()}
             self.layout = BucketLayout(template)
-        if self.layout.other:
-            raise NotImplementedError(
-                'ingress staging of non-fp32 keys %s' % list(self.layout.other))
         self.stack = ClientStack(self.layout, capacity, self.device)
         self.stack.slab.zero_()
         self.as_float = as_float
@@ -96,15 +99,40 @@ class DeviceIngress:
         self.next_slot += 1
         return slot
 
+    def accepts(self, model_para):
+        """Whether ``model_para`` has exactly this layout's keys, shapes and
+        dtypes (an upload of another shape is buffered as it came, and the
+        aggregator stages it the general way)."""
+        lay = self.layout
+        if len(model_para) != len(lay.keys) + len(lay.other):
+            return False
+        for k in lay.keys:
+            v = model_para.get(k) if isinstance(model_para, Mapping) else None
+            if v is None:
+                return False
+            t = param2tensor(v)
+            if not isinstance(t, torch.Tensor) or tuple(t.shape) != \
+                    tuple(lay.shapes[k]) or (not self.as_float and
+                                             t.dtype != torch.float32):
+                return False
+        for k, dt in lay.other.items():
+            v = model_para.get(k)
+            if not isinstance(v, torch.Tensor) or v.dtype != dt:
+                return False
+        return True
+
     def receive(self, sample_size, model_para, slot=None):
         """Stage one upload; returns (sample_size, StagedUpdate).  ``slot``
-        reuses the row of the same sender's earlier upload this round."""
+        reuses the row of the same sender's earlier upload this round.
+        fp32 keys go into the slot, keys of other dtypes to device copies
+        of their own dtype (StagedUpdate.typed)."""
+        if not self.accepts(model_para):
+            raise KeyError('upload does not match the staged layout')
         slot = self._slot(slot)
-        missing = [k for k in self.layout.keys if k not in model_para]
-        if missing:
-            raise KeyError('staged upload lacks keys %s' % missing)
         src = {k: (as_float_tensor(model_para[k]) if self.as_float else
                    param2tensor(model_para[k])) for k in self.layout.keys}
+        typed = {k: model_para[k].to(self.device, non_blocking=True)
+                 for k in self.layout.other}
         on_host = any(v.device.type != 'cuda' for v in src.values())
         if on_host:
             if self._stager is None:
@@ -112,7 +140,8 @@ class DeviceIngress:
             self._stager.put(self.layout, src, self.stack.slab[slot])
         else:
             self.layout.pack_device(src, self.stack.slab[slot])
-        return sample_size, StagedUpdate(self, slot, model_para.keys())
+        return sample_size, StagedUpdate(self, slot, model_para.keys(),
+                                         typed)
 
     def receive_quantized(self, sample_size, wire, slot=None):
         """Stage one quantised upload (the wire dict of

@@ -431,7 +431,8 @@ def normbounding_aggregate(models, bound, init):
         norm = f32(math.sqrt(float(np.dot(flat.astype(np.float64),
                                           flat.astype(np.float64)))))
         if norm > bound:
-            rate = f32(f32(bound) / norm)
+            # bound / torch.norm(...): Tensor.__rtruediv__ = reciprocal()·other
+            rate = f32(f32(f32(1.0) / norm) * f32(bound))
             scaled = rate * flat
             rec = OrderedDict()
             off = 0

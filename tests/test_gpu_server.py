@@ -57,7 +57,8 @@ def test_toy_lr_course_bit_exact(stage):
 
     model = LR()
     srv = AggregationServer(model, ClientsAvgAggregator(config=_cfg()),
-                            sample_client_num=5, stage_on_arrival=stage)
+                            sample_client_num=5, stage_on_arrival=stage,
+                            keep_history=1)
     for r, (ins, out) in enumerate(rounds):
         for i, (s, d) in enumerate(ins):
             moved = srv.callback_funcs_model_para(
@@ -221,7 +222,7 @@ def test_staged_with_stale_host_dicts_and_resend():
         model = M()
         srv = AggregationServer(model, AsynClientsAvgAggregator(
             model=model, config=_cfg()), sample_client_num=4,
-            staleness_toleration=2, stage_on_arrival=stage)
+            staleness_toleration=2, stage_on_arrival=stage, keep_history=3)
         for r, c, (s, d) in script:
             srv.callback_funcs_model_para(
                 r, c, (s, OrderedDict((k, v.clone()) for k, v in d.items())))
@@ -232,3 +233,42 @@ def test_staged_with_stale_host_dicts_and_resend():
     for a, b in zip(*results):
         for k in a:
             assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize('dev', ['cpu', 'cuda'])
+def test_server_stages_typed_keys_bit_exact(dev):
+    """A model sharing non-trainable keys (share_non_trainable_para: BN's
+    int64 num_batches_tracked; here the fedavg_dtypes fixture's int64, fp16,
+    bf16 and fp64 keys beside fp32 ones) through stage_on_arrival: the fp32
+    keys go into the ingress stack, the others stay typed device copies
+    (server.py:966-970 buffers any dict), and the round's FedAvg is
+    bit-exact against the reference's output."""
+    from golden_io import load_case
+    from test_gpu_golden import assert_bit_exact, to_torch
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    from federatedscope_amd.core.workers.ingress import StagedUpdate
+    from federatedscope_amd.core.workers.server import AggregationServer
+    meta, clients, out, _, _ = load_case('fedavg_dtypes')
+    keysets = {tuple(d.keys()) for _, d in clients}
+
+    class M(torch.nn.Module):
+        def state_dict(self, *a, **kw):
+            return OrderedDict()
+
+        def load_state_dict(self, sd, strict=True):
+            self.loaded = sd
+
+    srv = AggregationServer(M(), ClientsAvgAggregator(config=_cfg()),
+                            sample_client_num=len(clients),
+                            stage_on_arrival=True, keep_history=1)
+    for i, (s, d) in enumerate(clients):
+        srv.callback_funcs_model_para(
+            0, i, (s, OrderedDict((k, to_torch(v, dev))
+                                  for k, v in d.items())))
+        if i < len(clients) - 1 and len(keysets) == 1:
+            para = srv.msg_buffer['train'][0][i][1]
+            assert isinstance(para, StagedUpdate)
+            assert para.typed, 'non-fp32 keys kept beside the slot'
+    assert srv.state == 1
+    assert_bit_exact(srv.history[-1], out, 'server fedavg_dtypes ' + dev)
+    assert srv.ingress.layout.other

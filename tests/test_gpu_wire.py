@@ -79,7 +79,8 @@ def test_quantized_uploads_through_server(name, stage):
 
     srv = AggregationServer(M(), ClientsAvgAggregator(config=_cfg()),
                             sample_client_num=len(clients),
-                            stage_on_arrival=stage, dequantize=True)
+                            stage_on_arrival=stage, dequantize=True,
+                            keep_history=1)
     for sender, (s, wire) in enumerate(clients):
         srv.callback_funcs_model_para(0, sender, (s, _torch_wire(wire)))
     got = srv.history[-1]
