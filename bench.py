@@ -113,6 +113,64 @@ def cpu_baseline_leg(rows_slab, weights, P, n_sample, dev):
     return res, exact
 
 
+def plugin_surface_leg(args, dev, slab, rows, sizes, w_dev, P, rounds=5,
+                       calls=10):
+    """The plugin surface at the headline config: the reference's
+    ClientsAvgAggregator.aggregate(agg_info) (clients_avg_aggregator.py:
+    19-35) on 100 device-resident 25M-parameter state_dicts (views of the
+    bench's client rows, read in place), timed back to back against the
+    bare kernel on the same rows — interleaved rounds, median per call —
+    with the results compared bit for bit."""
+    import statistics
+    from types import SimpleNamespace
+
+    import torch
+    from federatedscope_amd import ops
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    n = len(sizes)
+    clients = [(sizes[i], {'w': slab[i, :P]}) for i in range(n)]
+    cfg = SimpleNamespace(federate=SimpleNamespace(ignore_weight=False,
+                                                   use_ss=False))
+    agg = ClientsAvgAggregator(device=dev, config=cfg)
+    info = {'client_feedback': clients, 'recover_fun': None}
+    flat = torch.empty(ops.round_up(P, 64), dtype=torch.float32, device=dev)
+
+    def run_agg():
+        return agg.aggregate(info)
+
+    def run_flat():
+        ops.weighted_sum(rows, w_dev, flat)
+
+    for _ in range(3):
+        res = run_agg()
+        run_flat()
+    torch.cuda.synchronize()
+    exact = torch.equal(res['w'], flat[:P])
+    t_agg, t_flat = [], []
+    for _ in range(rounds):
+        for fn, acc in ((run_agg, t_agg), (run_flat, t_flat)):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(calls):
+                fn()
+            torch.cuda.synchronize()
+            acc.append((time.perf_counter() - t0) / calls * 1e3)
+    a, f = statistics.median(t_agg), statistics.median(t_flat)
+    log('plugin surface: aggregate() %.4f ms/call, bare kernel %.4f ms '
+        '(ratio %.4f), bit-exact %s' % (a, f, a / f, exact))
+    return {
+        'what': 'ClientsAvgAggregator.aggregate(agg_info) on %d device '
+                'dicts x %d fp32 params, read in place; back-to-back calls, '
+                'median of %d interleaved rounds of %d' % (n, P, rounds,
+                                                           calls),
+        'ms_per_call': round(a, 4),
+        'GBps': round(4.0 * n * P / a / 1e6, 1),
+        'bare_kernel_ms': round(f, 4),
+        'ratio_vs_bare_kernel': round(a / f, 4),
+        'bit_exact_vs_kernel': exact,
+    }
+
+
 def e2e_leg(args, dev, weights, sizes):
     """Host state_dicts in, host state_dict out, through the drop-in
     ClientsAvgAggregator (pinned double-buffered staging, H2D, kernel, D2H).
@@ -303,6 +361,8 @@ def main():
     ap.add_argument('--cpu-clients', type=int, default=20,
                     help='clients (full width) timed on the CPU baseline')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-plugin', action='store_true',
+                    help='skip the ClientsAvgAggregator.aggregate() leg')
     ap.add_argument('--no-weak', action='store_true',
                     help='skip the secondary weak-scaling phase (N > 1)')
     ap.add_argument('--e2e', action='store_true',
@@ -458,6 +518,11 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    plugin = None
+    if world == 1 and not args.no_plugin:
+        plugin = plugin_surface_leg(args, dev, pieces[0][0], pieces[0][1],
+                                    sizes, w_dev, P)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         k = min(args.cpu_clients, n)
@@ -547,6 +612,7 @@ def main():
                 'ms_per_step': round(t_sharded * 1e3, 4),
                 'value': round(4.0 * n * P / t_sharded / 1e9, 2)},
             'weak_scaling': weak,
+            'plugin_surface': plugin,
             'assembled_bit_exact': ok,
         }
         print(json.dumps(rec), flush=True)

@@ -851,602 +851,6 @@ __global__ __launch_bounds__(kBlock) void pairdist_chunk_kernel(
   }
 }
 
-// ---- ring form: LDS-DMA stages, split roles --------------------------------
-// One 512-thread workgroup per CU (152 KiB of LDS): a chunk streams through
-// a 3-slot ring of stages written by 16-byte LDS-DMA
-// (global_load_lds_dwordx4: no VGPR round trip, no staging stores, no
-// prefetch registers) in the rows' own layout [row][coordinate] with a row
-// pitch P of 64·P64 floats.  Two stages are in flight while one is computed;
-// one raw barrier per stage (stage st+2 goes into the slot stage st−1
-// vacated; each wave counts its own DMAs with vmcnt).
-// Lanes take the split-form roles of PairPlan (the first wo waves the
-// off-diagonal tile pairs, the rest the paired diagonal tiles), k-slices
-// fastest: the lanes of a role read consecutive coordinates of a row (one
-// LDS bank each).  A lane's row pair (2h, 2h+1) of a tile at one coordinate
-// is one ds_read2st64_b32 (row offsets 2h·P64 and (2h+1)·P64 in units of
-// 64 dwords), so the packed updates need no operand moves.  Columns [S, P)
-// stay zero: a lane past the stage's coordinates reads them and adds 0.
-constexpr int kRingLds = 38912;  // floats: 152 KiB, one workgroup per CU
-
-struct RingPlan {
-  int ts, nt, ntp;  // tile layout (PairPlan's; partial[] has its layout)
-  int waves;        // workgroup waves (one workgroup per CU)
-  int pad;          // row pitch pad (floats) past 64·p64
-  int slots;        // ring slots (slots - 1 stages in flight)
-  int rw;           // DMA rows per wave per stage (staged rows rw·waves;
-                    // rows past n are never loaded nor read)
-  int p64;          // row pitch / 64 floats
-  int S;            // coordinates per stage (multiple of 4, <= 256)
-  int slot;         // floats per ring slot (rw·waves rows × pitch)
-  int red;          // reduction floats per thread (kRingLds / threads)
-  int wo, ro, ko, rd, kd;  // split roles (as PairPlan's wo, ro, kso, ...)
-  int mo, md;       // coordinate steps per stage of the two role kinds
-  int64_t chl, max_chunks;
-  int ok;
-};
-
-RingPlan make_ring_plan(int n, int64_t numel, int nseg, int waves = 12,
-                        int slots = 3, int pad = 0) {
-  const PairPlan pp = make_plan(n, numel, nseg);
-  RingPlan p{};
-  p.ts = pp.ts;
-  p.nt = pp.nt;
-  p.ntp = pp.ntp;
-  p.waves = waves;
-  p.slots = slots;
-  p.pad = pad;
-  p.red = kRingLds / (waves * kWave);
-  p.rw = (p.nt * p.ts + waves - 1) / waves;
-  p.ok = 0;
-  p.S = 4;
-  const int ro = p.nt * (p.nt - 1) / 2, rd = (p.nt + 1) / 2;
-  double best = 0.0;
-  if (p.nt >= 2 && p.rw <= 8) {
-    for (int wo = 1; wo < waves; ++wo) {
-      const int ko = kWave * wo / ro, kd = kWave * (waves - wo) / rd;
-      if (ko < 1 || kd < 1) continue;
-      for (int S = 4; S <= 4 * kWave; S += 4) {
-        const int mo = (S + ko - 1) / ko, md = (S + kd - 1) / kd;
-        // highest column read + 1: the zero column S included
-        const int reach = std::max(std::max(mo * ko, md * kd), S + 1);
-        const int p64 = (reach + 63) / 64;
-        if (p64 > 4) break;
-        const int slot = p.rw * waves * (64 * p64 + pad);
-        if (slots * slot > kRingLds) break;
-        const double eff = double(S) / std::max(mo, md);
-        if (eff > best || (eff == best && S > p.S)) {
-          best = eff;
-          p.ok = 1;
-          p.wo = wo;
-          p.ro = ro;
-          p.ko = ko;
-          p.rd = rd;
-          p.kd = kd;
-          p.mo = mo;
-          p.md = md;
-          p.S = S;
-          p.p64 = p64;
-          p.slot = slot;
-        }
-      }
-    }
-  }
-  p.ok = p.ok && p.ts * p.ts <= 2 * p.red;
-  // ≈ 4 rounds of the 256 resident workgroups, whole stages
-  const int64_t target = 1024 - nseg > 256 ? 1024 - nseg : 256;
-  int64_t chl = (numel + target - 1) / target;
-  const int64_t minl = int64_t(p.S) * 8;
-  if (chl < minl) chl = minl;
-  p.chl = (chl + p.S - 1) / p.S * p.S;
-  p.max_chunks = numel / chl + nseg + 1;
-  return p;
-}
-
-typedef __attribute__((address_space(3))) float lfloat_t;
-
-// 16-B LDS-DMA of one wave: lane l's 16 bytes at sbase + voff land at LDS
-// byte address lds_addr + 16·l.  Inline asm on purpose: issued through the
-// builtin, the DMA is a pending LDS write the compiler guards with
-// vmcnt(0) before every later ds_read — which would drain the ring's
-// in-flight stages every step.  The ring counts its DMAs itself.
-__device__ __forceinline__ void glds16(const float *sbase, uint32_t voff,
-                                       uint32_t lds_addr) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, %2\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(sbase), "s"(lds_addr)
-      : "memory");
-}
-
-// s_waitcnt vmcnt(k) for a wave-uniform k in [0, 16]
-__device__ __forceinline__ void wait_vmcnt(int k) {
-  switch (k) {
-#define FSAGG_VM(K) \
-  case K: asm volatile("s_waitcnt vmcnt(" #K ")" ::: "memory"); break;
-    FSAGG_VM(0) FSAGG_VM(1) FSAGG_VM(2) FSAGG_VM(3) FSAGG_VM(4) FSAGG_VM(5)
-    FSAGG_VM(6) FSAGG_VM(7) FSAGG_VM(8) FSAGG_VM(9) FSAGG_VM(10) FSAGG_VM(11)
-    FSAGG_VM(12) FSAGG_VM(13) FSAGG_VM(14) FSAGG_VM(15)
-#undef FSAGG_VM
-    default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-  }
-}
-
-template <int TS, int P64, int WAVES, int PADW>
-__global__ __launch_bounds__(WAVES * 64) void pairdist_ring_kernel(
-    const float *const *__restrict__ tab, int64_t ss, int n, RingPlan pl,
-    const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
-    int nseg, const int *__restrict__ prefix, float *__restrict__ partial) {
-  // row pitch: 64·P64 floats, + PADW so a lane's two rows of a pair sit in
-  // different banks
-  constexpr int P = 64 * P64 + PADW;
-  constexpr int kRingThreads = WAVES * kWave;
-  constexpr int kRingWaves = WAVES;
-  const int kRingSlots = pl.slots;
-  __shared__ __attribute__((aligned(16))) float lds[kRingLds];
-  const int c = blockIdx.x;
-  if (c >= prefix[nseg]) return;
-  int lo = 0, hi = nseg;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (prefix[mid] <= c) lo = mid;
-    else hi = mid;
-  }
-  const int s = lo;
-  const int64_t start = seg_lo[s] + int64_t(c - prefix[s]) * pl.chl;
-  int64_t end = start + pl.chl;
-  if (end > seg_end[s]) end = seg_end[s];
-  const float *const *__restrict__ rows = tab + int64_t(s) * ss;
-
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
-  const int lane = tid & (kWave - 1);
-  const bool diag = wave >= pl.wo;  // wave-uniform role kind
-  int role, k, K;
-  bool active;
-  int ti = 0, tj = 0;
-  if (!diag) {
-    role = tid / pl.ko;
-    k = tid - role * pl.ko;
-    K = pl.ko;
-    active = role < pl.ro;
-    od_to_tiles(active ? role : 0, pl.nt, ti, tj);
-  } else {
-    const int l = tid - kWave * pl.wo;
-    role = l / pl.kd;
-    k = l - role * pl.kd;
-    K = pl.kd;
-    active = role < pl.rd;
-    ti = 2 * (active ? role : 0);
-    tj = ti + 1 < pl.nt ? ti + 1 : ti;  // odd tile count: a repeat, unused
-  }
-
-  // 16-B DMA needs 16-B aligned sources: the chunk start and every row
-  bool vec = (start & 3) == 0;
-  for (int r = 0; r < n; ++r)
-    vec = vec && (reinterpret_cast<uintptr_t>(rows[r]) & 15u) == 0;
-  const int64_t end4 = vec ? start + ((end - start) & ~int64_t(3)) : start;
-  const int nstage = int((end4 - start + pl.S - 1) / pl.S);
-
-  f2 acc[TS / 2][TS];
-#pragma unroll
-  for (int h = 0; h < TS / 2; ++h)
-#pragma unroll
-    for (int v = 0; v < TS; ++v) acc[h][v] = f2{0.0f, 0.0f};
-
-  // zero columns [S, P) of every staged row of every slot (never DMA'd)
-  {
-    const int zc = P - pl.S, nrow = kRingSlots * pl.rw * kRingWaves;
-    for (int i = tid; i < nrow * zc; i += kRingThreads) {
-      const int r = i / zc;
-      lds[r * P + pl.S + (i - r * zc)] = 0.0f;
-    }
-  }
-  __syncthreads();
-
-  // this wave's DMA rows (wave + 8j, j < rw), pointers loaded once
-  const float *rp[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) rp[j] = rows[min(wave + kRingWaves * j, n - 1)];
-  const uint32_t lds_base = uint32_t(uintptr_t((lfloat_t *)lds));
-  // DMAs this wave issues per stage (its rows below n); a partial last
-  // stage issues as many (its lanes are masked, not its instructions)
-  int my_rows = 0;
-  for (int j = 0; j < pl.rw; ++j) my_rows += wave + kRingWaves * j < n;
-  auto issue = [&](int st) {
-    const int64_t cs = start + int64_t(st) * pl.S;
-    const int nq = int(min(int64_t(pl.S), end4 - cs) >> 2);
-    const uint32_t slot = lds_base + 4u * uint32_t((st % kRingSlots) * pl.slot);
-    // lanes past the stage's quads (its last, partial stage) load nothing:
-    // the columns they would fill are never read (c >= len maps to the
-    // zero column S); rows past the last client are never loaded
-    if (lane < nq) {
-      const uint32_t voff = 16u * uint32_t(lane);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j < pl.rw && wave + kRingWaves * j < n)
-          glds16(rp[j] + cs, voff,
-                 slot + 4u * uint32_t((wave + kRingWaves * j) * P));
-    }
-  };
-  // the lane's row pairs of tiles ti, tj at column cc of a slot
-  auto load = [&](const float *sb, int cc, f2 (&A)[TS / 2],
-                  f2 (&B)[TS / 2]) {
-    const float *pa = sb + ti * TS * P + cc;
-    const float *pb = sb + tj * TS * P + cc;
-#pragma unroll
-    for (int h = 0; h < TS / 2; ++h) {
-      A[h] = f2{pa[2 * h * P], pa[(2 * h + 1) * P]};
-      B[h] = f2{pb[2 * h * P], pb[(2 * h + 1) * P]};
-    }
-  };
-  auto run = [&](auto is_diag) {
-    constexpr bool D = decltype(is_diag)::value;
-    const int M = D ? pl.md : pl.mo;
-    // one stage's updates from slot sb (len coordinates; past them the
-    // zero column)
-    auto compute = [&](const float *sb, int len) {
-      for (int m = 0; m < M; ++m) {
-        const int cc0 = k + m * K;
-        const int cc = active && cc0 < len ? cc0 : pl.S;
-        f2 A[TS / 2], B[TS / 2];
-        load(sb, cc, A, B);
-        pair_update<TS, D>(acc, A, B);
-      }
-    };
-    for (int q = 0; q < kRingSlots - 1; ++q)
-      if (q < nstage) issue(q);
-    for (int st = 0; st < nstage; ++st) {
-      // this wave's DMAs of stage st have landed (later ones may fly)
-      const int later = min(nstage - 1 - st, kRingSlots - 2);
-      wait_vmcnt(later * my_rows);
-      __builtin_amdgcn_s_barrier();
-      if (st + kRingSlots - 1 < nstage) issue(st + kRingSlots - 1);
-      const int64_t cs = start + int64_t(st) * pl.S;
-      compute(lds + (st % kRingSlots) * pl.slot,
-              int(min(int64_t(pl.S), end4 - cs)));
-    }
-    // [end4, end): the sub-quad tail, or the whole chunk when a row is not
-    // 16-B aligned — staged by 4-B loads into slot 0
-    const int nrows = pl.nt * TS;
-    for (int64_t cs = end4; cs < end; cs += pl.S) {
-      const int len = int(min(int64_t(pl.S), end - cs));
-      __syncthreads();  // every wave is done with the slots
-      for (int i = tid; i < nrows * len; i += kRingThreads) {
-        const int r = i / len, col = i - r * len;
-        lds[r * P + col] = gld(rows[min(r, n - 1)] + cs + col);
-      }
-      __syncthreads();
-      compute(lds, len);
-    }
-  };
-  if (diag) run(std::true_type{});
-  else run(std::false_type{});
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // every stage read: the ring becomes the reduction buffer
-
-  // Σ over the k-slices of each role, in slice order
-  constexpr int kE = TS * TS;
-  constexpr int R = kRingLds / kRingThreads;
-#pragma unroll
-  for (int e0 = 0; e0 < kE; e0 += R) {
-    const int ne = kE - e0 < R ? kE - e0 : R;
-    if (active) {
-      float *slot = lds + tid * R;
-#pragma unroll
-      for (int e = e0; e < e0 + R && e < kE; ++e)
-        slot[e - e0] = pair_acc<TS>(acc, e / TS, e % TS);
-    }
-    __syncthreads();
-    const int nod = pl.ro * ne, outs = nod + pl.rd * ne;
-    for (int o = tid; o < outs; o += kRingThreads) {
-      const bool dg = o >= nod;
-      const int o2 = dg ? o - nod : o;
-      const int l = o2 / ne, e = o2 - l * ne;
-      const int base = dg ? kWave * pl.wo + l * pl.kd : l * pl.ko;
-      const int kk = dg ? pl.kd : pl.ko;
-      float sum = 0.0f;
-      for (int q = 0; q < kk; ++q) sum += lds[(base + q) * R + e];
-      int tp, idx;
-      if (split_slot(dg, l, e0 + e, TS, pl.nt, tp, idx))
-        partial[(int64_t(c) * pl.ntp + tp) * kE + idx] = sum;
-    }
-    __syncthreads();
-  }
-}
-
-// ---- block form: LDS-DMA stages in [block][row][16 coordinates] ----------
-// One 768-thread workgroup (12 waves, 3 per SIMD) per CU.  A chunk streams
-// through a ring of stages written by 16-byte LDS-DMA
-// (global_load_lds_dwordx4): no staging registers and no staging stores, so
-// the accumulators fit three waves per SIMD (two in the register-staged
-// kernel).  One DMA instruction moves 16 rows × 16 coordinates — four lanes
-// per row, 64 contiguous bytes each, so every request is a whole 64-B
-// segment — and lands as a [row][16 coordinates] block: value (r, k) of
-// block b sits at word b·NR·16 + r·16 + (k mod 16).  A lane's row pair
-// (2h, 2h+1) of a tile at one coordinate is then 16 words apart and its
-// tile's five pairs are one base plus immediates ≤ 144 words: five
-// ds_read2_b32 per tile per coordinate, no address arithmetic.  NR ≡ 1
-// (mod 4) rows per block: the four blocks a wave's k-slices span and the
-// two words of each read fall on distinct banks.  Rows past the last client
-// are never loaded; lanes past a stage's coordinates read a zero block.
-// Split roles as the register-staged kernel's (whole waves own the
-// off-diagonal tile pairs or pairs of diagonal tiles).
-constexpr int kDmaWaves = 12;
-constexpr int kDmaThreads = kDmaWaves * kWave;
-constexpr int kDmaLds = 38912;   // floats: 152 KiB, one workgroup per CU
-
-struct DmaPlan {
-  int ts, nt, ntp;   // tile layout (PairPlan's; partial[] has its layout)
-  int nr;            // rows per block (≥ nt·ts, ≡ 1 mod 4)
-  int groups;        // 16-row DMA groups (rows < n)
-  int S;             // coordinates per stage (multiple of 16)
-  int slots;         // ring slots (slots − 1 stages in flight)
-  int slot;          // floats per slot (S/16 blocks of nr·16)
-  int zero;          // float offset of the zero block
-  int wo, ro, ko, rd, kd;  // split roles
-  int mo, md;        // coordinate steps per stage of the two role kinds
-  int64_t chl, max_chunks;
-  int ok;
-};
-
-DmaPlan make_dma_plan(int n, int64_t numel, int nseg, int slots = 3) {
-  const PairPlan pp = make_plan(n, numel, nseg);
-  DmaPlan p{};
-  p.ts = pp.ts;
-  p.nt = pp.nt;
-  p.ntp = pp.ntp;
-  p.slots = slots;
-  p.nr = p.nt * p.ts;
-  while (p.nr % 4 != 1) ++p.nr;
-  p.groups = (n + 15) / 16;
-  p.ok = 0;
-  p.S = 16;
-  const int ro = p.nt * (p.nt - 1) / 2, rd = (p.nt + 1) / 2;
-  double best = 0.0;
-  // one row group per wave at least, the accumulators reducible through LDS
-  if (p.nt >= 2 && p.groups <= kDmaWaves &&
-      p.ts * p.ts <= 2 * (kDmaLds / kDmaThreads)) {
-    for (int wo = 1; wo < kDmaWaves; ++wo) {
-      const int ko = kWave * wo / ro, kd = kWave * (kDmaWaves - wo) / rd;
-      if (ko < 1 || kd < 1) continue;
-      for (int S = 16; S <= 1024; S += 16) {
-        const int slot = S / 16 * p.nr * 16;
-        if (slots * slot + p.nr * 16 + 4 > kDmaLds) break;
-        const int mo = (S + ko - 1) / ko, md = (S + kd - 1) / kd;
-        const double eff = double(S) / std::max(mo, md);
-        if (eff > best || (eff == best && S > p.S)) {
-          best = eff;
-          p.ok = 1;
-          p.wo = wo;
-          p.ro = ro;
-          p.ko = ko;
-          p.rd = rd;
-          p.kd = kd;
-          p.mo = mo;
-          p.md = md;
-          p.S = S;
-          p.slot = slot;
-        }
-      }
-    }
-  }
-  p.zero = slots * p.slot;
-  // ≈ 4 rounds of the 256 resident workgroups, whole stages
-  const int64_t target = 1024 - nseg > 256 ? 1024 - nseg : 256;
-  int64_t chl = (numel + target - 1) / target;
-  const int64_t minl = int64_t(p.S) * 4;
-  if (chl < minl) chl = minl;
-  p.chl = (chl + p.S - 1) / p.S * p.S;
-  p.max_chunks = numel / chl + nseg + 1;
-  return p;
-}
-
-// 16-B LDS-DMA of one wave from per-lane 64-bit addresses: lane l's 16
-// bytes land at LDS byte address lds_addr + 16·l (exec-masked lanes load
-// nothing).  Inline asm for the same reason as glds16: the ring counts its
-// DMAs with vmcnt itself.
-__device__ __forceinline__ void glds16v(const float *src, uint32_t lds_addr) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
-      : "memory");
-}
-
-template <int TS>
-__global__ __launch_bounds__(kDmaThreads) void pairdist_dma_kernel(
-    const float *const *__restrict__ tab, int64_t ss, int n, DmaPlan pl,
-    const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
-    int nseg, const int *__restrict__ prefix, float *__restrict__ partial) {
-  __shared__ __attribute__((aligned(16))) float lds[kDmaLds];
-  const int c = blockIdx.x;
-  if (c >= prefix[nseg]) return;
-  int lo = 0, hi = nseg;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (prefix[mid] <= c) lo = mid;
-    else hi = mid;
-  }
-  const int s = lo;
-  const int64_t start = seg_lo[s] + int64_t(c - prefix[s]) * pl.chl;
-  int64_t end = start + pl.chl;
-  if (end > seg_end[s]) end = seg_end[s];
-  const float *const *__restrict__ rows = tab + int64_t(s) * ss;
-
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
-  const int lane = tid & (kWave - 1);
-  const bool diag = wave >= pl.wo;  // wave-uniform role kind
-  int k, K, ti = 0, tj = 0;
-  bool active;
-  if (!diag) {
-    const int role = tid / pl.ko;
-    k = tid - role * pl.ko;
-    K = pl.ko;
-    active = role < pl.ro;
-    od_to_tiles(active ? role : 0, pl.nt, ti, tj);
-  } else {
-    const int l = tid - kWave * pl.wo;
-    const int role = l / pl.kd;
-    k = l - role * pl.kd;
-    K = pl.kd;
-    active = role < pl.rd;
-    ti = 2 * (active ? role : 0);
-    tj = ti + 1 < pl.nt ? ti + 1 : ti;  // odd tile count: a repeat, unused
-  }
-
-  // 16-B DMA needs 16-B aligned sources: the chunk start and every row
-  bool vec = (start & 3) == 0;
-  for (int r = 0; r < n; ++r)
-    vec = vec && (reinterpret_cast<uintptr_t>(rows[r]) & 15u) == 0;
-  const int64_t end4 = vec ? start + ((end - start) & ~int64_t(3)) : start;
-  const int nstage = int((end4 - start + pl.S - 1) / pl.S);
-
-  f2 acc[TS / 2][TS];
-#pragma unroll
-  for (int h = 0; h < TS / 2; ++h)
-#pragma unroll
-    for (int v = 0; v < TS; ++v) acc[h][v] = f2{0.0f, 0.0f};
-
-  // the zero block
-  for (int i = tid; i < pl.nr * 16; i += kDmaThreads) lds[pl.zero + i] = 0.0f;
-
-  // DMA work of this wave: row group g (16 rows), blocks b ≡ j (mod J)
-  const int G = pl.groups;
-  const int g = wave % G;
-  const int J = kDmaWaves / G + (wave % G < kDmaWaves % G ? 1 : 0);
-  const int j = wave / G;
-  const int myrow = 16 * g + (lane >> 2);
-  const bool rowok = myrow < n;
-  const float *rp = rows[rowok ? myrow : 16 * g] + 4 * (lane & 3);
-  const uint32_t lds_base = uint32_t(uintptr_t((lfloat_t *)lds));
-  const int nblk = pl.S / 16;
-  // DMAs this wave issues per stage (a partial last stage issues the same
-  // instructions, with its lanes past the chunk masked)
-  const int my_dma = (nblk - j + J - 1) / J;
-  // scratch word after the zero block: the target of a dead block's DMA
-  const uint32_t scratch = lds_base + 4u * uint32_t(pl.zero + pl.nr * 16);
-  auto issue = [&](int st) {
-    const int64_t cs = start + int64_t(st) * pl.S;
-    const uint32_t slot = lds_base + 4u * uint32_t((st % pl.slots) * pl.slot);
-    for (int b = j; b < nblk; b += J) {
-      // every wave issues my_dma instructions per stage, so its vmcnt
-      // waits count exactly: a block wholly past the chunk (its last,
-      // partial stage) still issues one, of lane 0 into the scratch word
-      if (cs + 16 * b < end4) {
-        if (rowok && cs + 16 * b + 4 * (lane & 3) < end4)
-          glds16v(rp + cs + 16 * b,
-                  slot + 4u * uint32_t(b * pl.nr * 16 + 256 * g));
-      } else if (lane == 0) {
-        glds16v(rp + start, scratch);
-      }
-    }
-  };
-  __syncthreads();
-  auto run = [&](auto is_diag) {
-    constexpr bool D = decltype(is_diag)::value;
-    const int M = D ? pl.md : pl.mo;
-    const float *const zblk = lds + pl.zero;
-    // one coordinate step m of a stage in slot sb (len coordinates; past
-    // them the zero block)
-    auto step = [&](const float *sb, int len, int m) {
-      const int cc = k + m * K;
-      const float *col = active && cc < len
-          ? sb + (cc >> 4) * pl.nr * 16 + (cc & 15) : zblk;
-      const float *A0 = col + ti * TS * 16, *B0 = col + tj * TS * 16;
-      f2 A[TS / 2], B[TS / 2];
-#pragma unroll
-      for (int h = 0; h < TS / 2; ++h) {
-        A[h] = f2{A0[32 * h], A0[32 * h + 16]};
-        B[h] = f2{B0[32 * h], B0[32 * h + 16]};
-      }
-      pair_update<TS, D>(acc, A, B);
-    };
-    auto compute = [&](const float *sb, int len) {
-      for (int m = 0; m < M; ++m) step(sb, len, m);
-    };
-    for (int q = 0; q < pl.slots - 1; ++q)
-      if (q < nstage) issue(q);
-    // one flat loop over (stage, step): nested stage/step loops made the
-    // compiler copy all 50 accumulator pairs on every step
-    const float *sb = lds;
-    int len = 0, st = -1, m = M;
-    for (int it = 0, total = nstage * M; it < total; ++it) {
-      if (m == M) {
-        m = 0;
-        ++st;
-        // this wave's DMAs of stage st have landed (later ones may fly)
-        const int later = min(nstage - 1 - st, pl.slots - 2);
-        wait_vmcnt(later * my_dma);
-        __builtin_amdgcn_s_barrier();
-        if (st + pl.slots - 1 < nstage) issue(st + pl.slots - 1);
-        sb = lds + (st % pl.slots) * pl.slot;
-        len = int(min(int64_t(pl.S), end4 - (start + int64_t(st) * pl.S)));
-      }
-      step(sb, len, m);
-      ++m;
-    }
-    // [end4, end): the sub-quad tail, or the whole chunk when a row is not
-    // 16-B aligned — staged by 4-B loads into slot 0, same block layout
-    const int nrows = pl.nt * TS;
-    for (int64_t cs = end4; cs < end; cs += pl.S) {
-      const int len = int(min(int64_t(pl.S), end - cs));
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // every wave is done with the slots
-      for (int i = tid; i < nrows * len; i += kDmaThreads) {
-        const int r = i / len, col = i - r * len;
-        lds[(col >> 4) * pl.nr * 16 + r * 16 + (col & 15)] =
-            gld(rows[min(r, n - 1)] + cs + col);
-      }
-      __syncthreads();
-      compute(lds, len);
-    }
-  };
-  if (diag) run(std::true_type{});
-  else run(std::false_type{});
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // every stage read: the ring becomes the reduction buffer
-
-  // Σ over the k-slices of each role, in slice order
-  constexpr int kE = TS * TS;
-  constexpr int R = kDmaLds / kDmaThreads;
-#pragma unroll
-  for (int e0 = 0; e0 < kE; e0 += R) {
-    const int ne = kE - e0 < R ? kE - e0 : R;
-    if (active) {
-      float *slotp = lds + tid * R;
-#pragma unroll
-      for (int e = e0; e < e0 + R && e < kE; ++e)
-        slotp[e - e0] = pair_acc<TS>(acc, e / TS, e % TS);
-    }
-    __syncthreads();
-    const int nod = pl.ro * ne, outs = nod + pl.rd * ne;
-    for (int o = tid; o < outs; o += kDmaThreads) {
-      const bool dg = o >= nod;
-      const int o2 = dg ? o - nod : o;
-      const int l = o2 / ne, e = o2 - l * ne;
-      const int base = dg ? kWave * pl.wo + l * pl.kd : l * pl.ko;
-      const int kk = dg ? pl.kd : pl.ko;
-      float sum = 0.0f;
-      for (int q = 0; q < kk; ++q) sum += lds[(base + q) * R + e];
-      int tp, idx;
-      if (split_slot(dg, l, e0 + e, TS, pl.nt, tp, idx))
-        partial[(int64_t(c) * pl.ntp + tp) * kE + idx] = sum;
-    }
-    __syncthreads();
-  }
-}
-
 // Σ over a segment's chunks in fp64 for every pair of the tile layout, in a
 // fixed order (deterministic, no atomics).  Block = (segment, 64 partial
 // columns); its 16 waves take every 16th chunk each (consecutive lanes read
@@ -1683,13 +1087,9 @@ extern "C" int fsagg_rows_sqnorm_f32(const fsagg_rows *rows,
   return check_launch("fsagg_rows_sqnorm_f32");
 }
 
-// chunks of the partial buffer: the larger of the two plans
+// chunks of the partial buffer
 static int64_t pairdist_max_chunks(int n, int64_t numel, int nseg) {
-  const PairPlan pl = make_plan(n, numel, nseg);
-  const RingPlan rp = make_ring_plan(n, numel, nseg);
-  const DmaPlan dp = make_dma_plan(n, numel, nseg);
-  int64_t m = pl.max_chunks > rp.max_chunks ? pl.max_chunks : rp.max_chunks;
-  return m > dp.max_chunks ? m : dp.max_chunks;
+  return make_plan(n, numel, nseg).max_chunks;
 }
 
 static size_t partial_bytes(int n, int64_t numel, int nseg) {
@@ -1706,19 +1106,6 @@ extern "C" size_t fsagg_pairdist_workspace_bytes(int n, int64_t numel,
          align256(sizeof(double) * size_t(nseg) * size_t(n) * size_t(n));
 }
 
-// Experiment switches exist only in the probe build (tools/probe/Makefile,
-// -DFSAGG_PROBE); the product library always takes the defaults.
-#ifdef FSAGG_PROBE
-static int probe_int(const char *name, int dflt) {
-  const char *e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-#else
-static int probe_int(const char *, int dflt) { return dflt; }
-#endif
-
-static bool ring_enabled() { return probe_int("FSAGG_PROBE_RING", 0) != 0; }
-
 // Enqueue the chunk and per-segment kernels; segsq receives [nseg][n][n].
 static int pairdist_segsq_impl(const float *const *tab, int64_t ss, int n,
                                int64_t numel,
@@ -1729,61 +1116,6 @@ static int pairdist_segsq_impl(const float *const *tab, int64_t ss, int n,
   int *prefix = static_cast<int *>(workspace);
   float *partial = reinterpret_cast<float *>(
       static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)));
-  const RingPlan rp = make_ring_plan(n, numel, nseg,
-                                     probe_int("FSAGG_PROBE_RING_WAVES", 12),
-                                     probe_int("FSAGG_PROBE_RING_SLOTS", 3),
-                                     probe_int("FSAGG_PROBE_RING_PAD", 0));
-  const DmaPlan dp = make_dma_plan(n, numel, nseg,
-                                   probe_int("FSAGG_PROBE_DMA_SLOTS", 3));
-  if (dp.ok && probe_int("FSAGG_PROBE_PAIR", 0) == 2 && numel > 0) {
-    hipLaunchKernelGGL(chunk_prefix_kernel, dim3(1), dim3(1), 0, s, seg_lo,
-                       seg_end, nseg, dp.chl, prefix);
-    const dim3 grid(unsigned(dp.max_chunks));
-    if (dp.ts == 10)
-      hipLaunchKernelGGL((pairdist_dma_kernel<10>), grid, dim3(kDmaThreads), 0,
-                         s, tab, ss, n, dp, seg_lo, seg_end, nseg, prefix,
-                         partial);
-    else
-      hipLaunchKernelGGL((pairdist_dma_kernel<8>), grid, dim3(kDmaThreads), 0,
-                         s, tab, ss, n, dp, seg_lo, seg_end, nseg, prefix,
-                         partial);
-    const int per_seg = pl.ntp * pl.ts * pl.ts;
-    hipLaunchKernelGGL(pairdist_segsq_kernel,
-                       dim3(unsigned(nseg), unsigned((per_seg + kWave - 1) / kWave)),
-                       dim3(kSegBlock), 0, s, partial, n, pl, nseg, prefix,
-                       segsq);
-    return FSAGG_OK;
-  }
-  if (rp.ok && ring_enabled() && numel > 0) {
-    hipLaunchKernelGGL(chunk_prefix_kernel, dim3(1), dim3(1), 0, s, seg_lo,
-                       seg_end, nseg, rp.chl, prefix);
-    const dim3 grid(unsigned(rp.max_chunks));
-#define FSAGG_RINGW(TS, P64, W, PADW)                                       \
-  hipLaunchKernelGGL((pairdist_ring_kernel<TS, P64, W, PADW>), grid,        \
-                     dim3(W * kWave), 0, s, tab, ss, n, rp, seg_lo,         \
-                     seg_end, nseg, prefix, partial)
-#define FSAGG_RING(TS, P64)                                                 \
-  do {                                                                      \
-    if (rp.waves == 8) FSAGG_RINGW(TS, P64, 8, 0);                          \
-    else if (rp.pad == 4) FSAGG_RINGW(TS, P64, 12, 4);                      \
-    else FSAGG_RINGW(TS, P64, 12, 0);                                       \
-  } while (0)
-    const bool t10 = rp.ts == 10;
-    switch (rp.p64) {
-      case 1: if (t10) FSAGG_RING(10, 1); else FSAGG_RING(8, 1); break;
-      case 2: if (t10) FSAGG_RING(10, 2); else FSAGG_RING(8, 2); break;
-      case 3: if (t10) FSAGG_RING(10, 3); else FSAGG_RING(8, 3); break;
-      default: if (t10) FSAGG_RING(10, 4); else FSAGG_RING(8, 4); break;
-    }
-#undef FSAGG_RING
-#undef FSAGG_RINGW
-    const int per_seg = pl.ntp * pl.ts * pl.ts;
-    hipLaunchKernelGGL(pairdist_segsq_kernel,
-                       dim3(unsigned(nseg), unsigned((per_seg + kWave - 1) / kWave)),
-                       dim3(kSegBlock), 0, s, partial, n, pl, nseg, prefix,
-                       segsq);
-    return FSAGG_OK;
-  }
   hipLaunchKernelGGL(chunk_prefix_kernel, dim3(1), dim3(1), 0, s, seg_lo,
                      seg_end, nseg, pl.chl, prefix);
   if (numel > 0) {

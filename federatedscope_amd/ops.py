@@ -804,16 +804,17 @@ class BaseRows:
     of the robust rules' init + update): per-key virtual bases of device
     tensors, or one flat bucket."""
 
-    def __init__(self, tab, bss, keepalive=()):
+    def __init__(self, tab, bss, keepalive=(), host=None):
         self.tab = tab
         self.bss = bss
+        self.host = host      # the per-key virtual bases (host copy)
         self._keep = tuple(keepalive)
 
     @classmethod
     def from_bucket(cls, flat):
         _check_f32_cuda(flat, 'base bucket')
         return cls(_h2d([flat.data_ptr()], torch.int64, flat.device), 0,
-                   keepalive=(flat, ))
+                   keepalive=(flat, ), host=[flat.data_ptr()])
 
     @classmethod
     def from_pointers(cls, layout, ptrs, device, keepalive=()):
@@ -822,7 +823,7 @@ class BaseRows:
                          dtype=_np.int64)
         virt = ptrs - 4 * offs
         return cls(_h2d_np(virt, _cuda_index(device)), 1,
-                   keepalive=keepalive)
+                   keepalive=keepalive, host=[int(v) for v in virt])
 
     def ptr(self):
         return self.tab.data_ptr()
@@ -847,6 +848,13 @@ def weighted_sum_rows(rs, weights, out, prescale=None, base=None, lo=0,
                          'tensors')
     _rows_out(rs, out, ALIGN_BYTES)
     lib = L.load()
+    if rs.nseg == 1 and not rs.missing and rs.layout.keys and (
+            base is None or base.host is not None):
+        # one key, every client holding it (a flat model, configs[2]): the
+        # row set IS a row table — the flat streaming kernel runs on it
+        # directly, without the chunk list
+        return _weighted_sum_rows_flat(rs, weights, out, prescale, base, lo,
+                                       hi, lib)
     unit = lib.fsagg_wsum_chunk_elems_n(rs.layout.numel, rs.n)
     chunks, nchunk = rs.layout.row_chunks(unit, rs.device, lo, hi)
     if nchunk == 0:
@@ -865,6 +873,40 @@ def weighted_sum_rows(rs, weights, out, prescale=None, base=None, lo=0,
         base.ptr() if base is not None else None,
         base.bss if base is not None else 0, out.data_ptr(),
         _stream(rs.device)), 'fsagg_weighted_sum_rows_f32')
+    return out
+
+
+def _weighted_sum_rows_flat(rs, weights, out, prescale, base, lo, hi, lib):
+    k = rs.layout.keys[0]
+    o, m = rs.layout.offsets[k], rs.layout.numels[k]
+    a = max(int(lo), o)
+    b = min(int(hi) if hi is not None else rs.layout.numel, o + m)
+    if b <= a:
+        return out
+    if a % 4:
+        raise ValueError('row range start %d is not 16-byte aligned' % a)
+    # entry i = the client's virtual base: coordinate p at entry + 4·p
+    if a == 0:
+        table = rs.tab
+    else:
+        table = _h2d_np(rs.host[:, 0] + 4 * a, rs.device)
+    w = weights if isinstance(weights, torch.Tensor) else _fp32_dev(
+        weights, rs.device)
+    pre = None
+    if prescale is not None:
+        if len(prescale) != rs.n:
+            raise ValueError('prescale length mismatch')
+        pre = prescale if isinstance(prescale, torch.Tensor) else _fp32_dev(
+            prescale, rs.device)
+    bptr = None
+    if base is not None:
+        bptr = int(base.host[0]) + 4 * a
+        if bptr % ALIGN_BYTES:
+            raise ValueError('base is not 16-byte aligned at %d' % a)
+    L.check(lib.fsagg_weighted_sum_f32(
+        table.data_ptr(), w.data_ptr(),
+        pre.data_ptr() if pre is not None else None, rs.n, b - a, bptr,
+        out.data_ptr() + 4 * a, _stream(rs.device)), 'fsagg_weighted_sum_f32')
     return out
 
 
