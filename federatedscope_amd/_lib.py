@@ -72,6 +72,9 @@ SIGNATURES['fsagg_server_opt_step_f64'] = (
            _c_p])
 
 FSAGG_WIRE_F32, FSAGG_WIRE_I8, FSAGG_WIRE_I16 = 0, 1, 2
+FSAGG_WIRE_B64_F32, FSAGG_WIRE_ZERO = 3, 4
+SIGNATURES['fsagg_b64_unpack_f32'] = (
+    _c_i, [_c_p, _c_i64, _c_p, _c_i, _c_i64, _c_p, _c_i64, _c_p, _c_p])
 SIGNATURES['fsagg_wire_unpack_f32'] = (
     _c_i, [_c_p, _c_i64, _c_p, _c_p, _c_i, _c_i, _c_i64, _c_p, _c_i64, _c_p])
 SIGNATURES['fsagg_ss_recover_f32'] = (

@@ -20,7 +20,8 @@ import torch
 
 from ... import ops
 from ...layout import BucketLayout, ClientStack
-from ..auxiliaries.utils import as_float_tensor, param2tensor
+from ..auxiliaries.utils import (as_float_tensor, as_float_upload,
+                                 param2tensor, param_meta)
 
 
 def compute_device(device=None):
@@ -184,8 +185,8 @@ class DeviceEngine:
         if as_float:
             template = OrderedDict(
                 (k, _as_float_proto(v)) for k, v in template.items())
-        sig = tuple((k, tuple(param2tensor(v).shape), param2tensor(v).dtype)
-                    for k, v in template.items())
+        sig = tuple((k, tuple(t.shape), t.dtype) for k, t in (
+            (k, param_meta(v)) for k, v in template.items()))
         lay = self._layouts.get(sig)
         if lay is None:
             lay = BucketLayout(template)
@@ -201,7 +202,7 @@ class DeviceEngine:
             st.slab.zero_()
             self._stacks[key] = st
         if as_float:
-            models = [OrderedDict((k, as_float_tensor(v))
+            models = [OrderedDict((k, as_float_upload(v))
                                   for k, v in m.items()) for m in models]
         st.load_many(models)
         return st
@@ -447,7 +448,7 @@ class _NoRows:
 
 
 def _as_float_proto(v):
-    t = param2tensor(v)
+    t = param_meta(v)
     if not isinstance(t, torch.Tensor):
         import numpy as np
         t = torch.as_tensor(np.asarray(t))

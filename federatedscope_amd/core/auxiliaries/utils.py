@@ -34,7 +34,32 @@ class _TensorUnpickler(pickle.Unpickler):
 
 
 def b64_to_tensor(s):
-    return _TensorUnpickler(io.BytesIO(base64.b64decode(s))).load()
+    """Decode one b64serializer payload (message.py:8-9) on the host: the
+    framing walker of core/compression/b64wire reads the pickle framing and
+    only the storage bytes are base64-decoded (no pickle machinery runs).
+    A payload it does not recognise (e.g. another pickle protocol's bytes
+    encoding) goes through the restricted unpickler; if that fails too, the
+    framing error is raised."""
+    from ..compression.b64wire import FramingError, decode_b64
+    try:
+        return decode_b64(s)
+    except FramingError as e:
+        try:
+            return _TensorUnpickler(io.BytesIO(base64.b64decode(s))).load()
+        except Exception:
+            raise e from None
+
+
+def param_meta(param):
+    """What param2tensor would return, as far as shape, dtype and device
+    go — without decoding base64 text (a meta tensor for it)."""
+    if isinstance(param, str):
+        from ..compression.b64wire import FramingError, parse_b64
+        try:
+            return parse_b64(param).meta()
+        except FramingError:
+            pass
+    return param2tensor(param)
 
 
 def param2tensor(param):
@@ -60,6 +85,14 @@ def as_float_tensor(param):
         return t.float()
     import numpy as np
     return torch.as_tensor(np.asarray(t)).float()
+
+
+def as_float_upload(param):
+    """as_float_tensor for staging: base64 text whose framing is already
+    fp32 stays text (the device decodes it, core/compression/b64wire)."""
+    if isinstance(param, str) and param_meta(param).dtype == torch.float32:
+        return param
+    return as_float_tensor(param)
 
 
 def merge_param_dict(raw_param, filtered_param):

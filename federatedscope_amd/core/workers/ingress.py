@@ -15,7 +15,8 @@ from collections.abc import Mapping
 import torch
 
 from ...layout import BucketLayout, ClientStack, HostStager
-from ..auxiliaries.utils import as_float_tensor, param2tensor
+from ..auxiliaries.utils import (as_float_tensor, as_float_upload,
+                                 param2tensor, param_meta)
 
 
 class StagedUpdate(Mapping):
@@ -69,7 +70,8 @@ class DeviceIngress:
             self.layout = self.plan.layout
         else:
             if as_float:
-                template = {k: torch.empty(param2tensor(v).shape)
+                template = {k: torch.empty(param_meta(v).shape,
+                                           device='meta')
                             for k, v in template.items()}
             self.layout = BucketLayout(template)
         self.stack = ClientStack(self.layout, capacity, self.device)
@@ -110,14 +112,15 @@ class DeviceIngress:
             v = model_para.get(k) if isinstance(model_para, Mapping) else None
             if v is None:
                 return False
-            t = param2tensor(v)
+            t = param_meta(v)
             if not isinstance(t, torch.Tensor) or tuple(t.shape) != \
                     tuple(lay.shapes[k]) or (not self.as_float and
                                              t.dtype != torch.float32):
                 return False
         for k, dt in lay.other.items():
             v = model_para.get(k)
-            if not isinstance(v, torch.Tensor) or v.dtype != dt:
+            t = param_meta(v) if isinstance(v, str) else v
+            if not isinstance(t, torch.Tensor) or t.dtype != dt:
                 return False
         return True
 
@@ -129,10 +132,21 @@ class DeviceIngress:
         if not self.accepts(model_para):
             raise KeyError('upload does not match the staged layout')
         slot = self._slot(slot)
+        typed = {k: param2tensor(model_para[k]).to(self.device,
+                                                   non_blocking=True)
+                 for k in self.layout.other}
+        if any(isinstance(model_para[k], str) for k in self.layout.keys):
+            # gRPC upload: HostStager decodes the base64 on the device
+            # (core/compression/b64wire), or on the host if not fp32 text
+            if self._stager is None:
+                self._stager = HostStager(self.device)
+            src = model_para if not self.as_float else {
+                k: as_float_upload(model_para[k]) for k in self.layout.keys}
+            self._stager.put(self.layout, src, self.stack.slab[slot])
+            return sample_size, StagedUpdate(self, slot, model_para.keys(),
+                                             typed)
         src = {k: (as_float_tensor(model_para[k]) if self.as_float else
                    param2tensor(model_para[k])) for k in self.layout.keys}
-        typed = {k: model_para[k].to(self.device, non_blocking=True)
-                 for k in self.layout.other}
         on_host = any(v.device.type != 'cuda' for v in src.values())
         if on_host:
             if self._stager is None:

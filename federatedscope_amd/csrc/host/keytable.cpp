@@ -28,7 +28,9 @@
 #include <torch/csrc/autograd/python_variable.h>
 
 #include <cstdint>
+#include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -130,9 +132,74 @@ PyObject *device_tensor(PyObject *, PyObject *args) {
   return THPVariable_Wrap(t);
 }
 
+// text_copy(text, lo, hi, dst_addr[, threads]) -> None
+// Copy characters [lo, hi) of a base64 upload into host memory at dst_addr
+// (a pinned staging buffer; core/compression/b64wire.B64Stager).  `text` is
+// what the gRPC transport hands the server (federatedscope/core/message.py
+// :187-188,236-249): a str — read in place when it is compact ASCII, the
+// form CPython keeps base64 text in — or any bytes-like object.  Large
+// ranges are copied by several threads with the GIL released.
+PyObject *text_copy(PyObject *, PyObject *args) {
+  PyObject *obj;
+  long long lo, hi;
+  unsigned long long dst;
+  int threads = 8;
+  if (!PyArg_ParseTuple(args, "OLLK|i", &obj, &lo, &hi, &dst, &threads))
+    return nullptr;
+  const char *src = nullptr;
+  Py_ssize_t len = 0;
+  Py_buffer view{};
+  bool have_view = false;
+  if (PyUnicode_Check(obj)) {
+    if (PyUnicode_READY(obj) != 0) return nullptr;
+    if (!PyUnicode_IS_COMPACT_ASCII(obj)) {
+      PyErr_SetString(PyExc_ValueError,
+                      "text_copy: base64 text must be ASCII");
+      return nullptr;
+    }
+    src = static_cast<const char *>(PyUnicode_DATA(obj));
+    len = PyUnicode_GET_LENGTH(obj);
+  } else {
+    if (PyObject_GetBuffer(obj, &view, PyBUF_SIMPLE) != 0) return nullptr;
+    have_view = true;
+    src = static_cast<const char *>(view.buf);
+    len = view.len;
+  }
+  if (lo < 0 || hi < lo || hi > len || dst == 0) {
+    if (have_view) PyBuffer_Release(&view);
+    PyErr_SetString(PyExc_ValueError, "text_copy: range out of bounds");
+    return nullptr;
+  }
+  char *out = reinterpret_cast<char *>(dst);
+  const size_t n = size_t(hi - lo);
+  src += lo;
+  Py_BEGIN_ALLOW_THREADS
+  const size_t per_min = size_t(4) << 20;  // below 4 MiB a thread is overhead
+  int t = threads < 1 ? 1 : threads;
+  if (size_t(t) > n / per_min) t = int(n / per_min) < 1 ? 1 : int(n / per_min);
+  if (t == 1) {
+    std::memcpy(out, src, n);
+  } else {
+    std::vector<std::thread> pool;
+    const size_t step = ((n + t - 1) / t + 4095) & ~size_t(4095);
+    for (int i = 0; i < t; ++i) {
+      const size_t a = size_t(i) * step;
+      if (a >= n) break;
+      const size_t b = a + step < n ? a + step : n;
+      pool.emplace_back([=] { std::memcpy(out + a, src + a, b - a); });
+    }
+    for (auto &th : pool) th.join();
+  }
+  Py_END_ALLOW_THREADS
+  if (have_view) PyBuffer_Release(&view);
+  Py_RETURN_NONE;
+}
+
 PyMethodDef kMethods[] = {
     {"device_tensor", device_tensor, METH_VARARGS,
      "device_tensor(ptr, numel, kind, device_index) -> Tensor (no ownership)"},
+    {"text_copy", text_copy, METH_VARARGS,
+     "text_copy(text, lo, hi, dst_addr[, threads]): copy chars [lo, hi)"},
     {"key_table", key_table, METH_VARARGS,
      "key_table(dicts, keys, shapes, device_index[, offs4]) -> (bytes, "
      "missing, aligned16) or None"},

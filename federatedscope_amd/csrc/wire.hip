@@ -74,6 +74,109 @@ __global__ __launch_bounds__(kBlock) void wire_unpack_kernel(
   }
 }
 
+// ---- base64 uploads (gRPC) ------------------------------------------------
+// The gRPC transport ships each tensor as base64(pickle(tensor))
+// (federatedscope/core/message.py:8-9,110-124) and the server decodes it on
+// the host (core/auxiliaries/utils.py:95-105, param2tensor).  Here the host
+// reads only the pickle framing (core/compression/b64wire.py) and sends the
+// base64 text of the storage bytes; this kernel decodes it straight into
+// the client's fp32 row.
+//
+// `src` of a FSAGG_WIRE_B64_F32 segment is a byte offset in the DECODED
+// image of `text`: decoded byte d is one of the three bytes of the 4-char
+// group at text + 4*(d/3).  Each thread emits 3 fp32 (12 decoded bytes, at
+// most 5 groups); the byte phase src % 3 is uniform per segment, so the
+// byte shuffle is a compile-time pattern (three instantiations).
+constexpr int kB64Elems = 3;
+
+__device__ __forceinline__ uint32_t b64_sextet(uint32_t c, uint32_t &bad) {
+  const uint32_t up = c - 'A', lo = c - 'a', dg = c - '0';
+  const uint32_t v = up < 26u   ? up
+                     : lo < 26u ? lo + 26u
+                     : dg < 10u ? dg + 52u
+                     : c == '+' ? 62u
+                     : c == '/' ? 63u
+                                : 64u;
+  bad |= v >> 6;
+  return v & 63u;
+}
+
+// 4 chars (little-endian in x) -> 24 bits, first decoded byte in 23..16
+__device__ __forceinline__ uint32_t b64_group(uint32_t x, uint32_t &bad) {
+  return (b64_sextet(x & 255u, bad) << 18) |
+         (b64_sextet((x >> 8) & 255u, bad) << 12) |
+         (b64_sextet((x >> 16) & 255u, bad) << 6) |
+         b64_sextet(x >> 24, bad);
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t b64_byte(const uint32_t (&g)[5]) {
+  return (g[K / 3] >> (16 - 8 * (K % 3))) & 255u;
+}
+
+template <int K>
+__device__ __forceinline__ float b64_word(const uint32_t (&g)[5]) {
+  return __uint_as_float(b64_byte<K>(g) | (b64_byte<K + 1>(g) << 8) |
+                         (b64_byte<K + 2>(g) << 16) |
+                         (b64_byte<K + 3>(g) << 24));
+}
+
+template <int S>
+__device__ __forceinline__ void b64_emit(const uint32_t (&g)[5], float *o,
+                                         int ne) {
+  static_assert(kB64Elems == 3, "b64_emit writes three words");
+  o[0] = b64_word<S>(g);
+  if (ne > 1) o[1] = b64_word<S + 4>(g);
+  if (ne > 2) o[2] = b64_word<S + 8>(g);
+}
+
+// grid = (ceil(max_len / (kBlock * 3)), nseg).  Segments live on the
+// device, so each block checks its own against the decoded extent of
+// `text` and the row; a bad segment or a non-alphabet character in a group
+// it decodes sets *status (2 / 1) instead of faulting or being silently
+// wrong — the host raises on it.
+__global__ __launch_bounds__(kBlock) void b64_unpack_kernel(
+    const uint32_t *__restrict__ text, int64_t text_groups,
+    const WireSeg *__restrict__ segs, int64_t out_len,
+    float *__restrict__ out, uint32_t *__restrict__ status) {
+  const WireSeg sg = segs[blockIdx.y];
+  const int64_t e0 =
+      (int64_t(blockIdx.x) * kBlock + threadIdx.x) * kB64Elems;
+  if (e0 >= sg.len) return;
+  const int64_t cap = 3 * text_groups;  // decoded bytes
+  const bool zero = sg.kind == FSAGG_WIRE_ZERO;
+  if (sg.len < 0 || sg.dst < 0 || sg.dst > out_len ||
+      sg.len > out_len - sg.dst ||
+      (!zero && (sg.kind != FSAGG_WIRE_B64_F32 || sg.src < 0 ||
+                 sg.src > cap || sg.len > (cap - sg.src) / 4))) {
+    status[0] = 2u;
+    return;
+  }
+  float *o = out + sg.dst + e0;
+  const int ne = int(min(int64_t(kB64Elems), sg.len - e0));
+  if (zero) {
+#pragma unroll
+    for (int e = 0; e < kB64Elems; ++e)
+      if (e < ne) o[e] = 0.0f;
+    return;
+  }
+  const int64_t d = sg.src + 4 * e0;
+  const int s = int(sg.src % 3);
+  const int64_t g0 = d / 3;
+  const int ng = (s + 4 * ne + 2) / 3;
+  uint32_t g[5], bad = 0;
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+    g[j] = j < ng ? b64_group(gld(text + g0 + j), bad) : 0u;
+  if (bad) status[0] = 1u;
+  if (s == 0)
+    b64_emit<0>(g, o, ne);
+  else if (s == 1)
+    b64_emit<1>(g, o, ne);
+  else
+    b64_emit<2>(g, o, ne);
+}
+
 // numpy's float64 remainder (npy_divmod): the result takes the divisor's
 // sign; an exact zero becomes +0.0 for a positive divisor.
 __device__ __forceinline__ double py_mod(double a, double b) {
@@ -199,6 +302,33 @@ extern "C" int fsagg_wire_unpack_f32(const void *src, int64_t src_bytes,
                      static_cast<const WireSeg *>(segs), scales, nscale,
                      src_bytes, out_len, out);
   return check_launch("fsagg_wire_unpack_f32");
+}
+
+extern "C" int fsagg_b64_unpack_f32(const void *text, int64_t text_bytes,
+                                    const void *segs, int nseg,
+                                    int64_t max_len, float *out,
+                                    int64_t out_len, uint32_t *status,
+                                    fsagg_stream_t stream) {
+  if (!text || !segs || !out || !status || nseg < 0 || max_len < 0 ||
+      text_bytes < 0 || out_len < 0 || text_bytes % 4 ||
+      reinterpret_cast<uintptr_t>(text) % 4) {
+    set_error("fsagg_b64_unpack_f32: invalid argument (text must be "
+              "4-byte aligned whole 4-char groups)");
+    return FSAGG_EINVAL;
+  }
+  if (nseg == 0 || max_len == 0) return FSAGG_OK;
+  if (nseg > 65535) {
+    set_error("fsagg_b64_unpack_f32: %d segments > 65535", nseg);
+    return FSAGG_EINVAL;
+  }
+  const int64_t per = int64_t(kBlock) * kB64Elems;
+  hipLaunchKernelGGL(b64_unpack_kernel,
+                     dim3(unsigned((max_len + per - 1) / per), unsigned(nseg)),
+                     dim3(kBlock), 0, as_stream(stream),
+                     static_cast<const uint32_t *>(text), text_bytes / 4,
+                     static_cast<const WireSeg *>(segs), out_len, out,
+                     status);
+  return check_launch("fsagg_b64_unpack_f32");
 }
 
 extern "C" int fsagg_ss_recover_f32(const void *const *rows,

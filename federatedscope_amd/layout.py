@@ -16,7 +16,7 @@ from collections import OrderedDict
 
 import torch
 
-from .core.auxiliaries.utils import param2tensor
+from .core.auxiliaries.utils import param2tensor, param_meta
 
 KEY_ALIGN = 16  # elements
 
@@ -31,7 +31,7 @@ class BucketLayout:
         self.order = list(template.keys())
         off = 0
         for k, v in template.items():
-            t = param2tensor(v)
+            t = param_meta(v)
             if not isinstance(t, torch.Tensor):
                 t = torch.as_tensor(t)
             if t.dtype == torch.float32:
@@ -153,7 +153,7 @@ class BucketLayout:
 
     def pack_device(self, model, out_row):
         """Pack into a device row (``out_row`` 1-D fp32 cuda tensor)."""
-        devs = {param2tensor(model[k]).device.type for k in self.keys
+        devs = {param_meta(model[k]).device.type for k in self.keys
                 if k in model}
         if devs <= {'cuda'}:
             # device-resident update: per-key device copies (padding and
@@ -231,10 +231,14 @@ class HostStager:
         self.nbuf = nbuf
         self.last = None
         self.i = 0
+        self._b64 = None
 
     def put(self, layout, model, dst_row):
         slot = self.i % self.nbuf
         self.i += 1
+        if isinstance(layout, BucketLayout) and self._put_b64(
+                layout, model, dst_row, slot):
+            return
         host = _pinned(layout.numel, slot)
         layout.pack_host(model, host)
         with torch.cuda.stream(self.stream):
@@ -244,8 +248,31 @@ class HostStager:
         _PINNED_EV[slot] = ev
         self.last = ev
 
+    def _put_b64(self, layout, model, dst_row, slot):
+        """gRPC uploads (every fp32 key base64 text, core/compression/
+        b64wire): the base64 characters cross PCIe and are decoded into the
+        row on the device.  False when the upload is not of that form."""
+        from .core.compression.b64wire import B64Stager, is_b64
+        if not any(is_b64(model.get(k)) for k in layout.keys):
+            return False
+        framings, host_keys = B64Stager.plan(layout, model)
+        if not framings:
+            return False
+        if self._b64 is None:
+            self._b64 = B64Stager(self.device, self.stream)
+        ev = self._b64.put(layout, framings, dst_row,
+                           lambda nb: _pinned(-(-nb // 4), slot).view(
+                               torch.uint8),
+                           host={k: model[k] for k in host_keys})
+        if ev is not None:
+            _PINNED_EV[slot] = ev
+            self.last = ev
+        return True
+
     def finish(self):
         torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        if self._b64 is not None:
+            self._b64.finish()
 
 
 class ClientStack:
@@ -284,7 +311,7 @@ class ClientStack:
             if srcs is not None:
                 gather.append((i, srcs))
                 continue
-            on_host = any(param2tensor(m[k]).device.type != 'cuda'
+            on_host = any(param_meta(m[k]).device.type != 'cuda'
                           for k in self.layout.keys if k in m)
             if on_host:
                 if stager is None:
@@ -409,7 +436,7 @@ class RangeStack:
         device tensors by slice copies."""
         stager = None
         for i, m in enumerate(models):
-            on_host = any(param2tensor(m[k]).device.type != 'cuda'
+            on_host = any(param_meta(m[k]).device.type != 'cuda'
                           for k in self.layout.keys if k in m)
             if on_host:
                 if stager is None:

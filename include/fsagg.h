@@ -245,11 +245,35 @@ int fsagg_server_opt_step_f64(double *param, const double *avg,
  * dequantisation step (federatedscope/core/workers/server.py:946-960).
  */
 enum fsagg_wire_kind { FSAGG_WIRE_F32 = 0, FSAGG_WIRE_I8 = 1,
-                       FSAGG_WIRE_I16 = 2 };
+                       FSAGG_WIRE_I16 = 2, FSAGG_WIRE_B64_F32 = 3,
+                       FSAGG_WIRE_ZERO = 4 };
 int fsagg_wire_unpack_f32(const void *src, int64_t src_bytes,
                           const void *segs, const float *scales, int nscale,
                           int nseg, int64_t max_len, float *out,
                           int64_t out_len, fsagg_stream_t stream);
+
+/*
+ * Base64 (gRPC) upload → fp32 client-stack row, in one launch.  Replaces
+ * the host decode of every tensor the gRPC transport ships as
+ * base64(pickle(tensor)) (federatedscope/core/message.py:8-9,110-124 →
+ * core/auxiliaries/utils.py:95-105 param2tensor, called per key by
+ * clients_avg_aggregator.py:86-87); the host parses only the pickle framing.
+ * `text` (device, 4-byte aligned, text_bytes a multiple of 4) holds base64
+ * characters; `segs` (device) the same 32-B records as above, with
+ *   kind FSAGG_WIRE_B64_F32: out[dst + i] = the fp32 whose 4 bytes are
+ *       decoded bytes src + 4i .. src + 4i + 3 of `text` (src counts
+ *       DECODED bytes: decoded byte b comes from the 4-char group at
+ *       text + 4*(b/3)); bit-exact little-endian reinterpretation;
+ *   kind FSAGG_WIRE_ZERO: out[dst + i] = 0 (padding, absent keys);
+ *   scale_idx is unused (-1).  max_len is the longest segment (elements).
+ * A segment outside the decoded extent or the row writes nothing and sets
+ * *status = 2; a non-alphabet character ('=' included) in a decoded group
+ * sets *status = 1 (`status`: a device word the caller zeroes and reads).
+ */
+int fsagg_b64_unpack_f32(const void *text, int64_t text_bytes,
+                         const void *segs, int nseg, int64_t max_len,
+                         float *out, int64_t out_len, uint32_t *status,
+                         fsagg_stream_t stream);
 
 /*
  * Secret-sharing FedAvg (cfg.federate.use_ss) in one pass:

@@ -28,7 +28,7 @@ __all__ = [
     'bulyan_aggregate', 'normbounding_aggregate', 'interpolate_aggregate',
     'add_init', 'f32', 'trimmed_tolerance', 'bulyan_select', 'asyn_weights',
     'FedOptState', 'dequantize', 'ss_fedavg', 'calc_l2_dissim',
-    'calc_blocal_dissim',
+    'calc_blocal_dissim', 'b64_tensor',
 ]
 
 f32 = np.float32
@@ -664,3 +664,85 @@ def calc_blocal_dissim(last, models):
             glob = glob + np.float32(w[i]) * g
         out[k] = math.sqrt(avg / float(np.sum(glob.astype(np.float64) ** 2)))
     return out
+
+
+# ---------------------------------------------------------------------------
+# gRPC uploads: base64(pickle(tensor))
+# ---------------------------------------------------------------------------
+_B64_STORAGE = {'FloatStorage': np.float32, 'DoubleStorage': np.float64,
+                'HalfStorage': np.float16, 'LongStorage': np.int64,
+                'IntStorage': np.int32, 'ShortStorage': np.int16,
+                'CharStorage': np.int8, 'ByteStorage': np.uint8,
+                'BoolStorage': np.bool_, 'BFloat16Storage': 'bf16'}
+
+
+def _pickle_ops(buf, pos=0):
+    """(ops, end) of the pickle starting at ``buf[pos:]`` — the stdlib
+    disassembler, which only reads opcodes and executes nothing."""
+    import pickletools
+    ops = list(pickletools.genops(buf[pos:]))
+    return ops, pos + ops[-1][2] + 1
+
+
+def b64_tensor(text):
+    """The tensor a b64serializer payload carries (message.py:8-9:
+    ``base64.b64encode(pickle.dumps(x))``; decoded by param2tensor,
+    utils.py:95-105), restated with the stdlib: base64-decode everything,
+    disassemble the outer pickle (torch's ``_rebuild_tensor_v2(
+    _load_from_bytes(payload), offset, size, stride, requires_grad, {})``)
+    and the legacy torch.save stream in the payload (magic, protocol,
+    sys_info, the ('storage', torch.<T>Storage, key, location, numel)
+    persistent id, [key], then numel as 8 LE bytes + raw elements).
+    Returns a contiguous numpy array (BF16 for bfloat16)."""
+    import base64
+    raw = base64.b64decode(text, validate=True)
+    ops, end = _pickle_ops(raw)
+    assert end == len(raw)
+    names = [op.name for op, _, _ in ops]
+    ib = next(i for i, n in enumerate(names)
+              if n in ('BINBYTES', 'SHORT_BINBYTES', 'BINBYTES8'))
+    payload = ops[ib][1]
+    # after the storage's REDUCE: offset, size tuple, stride tuple, bool
+    ir = names.index('REDUCE', ib)
+    stack = []
+    for op, arg, _ in ops[ir + 1:]:
+        n = op.name
+        if n in ('BININT', 'BININT1', 'BININT2', 'LONG1'):
+            stack.append(int(arg))
+        elif n == 'MARK':
+            stack.append('mark')
+        elif n in ('TUPLE1', 'TUPLE2', 'TUPLE3'):
+            k = int(n[-1])
+            t = tuple(stack[-k:])
+            del stack[-k:]
+            stack.append(t)
+        elif n == 'EMPTY_TUPLE':
+            stack.append(())
+        elif n == 'TUPLE':
+            m = len(stack) - 1 - stack[::-1].index('mark')
+            t = tuple(stack[m + 1:])
+            del stack[m:]
+            stack.append(t)
+        elif n in ('NEWFALSE', 'NEWTRUE'):
+            stack.append(n == 'NEWTRUE')
+            break
+    offset, size, stride, _ = stack[-4:]
+    # the legacy stream: five pickles, then numel + the raw storage
+    pos = 0
+    cls = None
+    for j in range(5):
+        pops, pos = _pickle_ops(payload, pos)
+        if j == 3:
+            cls = next(arg for op, arg, _ in pops if op.name == 'GLOBAL')
+    numel = int.from_bytes(payload[pos:pos + 8], 'little')
+    dt = _B64_STORAGE[cls.split()[1]]
+    if dt == 'bf16':
+        store = np.frombuffer(payload[pos + 8:], dtype=np.uint16)
+    else:
+        store = np.frombuffer(payload[pos + 8:], dtype=dt)
+    assert store.size == numel
+    es = store.itemsize
+    view = np.lib.stride_tricks.as_strided(
+        store[offset:], shape=size, strides=tuple(es * s for s in stride))
+    out = np.array(view)
+    return BF16(out) if dt == 'bf16' else out

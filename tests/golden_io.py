@@ -15,6 +15,8 @@ def _arr(z, name, dtypes):
     a = z[name]
     if dtypes.get(name) == 'bfloat16':
         return BF16(a)
+    if dtypes.get(name) == 'b64':          # gRPC upload text
+        return a.tobytes().decode('ascii')
     return a
 
 

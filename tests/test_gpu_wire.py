@@ -323,3 +323,140 @@ def test_wire_unpack_skips_malformed_segments():
     mask[:4] = False
     mask[60:68] = False
     assert (o[mask] == -1.0).all()
+
+
+# -- gRPC uploads: base64 text decoded on the device -------------------------
+def _b64_device_puts():
+    from federatedscope_amd.core.compression.b64wire import STATS
+    return STATS['device_puts']
+
+
+@pytest.mark.parametrize('name', case_names('b64_'))
+def test_b64_fedavg_golden(name):
+    """The reference's own gRPC uploads (str values from b64serializer)
+    aggregated by ClientsAvgAggregator on the GPU: the fp32 keys' base64
+    characters are decoded into the device stack by fsagg_b64_unpack_f32;
+    the aggregate is bit-identical to the reference's."""
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    meta, clients, out, _, _ = load_case(name)
+    c = _cfg()
+    c.federate.ignore_weight = meta.get('ignore_weight', False)
+    agg = ClientsAvgAggregator(device='cuda', config=c)
+    before = _b64_device_puts()
+    got = agg.aggregate({'client_feedback': [(s, OrderedDict(d))
+                                             for s, d in clients],
+                         'recover_fun': None})
+    # every client went through the kernel (the views case's transposed
+    # key alone is decoded on the host)
+    assert _b64_device_puts() - before == len(clients)
+    assert list(got.keys()) == list(out.keys())
+    for k in out:
+        _same_bits(got[k], out[k])
+
+
+@pytest.mark.parametrize('name', ['b64_fedavg_n5', 'b64_iw_n3'])
+def test_b64_uploads_through_server(name):
+    """Server.callback_funcs_model_para with gRPC uploads: each upload's
+    base64 is staged into its device-stack slot on arrival."""
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    from federatedscope_amd.core.workers.ingress import StagedUpdate
+    from federatedscope_amd.core.workers.server import AggregationServer
+    meta, clients, out, _, _ = load_case(name)
+    c = _cfg()
+    c.federate.ignore_weight = meta.get('ignore_weight', False)
+
+    class M(torch.nn.Module):
+        def state_dict(self, *a, **kw):
+            return OrderedDict()
+
+        def load_state_dict(self, sd, strict=True):
+            self.loaded = sd
+
+    srv = AggregationServer(M(), ClientsAvgAggregator(device='cuda',
+                                                      config=c),
+                            sample_client_num=len(clients), keep_history=1)
+    before = _b64_device_puts()
+    for sender, (s, d) in enumerate(clients):
+        srv.callback_funcs_model_para(0, sender, (s, OrderedDict(d)))
+        if sender < len(clients) - 1:
+            staged = srv.msg_buffer['train'][0][sender][1]
+            assert isinstance(staged, StagedUpdate)
+    assert _b64_device_puts() - before == len(clients)
+    got = srv.history[-1]
+    assert list(got.keys()) == list(out.keys())
+    for k in out:
+        _same_bits(got[k], out[k])
+
+
+def _b64(t):
+    import base64
+    import pickle
+    return base64.b64encode(pickle.dumps(t)).decode()
+
+
+def test_b64_rows_every_phase_and_size():
+    """HostStager's device decode of str uploads, row by row: keys of 1..40
+    and a few thousand elements, sliced out of larger storages at offsets
+    0..2 (so the data starts at every byte phase of a 4-char group), one
+    absent key; the row holds exactly the tensors' bytes and zero
+    padding."""
+    from federatedscope_amd.layout import BucketLayout, ClientStack
+    rng = np.random.default_rng(7)
+    sizes = list(range(1, 41)) + [1000, 4097, 65536 + 3]
+    tmpl = OrderedDict(('k%d' % i, torch.zeros(m))
+                       for i, m in enumerate(sizes))
+    lay = BucketLayout(tmpl)
+    ups, want = [], []
+    for c in range(3):
+        d, w = OrderedDict(), torch.zeros(lay.numel)
+        for i, m in enumerate(sizes):
+            if c == 1 and i == 5:
+                continue                       # an absent key
+            base = torch.from_numpy(
+                rng.standard_normal(m + 5).astype(np.float32))
+            t = base[c:c + m]
+            d['k%d' % i] = _b64(t)
+            w[lay.offsets['k%d' % i]:lay.offsets['k%d' % i] + m] = t
+        ups.append(d)
+        want.append(w)
+    st = ClientStack(lay, 3, 'cuda')
+    st.slab.fill_(float('nan'))                # padding must be written
+    before = _b64_device_puts()
+    st.load_many(ups)
+    torch.cuda.synchronize()
+    assert _b64_device_puts() - before == 3
+    for c in range(3):
+        g = st.slab[c].cpu().numpy()
+        assert g.tobytes() == want[c].numpy().tobytes(), c
+
+
+def test_b64_large_round_trip():
+    """A 25M-parameter key (the C3 model's size, 133 MB of base64): decode
+    on the device == the tensor that was pickled (encode→decode round
+    trip)."""
+    from federatedscope_amd.layout import BucketLayout, ClientStack
+    t = torch.randn(25_000_000)
+    lay = BucketLayout({'w': torch.zeros(25_000_000)})
+    st = ClientStack(lay, 1, 'cuda')
+    st.load_many([{'w': _b64(t)}])
+    torch.cuda.synchronize()
+    assert torch.equal(st.slab[0, :t.numel()].cpu(), t)
+
+
+def test_b64_bad_character_in_data_raises():
+    """A character outside the base64 alphabet inside the tensor data (the
+    host never reads those characters) is caught by the kernel and raised
+    when the staging finishes."""
+    from federatedscope_amd.core.compression.b64wire import FramingError
+    from federatedscope_amd.layout import BucketLayout, ClientStack
+    t = torch.randn(100_000)
+    txt = _b64(t)
+    mid = len(txt) // 2
+    bad = txt[:mid] + '*' + txt[mid + 1:]
+    lay = BucketLayout({'w': torch.zeros(100_000)})
+    st = ClientStack(lay, 1, 'cuda')
+    with pytest.raises(FramingError, match='alphabet'):
+        st.load_many([{'w': bad}])
+    st.load_many([{'w': txt}])                 # the stager state is clean
+    torch.cuda.synchronize()
+    assert torch.equal(st.slab[0, :100_000].cpu(), t)

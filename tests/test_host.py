@@ -155,7 +155,10 @@ def test_param2tensor_wire_format():
         def __reduce__(self):
             return (os.system, ('true', ))
 
-    with pytest.raises(pickle.UnpicklingError):
+    # the framing walker refuses the global; the restricted unpickler it
+    # falls back to refuses it too, and the framing error is raised
+    from federatedscope_amd.core.compression.b64wire import FramingError
+    with pytest.raises(FramingError, match='posix.system'):
         param2tensor(base64.b64encode(pickle.dumps(Evil())).decode())
 
 
@@ -290,3 +293,96 @@ def test_missing_library_fails_loudly():
     assert 'RAISED' in r.stdout and 'NO-ERROR' not in r.stdout, r.stdout + \
         r.stderr
     assert 'LOAD-RAISED' in r.stdout
+
+
+# -- gRPC uploads: the framing walker (core/compression/b64wire) -------------
+def _b64(x, protocol=None):
+    return base64.b64encode(pickle.dumps(x, protocol=protocol)).decode()
+
+
+@pytest.mark.parametrize('name', ['b64_fedavg_n5', 'b64_views_n4'])
+def test_b64_host_decode_matches_oracle(name):
+    """The product's host decode (param2tensor's str branch) of the
+    reference's own uploads is bit-identical to the oracle's stdlib
+    restatement, shape and dtype included."""
+    import oracle as O
+    from golden_io import load_case
+    from federatedscope_amd.core.auxiliaries.utils import param2tensor
+    _, clients, _, _, _ = load_case(name)
+    for _, d in clients:
+        for k, v in d.items():
+            t = param2tensor(v)
+            want = np.asarray(O.b64_tensor(v))
+            got = t.contiguous().numpy()
+            assert got.dtype == want.dtype and got.shape == want.shape, k
+            assert got.tobytes() == want.tobytes(), k
+
+
+def test_b64_framing_of_tensor_variants():
+    from federatedscope_amd.core.compression.b64wire import parse_b64
+    cases = [torch.arange(10, dtype=torch.float32), torch.randn(3, 5),
+             torch.randn(0), torch.tensor(3.5), torch.tensor(7),
+             torch.randn(4, 6).t(), torch.randn(10)[3:7],
+             torch.randn(5, dtype=torch.float64), torch.randn(6).half(),
+             torch.randn(6).bfloat16(), torch.randn(3, requires_grad=True),
+             torch.nn.Parameter(torch.randn(2, 2)), torch.zeros(2, 0, 3),
+             torch.tensor([True, False])]
+    for t in cases:
+        for proto in (3, 4, 5):
+            txt = _b64(t, proto)
+            f = parse_b64(txt)
+            ref = pickle.loads(base64.b64decode(txt))
+            assert f.dtype == ref.dtype and f.shape == tuple(ref.shape)
+            assert f.stride == ref.stride()
+            assert f.storage_offset == ref.storage_offset()
+            assert f.requires_grad == ref.requires_grad
+            got = f.to_tensor()
+            assert torch.equal(got.detach(), ref.detach())
+            assert parse_b64(txt.encode()).data_pos == f.data_pos   # bytes
+            if f.is_contiguous() and f.numel:
+                # the segment math of the device path: the characters
+                # [c0, c1) decode, after `skip` bytes, to the tensor's bytes
+                c0, c1, skip = f.char_range()
+                raw = base64.b64decode(txt[c0:c1])
+                nb = f.numel * f.itemsize
+                want = ref.detach().contiguous().view(-1).view(
+                    torch.uint8).numpy().tobytes() \
+                    if ref.dtype != torch.bool else \
+                    ref.contiguous().numpy().tobytes()
+                assert raw[skip:skip + nb] == want
+
+
+def test_b64_malformed_framing_raises():
+    from federatedscope_amd.core.compression.b64wire import (FramingError,
+                                                             parse_b64)
+    good = _b64(torch.randn(100))
+    raw = bytearray(base64.b64decode(good))
+    magic = raw.index(b'\x8a\x0al\xfc\x9cF\xf9 j\xa8P\x19')
+    bad_magic = bytearray(raw)
+    bad_magic[magic + 3] ^= 1
+
+    class Evil:
+        def __reduce__(self):
+            return (os.system, ('true', ))
+
+    bad = [good[:-4], good[:100], good + 'AAAA', 'hello', '',
+           good[:40] + '!' + good[41:],                  # char in framing
+           base64.b64encode(bytes(bad_magic)).decode(),
+           base64.b64encode(bytes(raw[:-1])).decode(),   # no STOP
+           base64.b64encode(bytes(raw) + b'.').decode(),  # trailing bytes
+           _b64({'a': torch.randn(2)}), _b64([1, 2]), _b64(3),
+           _b64(Evil()), _b64(torch.randn(3), 2)]        # protocol 2 bytes
+    for b in bad:
+        with pytest.raises(FramingError):
+            parse_b64(b)
+
+
+def test_b64_framing_cache_is_by_content():
+    from federatedscope_amd.core.compression.b64wire import parse_b64
+    a = torch.randn(50000)
+    ta, tb = _b64(a), _b64(a[1:])
+    fa = parse_b64(ta)
+    assert parse_b64(ta).data_pos == fa.data_pos
+    fb = parse_b64(tb)
+    assert fb.shape == (49999, ) and fb.storage_offset == 1
+    assert fa.shape == (50000, ) and fa.storage_offset == 0

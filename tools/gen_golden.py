@@ -85,6 +85,8 @@ class DictModel(torch.nn.Module):
 
 
 def to_np(t):
+    if isinstance(t, str):   # a gRPC upload value: base64 text, as bytes
+        return np.frombuffer(t.encode('ascii'), dtype=np.uint8), 'b64'
     t = t.detach().cpu()
     if t.dtype == torch.bfloat16:
         return t.view(torch.int16).numpy().view(np.uint16), 'bfloat16'
