@@ -307,6 +307,84 @@ class _PeerPlan:
         self.pp.close()
 
 
+def pmc_child(args):
+    """The traffic leg's profiled program: the C3 reduction a few times
+    (its launches are what rocprofv3 --pmc counts)."""
+    import torch
+    from federatedscope_amd import ops
+    from federatedscope_amd.core.aggregators._engine import fedavg_weights
+    dev = torch.device('cuda', 0)
+    n, P = args.clients, args.params
+    slab = torch.empty((n, ops.round_up(P, 64)), dtype=torch.float32,
+                       device=dev)
+    ops.fill_uniform(slab, P, seed=SEED)
+    rows = ops.RowTable.from_slab(slab, numel=P)
+    w = torch.tensor(fedavg_weights(sample_sizes(n)), dtype=torch.float32,
+                     device=dev)
+    out = torch.empty(ops.round_up(P, 64), dtype=torch.float32, device=dev)
+    for _ in range(4):
+        ops.weighted_sum(rows, w, out)
+    torch.cuda.synchronize()
+
+
+def live_traffic(args, kernel='wsum_f32_vec_kernel'):
+    """roofline.traffic measured in THIS run: two rocprofv3 --pmc passes,
+    FETCH_SIZE and WRITE_SIZE in separate runs (one TCC counter group
+    each), over a child ``bench.py --pmc-child`` started before this
+    process touches the GPU.  HBM bytes per launch with the gfx950
+    correction of /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE
+    counts half the bytes of 16-B-per-lane streaming reads (x2), WRITE_SIZE
+    is exact; both in KiB.  Returns (bytes, note)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which('rocprofv3')
+    if prof is None:
+        return None, 'rocprofv3 not on PATH'
+    tmp = tempfile.mkdtemp(prefix='fsagg_pmc_', dir='/tmp')
+    env = dict(os.environ, TMPDIR='/tmp')
+    kib = {}
+    try:
+        for ctr in ('FETCH_SIZE', 'WRITE_SIZE'):
+            d = os.path.join(tmp, ctr)
+            cmd = ['timeout', '-k', '10', '-s', 'KILL', '150', prof,
+                   '--pmc', ctr, '--output-format', 'csv', '-d', d, '-o',
+                   'run', '--', sys.executable, os.path.abspath(__file__),
+                   '--pmc-child', '--clients', str(args.clients),
+                   '--params', str(args.params)]
+            r = subprocess.run(cmd, cwd='/tmp', env=env,
+                               stdout=subprocess.DEVNULL,
+                               stderr=subprocess.PIPE, timeout=200)
+            if r.returncode != 0:
+                return None, '%s pass exited %d: %s' % (
+                    ctr, r.returncode, r.stderr.decode(
+                        'utf-8', 'replace')[-300:])
+            vals = []
+            for path in glob.glob(os.path.join(d, '**',
+                                               '*counter_collection.csv'),
+                                  recursive=True):
+                with open(path) as f:
+                    for row in csv.DictReader(f):
+                        if kernel in row.get('Kernel_Name', '') and \
+                                row.get('Counter_Name') == ctr:
+                            vals.append(float(row['Counter_Value']))
+            if not vals:
+                return None, 'no %s rows for %s' % (ctr, kernel)
+            kib[ctr] = sum(vals) / len(vals)
+    except (OSError, subprocess.SubprocessError) as e:
+        return None, '%s: %s' % (type(e).__name__, e)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    read_b = kib['FETCH_SIZE'] * 1024 * 2
+    write_b = kib['WRITE_SIZE'] * 1024
+    return read_b + write_b, (
+        'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) of %s in '
+        'this run: read %.4g B (FETCH_SIZE x2, gfx950 half count of 16-B '
+        'reads) + write %.4g B per launch' % (kernel, read_b, write_b))
+
+
 def default_split(world):
     """Rounds' relative sizes of the strong-scaling pipeline (None: equal
     rounds).  DESIGN §7."""
@@ -371,11 +449,27 @@ def main():
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
                     help='process-group backend (gloo: multi-process tests '
                          'on one GPU)')
-    ap.add_argument('--traffic', default=os.path.join(
-        ROOT, 'profiles', 'traffic_fedavg_c3.json'))
+    ap.add_argument('--no-pmc', action='store_true',
+                    help='skip the live PMC traffic passes (roofline.traffic '
+                         'null)')
+    ap.add_argument('--pmc-child', action='store_true',
+                    help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     import torch
+    if args.pmc_child:
+        return pmc_child(args)
+    # before this process touches the GPU: the profiled children must not
+    # be started from a GPU-initialised process
+    traffic, traffic_note = None, 'not measured (N > 1: per-rank pieces)'
+    single = args.gpus == 1 and int(os.environ.get('WORLD_SIZE', '1')) == 1
+    if single and args.no_pmc:
+        traffic_note = 'skipped (--no-pmc)'
+    elif single:
+        log('roofline.traffic: two rocprofv3 --pmc passes (FETCH_SIZE, '
+            'WRITE_SIZE) of the C3 kernel ...')
+        traffic, traffic_note = live_traffic(args)
+        log('traffic: %s (%s)' % (traffic, traffic_note))
     from federatedscope_amd import ops
     from federatedscope_amd.core.aggregators._engine import fedavg_weights
     from federatedscope_amd.core.sharding import PipelinedAssembly
@@ -508,16 +602,6 @@ def main():
         (t_step * 1e3, kern_ms, t_sharded * 1e3, mean_launch_ms, achieved,
          ok))
 
-    traffic = None
-    if world == 1 and os.path.exists(args.traffic):
-        try:
-            with open(args.traffic) as f:
-                tr = json.load(f)
-            if tr.get('clients') == n and tr.get('params') == P:
-                traffic = tr.get('hbm_bytes_per_launch')
-        except (OSError, ValueError):
-            traffic = None
-
     plugin = None
     if world == 1 and not args.no_plugin:
         plugin = plugin_surface_leg(args, dev, pieces[0][0], pieces[0][1],
@@ -604,6 +688,9 @@ def main():
                 'unit': 'GB/s',
                 'frac': round(achieved / HBM_PEAK_GBS, 4),
                 'traffic': traffic,
+                'traffic_over_algorithmic': round(traffic / algo_launch, 5)
+                if traffic and world == 1 else None,
+                'traffic_source': traffic_note,
             },
             'cpu_baseline': cpu,
             'per_rank_kernel_ms': round(kern_ms, 4),

@@ -33,6 +33,9 @@
 #include <thread>
 #include <vector>
 
+// host/b64frame.cpp: the framing walk of one gRPC tensor upload
+PyObject *b64_frame(PyObject *, PyObject *args);
+
 namespace {
 
 PyObject *key_table(PyObject *, PyObject *args) {
@@ -198,6 +201,9 @@ PyObject *text_copy(PyObject *, PyObject *args) {
 PyMethodDef kMethods[] = {
     {"device_tensor", device_tensor, METH_VARARGS,
      "device_tensor(ptr, numel, kind, device_index) -> Tensor (no ownership)"},
+    {"b64_frame", b64_frame, METH_VARARGS,
+     "b64_frame(text) -> (storage_class, shape, stride, storage_offset, "
+     "storage_numel, data_pos, requires_grad, nchars)"},
     {"text_copy", text_copy, METH_VARARGS,
      "text_copy(text, lo, hi, dst_addr[, threads]): copy chars [lo, hi)"},
     {"key_table", key_table, METH_VARARGS,

@@ -386,3 +386,45 @@ def test_b64_framing_cache_is_by_content():
     fb = parse_b64(tb)
     assert fb.shape == (49999, ) and fb.storage_offset == 1
     assert fa.shape == (50000, ) and fa.storage_offset == 0
+
+
+def test_b64_native_walk_matches_python_walk():
+    """_fsagg_host.b64_frame (csrc/host/b64frame.cpp) and the Python walker
+    agree field for field on every variant, and both refuse the malformed
+    uploads."""
+    from federatedscope_amd.core.compression import b64wire as B
+    if B._text_ext() is None:
+        pytest.skip('_fsagg_host.so not built')
+    variants = [torch.arange(10, dtype=torch.float32), torch.randn(3, 5),
+                torch.randn(0), torch.tensor(3.5), torch.tensor(7),
+                torch.randn(4, 6).t(), torch.randn(10)[3:7],
+                torch.randn(5, dtype=torch.float64), torch.randn(6).half(),
+                torch.randn(6).bfloat16(), torch.randn(3, requires_grad=True),
+                torch.nn.Parameter(torch.randn(2, 2)), torch.zeros(2, 0, 3),
+                torch.tensor([True, False]), torch.randn(70000)]
+    fields = ('dtype', 'shape', 'stride', 'storage_offset', 'storage_numel',
+              'data_pos', 'requires_grad', 'nchars')
+    for t in variants:
+        for proto in (3, 4, 5):
+            txt = _b64(t, proto)
+            a, b = B.parse_b64(txt), B.parse_b64_py(txt)
+            for f in fields:
+                assert getattr(a, f) == getattr(b, f), (f, proto, t.shape)
+    good = _b64(torch.randn(100))
+
+    class Evil:
+        def __reduce__(self):
+            return (os.system, ('true', ))
+
+    raw = base64.b64decode(good)
+    bad = [good[:-4], good[:100], good + 'AAAA', 'hello', '',
+           good[:40] + '!' + good[41:],
+           base64.b64encode(raw[:-1]).decode(),
+           base64.b64encode(raw + b'.').decode(),
+           _b64({'a': torch.randn(2)}), _b64([1, 2]), _b64(3),
+           _b64(Evil()), _b64(torch.randn(3), 2), 'é' * 8]
+    for x in bad:
+        with pytest.raises(B.FramingError):
+            B.parse_b64(x)
+        with pytest.raises(B.FramingError):
+            B.parse_b64_py(x)
