@@ -112,6 +112,9 @@ SIGNATURES['fsagg_coord_median_rows_f32'] = (
 SIGNATURES['fsagg_trimmed_mean_rows_f32'] = (
     _c_i, [_rows_p, _c_p, _c_i, _c_i64, _c_i, _c_f, _c_p, _c_i64, _c_p,
            _c_p])
+SIGNATURES['fsagg_pairgram_workspace_bytes'] = (_c_sz, [_c_i, _c_i64, _c_i])
+SIGNATURES['fsagg_pairgram_rows_segsq_f32'] = (
+    _c_i, [_c_p, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_sz, _c_p])
 SIGNATURES['fsagg_pairdist_rows_segsq_f32'] = (
     _c_i, [_rows_p, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_sz, _c_p])
 
@@ -122,6 +125,7 @@ SIGNATURES['fsagg_rows_sqnorm_f32'] = (
     _c_i, [_rows_p, _c_p, _c_i, _c_p, _c_p, _c_sz, _c_p])
 
 FSAGG_MAX_PEERS = 8
+FSAGG_PAIRGRAM_MAX_CLIENTS = 64
 _c_u32 = ctypes.c_uint32
 SIGNATURES['fsagg_peer_handle_bytes'] = (_c_sz, [])
 SIGNATURES['fsagg_peer_alloc'] = (_c_i, [_c_i, _c_sz, ctypes.POINTER(_c_p)])

@@ -164,9 +164,54 @@ class DeviceEngine:
         return acc
 
     def _pairdist(self, st):
-        """Krum's distance matrix D (fp32 [n][n], device) of a client set."""
-        segsq = self._sum_pieces(
-            st, lambda rs, lo, hi: ops.pairdist_rows_segsq(rs, lo, hi))
+        """Krum's distance matrix D (fp32 [n][n], device) of a client set:
+        per-key squared distances on the matrix cores for up to 64 clients
+        (fsagg_pairgram_rows_segsq_f32), recomputed by the VALU kernel when
+        the Gram form flags a pair it cannot resolve to the VALU kernel's
+        accuracy (near-duplicate clients far from every other), and always
+        on the VALU kernel above 64 clients."""
+        from ... import _lib
+        segsq = None
+        big = [k for k in st.layout.keys
+               if st.layout.numels[k] >= _GRAM_MIN_KEY]
+        if 2 <= st.n <= _lib.FSAGG_PAIRGRAM_MAX_CLIENTS and big:
+            # keys of >= _GRAM_MIN_KEY elements on the matrix cores; the
+            # small ones (biases, norms), where single pairs can sit much
+            # closer together than to any centre, on the VALU kernel
+            import numpy as np
+            ill = torch.zeros((st.n, st.n), dtype=torch.int32,
+                              device=self.compute_device)
+            segsq = self._sum_pieces(
+                st, lambda rs, lo, hi: ops.pairgram_rows_segsq(
+                    rs, ill, lo, hi, keep=_gram_key))
+            if st.plan is not None:
+                st.plan.comm.all_reduce_sum(ill)
+            flags = ill.cpu().numpy()
+            flags = (flags + flags.T) > 0
+            self.last_pairdist_path = 'mfma'
+            if flags.any():
+                # the flagged pairs (a cluster far from the centre) exactly:
+                # the VALU kernel over the clients involved
+                sel = sorted(set(np.nonzero(flags)[0].tolist()))
+                big_total = sum(st.layout.numels[k] for k in big)
+                exact = self._sum_pieces(
+                    st.subset(sel), lambda rs, lo, hi: ops.pairdist_rows_segsq(
+                        rs, lo, hi, keep=_gram_key, extent=big_total))
+                idx = torch.tensor(sel, device=segsq.device)
+                segsq[:, idx[:, None], idx[None, :]] = exact
+                self.last_pairdist_path = 'mfma + exact %d of %d clients' % (
+                    len(sel), st.n)
+            if len(big) < len(st.layout.keys):
+                small = sum(st.layout.numels[k] for k in st.layout.keys
+                            if _valu_key(st.layout.numels[k]))
+                segsq.add_(self._sum_pieces(
+                    st, lambda rs, lo, hi: ops.pairdist_rows_segsq(
+                        rs, lo, hi, keep=_valu_key, extent=small)))
+        else:
+            self.last_pairdist_path = 'valu'
+        if segsq is None:
+            segsq = self._sum_pieces(
+                st, lambda rs, lo, hi: ops.pairdist_rows_segsq(rs, lo, hi))
         return ops.pairdist_finish(segsq)
 
     def _sqnorms(self, st):
@@ -438,6 +483,18 @@ def _host_ext():
         except (_lib.FsaggError, ImportError, OSError):
             _HOST.append(None)
     return _HOST[0]
+
+
+# keys of at least this many elements take the matrix-core Krum distances
+_GRAM_MIN_KEY = 4096
+
+
+def _gram_key(numel):
+    return numel >= _GRAM_MIN_KEY
+
+
+def _valu_key(numel):
+    return numel < _GRAM_MIN_KEY
 
 
 class _NoRows:

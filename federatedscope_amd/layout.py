@@ -111,19 +111,21 @@ class BucketLayout:
                          len(arr))
         return cache[ck]
 
-    def seg_bounds(self, device, lo=0, hi=None):
+    def seg_bounds(self, device, lo=0, hi=None, keep=None):
         """Device int64 arrays (seg_lo, seg_end) of each fp32 key's exact
         coordinates clipped to [lo, hi) (empty segments where a key lies
-        outside), cached per range and device."""
+        outside, or where ``keep`` — a predicate on the key's element count
+        — is false), cached per range, predicate and device."""
         hi = self.numel if hi is None else hi
         device = torch.device(device)
         cache = self.__dict__.setdefault('_seg_bounds', {})
-        ck = (int(lo), int(hi), str(device))
+        ck = (int(lo), int(hi), str(device), keep)
         if ck not in cache:
             from .ops import _h2d
             a = [min(max(self.offsets[k], lo), hi) for k in self.keys]
             b = [min(max(self.offsets[k] + self.numels[k], lo), hi)
-                 for k in self.keys]
+                 if keep is None or keep(self.numels[k]) else
+                 min(max(self.offsets[k], lo), hi) for k in self.keys]
             cache[ck] = (_h2d(a, torch.int64, device),
                          _h2d(b, torch.int64, device))
         return cache[ck]

@@ -950,18 +950,22 @@ def trimmed_mean_rows(rs, k, out, divisor=None, base=None, lo=0, hi=None):
     return out
 
 
-def pairdist_rows_segsq(rs, lo=0, hi=None, workspace=None):
+def pairdist_rows_segsq(rs, lo=0, hi=None, workspace=None, keep=None,
+                        extent=None):
     """Per-key squared pair distances [nseg][n][n] (fp64) over the keys'
     coordinates in [lo, hi) (a rank's range: summed across ranks by the
-    caller, then :func:`pairdist_finish`)."""
+    caller, then :func:`pairdist_finish`); ``keep``: a predicate on a key's
+    element count — the other keys' entries are 0."""
     _require_all(rs, 'Krum')
     if rs.n < 2:
         raise ValueError('Krum needs at least two clients')
     lay = rs.layout
     hi = lay.numel if hi is None else hi
-    seg_lo, seg_end = lay.seg_bounds(rs.device, lo, hi)
+    seg_lo, seg_end = lay.seg_bounds(rs.device, lo, hi, keep)
     lib = L.load()
-    extent = max(hi - lo, 1)       # plans ~1000 chunks over the range
+    # plans ~1000 chunks over the range (``extent``: the coordinates the
+    # kept keys actually hold, when only some are)
+    extent = max(hi - lo if extent is None else int(extent), 1)
     need = lib.fsagg_pairdist_workspace_bytes(rs.n, extent, rs.nseg)
     ws = (workspace or _WS).get(rs.device, need)
     sq = torch.empty((rs.nseg, rs.n, rs.n), dtype=torch.float64,
@@ -970,6 +974,36 @@ def pairdist_rows_segsq(rs, lo=0, hi=None, workspace=None):
         rs.ptr(), seg_lo.data_ptr(), seg_end.data_ptr(), extent,
         sq.data_ptr(), ws.data_ptr(), ws.numel(), _stream(rs.device)),
         'fsagg_pairdist_rows_segsq_f32')
+    return sq
+
+
+def pairgram_rows_segsq(rs, ill, lo=0, hi=None, workspace=None, keep=None):
+    """As :func:`pairdist_rows_segsq`, on the matrix cores (n <= 64,
+    fsagg_pairgram_rows_segsq_f32): sets ``ill[a][b]`` (device int32
+    [n][n], zeroed by the caller) for the pairs the Gram form cannot
+    resolve to the VALU kernel's accuracy — the caller recomputes those
+    with :func:`pairdist_rows_segsq`."""
+    _require_all(rs, 'Krum')
+    if not 2 <= rs.n <= L.FSAGG_PAIRGRAM_MAX_CLIENTS:
+        raise ValueError('the Gram path takes 2..%d clients' %
+                         L.FSAGG_PAIRGRAM_MAX_CLIENTS)
+    if ill.dtype != torch.int32 or ill.device != rs.device or \
+            tuple(ill.shape) != (rs.n, rs.n) or not ill.is_contiguous():
+        raise ValueError('ill must be a contiguous int32 [n][n] device '
+                         'tensor')
+    lay = rs.layout
+    hi = lay.numel if hi is None else hi
+    seg_lo, seg_end = lay.seg_bounds(rs.device, lo, hi, keep)
+    lib = L.load()
+    extent = max(hi - lo, 1)
+    need = lib.fsagg_pairgram_workspace_bytes(rs.n, extent, rs.nseg)
+    ws = (workspace or _WS).get(rs.device, need)
+    sq = torch.empty((rs.nseg, rs.n, rs.n), dtype=torch.float64,
+                     device=rs.device)
+    L.check(lib.fsagg_pairgram_rows_segsq_f32(
+        rs.ptr(), seg_lo.data_ptr(), seg_end.data_ptr(), extent,
+        sq.data_ptr(), ill.data_ptr(), ws.data_ptr(), ws.numel(),
+        _stream(rs.device)), 'fsagg_pairgram_rows_segsq_f32')
     return sq
 
 

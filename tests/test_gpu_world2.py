@@ -62,8 +62,10 @@ def test_bench_strong_scaling_world2():
     assert r['config']['params'] == 1000003
 
 
-@pytest.mark.parametrize('world', [2, 4])
-def test_bench_peer_assembly(world):
+@pytest.mark.parametrize('world,clients,params', [
+    (2, 100, 25_000_000),       # configs[2] itself: 5 GB per rank
+    (4, 10, 1_000_003)])
+def test_bench_peer_assembly(world, clients, params):
     """bench.py's peer assembly (core/sharding.PeerAssembly): each rank's
     kernel stores its piece into every rank's uncached output buffer through
     IPC-imported pointers, then the flag barrier — here 2 / 4 processes on
@@ -71,8 +73,8 @@ def test_bench_peer_assembly(world):
     Every rank's assembled result must be bit-exact, and the barrier must
     not have timed out (bench.py calls PeerAssembly.check())."""
     recs = _run2(['bench.py', '--gpus', str(world), '--backend', 'gloo',
-                  '--assembly', 'p2p', '--clients', '10', '--params',
-                  '1000003', '--steps', '5', '--warmup', '2',
+                  '--assembly', 'p2p', '--clients', str(clients),
+                  '--params', str(params), '--steps', '5', '--warmup', '2',
                   '--no-cpu-baseline', '--no-weak'], nproc=world)
     assert len(recs) == 1
     r = recs[0]

@@ -112,9 +112,81 @@ def krum_c4(dev, n=50, f=10):
     margin = float((srt[1] - srt[0]) / srt[0])
     sel_gpu = torch.sort(s_gpu)[1][:5].tolist()
     sel_ref = torch.sort(s_ref)[1][:5].tolist()
+    # the matrix-core path the aggregators take for n <= 64 (big keys on
+    # fsagg_pairgram_rows_segsq_f32, small keys on the VALU kernel)
+    import numpy as np
+    from federatedscope_amd.core.aggregators._engine import (_gram_key,
+                                                             _valu_key)
+    rs = ops.RowSet(lay, np.array([[slab[i].data_ptr()] for i in range(n)],
+                                  dtype=np.int64), dev, keepalive=(slab, ))
+    ill = torch.zeros((n, n), dtype=torch.int32, device=dev)
+    small = sum(lay.numels[k] for k in lay.keys if _valu_key(lay.numels[k]))
+
+    def gram_D():
+        sq = ops.pairgram_rows_segsq(rs, ill, keep=_gram_key)
+        sq.add_(ops.pairdist_rows_segsq(rs, keep=_valu_key, extent=small))
+        return ops.pairdist_finish(sq)
+
+    Dg = gram_D().cpu()
+    # per key: the Gram path's worst relative distance error and the
+    # conditioning (Σ|x'|² / d², centred on the medoid) of that pair
+    sqg = ops.pairgram_rows_segsq(rs, torch.zeros_like(ill),
+                                  keep=_gram_key).cpu().numpy()
+    medoid = int(ref.clone().fill_diagonal_(0).sum(1).argmin())
+    per_key = []
+    for s_, k in enumerate(lay.keys):
+        if not _gram_key(lay.numels[k]):
+            continue
+        o, m = lay.offsets[k], lay.numels[k]
+        X = slab[:, o:o + m].double()
+        Y = X - X[medoid]
+        mag = (Y * Y).sum(1).cpu().numpy()
+        sq = torch.zeros((n, n), dtype=torch.float64, device=dev)
+        for a in range(n):
+            sq[a] = ((X - X[a]) ** 2).sum(1)
+        sq = sq.cpu().numpy()
+        offd = ~np.eye(n, dtype=bool)
+        err = np.abs(np.sqrt(sqg[s_]) - np.sqrt(sq))[offd] / \
+            np.sqrt(sq)[offd]
+        F = ((mag[:, None] + mag[None, :]) / np.where(sq > 0, sq, np.inf))[
+            offd]
+        i = int(err.argmax())
+        per_key.append({'key': k, 'len': m, 'max_rel_err': float(err[i]),
+                        'F_at_max': float(F[i]), 'F_max': float(F.max()),
+                        'err_over_F_max': float((err / F).max())})
+    gmed, gmn = timed(gram_D)
+    grel = ((Dg.double() - ref).abs() / ref)[off].max().item()
+    sel_gram = torch.sort(krum_scores(Dg, f))[1][:5].tolist()
+    # the drop-in: KrumAggregator's distance matrix on device dicts (views
+    # of the slab rows, read in place), D back on the host
+    from types import SimpleNamespace
+    from federatedscope_amd.core.aggregators import KrumAggregator
+    cfg = SimpleNamespace(
+        federate=SimpleNamespace(ignore_weight=False, use_ss=False,
+                                 client_num=1000, sample_client_rate=1.0),
+        aggregator=SimpleNamespace(byzantine_node_num=f,
+                                   BFT_args=SimpleNamespace(krum_agg_num=1)))
+    agg = KrumAggregator(device=dev, config=cfg)
+    models = [(1, {k: slab[i, lay.offsets[k]:lay.offsets[k] +
+                            lay.numels[k]].view(lay.shapes[k])
+                   for k in lay.keys}) for i in range(n)]
+    De, _ = agg.distance_matrix(models)
+    emed, emn = timed(lambda: agg.distance_matrix(models))
+    erel = ((De.double() - ref).abs() / ref)[off].max().item()
+    sel_eng = torch.sort(krum_scores(De, f))[1][:5].tolist()
     nbytes = 4.0 * n * P
     flops = 1.5 * n * (n - 1) * P
     return {
+        'engine_ms_median': emed, 'engine_ms_min': emn,
+        'engine_path': agg.last_pairdist_path,
+        'engine_max_rel_err_vs_fp64': erel,
+        'engine_selection_exact': sel_eng == sel_ref,
+        'gram_ms_median': gmed, 'gram_ms_min': gmn,
+        'gram_GBps': nbytes / gmed / 1e6,
+        'gram_max_rel_err_vs_fp64': grel,
+        'gram_flagged_pairs': int((ill > 0).sum().item()),
+        'gram_per_key': per_key,
+        'gram_selection_exact': sel_gram == sel_ref,
         'kernel': 'fsagg_pairdist_f32', 'config': 'C4 Krum n=%d P=%d f=%d' %
         (n, P, f), 'ms_median': med, 'ms_min': mn,
         'GBps': nbytes / med / 1e6, 'hbm_frac': nbytes / med / 1e6 / PEAK,
