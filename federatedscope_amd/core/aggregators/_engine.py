@@ -164,55 +164,24 @@ class DeviceEngine:
         return acc
 
     def _pairdist(self, st):
-        """Krum's distance matrix D (fp32 [n][n], device) of a client set:
-        per-key squared distances on the matrix cores for up to 64 clients
-        (fsagg_pairgram_rows_segsq_f32), recomputed by the VALU kernel when
-        the Gram form flags a pair it cannot resolve to the VALU kernel's
-        accuracy (near-duplicate clients far from every other), and always
-        on the VALU kernel above 64 clients."""
+        """Krum's distance matrix D (fp32 [n][n]) of a client set, as a
+        pending result whose ``.cpu()`` waits for it: for up to 64 clients
+        on the matrix cores (fsagg_pairgram_rows_segsq_f32 +
+        fsagg_pairgram_finish_f32, one copy of D and the flags back); the
+        pairs the Gram form cannot resolve to _GRAM_TOL of their distance
+        (near-duplicate clients far from every other, non-finite values)
+        are recomputed on the VALU kernel over the clients involved.  Above
+        64 clients: the VALU kernel."""
         from ... import _lib
-        segsq = None
-        big = [k for k in st.layout.keys
-               if st.layout.numels[k] >= _GRAM_MIN_KEY]
-        if 2 <= st.n <= _lib.FSAGG_PAIRGRAM_MAX_CLIENTS and big:
-            # keys of >= _GRAM_MIN_KEY elements on the matrix cores; the
-            # small ones (biases, norms), where single pairs can sit much
-            # closer together than to any centre, on the VALU kernel
-            import numpy as np
-            ill = torch.zeros((st.n, st.n), dtype=torch.int32,
-                              device=self.compute_device)
-            segsq = self._sum_pieces(
-                st, lambda rs, lo, hi: ops.pairgram_rows_segsq(
-                    rs, ill, lo, hi, keep=_gram_key))
-            if st.plan is not None:
-                st.plan.comm.all_reduce_sum(ill)
-            flags = ill.cpu().numpy()
-            flags = (flags + flags.T) > 0
-            self.last_pairdist_path = 'mfma'
-            if flags.any():
-                # the flagged pairs (a cluster far from the centre) exactly:
-                # the VALU kernel over the clients involved
-                sel = sorted(set(np.nonzero(flags)[0].tolist()))
-                big_total = sum(st.layout.numels[k] for k in big)
-                exact = self._sum_pieces(
-                    st.subset(sel), lambda rs, lo, hi: ops.pairdist_rows_segsq(
-                        rs, lo, hi, keep=_gram_key, extent=big_total))
-                idx = torch.tensor(sel, device=segsq.device)
-                segsq[:, idx[:, None], idx[None, :]] = exact
-                self.last_pairdist_path = 'mfma + exact %d of %d clients' % (
-                    len(sel), st.n)
-            if len(big) < len(st.layout.keys):
-                small = sum(st.layout.numels[k] for k in st.layout.keys
-                            if _valu_key(st.layout.numels[k]))
-                segsq.add_(self._sum_pieces(
-                    st, lambda rs, lo, hi: ops.pairdist_rows_segsq(
-                        rs, lo, hi, keep=_valu_key, extent=small)))
-        else:
-            self.last_pairdist_path = 'valu'
-        if segsq is None:
-            segsq = self._sum_pieces(
-                st, lambda rs, lo, hi: ops.pairdist_rows_segsq(rs, lo, hi))
-        return ops.pairdist_finish(segsq)
+        if 2 <= st.n <= _lib.FSAGG_PAIRGRAM_MAX_CLIENTS:
+            sq2 = self._sum_pieces(
+                st, lambda rs, lo, hi: ops.pairgram_rows_segsq(rs, lo, hi))
+            buf, _, _ = ops.pairgram_finish(sq2, _GRAM_TOL)
+            return _PendingD(self, st, buf=buf)
+        self.last_pairdist_path = 'valu'
+        segsq = self._sum_pieces(
+            st, lambda rs, lo, hi: ops.pairdist_rows_segsq(rs, lo, hi))
+        return _PendingD(self, st, D=ops.pairdist_finish(segsq))
 
     def _sqnorms(self, st):
         """[n][nseg] fp64 per-client, per-key squared norms."""
@@ -486,15 +455,44 @@ def _host_ext():
 
 
 # keys of at least this many elements take the matrix-core Krum distances
-_GRAM_MIN_KEY = 4096
+# relative bound on a Krum distance's error from the Gram form above which
+# the pair is recomputed on the VALU kernel (the bound is 2-5x
+# the measured error; the Gram path measures 2.3e-7 at C4, the VALU kernel
+# 1.6e-7)
+_GRAM_TOL = 1e-6
 
 
-def _gram_key(numel):
-    return numel >= _GRAM_MIN_KEY
+class _PendingD:
+    """Krum's distance matrix while its kernels run (``_pairdist``):
+    ``cpu()`` copies D (and the Gram path's flags) to the host, recomputes
+    the flagged pairs exactly and returns the host fp32 [n][n] matrix."""
 
+    def __init__(self, eng, st, buf=None, D=None):
+        self._eng, self._st, self._buf, self._D = eng, st, buf, D
 
-def _valu_key(numel):
-    return numel < _GRAM_MIN_KEY
+    def cpu(self):
+        if self._D is not None:
+            return self._D.cpu()
+        import numpy as np
+        eng, st = self._eng, self._st
+        host = self._buf.cpu()
+        D = host[0].view(torch.float32).clone()
+        flags = host[1].numpy()
+        flags = (flags + flags.T) > 0
+        eng.last_pairdist_path = 'mfma'
+        if flags.any():
+            # the flagged pairs exactly: the VALU kernel over the clients
+            # involved (every pair among them)
+            sel = sorted(set(np.nonzero(flags)[0].tolist()))
+            exact = eng._sum_pieces(
+                st.subset(sel), lambda rs, lo, hi: ops.pairdist_rows_segsq(
+                    rs, lo, hi))
+            sub = ops.pairdist_finish(exact).cpu()
+            idx = torch.tensor(sel)
+            D[idx[:, None], idx[None, :]] = sub
+            eng.last_pairdist_path = 'mfma + exact %d of %d clients' % (
+                len(sel), st.n)
+        return D
 
 
 class _NoRows:

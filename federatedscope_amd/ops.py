@@ -977,20 +977,16 @@ def pairdist_rows_segsq(rs, lo=0, hi=None, workspace=None, keep=None,
     return sq
 
 
-def pairgram_rows_segsq(rs, ill, lo=0, hi=None, workspace=None, keep=None):
+def pairgram_rows_segsq(rs, lo=0, hi=None, workspace=None, keep=None):
     """As :func:`pairdist_rows_segsq`, on the matrix cores (n <= 64,
-    fsagg_pairgram_rows_segsq_f32): sets ``ill[a][b]`` (device int32
-    [n][n], zeroed by the caller) for the pairs the Gram form cannot
-    resolve to the VALU kernel's accuracy — the caller recomputes those
-    with :func:`pairdist_rows_segsq`."""
+    fsagg_pairgram_rows_segsq_f32): returns ``[2][nseg][n][n]`` fp64 —
+    [0] the per-key squared distances, [1] their predicted absolute error
+    bounds (both may be summed over ranks); :func:`pairgram_finish` turns
+    them into D and the pairs to recompute."""
     _require_all(rs, 'Krum')
     if not 2 <= rs.n <= L.FSAGG_PAIRGRAM_MAX_CLIENTS:
         raise ValueError('the Gram path takes 2..%d clients' %
                          L.FSAGG_PAIRGRAM_MAX_CLIENTS)
-    if ill.dtype != torch.int32 or ill.device != rs.device or \
-            tuple(ill.shape) != (rs.n, rs.n) or not ill.is_contiguous():
-        raise ValueError('ill must be a contiguous int32 [n][n] device '
-                         'tensor')
     lay = rs.layout
     hi = lay.numel if hi is None else hi
     seg_lo, seg_end = lay.seg_bounds(rs.device, lo, hi, keep)
@@ -998,13 +994,32 @@ def pairgram_rows_segsq(rs, ill, lo=0, hi=None, workspace=None, keep=None):
     extent = max(hi - lo, 1)
     need = lib.fsagg_pairgram_workspace_bytes(rs.n, extent, rs.nseg)
     ws = (workspace or _WS).get(rs.device, need)
-    sq = torch.empty((rs.nseg, rs.n, rs.n), dtype=torch.float64,
-                     device=rs.device)
+    out = torch.empty((2, rs.nseg, rs.n, rs.n), dtype=torch.float64,
+                      device=rs.device)
     L.check(lib.fsagg_pairgram_rows_segsq_f32(
         rs.ptr(), seg_lo.data_ptr(), seg_end.data_ptr(), extent,
-        sq.data_ptr(), ill.data_ptr(), ws.data_ptr(), ws.numel(),
+        out[0].data_ptr(), out[1].data_ptr(), ws.data_ptr(), ws.numel(),
         _stream(rs.device)), 'fsagg_pairgram_rows_segsq_f32')
-    return sq
+    return out
+
+
+def pairgram_finish(sq2, tol):
+    """D (fp32 [n][n], device, as :func:`pairdist_finish`) and ill (int32
+    [n][n]: the pairs whose error bound exceeds ``tol``·D) from
+    :func:`pairgram_rows_segsq`'s output, both in one int32 [2][n][n]
+    device tensor (one copy to the host): returns (buf, D view, ill view)."""
+    if sq2.dim() != 4 or sq2.shape[0] != 2 or sq2.dtype != torch.float64 \
+            or not sq2.is_contiguous():
+        raise ValueError('sq2 must be a contiguous fp64 [2][nseg][n][n] '
+                         'tensor')
+    nseg, n = int(sq2.shape[1]), int(sq2.shape[2])
+    buf = torch.empty((2, n, n), dtype=torch.int32, device=sq2.device)
+    D = buf[0].view(torch.float32)
+    L.check(L.load().fsagg_pairgram_finish_f32(
+        sq2[0].data_ptr(), sq2[1].data_ptr(), n, nseg, float(tol),
+        buf[0].data_ptr(), buf[1].data_ptr(), _stream(sq2.device)),
+        'fsagg_pairgram_finish_f32')
+    return buf, D, buf[1]
 
 
 def pairdist_rows(rs, workspace=None):

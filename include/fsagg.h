@@ -451,27 +451,41 @@ int fsagg_pairdist_rows_segsq_f32(const fsagg_rows *rows,
                                   size_t workspace_bytes,
                                   fsagg_stream_t stream);
 
-/* Krum per-key squared distances on the matrix cores (n <= 64; output as
+/* Krum per-key squared distances on the matrix cores (n <= 64; segsq as
  * fsagg_pairdist_rows_segsq_f32).  d²(a, b) = G_aa + G_bb − 2·G_ab from a
  * Gram matrix of the rows centred on a central client (the argmin of the
- * summed distances over the first 4096 coordinates of every key), every
+ * summed distances over the first 2048 coordinates of every key), every
  * fp32 value split exactly into three bf16 limbs and the six limb products
  * of weight >= 2^-16 accumulated by v_mfma_f32_16x16x32_bf16, fp32 within
- * one k-step, fp64 beyond.  ill (device, n*n words the caller zeroes):
- * ill[a*n + b] = 1 for a pair whose predicted error, 1.8e-7 ·
- * (G'aa + G'bb) / d² · sqrt(32 / key length), exceeds 2e-7 in some key
- * (a cluster far from the centre) — the caller recomputes those pairs with
- * fsagg_pairdist_rows_segsq_f32 on the rows involved.  Replaces the same torch.dist loop
- * (krum_aggregator.py:41-73) as fsagg_pairdist_f32.  Workspace:
- * fsagg_pairgram_workspace_bytes(n, numel, nseg) (0 when n is outside
- * 2..64). */
+ * one k-step of 32 coordinates, fp64 beyond.  err[s][a][b] (fp64, same
+ * shape as segsq): the predicted bound of the part of d²'s error in key s
+ * that is random in sign, 5e-7 · (G'aa + G'bb) / sqrt(K) for a key of K
+ * k-steps (+inf where d² came out negative beyond it or is not finite); a
+ * further 2e-8 · d² is proportional to d² itself.  Sums of segsq and err
+ * over disjoint coordinate ranges (ranks) stay valid.  Replaces the same
+ * torch.dist loop (krum_aggregator.py:41-73) as fsagg_pairdist_f32, with
+ * fsagg_pairgram_finish_f32 in place of fsagg_pairdist_finish_f64.
+ * Workspace: fsagg_pairgram_workspace_bytes(n, numel, nseg) (0 when n is
+ * outside 2..64). */
 size_t fsagg_pairgram_workspace_bytes(int n, int64_t numel, int nseg);
 int fsagg_pairgram_rows_segsq_f32(const fsagg_rows *rows,
                                   const int64_t *seg_lo,
                                   const int64_t *seg_end, int64_t numel,
-                                  double *segsq, uint32_t *ill,
+                                  double *segsq, double *err,
                                   void *workspace, size_t workspace_bytes,
                                   fsagg_stream_t stream);
+
+/* Krum's n×n distance matrix from fsagg_pairgram_rows_segsq_f32's output:
+ * D[a][b] = Σ_s fl32(sqrt(segsq[s][a][b])) in key order (fp32, as
+ * fsagg_pairdist_finish_f64 and the reference's `distance +=
+ * torch.dist(...)`, krum_aggregator.py:45-56), D[a][a] = +inf, and
+ * ill[a*n + b] = 1 for a pair whose error bounds (the keys' random parts in
+ * quadrature plus the proportional part) could move D by more than tol·D,
+ * or whose D is not finite — the caller recomputes those pairs with
+ * fsagg_pairdist_rows_segsq_f32 on the clients involved. */
+int fsagg_pairgram_finish_f32(const double *segsq, const double *err, int n,
+                              int nseg, double tol, float *D, uint32_t *ill,
+                              fsagg_stream_t stream);
 
 /* Per-(client, key segment) squared L2 norms over a row set in fp64:
  * sq[i][s] = Σ_{p in s} x_i[p]^2 (0 for a NULL entry), summed in a fixed

@@ -1,19 +1,20 @@
-"""Krum distances on the matrix cores (fsagg_pairgram_rows_segsq_f32).
+"""Krum distances on the matrix cores (fsagg_pairgram_rows_segsq_f32 +
+fsagg_pairgram_finish_f32).
 
 The Gram form d² = G_aa + G_bb − 2·G_ab (centred on a central client, bf16
-limbs, fp32-within-4-k-steps / fp64 accumulation) against an fp64
-restatement of every per-key squared distance, and against the VALU
-kernel (pairdist.hip):
+limbs, fp32 within a k-step / fp64 beyond) against an fp64 restatement of
+every per-key squared distance, and against the VALU kernel (pairdist.hip):
 * n = 2 … 64 (1–4 MFMA tiles, ragged last tile), keys of 0, 1, 3, 5 … 300k
   elements (partial k-steps, chunk tails), keyed and stacked row sets;
 * rows that are not 16-B aligned (the per-element load path);
 * a common component 1000× the spread (cancellation without centring),
   with a far Byzantine client;
-* identical clients (d = 0 exactly, no flag) and near-duplicates far from
-  the others (their pair flagged; the engine recomputes the flagged
-  clients' pairs exactly on the VALU kernel).
-Tolerance: 2e-7 relative on each per-key distance (the VALU kernel's
-measured error is 1.6e-7 on C4)."""
+* identical and near-duplicate clients far from the others (their pair
+  flagged; the engine recomputes the flagged clients' pairs exactly on the
+  VALU kernel), and non-finite values (flagged, VALU semantics).
+Contract checked: every per-key |d²_got − d²_fp64| is within the kernel's
+own predicted bound (err + 2e-8·d²); unflagged Krum distances D are within
+_GRAM_TOL (1e-6) of fp64."""
 from collections import OrderedDict
 
 import numpy as np
@@ -63,25 +64,44 @@ def _fp64_segsq(clients, lay):
 
 
 def _gram(rs):
-    """The Gram path over the keys the engine gives it (>= 4096 elements);
-    returns (segsq, ill, mask of those keys)."""
+    """The Gram path over every key: (segsq, err, D, flags) on the host."""
     from federatedscope_amd import ops
-    from federatedscope_amd.core.aggregators._engine import _gram_key
-    ill = torch.zeros((rs.n, rs.n), dtype=torch.int32, device='cuda')
-    sq = ops.pairgram_rows_segsq(rs, ill, keep=_gram_key)
-    big = np.array([_gram_key(rs.layout.numels[k]) for k in rs.layout.keys])
-    got = sq.cpu().numpy()
-    assert np.all(got[~big] == 0.0)
+    from federatedscope_amd.core.aggregators._engine import _GRAM_TOL
+    sq2 = ops.pairgram_rows_segsq(rs)
+    _, D, ill = ops.pairgram_finish(sq2, _GRAM_TOL)
     flags = ill.cpu().numpy()
-    return got[big], (flags + flags.T) > 0, big
+    sq2 = sq2.cpu().numpy()
+    return sq2[0], sq2[1], D.cpu().numpy(), (flags + flags.T) > 0
 
 
-def _check(got, want, rtol=2e-7):
-    d_got, d_want = np.sqrt(got), np.sqrt(want)
-    pos = d_want > 0
-    assert np.all(d_got[~pos] == 0.0)
-    err = np.abs(d_got[pos] - d_want[pos]) / d_want[pos]
-    assert err.max() <= rtol, err.max()
+def _fp64_D(want):
+    """The reference's D (fp32 sum over keys of fp32 per-key distances),
+    from fp64 per-key squared distances."""
+    n = want.shape[1]
+    D = np.zeros((n, n), dtype=np.float32)
+    for s in range(want.shape[0]):
+        D = (D + np.sqrt(want[s]).astype(np.float32)).astype(np.float32)
+    np.fill_diagonal(D, np.inf)
+    return D
+
+
+# pairgram.hip kErrBias: the part of the error proportional to d²
+_BIAS = 2e-8
+
+
+def _check(got, err, D, flags, want, rtol=1e-6):
+    # the predicted bound holds on every key and pair
+    bound = err + _BIAS * want
+    assert np.all(np.abs(got - want) <= bound + 1e-300), \
+        np.max(np.abs(got - want) / (bound + 1e-300))
+    # identical d² = 0 rows stay 0
+    Dw = _fp64_D(want)
+    off = ~np.eye(D.shape[0], dtype=bool) & ~flags
+    pos = off & (Dw > 0)
+    assert np.all(D[off & (Dw == 0)] == 0.0)
+    if pos.any():
+        e = np.abs(D[pos].astype(np.float64) - Dw[pos]) / Dw[pos]
+        assert e.max() <= rtol, e.max()
 
 
 @pytest.mark.parametrize('n', [2, 5, 16, 17, 33, 50, 64])
@@ -91,11 +111,14 @@ def test_pairgram_vs_fp64_and_valu(n):
     lay, _, keyed, stacked = _sets(clients)
     want = _fp64_segsq(clients, lay)
     for rs in (keyed, stacked):
-        got, ill, big = _gram(rs)
-        assert not ill.any()
-        _check(got, want[big])
+        got, err, D, flags = _gram(rs)
+        assert flags.sum() <= 2, flags.sum()
+        _check(got, err, D, flags, want)
     valu = ops.pairdist_rows_segsq(keyed).cpu().numpy()
-    _check(valu, want)
+    d_got, d_want = np.sqrt(valu), np.sqrt(want)
+    pos = d_want > 0
+    assert np.all(d_got[~pos] == 0.0)
+    assert (np.abs(d_got[pos] - d_want[pos]) / d_want[pos]).max() <= 2e-7
 
 
 def test_pairgram_unaligned_rows():
@@ -113,9 +136,9 @@ def test_pairgram_unaligned_rows():
                     dtype=np.int64)
     rs = ops.RowSet.from_pointers(lay, ptrs, 'cuda', keepalive=clients,
                                   aligned16=False)
-    got, ill, big = _gram(rs)
-    assert not ill.any()
-    _check(got, _fp64_segsq(clients, lay)[big])
+    got, err, D, flags = _gram(rs)
+    assert not flags.any()
+    _check(got, err, D, flags, _fp64_segsq(clients, lay))
 
 
 def test_pairgram_common_component_and_byzantine():
@@ -132,77 +155,78 @@ def test_pairgram_common_component_and_byzantine():
 
     clients = _clients(n, sizes=[300_001, 4097, 9], seed=12, fn=fn)
     lay, _, keyed, _ = _sets(clients)
-    got, ill, big = _gram(keyed)
-    assert not ill.any()
-    _check(got, _fp64_segsq(clients, lay)[big], rtol=1e-6)
+    got, err, D, flags = _gram(keyed)
+    assert not flags.any()
+    _check(got, err, D, flags, _fp64_segsq(clients, lay))
 
 
-def test_pairgram_duplicates_and_fallback():
+def _krum(clients, f=2):
     from types import SimpleNamespace
     from federatedscope_amd.core.aggregators import KrumAggregator
-    n = 24
-
-    def dup(i, j, z):
-        # clients 3 and 4 identical, far from the rest
-        return torch.full_like(z, 50.0) if i in (3, 4) else z
-
-    clients = _clients(n, sizes=[10_000, 33], seed=5, fn=dup)
-    lay, _, keyed, _ = _sets(clients)
-    got, ill, big = _gram(keyed)
-    assert got[:, 3, 4].max() == 0.0 and not ill.any()
-    _check(got, _fp64_segsq(clients, lay)[big])
-
-    # near-duplicates far from the centre: flagged, and the engine
-    # recomputes with the VALU kernel
-    def near(i, j, z):
-        if i in (3, 4):
-            return 50.0 + 1e-6 * z
-        return z
-
-    clients = _clients(n, sizes=[10_000, 33], seed=6, fn=near)
-    lay, _, keyed, _ = _sets(clients)
-    _, ill, _ = _gram(keyed)
-    assert ill[3, 4] and ill.sum() <= 2 * (2 * n - 3)
     cfg = SimpleNamespace(
         federate=SimpleNamespace(ignore_weight=False, use_ss=False,
                                  client_num=1000, sample_client_rate=1.0),
         aggregator=SimpleNamespace(
-            byzantine_node_num=2,
+            byzantine_node_num=f,
             BFT_args=SimpleNamespace(krum_agg_num=1)))
+    return KrumAggregator(device='cuda', config=cfg)
 
-    class M(torch.nn.Module):
-        def state_dict(self, *a, **kw):
-            return OrderedDict((k, torch.zeros_like(v)) for k, v in
-                               clients[0].items())
 
-    agg = KrumAggregator(model=M(), device='cuda', config=cfg)
-    D, _ = agg.distance_matrix([(1, c) for c in clients])
+@pytest.mark.parametrize('case', ['identical', 'near', 'nonfinite'])
+def test_pairgram_flags_and_exact_repair(case):
+    n = 24
+
+    def fn(i, j, z):
+        if i in (3, 4):
+            if case == 'identical':
+                return torch.full_like(z, 50.0)
+            return 50.0 + 1e-6 * z
+        if case == 'nonfinite' and i == 9 and j == 0:
+            z = z.clone()
+            z[17] = float('inf')
+        return z
+
+    clients = _clients(n, sizes=[10_000, 33], seed=6, fn=fn)
+    lay, _, keyed, _ = _sets(clients)
+    got, err, D, flags = _gram(keyed)
+    want = _fp64_segsq(clients, lay)
+    if case == 'nonfinite':
+        assert flags[9].sum() == n - 1
+    else:
+        assert flags[3, 4]
+        assert flags.sum() <= 2 * (2 * n - 3)
+        assert got[:, 3, 4].max() == 0.0 or case == 'near'
+        _check(got, err, D, flags, want)
+    agg = _krum(clients)
+    De, _ = agg.distance_matrix([(1, c) for c in clients])
     assert agg.last_pairdist_path.startswith('mfma + exact')
-    want = np.sqrt(_fp64_segsq(clients, lay)).sum(axis=0)
-    off = ~np.eye(n, dtype=bool)
-    err = np.abs(D.numpy()[off] - want[off]) / want[off]
-    assert err.max() <= 2e-6
+    # the recomputed pairs are the VALU kernel's (its semantics for ±inf)
+    from federatedscope_amd import ops
+    Dv = ops.pairdist_finish(ops.pairdist_rows_segsq(keyed)).cpu().numpy()
+    sel = sorted(set(np.nonzero(flags)[0].tolist()))
+    ix = np.ix_(sel, sel)
+    assert np.allclose(De.numpy()[ix], Dv[ix], rtol=2e-7, atol=0,
+                       equal_nan=True)
+    if case != 'nonfinite':
+        Dw = _fp64_D(want)
+        off = ~np.eye(n, dtype=bool)
+        pos = off & (Dw > 0)
+        e = np.abs(De.numpy()[pos] - Dw[pos]) / Dw[pos]
+        assert e.max() <= 1e-6
+        assert De.numpy()[3, 4] == Dw[3, 4] or case == 'near'
 
 
 @pytest.mark.parametrize('n', [7, 50])
-def test_krum_distance_matrix_mixed_keys(n):
-    """Through the engine: big keys on the matrix cores, small keys on the
-    VALU kernel, one distance matrix; within 2e-7 of fp64 (summed over
-    keys in fp32 like the reference)."""
-    from types import SimpleNamespace
-    from federatedscope_amd.core.aggregators import KrumAggregator
+def test_krum_distance_matrix_engine(n):
+    """Through the engine: every key on the matrix cores, one distance
+    matrix within 1e-6 of fp64 (summed over keys in fp32 like the
+    reference), no pair recomputed."""
     clients = _clients(n, seed=40 + n)
     lay = _sets(clients)[0]
-    cfg = SimpleNamespace(
-        federate=SimpleNamespace(ignore_weight=False, use_ss=False,
-                                 client_num=1000, sample_client_rate=1.0),
-        aggregator=SimpleNamespace(
-            byzantine_node_num=1,
-            BFT_args=SimpleNamespace(krum_agg_num=1)))
-    agg = KrumAggregator(device='cuda', config=cfg)
+    agg = _krum(clients, f=1)
     D, _ = agg.distance_matrix([(1, c) for c in clients])
     assert agg.last_pairdist_path == 'mfma'
-    want = np.sqrt(_fp64_segsq(clients, lay)).sum(axis=0)
+    Dw = _fp64_D(_fp64_segsq(clients, lay))
     off = ~np.eye(n, dtype=bool)
-    err = np.abs(D.numpy()[off] - want[off]) / want[off]
+    err = np.abs(D.numpy()[off] - Dw[off]) / Dw[off]
     assert err.max() <= 1e-6

@@ -112,31 +112,28 @@ def krum_c4(dev, n=50, f=10):
     margin = float((srt[1] - srt[0]) / srt[0])
     sel_gpu = torch.sort(s_gpu)[1][:5].tolist()
     sel_ref = torch.sort(s_ref)[1][:5].tolist()
-    # the matrix-core path the aggregators take for n <= 64 (big keys on
-    # fsagg_pairgram_rows_segsq_f32, small keys on the VALU kernel)
+    # the matrix-core path the aggregators take for n <= 64
+    # (fsagg_pairgram_rows_segsq_f32 over every key + fsagg_pairgram_finish)
     import numpy as np
-    from federatedscope_amd.core.aggregators._engine import (_gram_key,
-                                                             _valu_key)
+    from federatedscope_amd.core.aggregators._engine import _GRAM_TOL
     rs = ops.RowSet(lay, np.array([[slab[i].data_ptr()] for i in range(n)],
                                   dtype=np.int64), dev, keepalive=(slab, ))
-    ill = torch.zeros((n, n), dtype=torch.int32, device=dev)
-    small = sum(lay.numels[k] for k in lay.keys if _valu_key(lay.numels[k]))
 
     def gram_D():
-        sq = ops.pairgram_rows_segsq(rs, ill, keep=_gram_key)
-        sq.add_(ops.pairdist_rows_segsq(rs, keep=_valu_key, extent=small))
-        return ops.pairdist_finish(sq)
+        sq2 = ops.pairgram_rows_segsq(rs)
+        buf, D_, ill_ = ops.pairgram_finish(sq2, _GRAM_TOL)
+        return sq2, D_, ill_
 
-    Dg = gram_D().cpu()
-    # per key: the Gram path's worst relative distance error and the
-    # conditioning (Σ|x'|² / d², centred on the medoid) of that pair
-    sqg = ops.pairgram_rows_segsq(rs, torch.zeros_like(ill),
-                                  keep=_gram_key).cpu().numpy()
+    sq2, Dg, ill = gram_D()
+    Dg, flags = Dg.cpu(), ill.cpu().numpy()
+    # per key: the Gram path's worst relative distance error, the predicted
+    # bound at that pair and the conditioning (Σ|x'|² / d², centred on the
+    # medoid) of the worst-conditioned pair
+    sqg = sq2[0].cpu().numpy()
+    errg = sq2[1].cpu().numpy()
     medoid = int(ref.clone().fill_diagonal_(0).sum(1).argmin())
     per_key = []
     for s_, k in enumerate(lay.keys):
-        if not _gram_key(lay.numels[k]):
-            continue
         o, m = lay.offsets[k], lay.numels[k]
         X = slab[:, o:o + m].double()
         Y = X - X[medoid]
@@ -146,6 +143,7 @@ def krum_c4(dev, n=50, f=10):
             sq[a] = ((X - X[a]) ** 2).sum(1)
         sq = sq.cpu().numpy()
         offd = ~np.eye(n, dtype=bool)
+        abserr = np.abs(sqg[s_] - sq)[offd]
         err = np.abs(np.sqrt(sqg[s_]) - np.sqrt(sq))[offd] / \
             np.sqrt(sq)[offd]
         F = ((mag[:, None] + mag[None, :]) / np.where(sq > 0, sq, np.inf))[
@@ -153,7 +151,16 @@ def krum_c4(dev, n=50, f=10):
         i = int(err.argmax())
         per_key.append({'key': k, 'len': m, 'max_rel_err': float(err[i]),
                         'F_at_max': float(F[i]), 'F_max': float(F.max()),
-                        'err_over_F_max': float((err / F).max())})
+                        'err_over_F_max': float((err / F).max()),
+                        # pairgram.hip: err + kErrBias (2e-8) · d²
+                        'bound_holds': bool(np.all(
+                            abserr <= errg[s_][offd] + 2e-8 * sq[offd])),
+                        'max_abserr_over_bound': float(
+                            (abserr / np.maximum(errg[s_][offd] + 2e-8 *
+                                                 sq[offd], 1e-300)).max()),
+                        'max_abserr_over_G': float((abserr / np.maximum(
+                            (mag[:, None] + mag[None, :])[offd],
+                            1e-300)).max())})
     gmed, gmn = timed(gram_D)
     grel = ((Dg.double() - ref).abs() / ref)[off].max().item()
     sel_gram = torch.sort(krum_scores(Dg, f))[1][:5].tolist()
@@ -184,7 +191,7 @@ def krum_c4(dev, n=50, f=10):
         'gram_ms_median': gmed, 'gram_ms_min': gmn,
         'gram_GBps': nbytes / gmed / 1e6,
         'gram_max_rel_err_vs_fp64': grel,
-        'gram_flagged_pairs': int((ill > 0).sum().item()),
+        'gram_flagged_pairs': int((flags > 0).sum()),
         'gram_per_key': per_key,
         'gram_selection_exact': sel_gram == sel_ref,
         'kernel': 'fsagg_pairdist_f32', 'config': 'C4 Krum n=%d P=%d f=%d' %
