@@ -29,8 +29,6 @@
 //     the smallest bitonic network that holds every lane's list and the ranks
 //     (and the kept partial sums) read off.
 // Register budget: SEL_N values + ~40 within 256 VGPRs (2 waves per SIMD).
-#include <cstdlib>
-
 #include "orderstat_sel.h"
 
 #ifndef SEL_N
@@ -41,14 +39,7 @@ namespace fsagg {
 namespace os {
 namespace {
 
-// SAMPLE: the octave digit's base from the largest |x| of the first
-// kBaseRows rows instead of the whole column, so the histogram pass runs as
-// the rows arrive (behind the loads of the later rows) instead of after the
-// last one.  Any base gives exact bins (values above it land in the top
-// bin, octave_bin), the sample only sets how finely the bulk is split.
-constexpr int kBaseRows = 32;
-
-template <int N, int MODE, bool SAMPLE>
+template <int N, int MODE>
 __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
     RowSrc rs, int n, int kk, float divisor, float *__restrict__ out) {
   // 16 KiB-aligned: a lane's word addresses are hb | (w << 8)
@@ -76,23 +67,12 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
     // with the rows, not at the end: a load issued as the wave's last act
     // exposes one full HBM round trip per wave (0.14 ms at C5)
     if (base) bval = ld_nt(base, off);
-    if (!SAMPLE) {
 #pragma unroll
-      for (int j = 0; j < N; ++j) amax = max(amax, u[j] & 0x7FFFFFFFu);
-    }
+    for (int j = 0; j < N; ++j) amax = max(amax, u[j] & 0x7FFFFFFFu);
   }
-  int obase;
-  if (SAMPLE) {
-    uint32_t smax = 0u;
-#pragma unroll
-    for (int j = 0; j < kBaseRows; ++j) {
-      const uint32_t a = u[j] & 0x7FFFFFFFu;
-      smax = a < 0x7F800000u ? max(smax, a) : smax;
-    }
-    obase = int(smax >> kMagShift) - (kCodes - 1);
-  } else {
-    obase = int(amax >> kMagShift) - (kCodes - 1);
-  }
+  const bool nan = amax > 0x7F800000u;
+  const bool nonfinite = amax >= 0x7F800000u;
+  const int obase = int(amax >> kMagShift) - (kCodes - 1);
   const int r1 = MODE == kMedian ? (n - 1) / 2 : kk;
   const int r2 = MODE == kMedian ? n / 2 : n - kk - 1;
 
@@ -102,11 +82,8 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
     hist_clear(H, 64);
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-      if (SAMPLE) amax = max(amax, u[j] & 0x7FFFFFFFu);
       if (j >= N - kSelStep && j >= n) continue;  // pads
       hist_inc(hb, octave_digit(u[j], obase));
-      // in row order, as the rows arrive (no per-value temporaries held)
-      if (SAMPLE) __builtin_amdgcn_sched_barrier(0);
     }
     uint32_t d1, d2;
     int b1, c1, b2, c2;
@@ -118,9 +95,6 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
     s2.below = b2;
     s2.cnt = c2;
   }
-
-  const bool nan = amax > 0x7F800000u;
-  const bool nonfinite = amax >= 0x7F800000u;
 
   // 3. refine while the two bins would overflow the list (rare)
   bool shared = same_bin(s1, s2);
@@ -267,25 +241,11 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
 
 }  // namespace
 
-#ifdef FSAGG_PROBE
-// probe build: FSAGG_PROBE_OS_SAMPLE=0 selects the whole-column base
-static bool probe_sample() {
-  const char *e = getenv("FSAGG_PROBE_OS_SAMPLE");
-  return !(e && e[0] == '0');
-}
-#else
-static bool probe_sample() { return true; }
-#endif
-
 template <int N, int MODE>
 void launch_select(const RowSrc &rs, unsigned grid, int n, int kk,
                    float divisor, float *out, hipStream_t s) {
-  if (n > kBaseRows && probe_sample())
-    hipLaunchKernelGGL((orderstat_select_kernel<N, MODE, true>), dim3(grid),
-                       dim3(kBlock), 0, s, rs, n, kk, divisor, out);
-  else
-    hipLaunchKernelGGL((orderstat_select_kernel<N, MODE, false>), dim3(grid),
-                       dim3(kBlock), 0, s, rs, n, kk, divisor, out);
+  hipLaunchKernelGGL((orderstat_select_kernel<N, MODE>), dim3(grid),
+                     dim3(kBlock), 0, s, rs, n, kk, divisor, out);
 }
 
 template void launch_select<SEL_N, kMedian>(const RowSrc &, unsigned, int,
