@@ -166,14 +166,19 @@ __device__ __forceinline__ int kofs(int g, int j) {
   return j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4);
 }
 
-// One k-step: centre (CENTRED: cs = the LDS centre values at this lane's
-// coordinates of the k-step, slots 0-3 at cs, 4-7 at cs + 16), split, and
-// the tile pairs' products into acc.
+// One k-step in two phases.  kstep_split: centre (CENTRED: cs = the LDS
+// centre values at this lane's coordinates of the k-step, slots 0-3 at cs,
+// 4-7 at cs + 16) and split into limbs; kstep_mfma: the tile pairs'
+// products into acc.
+template <int NT>
+struct Frags {
+  frag8 h[NT], m[NT], l[NT];
+};
+
 template <int NT, bool CENTRED>
-__device__ __forceinline__ void kstep(const float (&xb)[NT][8],
-                                      const float *cs, const Neg &k,
-                                      double (&acc)[ntp_of(NT)][4]) {
-  frag8 fh[NT], fm[NT], fl[NT];
+__device__ __forceinline__ void kstep_split(const float (&xb)[NT][8],
+                                            const float *cs, const Neg &k,
+                                            Frags<NT> &f) {
   float cb[8];
   if (CENTRED) {
     const f32x4 x = *reinterpret_cast<const f32x4 *>(cs);
@@ -181,40 +186,43 @@ __device__ __forceinline__ void kstep(const float (&xb)[NT][8],
     cb[0] = x.x; cb[1] = x.y; cb[2] = x.z; cb[3] = x.w;
     cb[4] = y.x; cb[5] = y.y; cb[6] = y.z; cb[7] = y.w;
   }
-  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     float x[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = CENTRED ? xb[t][j] - cb[j] : xb[t][j];
-    split3(x, k, fh[t], fm[t], fl[t]);
+    split3(x, k, f.h[t], f.m[t], f.l[t]);
   }
-  // per tile pair: the six limb products in fp32 (the small ones first, so
-  // their roundings happen at their own magnitude), then into fp64 — the
-  // previous pair's conversion behind this pair's chain, one pair per
-  // scheduling group (two chains' results live, not all of them)
-  f32x4 c[2];
+}
+
+// per tile pair: the six limb products in fp32 (the small ones first, so
+// their roundings happen at their own magnitude), then into fp64
+template <int NT>
+__device__ __forceinline__ void kstep_mfma(const Frags<NT> &f,
+                                           double (&acc)[ntp_of(NT)][4]) {
 #pragma unroll
   for (int p = 0; p < ntp_of(NT); ++p) {
     int t, u;
     tp_tiles(p, NT, t, u);
     f32x4 x = {0.0f, 0.0f, 0.0f, 0.0f};
-    x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fm[t], fm[u], x, 0, 0, 0);
-    x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[t], fl[u], x, 0, 0, 0);
-    x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fl[t], fh[u], x, 0, 0, 0);
-    x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[t], fm[u], x, 0, 0, 0);
-    x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fm[t], fh[u], x, 0, 0, 0);
-    x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[t], fh[u], x, 0, 0, 0);
-    c[p & 1] = x;
-    if (p > 0) {
+    x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.m[t], f.m[u], x, 0, 0, 0);
+    x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[t], f.l[u], x, 0, 0, 0);
+    x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.l[t], f.h[u], x, 0, 0, 0);
+    x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[t], f.m[u], x, 0, 0, 0);
+    x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.m[t], f.h[u], x, 0, 0, 0);
+    x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.h[t], f.h[u], x, 0, 0, 0);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[p - 1][r] += double(c[(p - 1) & 1][r]);
-    }
-    __builtin_amdgcn_sched_barrier(0);
+    for (int r = 0; r < 4; ++r) acc[p][r] += double(x[r]);
   }
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-    acc[ntp_of(NT) - 1][r] += double(c[(ntp_of(NT) - 1) & 1][r]);
+}
+
+template <int NT, bool CENTRED>
+__device__ __forceinline__ void kstep(const float (&xb)[NT][8],
+                                      const float *cs, const Neg &k,
+                                      double (&acc)[ntp_of(NT)][4]) {
+  Frags<NT> f;
+  kstep_split<NT, CENTRED>(xb, cs, k, f);
+  kstep_mfma<NT>(f, acc);
 }
 
 // 16-B loads of one full k-step: slots 0-3 at a, 4-7 at a + 16
@@ -293,11 +301,13 @@ __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
   for (int t = 0; t < NT; ++t) ok = ok && al16(row[t] + c0);
   const bool vec = __all(ok);
   int i = wv;   // this wave's next k-step
-  // one k-step in flight while the other is multiplied (ping-pong, so no
-  // register copies); the first two are issued before the centre staging
+  // one buffer: the next k-step's loads go out as soon as this one is split
+  // and fly while its products are formed (the load depth of a ping-pong
+  // pair of buffers measured the same); the first is issued
+  // before the centre staging
   constexpr int64_t stp = int64_t(kWaves) * kKStep;
   const float *a[NT];
-  float xa[NT][8], xb[NT][8];
+  float xa[NT][8];
   if (vec) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -305,10 +315,6 @@ __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
     if (i < nfull) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) ld8(a[t], xa[t]);
-    }
-    if (i + kWaves < nfull) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) ld8(a[t] + stp, xb[t]);
     }
   }
   if (CENTRED) {
@@ -328,22 +334,20 @@ __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
     __syncthreads();
   }
   if (vec) {
-    for (; i < nfull; i += 2 * kWaves) {
+    for (; i < nfull; i += kWaves) {
+      Frags<NT> f;
+      kstep_split<NT, CENTRED>(xa, cs + i * kKStep + 4 * g, kn, f);
+      __builtin_amdgcn_sched_barrier(0);
+      // unconditional (the last k-step re-reads itself, from L2): a load
+      // under a branch would make the buffer a phi and cost a copy of it
+      const int64_t adv = i + kWaves < nfull ? stp : 0;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) a[t] += 2 * stp;
-      kstep<NT, CENTRED>(xa, cs + i * kKStep + 4 * g, kn, acc);
-      if (i + 2 * kWaves < nfull) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) ld8(a[t], xa[t]);
+      for (int t = 0; t < NT; ++t) {
+        a[t] += adv;
+        ld8(a[t], xa[t]);
       }
-      if (i + kWaves < nfull) {
-        kstep<NT, CENTRED>(xb, cs + (i + kWaves) * kKStep + 4 * g, kn,
-                           acc);
-        if (i + 3 * kWaves < nfull) {
-#pragma unroll
-          for (int t = 0; t < NT; ++t) ld8(a[t] + stp, xb[t]);
-        }
-      }
+      __builtin_amdgcn_sched_barrier(0);
+      kstep_mfma<NT>(f, acc);
     }
     i = nfull + ((wv - nfull) % kWaves + kWaves) % kWaves;
   }
