@@ -199,10 +199,25 @@ def test_bulyan(name):
         f=meta['f'], rate=meta['rate'], client_num=4 * meta['f'] + 3))
     got = agg.aggregate({'client_feedback': feedback(clients)})
     keep = len(clients) - int(2 * meta['rate'] * meta['f'])
-    assert agg.last_selection == [int(i) for i in extra['order'][:keep]]
+    sel = [int(i) for i in extra['order'][:keep]]
+    assert agg.last_selection == sel
+    # the output is the trimmed mean of the selected clients
+    # (bulyan_aggregator.py:95-106: cat-sum / gamma, then init + update):
+    # the same bounds as the trimmed mean — the reference's own rounding
+    # bound over the selected clients, and a few ulps of the oracle's fp64
+    # middle sum
+    k = int(meta['rate'] * meta['f'])
+    chosen = [clients[i] for i in sel]
+    tol = O.trimmed_tolerance(chosen, k, divisor=keep - 2 * k)
+    ours, osel = O.bulyan_aggregate(clients, meta['f'], meta['rate'], init)
+    assert osel == sel
+    eps = np.finfo(np.float32).eps
     for key in out:
-        np.testing.assert_allclose(to_np(got[key]), out[key], rtol=1e-5,
-                                   atol=1e-6)
+        g = to_np(got[key]).astype(np.float64)
+        ref, o = out[key].astype(np.float64), np.asarray(ours[key])
+        ini = np.asarray(init[key], dtype=np.float64)
+        assert (np.abs(g - ref) <= tol[key] + 4 * eps * np.abs(ref)).all()
+        assert (np.abs(g - o) <= 4 * eps * (np.abs(o) + np.abs(ini))).all()
 
 
 @pytest.mark.parametrize('name', case_names('normbound_'))
@@ -212,9 +227,30 @@ def test_normbounding(name):
     agg = NormboundingAggregator(model=DictModel(init),
                                  config=cfg(bound=meta['bound']))
     got = agg.aggregate({'client_feedback': feedback(clients)})
+    # vs the oracle (the correctly rounded fp32 norm, the reference's rate
+    # and weighted-sum arithmetic): bit-exact
+    ours = O.normbounding_aggregate(clients, meta['bound'], init)
     for key in out:
-        np.testing.assert_allclose(to_np(got[key]), out[key], rtol=1e-6,
-                                   atol=1e-7)
+        assert to_np(got[key]).tobytes() == \
+            np.asarray(ours[key], dtype=np.float32).tobytes(), (name, key)
+    # vs the reference: its fp32 torch.norm may differ from the correctly
+    # rounded norm by its summation error, at most (log2(m) + 2)·ε over m
+    # squares (ATen's cascade sum); the rate carries that plus its two
+    # roundings into each scaled client, and the sums round differently
+    # from there (4ε of the result)
+    eps = np.finfo(np.float32).eps
+    m = max(sum(int(np.prod(np.shape(d[k]))) for k in init if k in d)
+            for _, d in clients)
+    eta = (np.ceil(np.log2(max(m, 2))) + 4) * eps
+    sizes = np.array([s for s, _ in clients], dtype=np.float64)
+    w = sizes / sizes.sum()
+    for key in out:
+        g = to_np(got[key]).astype(np.float64)
+        ref = out[key].astype(np.float64)
+        mag = sum(wi * np.abs(np.asarray(d.get(key, 0.0), dtype=np.float64))
+                  for wi, (_, d) in zip(w, clients))
+        assert (np.abs(g - ref) <= eta * mag + 4 * eps * np.abs(ref) +
+                1e-30).all(), (name, key)
 
 
 class ParamModel(torch.nn.Module):
