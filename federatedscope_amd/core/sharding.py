@@ -369,45 +369,68 @@ class PeerAssembly:
         idx = self.device.index
         self._own = []
         self._opened = []
+        # Every rank runs every exchange, whatever failed locally, and the
+        # ranks agree at the end: all of them use the peer copies or none
+        # does (a rank that gave up alone would leave the others waiting in
+        # a collective or at the flag barrier).
+        err = None
+        hb = int(self._lib.fsagg_peer_handle_bytes())
+        bus = ctypes.create_string_buffer(64)
         try:
             nbytes = self.padded * 4
             for _ in range(buffers):
                 self._own.append(self._alloc(nbytes))
             self._own.append(self._alloc(self.CTRL_WORDS * 4))
-            hb = int(self._lib.fsagg_peer_handle_bytes())
-            bus = ctypes.create_string_buffer(64)
             self._L.check(self._lib.fsagg_peer_pci_bus_id(idx, bus, 64),
                           'fsagg_peer_pci_bus_id')
-            buses = self.comm.all_gather_bytes(bus.value)
-            for k, b in enumerate(buses):
-                ok = self._lib.fsagg_peer_can_access(idx, b)
-                if ok < 0:
-                    self._L.check(ok, 'fsagg_peer_can_access')
-                if ok == 0:
-                    raise RuntimeError('GPU %s cannot access rank %d\'s GPU '
-                                       '%s' % (bus.value.decode(), k,
-                                               b.decode()))
-            mine = b''.join(self._handle(p, hb) for p in self._own)
-            every = self.comm.all_gather_bytes(mine)
-            # ptr[k] = rank k's allocations (buffers..., ctrl) as seen here
-            self._ptr = []
-            for k in range(W):
-                if k == self.rank:
-                    self._ptr.append(list(self._own))
-                    continue
-                if len(every[k]) != len(mine):
-                    raise RuntimeError('rank %d sent %d handle bytes, '
-                                       'expected %d' % (k, len(every[k]),
-                                                        len(mine)))
-                row = []
-                for a in range(len(self._own)):
-                    p = self._open(every[k][a * hb:(a + 1) * hb])
-                    self._opened.append(p)
-                    row.append(p)
-                self._ptr.append(row)
-        except Exception:
+        except Exception as e:          # noqa: BLE001 (agreed on below)
+            err = e
+        buses = self.comm.all_gather_bytes(bus.value if err is None else b'')
+        mine = b''
+        if err is None:
+            try:
+                for k, b in enumerate(buses):
+                    if not b:
+                        raise RuntimeError('rank %d has no peer buffers' % k)
+                    ok = self._lib.fsagg_peer_can_access(idx, b)
+                    if ok < 0:
+                        self._L.check(ok, 'fsagg_peer_can_access')
+                    if ok == 0:
+                        raise RuntimeError('GPU %s cannot access rank %d\'s '
+                                           'GPU %s' % (bus.value.decode(), k,
+                                                       b.decode()))
+                mine = b''.join(self._handle(p, hb) for p in self._own)
+            except Exception as e:      # noqa: BLE001
+                err = e
+        every = self.comm.all_gather_bytes(mine)
+        # ptr[k] = rank k's allocations (buffers..., ctrl) as seen here
+        self._ptr = []
+        if err is None:
+            try:
+                for k in range(W):
+                    if k == self.rank:
+                        self._ptr.append(list(self._own))
+                        continue
+                    if len(every[k]) != len(mine):
+                        raise RuntimeError('rank %d sent %d handle bytes, '
+                                           'expected %d' % (k, len(every[k]),
+                                                            len(mine)))
+                    row = []
+                    for a in range(len(self._own)):
+                        p = self._open(every[k][a * hb:(a + 1) * hb])
+                        self._opened.append(p)
+                        row.append(p)
+                    self._ptr.append(row)
+            except Exception as e:      # noqa: BLE001
+                err = e
+        verdicts = self.comm.all_gather_bytes(b'1' if err is None else b'0')
+        if err is not None or b'0' in verdicts:
             self._release()
-            raise
+            if err is not None:
+                raise err
+            raise RuntimeError('peer assembly unavailable on rank(s) %s' %
+                               [k for k, v in enumerate(verdicts)
+                                if v == b'0'])
         host = L.host()
         self.buffers = [host.device_tensor(p, self.padded, 0, idx)
                         for p in self._own[:-1]]

@@ -209,3 +209,90 @@ def test_pipelined_assembly_plan_world1():
     assert torch.equal(out, torch.arange(1000, dtype=torch.float32))
     with pytest.raises(ValueError):
         PipelinedAssembly(10, chunks=0)
+
+
+class _FakePeerLib:
+    """The peer-memory entry points of libfsagg as host stand-ins, so that
+    PeerAssembly's setup protocol runs without a GPU; ``deny`` makes this
+    rank's fsagg_peer_can_access refuse a peer (a GPU without a link)."""
+
+    def __init__(self, rank, deny):
+        self.rank, self.deny, self.n = rank, deny, 0
+        self.freed, self.closed = [], []
+
+    def fsagg_peer_handle_bytes(self):
+        return 8
+
+    def fsagg_peer_alloc(self, dev, nbytes, out):
+        self.n += 1
+        out._obj.value = 0x1000 * (self.rank + 1) + self.n
+        return 0
+
+    def fsagg_peer_pci_bus_id(self, dev, buf, size):
+        buf.value = b'0000:%02x:00.0' % self.rank
+        return 0
+
+    def fsagg_peer_can_access(self, dev, bus):
+        return 0 if self.deny else 1
+
+    def fsagg_peer_handle(self, ptr, buf):
+        buf.raw = int(ptr).to_bytes(8, 'little')
+        return 0
+
+    def fsagg_peer_open(self, dev, buf, out):
+        out._obj.value = int.from_bytes(buf.raw[:8], 'little') | 1 << 40
+        return 0
+
+    def fsagg_peer_close(self, dev, p):
+        self.closed.append(p)
+
+    def fsagg_peer_free(self, dev, p):
+        self.freed.append(p)
+
+
+def _peer_setup_worker(rank, world, port, deny_rank, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from federatedscope_amd import _lib as L
+        from federatedscope_amd.core import sharding
+        fake = _FakePeerLib(rank, rank == deny_rank)
+        L.load = lambda: fake
+        try:
+            sharding.PeerAssembly(1000, device='cuda:0')
+            q.put((rank, 'built', len(fake.freed)))
+        except RuntimeError as e:
+            # every allocation released, nothing left open
+            q.put((rank, 'refused:' + str(e)[:40], len(fake.freed),
+                   fake.n, len(fake.closed)))
+        # the ranks are still in step: a collective after the refusal
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        q.put((rank, 'sum', float(t)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_peer_assembly_setup_agrees_across_ranks():
+    """One rank cannot reach a peer: every rank refuses the peer assembly
+    (so all fall back to the collective together), every rank releases its
+    allocations, and the ranks stay in step for the next collective."""
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_peer_setup_worker,
+                      args=(r, world, port, 1, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(2 * world)]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    refused = sorted(o for o in out if o[1] != 'sum')
+    assert [o[0] for o in refused] == [0, 1]
+    for o in refused:
+        assert o[1].startswith('refused:')
+        assert o[2] == o[3]          # every allocation freed
+    assert sorted(o[2] for o in out if o[1] == 'sum') == [2.0, 2.0]
