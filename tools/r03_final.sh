@@ -4,6 +4,6 @@
 set -u
 R=$GRAFT_REPO_ROOT
 cd $R
-bash tools/gpu_job.sh pytestall smoke bench "python -u tools/bench_robust.py krum orderstat orderstat_large dropin" || exit $?
+bash tools/gpu_job.sh pytestall smoke bench "python -u tools/bench_robust.py krum orderstat orderstat_large dropin" "python -u tools/time_krum_host.py" || exit $?
 bash tools/profile_all.sh || exit $?
 bash tools/pmc.sh krum final
