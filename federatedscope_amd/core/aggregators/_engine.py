@@ -454,7 +454,6 @@ def _host_ext():
     return _HOST[0]
 
 
-# keys of at least this many elements take the matrix-core Krum distances
 # relative bound on a Krum distance's error from the Gram form above which
 # the pair is recomputed on the VALU kernel (the bound is 2-5x
 # the measured error; the Gram path measures 2.3e-7 at C4, the VALU kernel
