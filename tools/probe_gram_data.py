@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Probe: the Gram Krum path's time against the data and the memory
+layout at the C4 shape (50 clients, ConvNet2-h2048 keys): a slab with the
+C4 mix (common base, Byzantine cluster) or i.i.d. N(0,1), read as per-key
+views of the slab rows or as separately allocated key tensors.  GPU only."""
+import json
+import os
+import sys
+from collections import OrderedDict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'tools'))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from bench_robust import layout, timed  # noqa: E402
+
+
+def main():
+    from federatedscope_amd import ops
+    from federatedscope_amd.core.aggregators._engine import _GRAM_TOL
+    dev = torch.device('cuda', 0)
+    lay = layout()
+    P, n = lay.numel, 50
+    g = torch.Generator(device=dev).manual_seed(1234)
+    base = torch.randn(P, device=dev, generator=g)
+    slab = torch.empty((n, P), device=dev)
+    for kind in ('c4', 'iid', 'iid_scaled', 'zeros'):
+        for r in range(n):
+            z = torch.randn(P, device=dev, generator=g)
+            if kind == 'c4':
+                slab[r] = (0.1 + 0.05 * z) if r % 5 == 0 else \
+                    base + 0.01 * (1 + 0.05 * r) * z
+            elif kind == 'iid':
+                slab[r] = z
+            elif kind == 'iid_scaled':
+                slab[r] = 0.01 * z
+            else:
+                slab[r] = 0.0
+        for form in ('views', 'separate'):
+            if form == 'views':
+                ptrs = [[slab[i, lay.offsets[k]:].data_ptr() for k in
+                         lay.keys] for i in range(n)]
+                keep = (slab, )
+            else:
+                ts = [[slab[i, lay.offsets[k]:lay.offsets[k] +
+                            lay.numels[k]].clone() for k in lay.keys]
+                      for i in range(n)]
+                ptrs = [[t.data_ptr() for t in row] for row in ts]
+                keep = (ts, )
+            rs = ops.RowSet.from_pointers(lay, np.array(ptrs, dtype=np.int64),
+                                          dev, keepalive=keep)
+
+            def run():
+                sq2 = ops.pairgram_rows_segsq(rs)
+                return ops.pairgram_finish(sq2, _GRAM_TOL)
+            run()
+            med, mn = timed(run)
+            print(json.dumps({'data': kind, 'form': form, 'ms_median': med,
+                              'ms_min': mn}), flush=True)
+
+
+if __name__ == '__main__':
+    main()
