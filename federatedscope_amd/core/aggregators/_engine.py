@@ -171,9 +171,21 @@ class DeviceEngine:
         pairs the Gram form cannot resolve to _GRAM_TOL of their distance
         (near-duplicate clients far from every other, non-finite values)
         are recomputed on the VALU kernel over the clients involved.  Above
-        64 clients: the VALU kernel."""
+        64 clients, or when the clients' rows start at one offset within
+        a 2 MiB page (separately allocated device tensors, which the Gram
+        kernel's all-rows-at-once reads make camp on one HBM channel:
+        DESIGN §3.3): the VALU kernel."""
         from ... import _lib
-        if 2 <= st.n <= _lib.FSAGG_PAIRGRAM_MAX_CLIENTS:
+        gram = 2 <= st.n <= _lib.FSAGG_PAIRGRAM_MAX_CLIENTS and \
+            _rows_spread(st)
+        if st.plan is not None and 2 <= st.n <= \
+                _lib.FSAGG_PAIRGRAM_MAX_CLIENTS:
+            # one path on every rank (the exchanged partials differ)
+            v = torch.tensor([1.0 if gram else 0.0],
+                             device=self.compute_device)
+            st.plan.comm.all_reduce_sum(v)
+            gram = int(v.item()) == st.plan.comm.world
+        if gram:
             sq2 = self._sum_pieces(
                 st, lambda rs, lo, hi: ops.pairgram_rows_segsq(rs, lo, hi))
             buf, _, _ = ops.pairgram_finish(sq2, _GRAM_TOL)
@@ -459,6 +471,33 @@ def _host_ext():
 # the measured error; the Gram path measures 2.3e-7 at C4, the VALU kernel
 # 1.6e-7)
 _GRAM_TOL = 1e-6
+
+
+def _rows_spread(st):
+    """Whether the clients' rows of the largest key start at enough distinct
+    4-KiB offsets within a 2 MiB page for the Gram kernel, whose k-steps read
+    every row at the same coordinate at once: rows of one allocation (the
+    client stack, views of a slab) are spread; separately allocated device
+    tensors start 2 MiB-aligned, and the Gram path then measures 0.54 against
+    0.34 ms at C4 (the VALU kernel, which reads fewer rows at a time: 0.46)."""
+    import numpy as np
+    rs = None
+    for _, _, _, r in st.pieces:
+        if getattr(r, 'host', None) is not None:
+            rs = r
+            break
+    if rs is None:
+        return True
+    lay = rs.layout
+    if not lay.keys:
+        return True
+    s = max(range(len(lay.keys)), key=lambda i: lay.numels[lay.keys[i]])
+    col = rs.host[:, s if rs.host.shape[1] > 1 else 0]
+    col = col[col != 0] + 4 * int(lay.offsets[lay.keys[s]])
+    if col.size < 2:
+        return True
+    pages = np.unique((col >> 12) & 511).size
+    return pages >= max(2, col.size // 4)
 
 
 class _PendingD:

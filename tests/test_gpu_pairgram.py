@@ -38,6 +38,25 @@ def _clients(n, sizes=SIZES, seed=9, fn=None):
     return out
 
 
+def _as_slab(clients):
+    """The same clients as views of one allocation (each client's keys
+    contiguous, as in the client stack): rows at spread offsets, the layout
+    the engine gives the matrix cores (_engine._rows_spread)."""
+    keys = list(clients[0].keys())
+    sizes = [clients[0][k].numel() for k in keys]
+    total = sum(sizes) + 16 * len(keys)
+    slab = torch.zeros((len(clients), total), device='cuda')
+    out = []
+    for i, c in enumerate(clients):
+        d, o = OrderedDict(), 0
+        for k, sz in zip(keys, sizes):
+            d[k] = slab[i, o:o + sz].view(c[k].shape)
+            d[k].copy_(c[k])
+            o += (sz + 15) // 16 * 16
+        out.append(d)
+    return out
+
+
 def _sets(clients):
     from federatedscope_amd import ops
     from federatedscope_amd.layout import BucketLayout, ClientStack
@@ -198,7 +217,7 @@ def test_pairgram_flags_and_exact_repair(case):
         assert got[:, 3, 4].max() == 0.0 or case == 'near'
         _check(got, err, D, flags, want)
     agg = _krum(clients)
-    De, _ = agg.distance_matrix([(1, c) for c in clients])
+    De, _ = agg.distance_matrix([(1, c) for c in _as_slab(clients)])
     assert agg.last_pairdist_path.startswith('mfma + exact')
     # the recomputed pairs are the VALU kernel's (its semantics for ±inf)
     from federatedscope_amd import ops
@@ -224,9 +243,31 @@ def test_krum_distance_matrix_engine(n):
     clients = _clients(n, seed=40 + n)
     lay = _sets(clients)[0]
     agg = _krum(clients, f=1)
-    D, _ = agg.distance_matrix([(1, c) for c in clients])
+    D, _ = agg.distance_matrix([(1, c) for c in _as_slab(clients)])
     assert agg.last_pairdist_path == 'mfma'
     Dw = _fp64_D(_fp64_segsq(clients, lay))
     off = ~np.eye(n, dtype=bool)
     err = np.abs(D.numpy()[off] - Dw[off]) / Dw[off]
     assert err.max() <= 1e-6
+
+
+def test_krum_distance_path_by_row_placement():
+    """Rows that all start at one offset within a 2 MiB page (separately
+    allocated 2 MiB-aligned tensors) take the VALU kernel, rows of one
+    allocation the matrix cores; both within 1e-6 of fp64."""
+    n = 12
+    m = 600_000
+    stride = 1 << 19                 # floats: rows 2 MiB apart
+    g = torch.Generator(device='cuda').manual_seed(77)
+    big = torch.randn((n, stride), device='cuda', generator=g)
+    sep = [OrderedDict(w=big[i, :m]) for i in range(n)]
+    assert len({c['w'].data_ptr() % (1 << 21) for c in sep}) == 1
+    lay = _sets(sep)[0]
+    Dw = _fp64_D(_fp64_segsq(sep, lay))
+    off = ~np.eye(n, dtype=bool)
+    for clients, path in ((sep, 'valu'), (_as_slab(sep), 'mfma')):
+        agg = _krum(clients, f=1)
+        D, _ = agg.distance_matrix([(1, c) for c in clients])
+        assert agg.last_pairdist_path == path
+        err = np.abs(D.numpy()[off] - Dw[off]) / Dw[off]
+        assert err.max() <= 1e-6

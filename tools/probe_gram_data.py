@@ -26,7 +26,7 @@ def main():
     g = torch.Generator(device=dev).manual_seed(1234)
     base = torch.randn(P, device=dev, generator=g)
     slab = torch.empty((n, P), device=dev)
-    for kind in ('c4', 'iid', 'iid_scaled', 'zeros'):
+    for kind in ('c4', ):
         for r in range(n):
             z = torch.randn(P, device=dev, generator=g)
             if kind == 'c4':
@@ -38,8 +38,32 @@ def main():
                 slab[r] = 0.01 * z
             else:
                 slab[r] = 0.0
-        for form in ('views', 'separate'):
-            if form == 'views':
+        for form in ('views', 'separate', 'separate_skewed', 'views_aligned'):
+            if form == 'separate_skewed':
+                # separately allocated rows, each at a different offset mod
+                # 2 MiB (i x 4 KiB + i x 256 B into an oversized buffer)
+                ts = []
+                for i in range(n):
+                    row = []
+                    for k in lay.keys:
+                        m = lay.numels[k]
+                        sk = (i * 1088) % 524288
+                        buf = torch.empty(m + sk, device=dev)
+                        buf[sk:] = slab[i, lay.offsets[k]:lay.offsets[k] + m]
+                        row.append(buf[sk:])
+                    ts.append(row)
+                ptrs = [[t.data_ptr() for t in row] for row in ts]
+                keep = (ts, )
+            elif form == 'views_aligned':
+                # one allocation, rows 2 MiB-aligned (stride a multiple of
+                # 2 MiB)
+                stride = (P + 524287) // 524288 * 524288
+                big = torch.zeros((n, stride), device=dev)
+                big[:, :P] = slab
+                ptrs = [[big[i, lay.offsets[k]:].data_ptr() for k in
+                         lay.keys] for i in range(n)]
+                keep = (big, )
+            elif form == 'views':
                 ptrs = [[slab[i, lay.offsets[k]:].data_ptr() for k in
                          lay.keys] for i in range(n)]
                 keep = (slab, )
@@ -49,6 +73,8 @@ def main():
                       for i in range(n)]
                 ptrs = [[t.data_ptr() for t in row] for row in ts]
                 keep = (ts, )
+            fc1 = lay.keys.index('fc1.weight')
+            offs = len({row[fc1] % (1 << 21) for row in ptrs})
             rs = ops.RowSet.from_pointers(lay, np.array(ptrs, dtype=np.int64),
                                           dev, keepalive=keep)
 
@@ -58,7 +84,9 @@ def main():
             run()
             med, mn = timed(run)
             print(json.dumps({'data': kind, 'form': form, 'ms_median': med,
-                              'ms_min': mn}), flush=True)
+                              'ms_min': mn,
+                              'distinct_fc1_offsets_mod_2MiB': offs}),
+                  flush=True)
 
 
 if __name__ == '__main__':
