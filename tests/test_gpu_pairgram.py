@@ -257,7 +257,7 @@ def test_krum_distance_path_by_row_placement():
     allocation the matrix cores; both within 1e-6 of fp64."""
     n = 12
     m = 600_000
-    stride = 1 << 19                 # floats: rows 2 MiB apart
+    stride = 1 << 20                 # floats: rows 4 MiB apart
     g = torch.Generator(device='cuda').manual_seed(77)
     big = torch.randn((n, stride), device='cuda', generator=g)
     sep = [OrderedDict(w=big[i, :m]) for i in range(n)]
