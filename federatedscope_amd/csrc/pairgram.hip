@@ -39,8 +39,6 @@
 // both operands use it), so each load instruction reads 64 contiguous bytes
 // of 16 rows, every value is read from HBM once and nothing goes through
 // LDS on the way in.
-#include <cstdlib>
-
 #include "common.h"
 
 namespace fsagg {
@@ -255,8 +253,7 @@ __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n,
     const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
     int nseg, const int *__restrict__ prefix, int64_t w, int64_t cap,
-    const int *__restrict__ centre, double *__restrict__ partial,
-    int blocked_ks) {
+    const int *__restrict__ centre, double *__restrict__ partial) {
   constexpr int NTP = ntp_of(NT);
   constexpr int kRedWords = 2 * NTP * 4 * kWave;   // two waves' sums
   constexpr int kSmem = kRedWords * 8 > kMaxW * 4 ? kRedWords * 8
@@ -303,27 +300,19 @@ __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
 #pragma unroll
   for (int t = 0; t < NT; ++t) ok = ok && al16(row[t] + c0);
   const bool vec = __all(ok);
-  // this wave's full k-steps: [kb, ke) by `ks` (interleaved: v, v + 4, ...;
-  // blocked: a contiguous quarter of the chunk, so the four waves read
-  // offsets a quarter-chunk apart rather than within one 512-B span)
-  const bool blocked = blocked_ks != 0;
-  const int qw = (nfull + kWaves - 1) / kWaves;
-  const int kb = blocked ? min(wv * qw, nfull) : wv;
-  const int ke = blocked ? min(kb + qw, nfull) : nfull;
-  const int ks = blocked ? 1 : kWaves;
-  int i = kb;   // this wave's next k-step
+  int i = wv;   // this wave's next k-step: wv, wv + 4, ...
   // one buffer: the next k-step's loads go out as soon as this one is split
   // and fly while its products are formed (the load depth of a ping-pong
   // pair of buffers measured the same); the first is issued
   // before the centre staging
-  const int64_t stp = int64_t(ks) * kKStep;
+  constexpr int64_t stp = int64_t(kWaves) * kKStep;
   const float *a[NT];
   float xa[NT][8];
   if (vec) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
       a[t] = row[t] + c0 + int64_t(i) * kKStep + 4 * g;
-    if (i < ke) {
+    if (i < nfull) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) ld8(a[t], xa[t]);
     }
@@ -345,13 +334,13 @@ __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
     __syncthreads();
   }
   if (vec) {
-    for (; i < ke; i += ks) {
+    for (; i < nfull; i += kWaves) {
       Frags<NT> f;
       kstep_split<NT, CENTRED>(xa, cs + i * kKStep + 4 * g, kn, f);
       __builtin_amdgcn_sched_barrier(0);
       // unconditional (the last k-step re-reads itself, from L2): a load
       // under a branch would make the buffer a phi and cost a copy of it
-      const int64_t adv = i + ks < ke ? stp : 0;
+      const int64_t adv = i + kWaves < nfull ? stp : 0;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         a[t] += adv;
@@ -360,7 +349,6 @@ __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
       __builtin_amdgcn_sched_barrier(0);
       kstep_mfma<NT>(f, acc);
     }
-    // the partial last k-step (index nfull): wave nfull % 4
     i = nfull + ((wv - nfull) % kWaves + kWaves) % kWaves;
   }
   // unaligned rows: every k-step; aligned: the partial last one (if any)
@@ -633,17 +621,6 @@ size_t gram_ws_layout(int n, int64_t numel, int nseg, void *ws, GramWs *w) {
   return off;
 }
 
-// Each wave's k-steps: interleaved (v, v + 4, ...) or, blocked, a
-// contiguous quarter of the chunk.
-#ifdef FSAGG_PROBE
-static int gram_blocked() {   // probe build: FSAGG_PROBE_GRAM_BLOCKED=0/1
-  const char *e = getenv("FSAGG_PROBE_GRAM_BLOCKED");
-  return e && e[0] == '1';
-}
-#else
-static int gram_blocked() { return 0; }
-#endif
-
 template <int NT>
 void gram_launch(const float *const *tab, int64_t ss, int n,
                  const int64_t *seg_lo, const int64_t *seg_end, int nseg,
@@ -658,8 +635,7 @@ void gram_launch(const float *const *tab, int64_t ss, int n,
                      dim3(unsigned(pl.sample_chunks)), dim3(kBlk), 0, st,
                      tab, ss, n, seg_lo, seg_end, nseg, w.prefix_sample,
                      kSampleChunk, kSampleCoords,
-                     static_cast<const int *>(nullptr), w.partial,
-                     gram_blocked());
+                     static_cast<const int *>(nullptr), w.partial);
   hipLaunchKernelGGL((gram_reduce1_kernel<NT>),
                      dim3(unsigned(pl.sample_groups), unsigned(NTP)),
                      dim3(256), 0, st, w.partial, w.prefix_sample,
@@ -677,7 +653,7 @@ void gram_launch(const float *const *tab, int64_t ss, int n,
                      dim3(unsigned(pl.main_chunks)), dim3(kBlk), 0, st, tab,
                      ss, n, seg_lo, seg_end, nseg, w.prefix_main, pl.w,
                      int64_t(0), static_cast<const int *>(w.centre),
-                     w.partial, gram_blocked());
+                     w.partial);
   hipLaunchKernelGGL((gram_reduce1_kernel<NT>),
                      dim3(unsigned(pl.main_groups), unsigned(NTP)),
                      dim3(256), 0, st, w.partial, w.prefix_main,
