@@ -125,6 +125,8 @@ SIGNATURES['fsagg_online_inc_typed'] = (
 SIGNATURES['fsagg_rows_sqnorm_workspace_bytes'] = (_c_sz, [_c_i, _c_i])
 SIGNATURES['fsagg_rows_sqnorm_f32'] = (
     _c_i, [_rows_p, _c_p, _c_i, _c_p, _c_p, _c_sz, _c_p])
+SIGNATURES['fsagg_normbound_prescale_f32'] = (
+    _c_i, [_c_p, _c_i, _c_i, ctypes.c_float, _c_p, _c_p])
 
 FSAGG_MAX_PEERS = 8
 FSAGG_PAIRGRAM_MAX_CLIENTS = 64

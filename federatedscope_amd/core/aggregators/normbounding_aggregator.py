@@ -55,8 +55,9 @@ class NormboundingAggregator(ClientsAvgAggregator):
 
     def _aggregate_same_keys(self, models, init, out_dev):
         st = self._stage_all(models)
-        sq = self._sqnorms(st).sum(1).cpu().numpy()
-        pre = [1.0 if r is None else r for r in self._rates(sq)]
+        # the rates stay on the device: no host round trip between the norm
+        # pass and the weighted sum
+        pre = ops.normbound_prescale(self._sqnorms(st), self.norm_bound)
         weights = self._weights(models)
         layout, flat, extra, keys = self._weighted_avg_device(
             models, weights, as_float=True, base_model=init, prescale=pre,

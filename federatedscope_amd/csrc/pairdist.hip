@@ -1047,6 +1047,24 @@ __global__ __launch_bounds__(kBlock) void rows_sqnorm_final_kernel(
   if (lane == 0) sq[q] = t;
 }
 
+// One lane per client: the norm bounding rate from its per-key squared
+// norms (normbounding_aggregator.py:39-40).  norm = fl32(sqrt(Σ_s sq)) as
+// torch.norm returns it; the test `norm > bound` is fp32 against fp32 (a
+// 0-dim fp32 tensor against a Python float); the rate bound / norm is
+// Tensor.__rtruediv__ = fl32(fl32(1 / norm) · bound).  Unscaled clients get
+// 1.0 (fl32(x · 1) = x in the weighted sum's prescale).  fp32 division and
+// fp64 sqrt are correctly rounded (hipcc's defaults).
+__global__ __launch_bounds__(kBlock) void normbound_prescale_kernel(
+    const double *__restrict__ sq, int n, int nseg, float bound,
+    float *__restrict__ prescale) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  double t = 0.0;
+  for (int s = 0; s < nseg; ++s) t += sq[int64_t(i) * nseg + s];
+  const float norm = float(sqrt(t));
+  prescale[i] = norm > bound ? (1.0f / norm) * bound : 1.0f;
+}
+
 }  // namespace
 }  // namespace fsagg
 
@@ -1085,6 +1103,19 @@ extern "C" int fsagg_rows_sqnorm_f32(const fsagg_rows *rows,
                      dim3(unsigned((waves + per - 1) / per)), dim3(kBlock), 0,
                      s, chunks, nchunk, rows->n, rows->nseg, partial, sq);
   return check_launch("fsagg_rows_sqnorm_f32");
+}
+
+extern "C" int fsagg_normbound_prescale_f32(const double *sq, int n, int nseg,
+                                            float bound, float *prescale,
+                                            fsagg_stream_t stream) {
+  if (!sq || !prescale || n < 1 || nseg < 1) {
+    set_error("fsagg_normbound_prescale_f32: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  hipLaunchKernelGGL(normbound_prescale_kernel,
+                     dim3(unsigned((n + kBlock - 1) / kBlock)), dim3(kBlock),
+                     0, as_stream(stream), sq, n, nseg, bound, prescale);
+  return check_launch("fsagg_normbound_prescale_f32");
 }
 
 // chunks of the partial buffer

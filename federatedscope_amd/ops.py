@@ -1041,3 +1041,17 @@ def rows_sqnorm(rs, lo=0, hi=None, workspace=None):
         sq.data_ptr(), ws.data_ptr(), ws.numel(), _stream(rs.device)),
         'fsagg_rows_sqnorm_f32')
     return sq
+
+
+def normbound_prescale(sq, bound):
+    """Norm bounding's per-client scale (fp32 [n], device) from
+    :func:`rows_sqnorm`'s [n][nseg] fp64: fl32(fl32(1/norm)·fl32(bound))
+    where norm = fl32(sqrt(Σ sq)) > fl32(bound), else 1."""
+    lib = L.load()
+    if sq.dim() != 2 or sq.dtype != torch.float64 or not sq.is_contiguous():
+        raise ValueError('sq must be contiguous fp64 [n][nseg]')
+    pre = torch.empty(sq.shape[0], dtype=torch.float32, device=sq.device)
+    L.check(lib.fsagg_normbound_prescale_f32(
+        sq.data_ptr(), sq.shape[0], sq.shape[1], float(_np.float32(bound)),
+        pre.data_ptr(), _stream(sq.device)), 'fsagg_normbound_prescale_f32')
+    return pre

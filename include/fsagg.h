@@ -497,6 +497,16 @@ int fsagg_rows_sqnorm_f32(const fsagg_rows *rows, const fsagg_chunk *chunks,
                           int nchunk, double *sq, void *workspace,
                           size_t workspace_bytes, fsagg_stream_t stream);
 
+/* Norm bounding's per-client scale from sq [n][nseg] (device, as
+ * fsagg_rows_sqnorm_f32 writes it), on the device so the weighted sum that
+ * consumes it (its `prescale`) follows without a host round trip
+ * (normbounding_aggregator.py:39-40): norm = fl32(sqrt(Σ_s sq[i][s]));
+ * prescale[i] = fl32(fl32(1 / norm) · bound) if norm > bound (fp32
+ * compare), else 1.  ``bound`` is fl32 of the configured bound. */
+int fsagg_normbound_prescale_f32(const double *sq, int n, int nseg,
+                                 float bound, float *prescale,
+                                 fsagg_stream_t stream);
+
 /*
  * Peer assembly over xGMI (strong scaling across the GPUs of one node,
  * SURVEY §8(e)).  Each GPU owns a parameter range of every client, reduces

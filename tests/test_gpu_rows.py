@@ -160,6 +160,41 @@ def test_pairdist_rows(n):
         assert sq[i].sum() == pytest.approx((X[i] ** 2).sum(), rel=1e-12)
 
 
+@pytest.mark.parametrize('bound', [0.5, 1.0, 5.0, 3.3, 1e-3])
+def test_normbound_prescale_matches_host_rates(bound):
+    """fsagg_normbound_prescale_f32 against NormboundingAggregator._rates
+    (itself pinned bit for bit to torch's ``bound / torch.norm(x)``,
+    tests/test_server_logic.py): random norms around the bound, norms that
+    round to exactly fl32(bound) or one ulp either side, 0, inf and NaN;
+    the per-key sums added in the same order on both sides."""
+    from federatedscope_amd import ops
+    from federatedscope_amd.core.aggregators import NormboundingAggregator
+    rng = np.random.default_rng(int(bound * 1000))
+    b32 = np.float32(bound)
+    edge = [np.nextafter(b32, np.float32(0)), b32,
+            np.nextafter(b32, np.float32(np.inf))]
+    norms = np.concatenate([rng.uniform(0.0, 4.0 * bound, 4000),
+                            np.array(edge, dtype=np.float64)])
+    sq = np.zeros((norms.size + 3, 3))
+    sq[:norms.size, 0] = norms ** 2 * 0.25
+    sq[:norms.size, 1] = norms ** 2 * 0.5
+    sq[:norms.size, 2] = norms ** 2 * 0.25
+    sq[-2, 1] = np.inf
+    sq[-1, 2] = np.nan
+    cfg = SimpleNamespace(aggregator=SimpleNamespace(
+        BFT_args=SimpleNamespace(normbounding_norm_bound=bound)),
+        federate=SimpleNamespace(ignore_weight=False, use_ss=False))
+    agg = NormboundingAggregator(model=torch.nn.Linear(1, 1), config=cfg)
+    host = [1.0 if r is None else r for r in
+            agg._rates((sq[:, 0] + sq[:, 1]) + sq[:, 2])]
+    got = ops.normbound_prescale(torch.from_numpy(sq).cuda(), bound)
+    got = got.cpu().numpy()
+    want = np.array(host, dtype=np.float32)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), \
+        np.nonzero(got.view(np.uint32) != want.view(np.uint32))
+    assert got[-3] == 1.0 and got[-2] == 0.0 and got[-1] == 1.0
+
+
 def _cfg(**kw):
     bft = SimpleNamespace(krum_agg_num=kw.get('agg_num', 3),
                           trimmedmean_excluded_ratio=0.2,
