@@ -59,18 +59,28 @@ __device__ __forceinline__ bool same_bin(const RankSel &a, const RankSel &b) {
   return a.lo == b.lo && a.hi == b.hi;
 }
 
-// Octave digit of float bits u (monotone in the value):
-//   t = clamp(m(u) - base, 0, 127); digit = negative ? 127 - t : 128 + t
-// ((t ^ sign) + 128 with sign = -1 or 0: v_xad_u32).
-__device__ __forceinline__ uint32_t octave_digit(uint32_t u, int base) {
-  const int m = int(__builtin_amdgcn_ubfe(u, uint32_t(kMagShift), 11u));
-  const int t = min(max(m - base, 0), kCodes - 1);
-  return (uint32_t(t) ^ uint32_t(int32_t(u) >> 31)) + 128u;
+// Octave digit of float bits u (monotone in the value), base >= 0:
+//   t = max(m(u) - base, 0); digit = negative ? 127 - t : 128 + t
+// (t <= 127 because m(u) <= the column's largest code, which the launch
+// puts at most 127 above base; one saturating v_sub_u32 for the clamp;
+// (t ^ sign) + 128 with sign = -1 or 0: v_xad_u32).
+__device__ __forceinline__ uint32_t octave_digit(uint32_t u, uint32_t base) {
+  const uint32_t m = __builtin_amdgcn_ubfe(u, uint32_t(kMagShift), 11u);
+  const uint32_t t = __builtin_elementwise_sub_sat(m, base);
+  return (t ^ uint32_t(int32_t(u) >> 31)) + 128u;
+}
+
+// The digit base of a column whose largest magnitude bits are amax: its
+// code 127 digits up, clamped at 0 (a column of tiny values then uses the
+// codes from 0: still monotone, octave_bin takes the same base).
+__device__ __forceinline__ uint32_t octave_base(uint32_t amax) {
+  return uint32_t(max(int(amax >> kMagShift) - (kCodes - 1), 0));
 }
 
 // The key interval of octave digit d (given the launch's base).
-__device__ __forceinline__ void octave_bin(uint32_t d, int base, uint32_t &lo,
-                                           uint32_t &hi) {
+__device__ __forceinline__ void octave_bin(uint32_t d, uint32_t ubase,
+                                           uint32_t &lo, uint32_t &hi) {
+  const int base = int(ubase);
   const bool pos = d >= 128u;
   const int t = pos ? int(d) - 128 : 127 - int(d);
   const int mlo = t == 0 ? 0 : base + t;

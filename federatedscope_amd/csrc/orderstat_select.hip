@@ -72,7 +72,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
   }
   const bool nan = amax > 0x7F800000u;
   const bool nonfinite = amax >= 0x7F800000u;
-  const int obase = int(amax >> kMagShift) - (kCodes - 1);
+  const uint32_t obase = octave_base(amax);
   const int r1 = MODE == kMedian ? (n - 1) / 2 : kk;
   const int r2 = MODE == kMedian ? n / 2 : n - kk - 1;
 
