@@ -6,7 +6,7 @@
 // loads its n values with coalesced 4-B loads (64 consecutive coordinates per
 // wave-instruction, one row at a time) and maps them to order-preserving
 // uint32 keys.
-//  - n <= 64: the keys are sorted in registers by a bitonic network generated
+//  - n <= 64: the keys are sorted in registers by a sorting network generated
 //    at compile time as straight-line min/max code (padding keys 0xFFFFFFFF
 //    sort last).
 //  - 64 < n <= 255: range-adaptive radix select + LDS compaction
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_reg_kernel(
   // would be exposed at the end of every wave)
   const float bval = base ? gld_nt(base + p) : 0.0f;
   load_column<N>(br.rows, n, p, k, nan, nonfinite);
-  bitonic_sort<N>(k);
+  sort_network<N>(k);
   using Seq = std::make_integer_sequence<int, N>;
   float r;
   if constexpr (MODE == kMedian) {

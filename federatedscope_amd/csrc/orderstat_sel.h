@@ -274,7 +274,7 @@ __device__ __forceinline__ void list_select(const uint32_t *H, int cnt,
     const uint32_t x = ukey(H[i * kWave]);
     a[i] = i < cnt ? x : kPad;
   }
-  bitonic_sort<S>(a);
+  sort_network<S>(a);
   double acc = 0.0;
   if (SUM) {
     // [lo, hi] as one unsigned range test; an empty range (hi < lo) moves

@@ -26,7 +26,7 @@
 //  4. One compaction pass writes the keys of both bins to one per-lane LDS
 //     list (bin 1 before bin 2 in key order) and, for the trimmed mean, sums
 //     every value strictly between the bins in fp64.  The list is sorted with
-//     the smallest bitonic network that holds every lane's list and the ranks
+//     the smallest sorting network that holds every lane's list and the ranks
 //     (and the kept partial sums) read off.
 // Register budget: SEL_N values + ~40 within 256 VGPRs (2 waves per SIMD).
 #include "orderstat_sel.h"
