@@ -6,11 +6,12 @@
 // loads its n values with coalesced 4-B loads (64 consecutive coordinates per
 // wave-instruction, one row at a time) and maps them to order-preserving
 // uint32 keys.
-//  - n <= 64: the keys are sorted in registers by a sorting network generated
-//    at compile time as straight-line min/max code (padding keys 0xFFFFFFFF
-//    sort last).
-//  - 64 < n <= 255: range-adaptive radix select + LDS compaction
-//    (orderstat_select.hip, one translation unit per register-array size).
+//  - n <= 32 and 56 < n <= 64: the keys are sorted in registers by a sorting
+//    network generated at compile time as straight-line min/max code
+//    (padding keys 0xFFFFFFFF sort last).
+//  - 32 < n <= 56 and 64 < n <= 255: range-adaptive radix select + LDS
+//    compaction (orderstat_select.hip, one translation unit per
+//    register-array size).
 //  - 255 < n <= 65535: the same select streaming the column from memory in
 //    each pass (orderstat_stream.hip).
 //  - more than 65535 clients or 2^30 columns: bit-by-bit radix select that
@@ -164,10 +165,16 @@ int launch(const RowSrc &rs, int nchunk, int n, int kk, float divisor,
   else if (n <= 8) FSAGG_OS(8);
   else if (n <= 16) FSAGG_OS(16);
   else if (n <= 32) FSAGG_OS(32);
-  else if (n <= 64) FSAGG_OS(64);
+  // 33..56: the select kernel (n = 50: median −6 %, trimmed −11 % against
+  // the 64-key sort); 57..64 the sort (n = 64: equal or 4 % faster)
+  else if (n <= 64 && (n > 56 || rs.numel > (int64_t(1) << 30)))
+    FSAGG_OS(64);
 #define FSAGG_RX(NN) launch_select<NN, MODE>(rs, grid, n, kk, divisor, out, s)
   else if (n <= 255 && rs.numel <= (int64_t(1) << 30)) {
     switch ((n + kSelStep - 1) / kSelStep * kSelStep) {
+    case 40: FSAGG_RX(40); break;
+    case 48: FSAGG_RX(48); break;
+    case 56: FSAGG_RX(56); break;
     case 72: FSAGG_RX(72); break;
     case 80: FSAGG_RX(80); break;
     case 88: FSAGG_RX(88); break;

@@ -1,6 +1,7 @@
 // Internal to libfsagg: device helpers of the radix-select order-statistic
-// kernels — the register form (orderstat_select.hip, 64 < n <= 255) and the
-// streaming form (orderstat_stream.hip, n > 255).  Not part of the public ABI.
+// kernels — the register form (orderstat_select.hip, 32 < n <= 56 and
+// 64 < n <= 255) and the streaming form (orderstat_stream.hip, n > 255).
+// Not part of the public ABI.
 #pragma once
 
 #include "orderstat.h"

@@ -98,12 +98,13 @@ def test_weighted_sum_row_order_is_reduction_order():
     assert b.cpu().numpy().tobytes() == wb.tobytes()
 
 
-@pytest.mark.parametrize('n', [1, 2, 3, 4, 7, 8, 31, 64, 65, 72, 73, 100,
-                               127, 200, 233, 250, 255, 256, 257, 300, 511,
-                               1000, 2049])
+@pytest.mark.parametrize('n', [1, 2, 3, 4, 7, 8, 31, 32, 33, 40, 41, 48, 50,
+                               56, 57, 64, 65, 72, 73, 100, 127, 200, 233,
+                               250, 255, 256, 257, 300, 511, 1000, 2049])
 def test_median_trimmed_all_kernels(n):
-    """Every order-statistic kernel (register network n <= 64, register
-    select 64 < n <= 255, streaming select n > 255) against the oracle on
+    """Every order-statistic kernel (register network n <= 32 and
+    56 < n <= 64, register select 32 < n <= 56 and 64 < n <= 255, streaming
+    select n > 255) against the oracle on
     ties, signed zeros and columns spanning > 16 octaves (the refinement
     rounds)."""
     from federatedscope_amd import ops
