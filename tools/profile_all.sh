@@ -14,3 +14,4 @@ prof() {  # prof <name> <cmd...>
 prof bench python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline
 prof robust python3 tools/bench_robust.py
 prof wire python3 tools/bench_wire.py ss dissim
+prof smalln python3 tools/bench_smalln.py
