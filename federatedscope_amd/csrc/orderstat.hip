@@ -58,7 +58,14 @@ __global__ __launch_bounds__(kBlock) void orderstat_reg_kernel(
   // would be exposed at the end of every wave)
   const float bval = base ? gld_nt(base + p) : 0.0f;
   load_column<N>(br.rows, n, p, k, nan, nonfinite);
-  sort_network<N>(k);
+  if constexpr (MODE == kMedian) {
+    // the two middle positions of every n this size serves: n <= 4 at
+    // N = 4, N/2 < n <= N otherwise, and 32 < n <= 64 at N = 64 (launch)
+    constexpr int lo = N <= 4 ? 0 : (N == 64 ? 16 : N / 4);
+    select_network<N, lo, N / 2>(k);
+  } else {
+    sort_network<N>(k);
+  }
   using Seq = std::make_integer_sequence<int, N>;
   float r;
   if constexpr (MODE == kMedian) {
