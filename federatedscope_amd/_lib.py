@@ -142,6 +142,8 @@ SIGNATURES['fsagg_peer_can_access'] = (_c_i, [_c_i, ctypes.c_char_p])
 SIGNATURES['fsagg_weighted_sum_bcast_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i, _c_i64, _c_p, ctypes.POINTER(_c_p), _c_i,
            _c_p])
+SIGNATURES['fsagg_peer_push_f32'] = (
+    _c_i, [_c_p, ctypes.POINTER(_c_p), _c_i, _c_i64, _c_p])
 SIGNATURES['fsagg_peer_barrier'] = (
     _c_i, [ctypes.POINTER(_c_p), _c_i, _c_i, _c_u32, ctypes.c_uint64, _c_p,
            _c_p])

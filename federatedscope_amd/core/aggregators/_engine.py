@@ -123,20 +123,49 @@ class DeviceEngine:
         return comm, int(getattr(agg, 'shard_chunks', 2) or 1)
 
     def _plan(self, layout, comm, chunks):
-        from ..sharding import PipelinedAssembly
-        key = (layout.signature(), chunks)
+        """The assembly of a sharded call, cached per layout.
+        ``aggregator.shard_assembly``: 'auto' (default) — the peer assembly
+        (each rank's kernel stores its piece into every GPU's copy over
+        xGMI, then a flag barrier: core/sharding.PeerAssembly), or, when the
+        ranks agree it cannot be set up (a GPU that cannot reach a peer, no
+        IPC), the pipelined all-gathers; 'p2p' — the peer assembly or an
+        error; 'rccl' — the pipelined all-gathers."""
+        from ..sharding import PeerAssembly, PipelinedAssembly
+        agg = getattr(getattr(self, 'cfg', None), 'aggregator', None)
+        mode = str(getattr(agg, 'shard_assembly', 'auto') or 'auto')
+        if mode not in ('auto', 'p2p', 'rccl'):
+            raise ValueError("aggregator.shard_assembly must be 'auto', "
+                             "'p2p' or 'rccl', got %r" % mode)
+        key = (layout.signature(), chunks, mode)
         pa = self._plans.get(key)
+        if pa is not None:
+            return pa
+        if mode != 'rccl':
+            try:
+                # collective: every rank takes the same branch (the
+                # constructor agrees on success or failure across ranks)
+                pa = PeerAssembly(
+                    layout.numel, comm=comm, device=self.compute_device,
+                    timeout_s=getattr(agg, 'shard_peer_timeout_s', None))
+            except Exception:  # noqa: BLE001 (agreed by every rank)
+                if mode == 'p2p':
+                    raise
+                pa = None
         if pa is None:
-            pa = self._plans[key] = PipelinedAssembly(layout.numel,
-                                                      chunks=chunks,
-                                                      comm=comm)
+            pa = PipelinedAssembly(layout.numel, chunks=chunks, comm=comm)
+        self._plans[key] = pa
         return pa
 
-    def _run_pieces(self, st, fn):
+    def _run_pieces(self, st, fn, bcast=None):
         """Flat result bucket on the compute device from fn(rows, out, lo,
-        hi) over the set's pieces; sharded, the ranks' pieces are
-        all-gathered (the gather of round j overlapping round j+1) so every
-        rank holds the whole bucket.  Coordinates are bucket coordinates."""
+        hi) over the set's pieces; sharded, every rank ends up holding the
+        whole bucket: the peer assembly stores each rank's piece into every
+        GPU's copy (``bcast(rows, out, peers, lo, hi)`` — a kernel whose
+        epilogue does that itself, returning False when it has no such form
+        — or fn followed by a push), the pipelined assembly all-gathers the
+        pieces (the gather of round j overlapping round j+1).  Coordinates
+        are bucket coordinates."""
+        from ..sharding import PeerAssembly
         dev = self.compute_device
         if st.plan is None:
             out = torch.empty(st.layout.numel, dtype=torch.float32,
@@ -144,6 +173,15 @@ class DeviceEngine:
             for _, lo, hi, rs in st.pieces:
                 fn(rs, out, lo, hi)
             return out
+        if isinstance(st.plan, PeerAssembly):
+            rows = st.pieces[0][3]
+
+            def compute(lo, hi, own, peers):
+                if bcast is not None and bcast(rows, own, peers, lo, hi):
+                    return True
+                fn(rows, own, lo, hi)
+                return False
+            return st.plan.run_bucket(compute)
         out = torch.empty(st.plan.padded, dtype=torch.float32, device=dev)
         rows = {j: rs for j, _, _, rs in st.pieces}
         st.plan.run(lambda j, lo, hi, view: fn(rows[j], out, lo, hi),
@@ -327,8 +365,12 @@ class DeviceEngine:
         base = None
         if base_model is not None:
             base = self._base(layout, base_model, as_float=as_float)
-        out = self._run_pieces(st, lambda rs, o, lo, hi: ops.weighted_sum_rows(
-            rs, weights, o, prescale=prescale, base=base, lo=lo, hi=hi))
+        out = self._run_pieces(
+            st, lambda rs, o, lo, hi: ops.weighted_sum_rows(
+                rs, weights, o, prescale=prescale, base=base, lo=lo, hi=hi),
+            bcast=lambda rs, o, peers, lo, hi: ops.weighted_sum_rows_bcast(
+                rs, weights, o, peers, prescale=prescale, base=base, lo=lo,
+                hi=hi))
         extra = OrderedDict()
         for k, dt in layout.other.items():
             have = [i for i in range(n) if k in dicts[i]]

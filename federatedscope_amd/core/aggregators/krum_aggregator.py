@@ -60,7 +60,9 @@ class KrumAggregator(ClientsAvgAggregator):
         self.last_selection = sel
         sizes = [models[i][0] for i in sel]
         weights = fedavg_weights(sizes, self.cfg.federate.ignore_weight)
-        out = self._run_pieces(st.subset(sel), lambda rs, o, lo, hi:
-                               ops.weighted_sum_rows(rs, weights, o,
-                                                     base=base, lo=lo, hi=hi))
+        out = self._run_pieces(
+            st.subset(sel), lambda rs, o, lo, hi: ops.weighted_sum_rows(
+                rs, weights, o, base=base, lo=lo, hi=hi),
+            bcast=lambda rs, o, peers, lo, hi: ops.weighted_sum_rows_bcast(
+                rs, weights, o, peers, base=base, lo=lo, hi=hi))
         return layout, out, list(models[0][1].keys())

@@ -336,8 +336,12 @@ class PeerAssembly:
     The output copies are double-buffered (round k writes buffer k mod 2): a
     rank can be one round ahead, and the barrier of round k + 1 proves that
     every rank has finished round k — so a rank never writes into a buffer a
-    peer is still reading.  Results of :meth:`run` stay valid until the next
-    call but one; callers that keep them longer copy them out.
+    peer is still reading.  A result of :meth:`run` is valid until this
+    rank's next :meth:`run`, and only for reads enqueued on the stream
+    before it: once this rank reaches barrier k + 1, a peer may start round
+    k + 2 and store into the buffer of round k.  :meth:`run_bucket` (the
+    Aggregator.aggregate() path) copies the assembled bucket out before it
+    returns.
 
     Uploads stay where they are: each rank reads only its range of every
     client (device-resident, as in the reference's multi-GPU mode where
@@ -349,8 +353,10 @@ class PeerAssembly:
     STATUS = 32
 
     def __init__(self, numel, comm=None, device=None, align=ALIGN,
-                 group=None, buffers=2):
+                 group=None, buffers=2, timeout_s=None):
         from .. import _lib as L
+        if timeout_s is not None:
+            self.TIMEOUT_S = float(timeout_s)
         self.comm = comm if comm is not None else Comm(group)
         self.world = self.comm.world
         self.rank = self.comm.rank
@@ -475,12 +481,16 @@ class PeerAssembly:
         lo = r * self.pc
         return min(lo, self.numel), min(lo + self.pc, self.numel)
 
+    def local_pieces(self):
+        """This rank's pieces of the bucket (one), as PipelinedAssembly."""
+        return [self.piece()]
+
     def run(self, compute):
         """compute(lo, hi, outs) launches, on the current stream, the
         reduction of this rank's piece [lo, hi) into every address of
         ``outs`` (own buffer first, then the peers'; hi − lo floats each).
         Returns this GPU's assembled [numel] result (valid until the next
-        run() but one)."""
+        run(), see the class docstring)."""
         b = self.epoch % len(self.buffers)
         self.epoch += 1
         lo, hi = self.piece()
@@ -489,13 +499,46 @@ class PeerAssembly:
             outs = [self._ptr[(self.rank + k) % W][b] + 4 * lo
                     for k in range(W)]
             compute(lo, hi, outs)
+        self._barrier()
+        return self.buffers[b][:self.numel]
+
+    def run_bucket(self, compute):
+        """The Aggregator.aggregate() form.  ``compute(lo, hi, own, peers)``
+        reduces this rank's piece [lo, hi) of the bucket into ``own`` (this
+        GPU's copy, a [padded] fp32 tensor in bucket coordinates) on the
+        current stream; ``peers`` are the device addresses of the other
+        GPUs' copies (same coordinates).  It returns True when its kernel
+        stored the piece into the peers' copies itself (the fused broadcast
+        epilogue of FedAvg), else the piece is pushed to them here
+        (fsagg_peer_push_f32).  After the flag barrier the assembled bucket
+        is copied into a fresh tensor — the caller owns it, the rotating
+        copies are reused — and the barrier's status is checked (raises if
+        a peer never arrived)."""
+        from .. import ops
+        b = self.epoch % len(self.buffers)
+        self.epoch += 1
+        lo, hi = self.piece()
+        W = self.world
+        own = self.buffers[b]
+        peers = [self._ptr[(self.rank + k) % W][b] for k in range(1, W)]
+        if hi > lo:
+            if not compute(lo, hi, own, peers) and peers:
+                ops.peer_push(own.data_ptr() + 4 * lo,
+                              [p + 4 * lo for p in peers], hi - lo,
+                              self.device)
+        self._barrier()
+        res = torch.empty(self.numel, dtype=torch.float32, device=self.device)
+        res.copy_(own[:self.numel])
+        self.check()
+        return res
+
+    def _barrier(self):
         st = torch.cuda.current_stream(self.device).cuda_stream
         ticks = int(self.TIMEOUT_S * 1e8)
         self._L.check(self._lib.fsagg_peer_barrier(
-            self._flags, W, self.rank, self.epoch & 0xFFFFFFFF, ticks,
-            self.ctrl.data_ptr() + 4 * self.STATUS, st or None),
+            self._flags, self.world, self.rank, self.epoch & 0xFFFFFFFF,
+            ticks, self.ctrl.data_ptr() + 4 * self.STATUS, st or None),
             'fsagg_peer_barrier')
-        return self.buffers[b][:self.numel]
 
     def check(self):
         """Raise if a barrier gave up waiting for a peer (synchronises)."""

@@ -51,6 +51,29 @@ __global__ void peer_barrier_kernel(Flags f, int world, int rank,
   }
 }
 
+struct Dsts {
+  float *p[FSAGG_MAX_PEERS];
+};
+
+// The peer assembly's epilogue for reductions without a fused broadcast
+// (order statistics, row-set averages): this rank's finished piece is read
+// once and stored into each peer's copy (16-B vector stores over xGMI).
+__global__ __launch_bounds__(256) void peer_push_kernel(const float *src,
+                                                        Dsts d, int nd,
+                                                        int64_t n) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  const int64_t n4 = n / 4;
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n4;
+       i += stride) {
+    const f32x4 v = reinterpret_cast<const f32x4 *>(src)[i];
+    for (int k = 0; k < nd; ++k) reinterpret_cast<f32x4 *>(d.p[k])[i] = v;
+  }
+  const int64_t t = 4 * n4 + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t < n)
+    for (int k = 0; k < nd; ++k) d.p[k][t] = src[t];
+}
+
 int hip_fail(const char *what, hipError_t e) {
   set_error("%s: %s", what, hipGetErrorString(e));
   return FSAGG_EHIP;
@@ -153,6 +176,33 @@ extern "C" int fsagg_peer_can_access(int device, const char *peer_bus_id) {
   hipError_t e = hipDeviceCanAccessPeer(&ok, device, peer);
   if (e != hipSuccess) return hip_fail("fsagg_peer_can_access", e);
   return ok ? 1 : 0;
+}
+
+extern "C" int fsagg_peer_push_f32(const float *src, float *const *dsts,
+                                   int ndst, int64_t n,
+                                   fsagg_stream_t stream) {
+  if (!src || !dsts || ndst < 0 || ndst > FSAGG_MAX_PEERS || n < 0 ||
+      !aligned16(src)) {
+    set_error("fsagg_peer_push_f32: invalid argument (ndst=%d n=%lld)", ndst,
+              static_cast<long long>(n));
+    return FSAGG_EINVAL;
+  }
+  Dsts d{};
+  for (int k = 0; k < ndst; ++k) {
+    if (!dsts[k] || !aligned16(dsts[k])) {
+      set_error("fsagg_peer_push_f32: destination %d is NULL or not 16-byte "
+                "aligned", k);
+      return FSAGG_EINVAL;
+    }
+    d.p[k] = dsts[k];
+  }
+  if (n == 0 || ndst == 0) return FSAGG_OK;
+  int64_t blocks = (n / 4 + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 4 * int64_t(device_cu_count())) blocks = 4 * device_cu_count();
+  hipLaunchKernelGGL(peer_push_kernel, dim3(unsigned(blocks)), dim3(256), 0,
+                     as_stream(stream), src, d, ndst, n);
+  return check_launch("fsagg_peer_push_f32");
 }
 
 extern "C" int fsagg_peer_barrier(uint32_t *const *flags, int world, int rank,

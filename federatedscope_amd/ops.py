@@ -258,6 +258,18 @@ def weighted_sum_bcast(rows, weights, outs, prescale=None, base=None,
         arr, len(outs), st), 'fsagg_weighted_sum_bcast_f32')
 
 
+def peer_push(src, dsts, n, device, stream=None):
+    """Store ``n`` fp32 from device address ``src`` into each device address
+    of ``dsts`` (peer copies of the output; fsagg_peer_push_f32)."""
+    if not 0 <= len(dsts) <= L.FSAGG_MAX_PEERS:
+        raise ValueError('0..%d destinations, got %d' % (L.FSAGG_MAX_PEERS,
+                                                         len(dsts)))
+    arr = (ctypes.c_void_p * max(len(dsts), 1))(*[int(p) for p in dsts])
+    st = stream if stream is not None else _stream(device)
+    L.check(L.load().fsagg_peer_push_f32(int(src), arr, len(dsts), int(n),
+                                         st), 'fsagg_peer_push_f32')
+
+
 _TYPED = {
     torch.float16: (L.FSAGG_F16, torch.float16),
     torch.bfloat16: (L.FSAGG_BF16, torch.bfloat16),
@@ -848,8 +860,7 @@ def weighted_sum_rows(rs, weights, out, prescale=None, base=None, lo=0,
                          'tensors')
     _rows_out(rs, out, ALIGN_BYTES)
     lib = L.load()
-    if rs.nseg == 1 and not rs.missing and rs.layout.keys and (
-            base is None or base.host is not None):
+    if _flat_rows(rs, base):
         # one key, every client holding it (a flat model, configs[2]): the
         # row set IS a row table — the flat streaming kernel runs on it
         # directly, without the chunk list
@@ -876,7 +887,34 @@ def weighted_sum_rows(rs, weights, out, prescale=None, base=None, lo=0,
     return out
 
 
-def _weighted_sum_rows_flat(rs, weights, out, prescale, base, lo, hi, lib):
+def _flat_rows(rs, base):
+    """Whether a row set runs the flat streaming kernel (one key, every
+    client holding it)."""
+    return rs.nseg == 1 and not rs.missing and bool(rs.layout.keys) and (
+        base is None or base.host is not None)
+
+
+def weighted_sum_rows_bcast(rs, weights, out, peers, prescale=None,
+                            base=None, lo=0, hi=None):
+    """:func:`weighted_sum_rows` whose result also lands in the peer copies
+    ``peers`` (device addresses of other GPUs' output buckets, same
+    coordinates) from the reducing kernel's own epilogue
+    (fsagg_weighted_sum_bcast_f32, core/sharding.PeerAssembly).  Returns
+    False, computing nothing, when the row set has no fused form (several
+    keys or absent keys): the caller then computes and pushes."""
+    if len(weights) != rs.n:
+        raise ValueError('%d weights for %d rows' % (len(weights), rs.n))
+    if not (rs.aligned16 and _flat_rows(rs, base)) or \
+            len(peers) + 1 > L.FSAGG_MAX_PEERS:
+        return False
+    _rows_out(rs, out, ALIGN_BYTES)
+    _weighted_sum_rows_flat(rs, weights, out, prescale, base, lo, hi,
+                            L.load(), peers=peers)
+    return True
+
+
+def _weighted_sum_rows_flat(rs, weights, out, prescale, base, lo, hi, lib,
+                            peers=None):
     k = rs.layout.keys[0]
     o, m = rs.layout.offsets[k], rs.layout.numels[k]
     a = max(int(lo), o)
@@ -903,6 +941,15 @@ def _weighted_sum_rows_flat(rs, weights, out, prescale, base, lo, hi, lib):
         bptr = int(base.host[0]) + 4 * a
         if bptr % ALIGN_BYTES:
             raise ValueError('base is not 16-byte aligned at %d' % a)
+    if peers is not None:
+        outs = [out.data_ptr() + 4 * a] + [int(p) + 4 * a for p in peers]
+        arr = (ctypes.c_void_p * len(outs))(*outs)
+        L.check(lib.fsagg_weighted_sum_bcast_f32(
+            table.data_ptr(), w.data_ptr(),
+            pre.data_ptr() if pre is not None else None, rs.n, b - a, bptr,
+            arr, len(outs), _stream(rs.device)),
+            'fsagg_weighted_sum_bcast_f32')
+        return out
     L.check(lib.fsagg_weighted_sum_f32(
         table.data_ptr(), w.data_ptr(),
         pre.data_ptr() if pre is not None else None, rs.n, b - a, bptr,

@@ -535,6 +535,12 @@ int fsagg_normbound_prescale_f32(const double *sq, int n, int nseg,
  *                    `nout` (<= FSAGG_MAX_PEERS) outputs: outs is a HOST
  *                    array of device pointers (own and peer buffers, each
  *                    16-byte aligned), every one receiving the same bits.
+ * fsagg_peer_push_f32  the epilogue of the rules without a fused broadcast
+ *                    (order statistics, row-set averages through
+ *                    Aggregator.aggregate()): src[0, n) — this rank's
+ *                    finished piece in its own copy — stored into each of
+ *                    the `ndst` peer copies (dsts: a HOST array of device
+ *                    pointers, all 16-byte aligned, like src).
  * fsagg_peer_barrier  after the bcast kernel, on the same stream: stores
  *                    `epoch` into every rank's flag word for `rank`
  *                    (flags[r] = rank r's array of `world` uint32, own and
@@ -559,6 +565,8 @@ int fsagg_weighted_sum_bcast_f32(const float *const *rows,
                                  int n, int64_t numel, const float *base,
                                  float *const *outs, int nout,
                                  fsagg_stream_t stream);
+int fsagg_peer_push_f32(const float *src, float *const *dsts, int ndst,
+                        int64_t n, fsagg_stream_t stream);
 int fsagg_peer_barrier(uint32_t *const *flags, int world, int rank,
                        uint32_t epoch, uint64_t timeout_ticks,
                        uint32_t *status, fsagg_stream_t stream);

@@ -1,0 +1,131 @@
+"""Rank body of tests/test_gpu_world2.py's peer-assembly cases (run under
+torch.distributed.run, gloo for the handle exchange, every rank on the
+box's one GPU: same-device IPC stands in for the xGMI peers).
+
+argv[1] = 'aggregate': the drop-in aggregators with
+``aggregator.shard_by_param_range`` and ``shard_assembly = 'p2p'`` on
+device-resident client dicts — FedAvg on one key (the fused broadcast
+epilogue), FedAvg on several keys, median, trimmed mean, Krum (the pushed
+piece) — every rank's result bit-identical to the unsharded aggregate() on
+the same dicts.
+
+argv[1] = 'lost': rank 1 never runs its round; rank 0's flag barrier must
+give up within the timeout, ``run_bucket`` must raise, and both ranks must
+release the peer buffers and exit cleanly."""
+import json
+import os
+import sys
+import time
+from collections import OrderedDict
+from types import SimpleNamespace
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def cfg(sharded, f=0, agg_num=1, ratio=0.2, n=1000):
+    bft = SimpleNamespace(krum_agg_num=agg_num,
+                          trimmedmean_excluded_ratio=ratio,
+                          normbounding_norm_bound=1.0)
+    agg = SimpleNamespace(byzantine_node_num=f, BFT_args=bft,
+                          shard_by_param_range=sharded,
+                          shard_assembly='p2p', shard_chunks=2)
+    return SimpleNamespace(
+        federate=SimpleNamespace(ignore_weight=False, use_ss=False,
+                                 client_num=n, sample_client_rate=1.0),
+        aggregator=agg)
+
+
+class DictModel(torch.nn.Module):
+    def __init__(self, sd):
+        super().__init__()
+        self.sd = sd
+
+    def state_dict(self, *a, **kw):
+        return self.sd
+
+
+def clients(shapes, n, seed):
+    g = torch.Generator(device='cuda').manual_seed(seed)
+    return [(int(1 + (7 * i) % 13), OrderedDict(
+        (k, torch.randn(s, device='cuda', generator=g))
+        for k, s in shapes)) for i in range(n)]
+
+
+def aggregate_mode(rank, world):
+    from federatedscope_amd.core.aggregators import (ClientsAvgAggregator,
+                                                     KrumAggregator,
+                                                     MedianAggregator,
+                                                     TrimmedmeanAggregator)
+    from federatedscope_amd.core.sharding import PeerAssembly
+    done = []
+    one = [('w', (1_000_003, ))]
+    multi = [('a', (300_001, )), ('b', (64, 70)), ('c', (1, )),
+             ('d', (70_000, ))]
+    init1 = OrderedDict((k, torch.randn(s, device='cuda')) for k, s in one)
+    initm = OrderedDict((k, torch.randn(s, device='cuda')) for k, s in multi)
+    cases = [
+        ('fedavg_one_key', ClientsAvgAggregator, one, None, {}, 20),
+        ('fedavg_multi_key', ClientsAvgAggregator, multi, None, {}, 20),
+        ('median', MedianAggregator, multi, initm, {'f': 1}, 21),
+        ('trimmed_mean', TrimmedmeanAggregator, one, init1, {'f': 1}, 30),
+        ('krum', KrumAggregator, multi, initm, {'f': 2, 'agg_num': 3}, 12),
+    ]
+    for name, cls, shapes, init, kw, n in cases:
+        fb = clients(shapes, n, seed=len(name) + n)
+        info = {'client_feedback': fb, 'recover_fun': None}
+        model = DictModel(init) if init is not None else None
+        a = cls(model=model, device='cuda', config=cfg(True, **kw))
+        b = cls(model=model, device='cuda', config=cfg(False, **kw))
+        for rnd in range(3):       # rounds rotate the double buffers
+            got = a.aggregate(info)
+            want = b.aggregate(info)
+            for k in want:
+                assert torch.equal(got[k], want[k]), (name, k, rnd)
+        assert all(isinstance(p, PeerAssembly) for p in a._plans.values())
+        if name == 'krum':
+            assert a.last_selection == b.last_selection
+        done.append(name)
+    return {'ok': done}
+
+
+def lost_mode(rank, world):
+    from federatedscope_amd.core.sharding import Comm, PeerAssembly
+    pa = PeerAssembly(4096, comm=Comm(), device=torch.device('cuda', 0),
+                      timeout_s=1.0)
+    raised = None
+    t0 = time.time()
+    def compute(lo, hi, own, peers):
+        own[lo:hi].fill_(1.0)
+        return False
+
+    if rank == 0:
+        try:
+            pa.run_bucket(compute)
+        except RuntimeError as e:
+            raised = str(e)
+    waited = time.time() - t0
+    dist.barrier()
+    pa.close()
+    return {'raised': raised, 'waited_s': round(waited, 3)}
+
+
+def main():
+    dist.init_process_group('gloo')
+    rank, world = dist.get_rank(), dist.get_world_size()
+    torch.cuda.set_device(0)
+    mode = sys.argv[1]
+    res = aggregate_mode(rank, world) if mode == 'aggregate' else \
+        lost_mode(rank, world)
+    res.update(rank=rank, world=world, mode=mode)
+    sys.stdout.write(json.dumps(res) + '\n')
+    sys.stdout.flush()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,5 +1,8 @@
 """Rank body of tests/test_gpu_world2.py (run under torch.distributed.run
-with the gloo backend: two ranks sharing the box's one GPU).
+with the gloo backend: two ranks sharing the box's one GPU).  argv[1]:
+the assembly (``aggregator.shard_assembly``), 'rccl' (pipelined
+all-gathers) or 'p2p' (peer assembly: IPC-imported output copies, stores
+from the reducing kernel or a push, flag barrier).
 
 Every rank builds the drop-in aggregators with
 ``aggregator.shard_by_param_range`` and calls aggregate() on the same client
@@ -33,9 +36,12 @@ def main():
         BulyanAggregator, ClientsAvgAggregator, KrumAggregator,
         MedianAggregator, NormboundingAggregator, TrimmedmeanAggregator)
 
+    mode = sys.argv[1] if len(sys.argv) > 1 else 'rccl'
+
     def sharded(c, chunks=2):
         c.aggregator.shard_by_param_range = True
         c.aggregator.shard_chunks = chunks
+        c.aggregator.shard_assembly = mode
         return c
 
     done = []
@@ -111,7 +117,13 @@ def main():
     for k in b:
         assert torch.equal(a[k], b[k]), k
     done.append('synthetic')
-    sys.stdout.write(json.dumps({'rank': rank, 'world': world, 'ok': done})
+    from federatedscope_amd.core.sharding import (PeerAssembly,
+                                                  PipelinedAssembly)
+    kind = PeerAssembly if mode == 'p2p' else PipelinedAssembly
+    plans = [p for p in agg._plans.values()]
+    assert plans and all(isinstance(p, kind) for p in plans), plans
+    sys.stdout.write(json.dumps({'rank': rank, 'world': world, 'ok': done,
+                                 'mode': mode})
                      + '\n')  # one write: the ranks share the pipe
     sys.stdout.flush()
     dist.barrier()

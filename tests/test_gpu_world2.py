@@ -83,8 +83,38 @@ def test_bench_peer_assembly(world, clients, params):
     assert r['assembled_bit_exact'] is True
 
 
-def test_sharded_aggregators_world2():
-    recs = _run2([os.path.join('tests', '_world2_worker.py')])
+@pytest.mark.parametrize('mode', ['rccl', 'p2p'])
+def test_sharded_aggregators_world2(mode):
+    """The reference's goldens through aggregate() sharded over two ranks,
+    assembled by the pipelined all-gathers ('rccl') and by the peer
+    assembly ('p2p')."""
+    recs = _run2([os.path.join('tests', '_world2_worker.py'), mode])
     assert sorted(r['rank'] for r in recs) == [0, 1]
     for r in recs:
         assert 'synthetic' in r['ok'] and len(r['ok']) >= 18, r
+        assert r['mode'] == mode
+
+
+@pytest.mark.parametrize('world', [2, 4])
+def test_peer_assembly_aggregate(world):
+    """aggregate() on device dicts through the peer assembly (fused
+    broadcast for one-key FedAvg, pushed pieces for the other rules), three
+    rounds each: bit-identical to the unsharded call on every rank."""
+    recs = _run2([os.path.join('tests', '_peer_worker.py'), 'aggregate'],
+                 nproc=world)
+    assert sorted(r['rank'] for r in recs) == list(range(world))
+    for r in recs:
+        assert r['ok'] == ['fedavg_one_key', 'fedavg_multi_key', 'median',
+                           'trimmed_mean', 'krum'], r
+
+
+def test_peer_assembly_lost_rank():
+    """Rank 1 never runs its round: rank 0's barrier gives up after the 1 s
+    timeout, run_bucket raises naming rank 1, and both ranks release the
+    peer buffers and exit 0."""
+    recs = _run2([os.path.join('tests', '_peer_worker.py'), 'lost'])
+    by = {r['rank']: r for r in recs}
+    assert set(by) == {0, 1}
+    assert by[1]['raised'] is None
+    assert 'rank 1' in (by[0]['raised'] or ''), by[0]
+    assert 0.9 <= by[0]['waited_s'] <= 30.0, by[0]
