@@ -115,6 +115,9 @@ SIGNATURES['fsagg_trimmed_mean_rows_f32'] = (
 SIGNATURES['fsagg_pairgram_workspace_bytes'] = (_c_sz, [_c_i, _c_i64, _c_i])
 SIGNATURES['fsagg_pairgram_rows_segsq_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_sz, _c_p])
+SIGNATURES['fsagg_pairgram_rows_f32'] = (
+    _c_i, [_c_p, _c_p, _c_p, _c_i64, ctypes.c_double, _c_p, _c_p, _c_p, _c_p,
+           _c_p, _c_sz, _c_p])
 SIGNATURES['fsagg_pairgram_finish_f32'] = (
     _c_i, [_c_p, _c_p, _c_i, _c_i, ctypes.c_double, _c_p, _c_p, _c_p])
 SIGNATURES['fsagg_pairdist_rows_segsq_f32'] = (

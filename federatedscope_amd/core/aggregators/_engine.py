@@ -223,6 +223,9 @@ class DeviceEngine:
                              device=self.compute_device)
             st.plan.comm.all_reduce_sum(v)
             gram = int(v.item()) == st.plan.comm.world
+        if gram and st.plan is None:
+            buf, _, _, _ = ops.pairgram_rows_dist(st.rows(), _GRAM_TOL)
+            return _PendingD(self, st, buf=buf)
         if gram:
             sq2 = self._sum_pieces(
                 st, lambda rs, lo, hi: ops.pairgram_rows_segsq(rs, lo, hi))

@@ -11,9 +11,11 @@
 // * Every fp32 value is split exactly into three bf16 limbs, x = h + m + l
 //   (each the round-to-nearest bf16 of what the previous ones leave; the
 //   residuals x − h and x − h − m are exact in fp32 and come from one
-//   v_dot2c_f32_bf16 each).  The six limb products of weight >= 2^-16 (hh,
-//   hm, mh, hl, lh, mm) are exact in the MFMA; the dropped ones are
-//   < 2^-24 of |x_a·x_b|.  Each k-step's six products of a tile pair are
+//   v_dot2c_f32_bf16 each; x − h holds at most 16 significant bits and
+//   x − h − m at most 8, so l takes the rest exactly).  The six limb
+//   products of weight >= 2^-16 (hh, hm, mh, hl, lh, mm) are exact in the
+//   MFMA; the dropped ones (ml, lm, ll) are <= 2.02·2^-24 of |x_a·x_b|.
+//   Each k-step's six products of a tile pair are
 //   chained through the MFMA in fp32 (small limbs first) and added into fp64
 //   accumulators; the four waves of a workgroup are summed in LDS and the
 //   chunks of a key in fp64 in a fixed order (deterministic).
@@ -24,12 +26,13 @@
 //   the smallest sum of distances to the others over a sample of the
 //   coordinates (the first kSampleCoords of every key) — a central client,
 //   so (G'_aa + G'_bb) / d² stays O(1) for every pair near the centre.
-//   Every per-key d² leaves with a predicted error bound err (the fp32
-//   roundings of the k-step sums), and fsagg_pairgram_finish_f32 flags the
-//   pairs whose Krum distance (the sum over keys) that bound could move by
-//   more than the tolerance — a cluster far from the centre (near-duplicate
-//   or colluding clients), or a non-finite value; the caller recomputes
-//   those pairs exactly on the VALU kernel.
+//   Every per-key d² leaves with a worst-case error bound err (limb
+//   products, the MFMA's rounding, fp64 sums, centring, underflow: see
+//   kCoefLimb below), and fsagg_pairgram_finish_f32 flags the pairs whose
+//   per-key distances that bound does not certify to the tolerance — a
+//   cluster far from the centre (near-duplicate or colluding clients), or a
+//   non-finite value; the caller recomputes those pairs exactly on the VALU
+//   kernel.
 //
 // Work: a workgroup of 4 waves per chunk of one key; wave v takes the
 // chunk's k-steps v, v + 4, ...  A lane loads its 16-client tile rows
@@ -60,40 +63,100 @@ constexpr int kMainChunks = 1024;         // ~2 rounds at 2 blocks per CU
 constexpr int64_t kMaxW = 16384;          // chunk length cap (LDS centre)
 constexpr int64_t kSampleCoords = 2048;   // per key, for the centre choice
 constexpr int64_t kSampleChunk = 512;
-// error model of d² = G'aa + G'bb − 2G'ab over a key of K k-steps: a part
-// random in sign, kErrCoef · (G'aa + G'bb) / sqrt(K) (the fp32 roundings of
-// the k-step sums; measured up to 2.4e-7 · (G'aa + G'bb) / sqrt(K) at C4),
-// which err carries, and a part proportional to d² itself that the finish
-// adds (fsagg_pairgram_finish_f32: 2e-8 · d², measured up to 3.6e-9 · d²;
-// DESIGN §3.3)
-constexpr double kErrCoef = 5e-7;
-constexpr double kErrBias = 2e-8;
+
+// Worst-case error bound of a key's d²(a, b) (gram_segsq_kernel; DESIGN
+// §3.3 derives each term).  u = 2^-24; S = sqrt(G'aa) + sqrt(G'bb), so
+// Σ_p |x'_a[p]·x'_b[p]| <= sqrt(G'aa·G'bb) and G'aa + G'bb + 2·sqrt(G'aa·G'bb)
+// = S² bound every Gram entry's magnitude sum (Cauchy-Schwarz):
+// * limbs: x = h + m + l EXACTLY (8 + 8 + 8 significant bits of a 24-bit
+//   significand, the residuals' signs absorbing the rounding), so the only
+//   product error is the three dropped limb products ml, lm, ll:
+//   <= (2·2^-24 + 2^-32)·(1 + 2^-8)²·|x·y|            -> kCoefLimb · u · S²
+// * MFMA accumulation: each v_mfma_f32_16x16x32_bf16 returns C + Σ of its
+//   32 exact products with an error <= kMfmaRound · u · (|C| + Σ|products|)
+//   (gfx950's rounding of the dot, tools/probe/mfma_numerics.py); over the
+//   chain mm, hl, lh, hm, mh, hh those sums total <= 1.035 · Σ|x·y|
+//                                                       -> 1.035·kMfmaRound
+// * fp64: the K k-step sums, four waves and two reduction levels add
+//   <= (K + 1024) · 2^-53 relative                     -> (K + 1024)·2^-29
+// * centring x' = fl32(x − x_c) perturbs the rows by <= u·|x'|: d² moves by
+//   <= 2u·d·S + u²·S²
+// * underflow (limbs or products below 2^-126, flushed or subnormal):
+//   <= 2^-126 · (12·sqrt(P)·S + 800·K) absolute
+constexpr double kU = 5.9604644775390625e-08;   // 2^-24
+constexpr double kCoefLimb = 2.02;
+constexpr double kMfmaRound = 1.0;
+constexpr double kMfmaChain = 1.035;
+constexpr double kTiny = 1.1754943508222875e-38;  // 2^-126
 
 constexpr int ntp_of(int nt) { return nt * (nt + 1) / 2; }
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-// Chunks and first-level groups per key: chunk q of key s covers
+// Per-pass control block (device workspace ints): chunk q of key s covers
 // [seg_lo[s] + q·w, min(seg_lo[s] + (q+1)·w, cap_s)), cap_s = seg_end[s]
-// (or seg_lo[s] + cap for the sample plan).  Group b of key s sums its
-// chunks kRed·b .. kRed·b + kRed − 1.
-__global__ void gram_prefix_kernel(const int64_t *__restrict__ seg_lo,
-                                   const int64_t *__restrict__ seg_end,
-                                   int nseg, int64_t w, int64_t cap,
-                                   int *prefix, int *gprefix) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  int acc = 0, gacc = 0;
-  prefix[0] = 0;
-  gprefix[0] = 0;
+// (or seg_lo[s] + cap for the sample pass); its chunks are prefix[s] ..
+// prefix[s+1] − 1 and its first-level groups (kRed chunks each)
+// gprefix[s] .. gprefix[s+1] − 1.  The completion counters let the last
+// workgroup of a group / key / pass run that level's reduction (fixed
+// summation order whichever workgroup arrives last: deterministic).
+struct GramCtl {
+  int *prefix;      // [nseg + 1]
+  int *gprefix;     // [nseg + 1]
+  int *cnt_key;     // [nseg]
+  int *cnt_all;     // [1]
+  int *nonempty;    // [1]: keys with at least one chunk
+  int *cnt_group;   // [groups]
+  int groups;       // capacity of cnt_group
+};
+
+__device__ void plan_pass(const int64_t *__restrict__ seg_lo,
+                          const int64_t *__restrict__ seg_end, int nseg,
+                          int64_t w, int64_t cap, const GramCtl &c) {
+  int acc = 0, gacc = 0, ne = 0;
+  c.prefix[0] = 0;
+  c.gprefix[0] = 0;
   for (int s = 0; s < nseg; ++s) {
     int64_t len = seg_end[s] - seg_lo[s];
     if (cap > 0 && len > cap) len = cap;
     if (len < 0) len = 0;
-    const int c = int((len + w - 1) / w);
-    acc += c;
-    gacc += (c + kRed - 1) / kRed;
-    prefix[s + 1] = acc;
-    gprefix[s + 1] = gacc;
+    const int k = int((len + w - 1) / w);
+    acc += k;
+    gacc += (k + kRed - 1) / kRed;
+    ne += k > 0;
+    c.prefix[s + 1] = acc;
+    c.gprefix[s + 1] = gacc;
+  }
+  *c.nonempty = ne;
+}
+
+// Both passes' plans in one launch; clears their completion counters and
+// zeroes what no workgroup writes: the per-key Gram, d² and bounds of empty
+// keys.
+__global__ __launch_bounds__(256) void gram_prefix_kernel(
+    const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
+    int nseg, int64_t w_sample, int64_t cap_sample, int64_t w_main,
+    GramCtl cs, GramCtl cm, double *g_key, double *segsq, double *err,
+    int n) {
+  if (threadIdx.x == 0) {
+    plan_pass(seg_lo, seg_end, nseg, w_sample, cap_sample, cs);
+    plan_pass(seg_lo, seg_end, nseg, w_main, 0, cm);
+  }
+  for (int i = threadIdx.x; i < nseg + 1 + cs.groups; i += 256) {
+    if (i < nseg) cs.cnt_key[i] = cm.cnt_key[i] = 0;
+    else if (i == nseg) *cs.cnt_all = *cm.cnt_all = 0;
+    else cs.cnt_group[i - nseg - 1] = 0;
+  }
+  for (int i = threadIdx.x; i < cm.groups; i += 256) cm.cnt_group[i] = 0;
+  __syncthreads();
+  const int nn = n * n;
+  for (int s = 0; s < nseg; ++s) {
+    if (cm.prefix[s + 1] > cm.prefix[s]) continue;
+    for (int i = threadIdx.x; i < 64 * 64; i += 256)
+      g_key[int64_t(s) * 64 * 64 + i] = 0.0;
+    if (segsq)
+      for (int i = threadIdx.x; i < nn; i += 256)
+        segsq[int64_t(s) * nn + i] = err[int64_t(s) * nn + i] = 0.0;
   }
 }
 
@@ -136,8 +199,8 @@ __device__ __forceinline__ float res_hi(uint32_t hp, float b, const Neg &k) {
                                          false);
 }
 
-// Split 8 fp32 into three packed bf16 limbs: x = h + m + l to within
-// 2^-24·|x|, residuals of both signs (no bias in the dropped products).
+// Split 8 fp32 into three packed bf16 limbs: x = h + m + l exactly (for
+// |x| >= 2^-102, where l stays a normal bf16), residuals of both signs.
 __device__ __forceinline__ void split3(const float (&x)[8], const Neg &k,
                                        frag8 &h, frag8 &m, frag8 &l) {
   u32x4 ph, pm, pl;
@@ -243,18 +306,219 @@ __device__ __forceinline__ void ld8_tail(const float *row, int64_t k0,
   }
 }
 
+// d²(a, b) of one key from its Gram matrix g (64 x 64, both triangles) and
+// its worst-case error bound (the terms at kCoefLimb); +inf when d² came out
+// negative beyond that bound or is not finite (the pair is recomputed).
+__device__ __forceinline__ void segsq_pair(const double *g, int a, int b,
+                                           int64_t len, double &d2o,
+                                           double &eo) {
+  if (a == b) {
+    d2o = 0.0;
+    eo = 0.0;
+    return;
+  }
+  const double gaa = g[a * 64 + a], gbb = g[b * 64 + b];
+  const double d2 = gaa + gbb - 2.0 * g[a * 64 + b];
+  const double K = double((len + kKStep - 1) / kKStep);
+  // S from the computed diagonal, inflated for its own error (the relative
+  // bound below is < 1e-5 of it)
+  const double S = (sqrt(fmax(gaa, 0.0)) + sqrt(fmax(gbb, 0.0))) *
+                   (1.0 + 1e-5);
+  const double S2 = S * S;
+  const double coef = kCoefLimb + kMfmaChain * kMfmaRound +
+                      (K + 1024.0) * 0x1p-29 + 4.0 * 0x1p-29;
+  const double e_gram = coef * kU * S2;
+  const double d_up = fmin(S, sqrt(fmax(d2, 0.0) + e_gram));
+  const double e_centre = 2.0 * kU * d_up * S + kU * kU * S2;
+  const double e_tiny = kTiny * (12.0 * sqrt(double(len)) * S + 800.0 * K);
+  double e = len > 0 ? (e_gram + e_centre + e_tiny) * (1.0 + 1e-9) : 0.0;
+  if (!(d2 >= -e) || !(e < __builtin_inf())) e = __builtin_inf();
+  d2o = d2 > 0.0 ? d2 : 0.0;
+  eo = e;
+}
+
+// D[q] = Σ_s fl32(sqrt(segsq[s][q])) in key order (fp32, as
+// pairdist_finish_kernel and the reference's `distance += torch.dist`),
+// D[a][a] = +inf; ill[q] = 1 unless the keys' distances are certified to tol
+// of the exact ones: Σ_s δ_s <= tol · Σ_s d_s, where δ_s is the worst move
+// of d = sqrt(d²) over the d² interval [d² − e, d² + e] (at most
+// e / (sqrt(d²) + sqrt(d² − e)) and sqrt(e)), summed linearly over the keys.
+// D itself is the reference's fp32 formation of those per-key distances.
+__device__ __forceinline__ void finish_pair(int q, const double *segsq,
+                                            const double *err, int n,
+                                            int nseg, double tol, float *D,
+                                            uint32_t *ill) {
+  if (q / n == q % n) {
+    D[q] = __builtin_inff();
+    ill[q] = 0u;
+    return;
+  }
+  float dist = 0.0f;
+  double sum_d = 0.0, bound = 0.0;
+  bool inf = false;
+  for (int s = 0; s < nseg; ++s) {
+    const double d2 = segsq[int64_t(s) * n * n + q];
+    const double e = err[int64_t(s) * n * n + q];
+    const double d = sqrt(d2);
+    dist = add_rn(dist, float(d));
+    sum_d += d;
+    inf = inf || !(e < __builtin_inf());
+    if (e > 0.0) {
+      const double up = sqrt(d2 + e) - d;
+      const double dn = d - sqrt(fmax(d2 - e, 0.0));
+      bound += fmax(up, dn);
+    }
+  }
+  D[q] = dist;
+  ill[q] = (!inf && bound <= tol * sum_d && dist < __builtin_inff()) ? 0u
+                                                                      : 1u;
+}
+
+// The centre: argmin_a Σ_b sqrt(d²(a, b)) over a Gram matrix G (64 x 64 in
+// LDS; 256 threads; part: 4 x 64 doubles of LDS).
+__device__ void centre_of(const double *G, int n, int *centre,
+                          double (*part)[64]) {
+  const int a = threadIdx.x & 63, h = threadIdx.x >> 6;
+  double sum = 0.0;
+  if (a < n) {
+    const double gaa = G[a * 64 + a];
+    for (int b = h; b < n; b += 4) {
+      const double d2 = gaa + G[b * 64 + b] - 2.0 * G[a * 64 + b];
+      sum += d2 > 0.0 ? sqrt(d2) : 0.0;
+    }
+  }
+  part[h][a] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int best = 0;
+    double bv = 0.0;
+    for (int b = 0; b < n; ++b) {
+      const double v = ((part[0][b] + part[1][b]) + part[2][b]) + part[3][b];
+      if (b == 0 || v < bv) {
+        bv = v;
+        best = b;
+      }
+    }
+    *centre = best;
+  }
+}
+
+// One arrival at a completion counter of `total` arrivals; true (on every
+// thread) for the last one, which then sees every other arrival's stores.
+__device__ __forceinline__ bool arrive(int *cnt, int total, int *flag) {
+  __syncthreads();                 // the workgroup's stores are issued
+  if (threadIdx.x == 0) {
+    __threadfence();               // release them device-wide
+    *flag = atomicAdd(cnt, 1) == total - 1;
+  }
+  __syncthreads();
+  const bool last = *flag != 0;
+  if (last) __threadfence();       // acquire the others'
+  return last;
+}
+
+// What runs after a chunk's partial is stored.  The last chunk of a group
+// sums the group's chunks in order into grp[b]; the last group of a key sums
+// the key's groups in order into the key's Gram matrix (LDS) and — main
+// pass — writes the key's d² and bounds; the last key of the pass runs the
+// finish (main pass, when D is given) or the centre choice (sample pass,
+// from the per-key matrices in g_key).  Every sum is in a fixed order,
+// whichever workgroup arrives last.
+template <int NT, bool CENTRED>
+__device__ void gram_tail(int chunk, int s, int n, int nseg,
+                          const int64_t *__restrict__ seg_lo,
+                          const int64_t *__restrict__ seg_end,
+                          const GramCtl &ctl, const double *partial,
+                          double *grp, double *g_key, int *centre,
+                          double *segsq, double *err, double tol, float *D,
+                          uint32_t *ill, double *lds, int *flag) {
+  constexpr int NTP = ntp_of(NT);
+  const int e = threadIdx.x;
+  const int q = chunk - ctl.prefix[s];
+  const int b = ctl.gprefix[s] + q / kRed;
+  const int qa = ctl.prefix[s] + (q / kRed) * kRed;
+  const int qb = min(qa + kRed, ctl.prefix[s + 1]);
+  if (!arrive(&ctl.cnt_group[b], qb - qa, flag)) return;
+#pragma unroll 1
+  for (int p = 0; p < NTP; ++p) {
+    double v[kRed];
+#pragma unroll
+    for (int j = 0; j < kRed; ++j)
+      v[j] = qa + j < qb ? partial[((int64_t(qa) + j) * NTP + p) * 256 + e]
+                         : 0.0;
+    double sum = 0.0;
+#pragma unroll
+    for (int j = 0; j < kRed; ++j) sum += v[j];
+    grp[(int64_t(b) * NTP + p) * 256 + e] = sum;
+  }
+  const int ga = ctl.gprefix[s], gb = ctl.gprefix[s + 1];
+  if (!arrive(&ctl.cnt_key[s], gb - ga, flag)) return;
+  const int r = e >> 6, ln = e & 63;
+#pragma unroll 1
+  for (int p = 0; p < NTP; ++p) {
+    constexpr int U = 8;
+    double sum = 0.0;
+    for (int c = ga; c < gb; c += U) {
+      double v[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        v[j] = c + j < gb ? grp[(int64_t(c + j) * NTP + p) * 256 + e] : 0.0;
+#pragma unroll
+      for (int j = 0; j < U; ++j) sum += v[j];
+    }
+    int t, u;
+    tp_tiles(p, NT, t, u);
+    const int ra = 16 * t + 4 * (ln >> 4) + r, rc = 16 * u + (ln & 15);
+    lds[ra * 64 + rc] = sum;
+    if (t != u) lds[rc * 64 + ra] = sum;
+    if (!CENTRED) {
+      double *gk = g_key + int64_t(s) * 64 * 64;
+      gk[ra * 64 + rc] = sum;
+      if (t != u) gk[rc * 64 + ra] = sum;
+    }
+  }
+  __syncthreads();
+  const int nn = n * n;
+  if (CENTRED) {
+    const int64_t len = seg_end[s] - seg_lo[s];
+    for (int i = e; i < nn; i += 256)
+      segsq_pair(lds, i / n, i % n, len, segsq[int64_t(s) * nn + i],
+                 err[int64_t(s) * nn + i]);
+    if (!D) return;
+  }
+  if (!arrive(ctl.cnt_all, *ctl.nonempty, flag)) return;
+  if (CENTRED) {
+    for (int i = e; i < nn; i += 256)
+      finish_pair(i, segsq, err, n, nseg, tol, D, ill);
+  } else {
+    // Σ over keys (key order) of the per-key sample matrices
+    for (int i = e; i < 64 * 64; i += 256) {
+      double sum = 0.0;
+      for (int k = 0; k < nseg; ++k) sum += g_key[int64_t(k) * 64 * 64 + i];
+      lds[i] = sum;
+    }
+    __syncthreads();
+    centre_of(lds, n, centre,
+              reinterpret_cast<double(*)[64]>(lds + 64 * 64));
+  }
+}
+
 // One workgroup (4 waves) per chunk.  partial[chunk][tp][reg][lane] (fp64):
 // the chunk's (centred) Gram blocks in MFMA C-layout (row 4(lane>>4) + reg
 // of tile t, column lane & 15 of tile u).  !CENTRED: raw values (sample).
 // The centre's values of the chunk (<= kMaxW) are staged in LDS once and
-// read by every wave (registers go to the k-steps in flight).
+// read by every wave (registers go to the k-steps in flight).  Then
+// gram_tail: the reductions, d² and bounds, finish / centre — the last
+// workgroup to arrive at each level runs it, in the same launch.
 template <int NT, bool CENTRED>
 __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n,
     const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
-    int nseg, const int *__restrict__ prefix, int64_t w, int64_t cap,
-    const int *__restrict__ centre, double *__restrict__ partial) {
+    int nseg, GramCtl ctl, int64_t w, int64_t cap, int *centre,
+    double *__restrict__ partial, double *grp, double *g_key, double *segsq,
+    double *err, double tol, float *D, uint32_t *ill) {
   constexpr int NTP = ntp_of(NT);
+  const int *__restrict__ prefix = ctl.prefix;
   constexpr int kRedWords = 2 * NTP * 4 * kWave;   // two waves' sums
   constexpr int kSmem = kRedWords * 8 > kMaxW * 4 ? kRedWords * 8
                                                    : int(kMaxW) * 4;
@@ -404,155 +668,19 @@ __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
         out[(p * 4 + r) * 64 + lane] = acc[p][r] + red[0][p * 4 + r][lane];
     }
   }
+  __shared__ int flag;
+  gram_tail<NT, CENTRED>(chunk, s, n, nseg, seg_lo, seg_end, ctl, partial,
+                         grp, g_key, centre, segsq, err, tol, D, ill,
+                         reinterpret_cast<double *>(smem), &flag);
 }
 
-// Level 1, grid (groups, NTP): group b (of key s) sums its <= kRed chunks
-// in order into red[b][p][256].
-template <int NT>
-__global__ __launch_bounds__(256) void gram_reduce1_kernel(
-    const double *__restrict__ partial, const int *__restrict__ prefix,
-    const int *__restrict__ gprefix, int nseg, double *__restrict__ red) {
-  constexpr int NTP = ntp_of(NT);
-  const int b = blockIdx.x, p = blockIdx.y, e = threadIdx.x;
-  if (b >= gprefix[nseg]) return;
-  int s = 0;
-  while (gprefix[s + 1] <= b) ++s;
-  const int q0 = prefix[s] + (b - gprefix[s]) * kRed;
-  const int q1 = min(q0 + kRed, prefix[s + 1]);
-  double v[kRed];
-#pragma unroll
-  for (int q = 0; q < kRed; ++q)
-    v[q] = q0 + q < q1 ? partial[((int64_t(q0) + q) * NTP + p) * 256 + e]
-                       : 0.0;
-  double sum = 0.0;
-#pragma unroll
-  for (int q = 0; q < kRed; ++q) sum += v[q];
-  red[(int64_t(b) * NTP + p) * 256 + e] = sum;
-}
-
-// Level 2, grid (nseg or 1, NTP): each key's groups in order into
-// G[seg][64][64] (both triangles of the tile pairs); all_in_one sums every
-// group into one matrix (the sample plan).
-template <int NT>
-__global__ __launch_bounds__(256) void gram_reduce2_kernel(
-    const double *__restrict__ red, const int *__restrict__ gprefix,
-    int nseg, int all_in_one, double *__restrict__ G) {
-  constexpr int NTP = ntp_of(NT);
-  constexpr int U = 8;
-  const int s = blockIdx.x, p = blockIdx.y;
-  const int r = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int b0 = all_in_one ? 0 : gprefix[s];
-  const int b1 = all_in_one ? gprefix[nseg] : gprefix[s + 1];
-  double sum = 0.0;
-  for (int b = b0; b < b1; b += U) {
-    double v[U];
-#pragma unroll
-    for (int j = 0; j < U; ++j)
-      v[j] = b + j < b1 ? red[(int64_t(b + j) * NTP + p) * 256 + threadIdx.x]
-                        : 0.0;
-#pragma unroll
-    for (int j = 0; j < U; ++j) sum += v[j];
-  }
-  int t, u;
-  tp_tiles(p, NT, t, u);
-  const int a = 16 * t + 4 * (lane >> 4) + r;
-  const int c = 16 * u + (lane & 15);
-  double *gm = G + int64_t(s) * 64 * 64;
-  gm[a * 64 + c] = sum;
-  if (t != u) gm[c * 64 + a] = sum;
-}
-
-// The centre: argmin_a Σ_b sqrt(d²(a, b)) over the sample Gram.
-__global__ __launch_bounds__(256) void gram_centre_kernel(
-    const double *__restrict__ G, int n, int *__restrict__ centre) {
-  __shared__ double part[4][64];
-  const int a = threadIdx.x & 63, h = threadIdx.x >> 6;
-  double sum = 0.0;
-  if (a < n) {
-    const double gaa = G[a * 64 + a];
-    for (int b = h; b < n; b += 4) {
-      const double d2 = gaa + G[b * 64 + b] - 2.0 * G[a * 64 + b];
-      sum += d2 > 0.0 ? sqrt(d2) : 0.0;
-    }
-  }
-  part[h][a] = sum;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int best = 0;
-    double bv = 0.0;
-    for (int b = 0; b < n; ++b) {
-      const double v = ((part[0][b] + part[1][b]) + part[2][b]) + part[3][b];
-      if (b == 0 || v < bv) {
-        bv = v;
-        best = b;
-      }
-    }
-    *centre = best;
-  }
-}
-
-// segsq[s][a][b] = G_aa + G_bb − 2·G_ab (diag 0, clamped at 0) and its
-// predicted absolute error err[s][a][b] (+inf when d² came out negative
-// beyond that bound or is not finite: the pair is recomputed).
-__global__ __launch_bounds__(256) void gram_segsq_kernel(
-    const double *__restrict__ G, const int64_t *__restrict__ seg_lo,
-    const int64_t *__restrict__ seg_end, int n, int nseg,
-    double *__restrict__ segsq, double *__restrict__ err) {
-  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (i >= int64_t(nseg) * n * n) return;
-  const int s = int(i / (int64_t(n) * n));
-  const int a = int((i / n) % n), b = int(i % n);
-  const double *g = G + int64_t(s) * 64 * 64;
-  if (a == b) {
-    segsq[i] = 0.0;
-    err[i] = 0.0;
-    return;
-  }
-  const double gaa = g[a * 64 + a], gbb = g[b * 64 + b];
-  const double d2 = gaa + gbb - 2.0 * g[a * 64 + b];
-  // K k-steps: K roundings of k-step sums, random in sign
-  const double ksteps = ceil(double(seg_end[s] - seg_lo[s]) / kKStep);
-  double e = ksteps > 0.0 ? kErrCoef * (gaa + gbb) / sqrt(ksteps) : 0.0;
-  if (!(d2 >= -e) || !(e < __builtin_inf())) e = __builtin_inf();
-  segsq[i] = d2 > 0.0 ? d2 : 0.0;
-  err[i] = e;
-}
-
-// D[a][b] = Σ_s fl32(sqrt(segsq[s][a][b])) in key order (fp32, as
-// pairdist_finish_kernel and the reference's `distance += torch.dist`),
-// D[a][a] = +inf; ill[a][b] = 1 when the keys' error bounds could move
-// the distance by more than tol·D (or it is not finite).  Per key the
-// random part δ = err moves d = sqrt(d²) by at most min(δ / 2d, sqrt(δ));
-// the keys' parts are independent (summed in quadrature); the part
-// proportional to d² moves D by kErrBias / 2 · D.
+// The finish of a sharded call, after the ranks' d² and bounds were summed
+// (fsagg_pairgram_finish_f32): finish_pair on every pair.
 __global__ __launch_bounds__(256) void gram_finish_kernel(
     const double *__restrict__ segsq, const double *__restrict__ err, int n,
     int nseg, double tol, float *__restrict__ D, uint32_t *__restrict__ ill) {
   const int q = blockIdx.x * 256 + threadIdx.x;
-  if (q >= n * n) return;
-  if (q / n == q % n) {
-    D[q] = __builtin_inff();
-    ill[q] = 0u;
-    return;
-  }
-  float dist = 0.0f;
-  double var = 0.0;
-  bool inf = false;
-  for (int s = 0; s < nseg; ++s) {
-    const double d2 = segsq[int64_t(s) * n * n + q];
-    const double e = err[int64_t(s) * n * n + q];
-    const double d = sqrt(d2);
-    dist = add_rn(dist, float(d));
-    inf = inf || !(e < __builtin_inf());
-    if (e > 0.0) {
-      const double m = d2 > 0.0 ? fmin(e / (2.0 * d), sqrt(e)) : sqrt(e);
-      var += m * m;
-    }
-  }
-  D[q] = dist;
-  const double bound = sqrt(var) + 0.5 * kErrBias * double(dist);
-  ill[q] = (!inf && bound <= tol * double(dist) && dist < __builtin_inff())
-               ? 0u : 1u;
+  if (q < n * n) finish_pair(q, segsq, err, n, nseg, tol, D, ill);
 }
 
 struct GramPlan {
@@ -581,14 +709,14 @@ GramPlan gram_plan(int n, int64_t numel, int nseg) {
 }
 
 struct GramWs {
-  int *prefix_main, *gprefix_main, *prefix_sample, *gprefix_sample, *centre;
-  double *partial, *g_sample, *g_main, *red;
+  GramCtl cs, cm;          // sample and main pass control blocks
+  int *centre;
+  double *partial, *g_key, *grp;
 };
 
 size_t gram_ws_layout(int n, int64_t numel, int nseg, void *ws, GramWs *w) {
   const GramPlan pl = gram_plan(n, numel, nseg);
   const size_t ntp = size_t(ntp_of(pl.nt));
-  const size_t ints = align256(sizeof(int) * size_t(nseg + 1));
   const size_t chunks = size_t(pl.main_chunks > pl.sample_chunks
                                    ? pl.main_chunks
                                    : pl.sample_chunks);
@@ -601,70 +729,64 @@ size_t gram_ws_layout(int n, int64_t numel, int nseg, void *ws, GramWs *w) {
     off += align256(bytes);
     return static_cast<char *>(ws) + o;
   };
-  char *p_pm = take(ints), *p_gm = take(ints), *p_ps = take(ints),
-       *p_gs = take(ints), *p_c = take(256),
-       *p_gsm = take(sizeof(double) * 64 * 64),
-       *p_gmn = take(sizeof(double) * 64 * 64 * size_t(nseg)),
-       *p_red = take(sizeof(double) * groups * ntp * 256),
+  auto ctl = [&](int g) {
+    // prefix, gprefix, cnt_key, cnt_all, nonempty, cnt_group
+    const size_t k = size_t(nseg);
+    int *p = reinterpret_cast<int *>(
+        take(sizeof(int) * (3 * k + 4 + size_t(g))));
+    GramCtl c;
+    c.prefix = p;
+    c.gprefix = p + (k + 1);
+    c.cnt_key = p + 2 * (k + 1);
+    c.cnt_all = c.cnt_key + k;
+    c.nonempty = c.cnt_all + 1;
+    c.cnt_group = c.nonempty + 1;
+    c.groups = g;
+    return c;
+  };
+  const GramCtl cs = ctl(pl.sample_groups), cm = ctl(pl.main_groups);
+  char *p_c = take(256),
+       *p_gk = take(sizeof(double) * 64 * 64 * size_t(nseg)),
+       *p_grp = take(sizeof(double) * groups * ntp * 256),
        *p_part = take(sizeof(double) * chunks * ntp * 256);
   if (w) {
-    w->prefix_main = reinterpret_cast<int *>(p_pm);
-    w->gprefix_main = reinterpret_cast<int *>(p_gm);
-    w->prefix_sample = reinterpret_cast<int *>(p_ps);
-    w->gprefix_sample = reinterpret_cast<int *>(p_gs);
+    w->cs = cs;
+    w->cm = cm;
     w->centre = reinterpret_cast<int *>(p_c);
-    w->g_sample = reinterpret_cast<double *>(p_gsm);
-    w->g_main = reinterpret_cast<double *>(p_gmn);
-    w->red = reinterpret_cast<double *>(p_red);
+    w->g_key = reinterpret_cast<double *>(p_gk);
+    w->grp = reinterpret_cast<double *>(p_grp);
     w->partial = reinterpret_cast<double *>(p_part);
   }
   return off;
 }
 
+// Three launches: the plans (and counters), the sample pass (its tail picks
+// the centre), the centred main pass (its tail writes every key's d² and
+// bounds, and with D the finish).
 template <int NT>
 void gram_launch(const float *const *tab, int64_t ss, int n,
                  const int64_t *seg_lo, const int64_t *seg_end, int nseg,
                  const GramPlan &pl, const GramWs &w, double *segsq,
-                 double *err, hipStream_t st) {
-  constexpr int NTP = ntp_of(NT);
+                 double *err, double tol, float *D, uint32_t *ill,
+                 hipStream_t st) {
+  hipLaunchKernelGGL(gram_prefix_kernel, dim3(1), dim3(256), 0, st, seg_lo,
+                     seg_end, nseg, kSampleChunk, kSampleCoords, pl.w, w.cs,
+                     w.cm, w.g_key, segsq, err, n);
   // 1. the centre: Gram of the first kSampleCoords of every key, raw
-  hipLaunchKernelGGL(gram_prefix_kernel, dim3(1), dim3(1), 0, st, seg_lo,
-                     seg_end, nseg, kSampleChunk, kSampleCoords,
-                     w.prefix_sample, w.gprefix_sample);
   hipLaunchKernelGGL((gram_chunk_kernel<NT, false>),
                      dim3(unsigned(pl.sample_chunks)), dim3(kBlk), 0, st,
-                     tab, ss, n, seg_lo, seg_end, nseg, w.prefix_sample,
-                     kSampleChunk, kSampleCoords,
-                     static_cast<const int *>(nullptr), w.partial);
-  hipLaunchKernelGGL((gram_reduce1_kernel<NT>),
-                     dim3(unsigned(pl.sample_groups), unsigned(NTP)),
-                     dim3(256), 0, st, w.partial, w.prefix_sample,
-                     w.gprefix_sample, nseg, w.red);
-  hipLaunchKernelGGL((gram_reduce2_kernel<NT>), dim3(1, unsigned(NTP)),
-                     dim3(256), 0, st, w.red, w.gprefix_sample, nseg, 1,
-                     w.g_sample);
-  hipLaunchKernelGGL(gram_centre_kernel, dim3(1), dim3(256), 0, st,
-                     w.g_sample, n, w.centre);
-  // 2. the centred Gram of every key
-  hipLaunchKernelGGL(gram_prefix_kernel, dim3(1), dim3(1), 0, st, seg_lo,
-                     seg_end, nseg, pl.w, int64_t(0), w.prefix_main,
-                     w.gprefix_main);
+                     tab, ss, n, seg_lo, seg_end, nseg, w.cs, kSampleChunk,
+                     kSampleCoords, w.centre, w.partial, w.grp, w.g_key,
+                     static_cast<double *>(nullptr),
+                     static_cast<double *>(nullptr), 0.0,
+                     static_cast<float *>(nullptr),
+                     static_cast<uint32_t *>(nullptr));
+  // 2. the centred Gram of every key, its d² and bounds (and D)
   hipLaunchKernelGGL((gram_chunk_kernel<NT, true>),
                      dim3(unsigned(pl.main_chunks)), dim3(kBlk), 0, st, tab,
-                     ss, n, seg_lo, seg_end, nseg, w.prefix_main, pl.w,
-                     int64_t(0), static_cast<const int *>(w.centre),
-                     w.partial);
-  hipLaunchKernelGGL((gram_reduce1_kernel<NT>),
-                     dim3(unsigned(pl.main_groups), unsigned(NTP)),
-                     dim3(256), 0, st, w.partial, w.prefix_main,
-                     w.gprefix_main, nseg, w.red);
-  hipLaunchKernelGGL((gram_reduce2_kernel<NT>),
-                     dim3(unsigned(nseg), unsigned(NTP)), dim3(256), 0, st,
-                     w.red, w.gprefix_main, nseg, 0, w.g_main);
-  const int64_t tot = int64_t(nseg) * n * n;
-  hipLaunchKernelGGL(gram_segsq_kernel, dim3(unsigned((tot + 255) / 256)),
-                     dim3(256), 0, st, w.g_main, seg_lo, seg_end, n, nseg,
-                     segsq, err);
+                     ss, n, seg_lo, seg_end, nseg, w.cm, pl.w, int64_t(0),
+                     w.centre, w.partial, w.grp, w.g_key, segsq, err, tol, D,
+                     ill);
 }
 
 }  // namespace
@@ -678,25 +800,24 @@ extern "C" size_t fsagg_pairgram_workspace_bytes(int n, int64_t numel,
   return gram_ws_layout(n, numel, nseg, nullptr, nullptr);
 }
 
-extern "C" int fsagg_pairgram_rows_segsq_f32(const fsagg_rows *rows,
-                                             const int64_t *seg_lo,
-                                             const int64_t *seg_end,
-                                             int64_t numel, double *segsq,
-                                             double *err, void *workspace,
-                                             size_t workspace_bytes,
-                                             fsagg_stream_t stream) {
+namespace {
+int pairgram_rows(const char *what, const fsagg_rows *rows,
+                  const int64_t *seg_lo, const int64_t *seg_end,
+                  int64_t numel, double *segsq, double *err, double tol,
+                  float *D, uint32_t *ill, void *workspace,
+                  size_t workspace_bytes, fsagg_stream_t stream) {
   if (!rows || !rows->tab || !seg_lo || !seg_end || !segsq || !err ||
       rows->n < 2 || rows->n > 16 * kGramMaxTiles || rows->nseg < 1 ||
-      numel < 0 || (rows->ss != 0 && rows->ss < rows->n)) {
-    set_error("fsagg_pairgram_rows_segsq_f32: invalid argument (n must be "
-              "2..%d)", 16 * kGramMaxTiles);
+      numel < 0 || (rows->ss != 0 && rows->ss < rows->n) ||
+      (D && (!ill || !(tol >= 0.0)))) {
+    set_error("%s: invalid argument (n must be 2..%d)", what,
+              16 * kGramMaxTiles);
     return FSAGG_EINVAL;
   }
   const int n = rows->n, nseg = rows->nseg;
   const size_t need = gram_ws_layout(n, numel, nseg, nullptr, nullptr);
   if (!workspace || workspace_bytes < need) {
-    set_error("fsagg_pairgram_rows_segsq_f32: workspace %zu < %zu bytes",
-              workspace_bytes, need);
+    set_error("%s: workspace %zu < %zu bytes", what, workspace_bytes, need);
     return FSAGG_ESPACE;
   }
   const GramPlan pl = gram_plan(n, numel, nseg);
@@ -705,15 +826,45 @@ extern "C" int fsagg_pairgram_rows_segsq_f32(const fsagg_rows *rows,
   hipStream_t st = as_stream(stream);
   switch (pl.nt) {
     case 1: gram_launch<1>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg, pl,
-                           w, segsq, err, st); break;
+                           w, segsq, err, tol, D, ill, st); break;
     case 2: gram_launch<2>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg, pl,
-                           w, segsq, err, st); break;
+                           w, segsq, err, tol, D, ill, st); break;
     case 3: gram_launch<3>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg, pl,
-                           w, segsq, err, st); break;
+                           w, segsq, err, tol, D, ill, st); break;
     default: gram_launch<4>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg, pl,
-                            w, segsq, err, st); break;
+                            w, segsq, err, tol, D, ill, st); break;
   }
-  return check_launch("fsagg_pairgram_rows_segsq_f32");
+  return check_launch(what);
+}
+}  // namespace
+
+extern "C" int fsagg_pairgram_rows_segsq_f32(const fsagg_rows *rows,
+                                             const int64_t *seg_lo,
+                                             const int64_t *seg_end,
+                                             int64_t numel, double *segsq,
+                                             double *err, void *workspace,
+                                             size_t workspace_bytes,
+                                             fsagg_stream_t stream) {
+  return pairgram_rows("fsagg_pairgram_rows_segsq_f32", rows, seg_lo,
+                       seg_end, numel, segsq, err, 0.0, nullptr, nullptr,
+                       workspace, workspace_bytes, stream);
+}
+
+extern "C" int fsagg_pairgram_rows_f32(const fsagg_rows *rows,
+                                       const int64_t *seg_lo,
+                                       const int64_t *seg_end, int64_t numel,
+                                       double tol, double *segsq,
+                                       double *err, float *D, uint32_t *ill,
+                                       void *workspace,
+                                       size_t workspace_bytes,
+                                       fsagg_stream_t stream) {
+  if (!D) {
+    set_error("fsagg_pairgram_rows_f32: D is NULL");
+    return FSAGG_EINVAL;
+  }
+  return pairgram_rows("fsagg_pairgram_rows_f32", rows, seg_lo, seg_end,
+                       numel, segsq, err, tol, D, ill, workspace,
+                       workspace_bytes, stream);
 }
 
 extern "C" int fsagg_pairgram_finish_f32(const double *segsq,

@@ -1069,6 +1069,31 @@ def pairgram_finish(sq2, tol):
     return buf, D, buf[1]
 
 
+def pairgram_rows_dist(rs, tol, workspace=None):
+    """:func:`pairgram_rows_segsq` and :func:`pairgram_finish` in one call
+    (fsagg_pairgram_rows_f32: the finish runs in the main pass's last
+    workgroup).  Returns (buf, D view, ill view, sq2) as those two."""
+    _require_all(rs, 'Krum')
+    if not 2 <= rs.n <= L.FSAGG_PAIRGRAM_MAX_CLIENTS:
+        raise ValueError('the Gram path takes 2..%d clients' %
+                         L.FSAGG_PAIRGRAM_MAX_CLIENTS)
+    lay = rs.layout
+    seg_lo, seg_end = lay.seg_bounds(rs.device, 0, lay.numel, None)
+    lib = L.load()
+    extent = max(lay.numel, 1)
+    need = lib.fsagg_pairgram_workspace_bytes(rs.n, extent, rs.nseg)
+    ws = (workspace or _WS).get(rs.device, need)
+    sq2 = torch.empty((2, rs.nseg, rs.n, rs.n), dtype=torch.float64,
+                      device=rs.device)
+    buf = torch.empty((2, rs.n, rs.n), dtype=torch.int32, device=rs.device)
+    L.check(lib.fsagg_pairgram_rows_f32(
+        rs.ptr(), seg_lo.data_ptr(), seg_end.data_ptr(), extent, float(tol),
+        sq2[0].data_ptr(), sq2[1].data_ptr(), buf[0].data_ptr(),
+        buf[1].data_ptr(), ws.data_ptr(), ws.numel(), _stream(rs.device)),
+        'fsagg_pairgram_rows_f32')
+    return buf, buf[0].view(torch.float32), buf[1], sq2
+
+
 def pairdist_rows(rs, workspace=None):
     """Krum's distance matrix D[n][n] (fp32, device) over a row set."""
     return pairdist_finish(pairdist_rows_segsq(rs, workspace=workspace))

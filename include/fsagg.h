@@ -458,15 +458,19 @@ int fsagg_pairdist_rows_segsq_f32(const fsagg_rows *rows,
  * fp32 value split exactly into three bf16 limbs and the six limb products
  * of weight >= 2^-16 accumulated by v_mfma_f32_16x16x32_bf16, fp32 within
  * one k-step of 32 coordinates, fp64 beyond.  err[s][a][b] (fp64, same
- * shape as segsq): the predicted bound of the part of d²'s error in key s
- * that is random in sign, 5e-7 · (G'aa + G'bb) / sqrt(K) for a key of K
- * k-steps (+inf where d² came out negative beyond it or is not finite); a
- * further 2e-8 · d² is proportional to d² itself.  Sums of segsq and err
- * over disjoint coordinate ranges (ranks) stay valid.  Replaces the same
- * torch.dist loop (krum_aggregator.py:41-73) as fsagg_pairdist_f32, with
- * fsagg_pairgram_finish_f32 in place of fsagg_pairdist_finish_f64.
- * Workspace: fsagg_pairgram_workspace_bytes(n, numel, nseg) (0 when n is
- * outside 2..64). */
+ * shape as segsq): a worst-case bound on |segsq − the exact squared
+ * distance of key s's fp32 rows| — the dropped limb products, the MFMA's
+ * rounding of each 32-product dot, the fp64 sums, the centring and
+ * underflow, each bounded through S = sqrt(G'aa) + sqrt(G'bb) (DESIGN
+ * §3.3) — or +inf where d² came out negative beyond it or is not finite.
+ * Sums of segsq and err over disjoint coordinate ranges (ranks) stay
+ * valid.  Replaces the same torch.dist loop (krum_aggregator.py:41-73) as
+ * fsagg_pairdist_f32, with fsagg_pairgram_finish_f32 in place of
+ * fsagg_pairdist_finish_f64.  Three launches (plans; the sample pass, whose
+ * last workgroup picks the centre; the main pass, whose last workgroup of
+ * each chunk group / key runs that level's fixed-order reduction and the
+ * key's d² and bounds).  Workspace: fsagg_pairgram_workspace_bytes(n,
+ * numel, nseg) (0 when n is outside 2..64). */
 size_t fsagg_pairgram_workspace_bytes(int n, int64_t numel, int nseg);
 int fsagg_pairgram_rows_segsq_f32(const fsagg_rows *rows,
                                   const int64_t *seg_lo,
@@ -479,13 +483,22 @@ int fsagg_pairgram_rows_segsq_f32(const fsagg_rows *rows,
  * D[a][b] = Σ_s fl32(sqrt(segsq[s][a][b])) in key order (fp32, as
  * fsagg_pairdist_finish_f64 and the reference's `distance +=
  * torch.dist(...)`, krum_aggregator.py:45-56), D[a][a] = +inf, and
- * ill[a*n + b] = 1 for a pair whose error bounds (the keys' random parts in
- * quadrature plus the proportional part) could move D by more than tol·D,
- * or whose D is not finite — the caller recomputes those pairs with
- * fsagg_pairdist_rows_segsq_f32 on the clients involved. */
+ * ill[a*n + b] = 1 for a pair whose per-key distances the bounds do not
+ * certify to tol (Σ_s worst move of sqrt(d²_s) over [d²_s ± err_s] >
+ * tol · Σ_s sqrt(d²_s)), or whose D is not finite — the caller recomputes
+ * those pairs with fsagg_pairdist_rows_segsq_f32 on the clients involved. */
 int fsagg_pairgram_finish_f32(const double *segsq, const double *err, int n,
                               int nseg, double tol, float *D, uint32_t *ill,
                               fsagg_stream_t stream);
+
+/* fsagg_pairgram_rows_segsq_f32 and fsagg_pairgram_finish_f32 in the same
+ * three launches (the finish runs in the last workgroup of the main pass):
+ * the unsharded call. */
+int fsagg_pairgram_rows_f32(const fsagg_rows *rows, const int64_t *seg_lo,
+                            const int64_t *seg_end, int64_t numel, double tol,
+                            double *segsq, double *err, float *D,
+                            uint32_t *ill, void *workspace,
+                            size_t workspace_bytes, fsagg_stream_t stream);
 
 /* Per-(client, key segment) squared L2 norms over a row set in fp64:
  * sq[i][s] = Σ_{p in s} x_i[p]^2 (0 for a NULL entry), summed in a fixed

@@ -7,9 +7,11 @@
   drop-in over 100 device tensors, bit-exact on every coordinate (2M-column
   blocks, 64-bit offsets, the ragged tail) against the oracle.
 * C4 — Krum over 50 x 6,603,902 (ConvNet2 hidden 2048) with the SURVEY
-  §8(d) generator: the score margin asserted (>= 1e-3: 500x the kernel's
-  distance error), the selection exact against
-  an fp64 restatement of the distances, the multi-Krum output bit-exact.
+  §8(d) generator, once on rows of one allocation (the matrix-core path,
+  asserted) and once on separately allocated tensors (the VALU path,
+  asserted): the score margin asserted (>= 1e-3: 1000x the certified
+  distance error), the selection exact against an fp64 restatement of the
+  distances, the multi-Krum output bit-exact.
 * C5 — 200 x 6,603,902 with 10 % x100 outliers: median bit-exact and
   trimmed mean (k = 40) within its tolerance on sampled column blocks.
 
@@ -129,7 +131,15 @@ def _fp64_distances(X, bounds):
     return D
 
 
-def test_c4_krum_50x6p6M_selection_and_average():
+@pytest.mark.parametrize('placement', ['slab', 'separate'])
+def test_c4_krum_50x6p6M_selection_and_average(placement):
+    """C4 through KrumAggregator.aggregate() on device dicts, in both row
+    placements the engine routes differently: 'slab' — every
+    client's keys are views of one allocation (the client stack's layout,
+    rows at spread offsets): the matrix-core Gram path, its flagged pairs
+    (the clustered Byzantine clients far from the honest centre) recomputed
+    on the VALU kernel; 'separate' — 50 x 12 separately allocated tensors
+    (2 MiB-aligned, one HBM channel per k-step): the VALU kernel."""
     from federatedscope_amd.core.aggregators import KrumAggregator
     n, f, agg_num = 50, 10, 5
     keys = CONVNET2(2048)
@@ -140,13 +150,22 @@ def test_c4_krum_50x6p6M_selection_and_average():
     g = torch.Generator(device='cuda').manual_seed(1234)
     base = OrderedDict((k, torch.randn(s, device='cuda', generator=g))
                        for k, s in keys)
+    slab = torch.empty((n, P + 16 * len(keys)), device='cuda') \
+        if placement == 'slab' else None
     clients = []
     for i in range(n):
-        d = OrderedDict()
+        d, o = OrderedDict(), 0
         for k, s in keys:
             z = torch.randn(s, device='cuda', generator=g)
-            d[k] = (0.1 + 0.05 * z) if i in byz else \
+            v = (0.1 + 0.05 * z) if i in byz else \
                 (base[k] + 0.01 * (1 + 0.05 * i) * z)
+            if slab is not None:
+                m = int(np.prod(s))
+                d[k] = slab[i, o:o + m].view(s)
+                d[k].copy_(v)
+                o += (m + 15) // 16 * 16
+            else:
+                d[k] = v
         clients.append(d)
     sizes = _sizes(n, 4)
     init = OrderedDict((k, torch.randn(s, device='cuda', generator=g))
@@ -155,6 +174,11 @@ def test_c4_krum_50x6p6M_selection_and_average():
                          config=_cfg(f=f, agg_num=agg_num, client_num=n))
     fb = [(s, d) for s, d in zip(sizes, clients)]
     got = agg.aggregate({'client_feedback': fb})
+    if placement == 'slab':
+        assert agg.last_pairdist_path.startswith('mfma'), \
+            agg.last_pairdist_path
+    else:
+        assert agg.last_pairdist_path == 'valu', agg.last_pairdist_path
     # fp64 restatement of the distances → scores → selection
     X = np.concatenate([np.stack([d[k].reshape(-1).cpu().numpy()
                                   for d in clients]) for k, _ in keys], 1)
@@ -166,8 +190,9 @@ def test_c4_krum_50x6p6M_selection_and_average():
     scores = np.sort(D, axis=1)[:, :n - f - 2].sum(-1)
     srt = np.sort(scores)
     # the best-vs-second score margin (0.84 % with this generator and the
-    # 12-key layout) must dwarf the kernel's distance error (<= 2e-6
-    # relative, tests/test_gpu_kernels.py): 1e-3 leaves a 500x guard
+    # 12-key layout) must dwarf the distance error (certified <= 1e-6
+    # relative on the Gram path, tests/test_gpu_pairgram.py): 1e-3 leaves a
+    # 1000x guard
     assert (srt[1] - srt[0]) / srt[0] >= 1e-3
     want_sel = [int(i) for i in np.argsort(scores, kind='stable')[:agg_num]]
     assert agg.last_selection == want_sel
