@@ -57,7 +57,9 @@ class FedOptAggregator(ClientsAvgAggregator):
                 '(supported: %s)' % (self.opt_type, ', '.join(_SUPPORTED)))
         for k in _IGNORED:
             opt.pop(k, None)
-        self.kw = opt
+        # the constructor arguments as configured (the loop below consumes
+        # ``opt``)
+        self.opt_kwargs = dict(opt)
         self.maximize = bool(opt.pop('maximize', False))
         t = self.opt_type
         # torch.optim defaults per class
@@ -87,6 +89,7 @@ class FedOptAggregator(ClientsAvgAggregator):
         if opt:
             raise TypeError('%s got unexpected arguments %s' %
                             (self.opt_type, sorted(opt)))
+        self._validate()
         fo = config.fedopt
         self._annealing = bool(getattr(fo, 'annealing', False))
         self._anneal_step = int(getattr(fo, 'annealing_step_size', 2000))
@@ -95,6 +98,42 @@ class FedOptAggregator(ClientsAvgAggregator):
         # optimizer state per parameter name, as torch.optim keeps it:
         # name -> [state0, state1, state2, steps]
         self._state = {}
+
+    def _validate(self):
+        """The argument checks of the torch.optim constructors the
+        reference's get_optimizer calls (optimizer_builder.py:53-56), with
+        their messages: an invalid config fails here as it does there."""
+        t = self.opt_type
+
+        def need(ok, msg, v):
+            if not ok:
+                raise ValueError(msg % (v, ))
+        need(0.0 <= self.lr0, 'Invalid learning rate: %s', self.lr0)
+        if t in ('Adam', 'AdamW', 'Adagrad', 'RMSprop'):
+            need(0.0 <= self.eps, 'Invalid epsilon value: %s', self.eps)
+        if t == 'SGD':
+            need(0.0 <= self.momentum, 'Invalid momentum value: %s',
+                 self.momentum)
+        if t in ('Adam', 'AdamW'):
+            need(0.0 <= self.beta1 < 1.0,
+                 'Invalid beta parameter at index 0: %s', self.beta1)
+            need(0.0 <= self.beta2 < 1.0,
+                 'Invalid beta parameter at index 1: %s', self.beta2)
+        need(0.0 <= self.weight_decay, 'Invalid weight_decay value: %s',
+             self.weight_decay)
+        if t == 'SGD' and self.nesterov and (self.momentum <= 0 or
+                                             self.dampening != 0):
+            raise ValueError('Nesterov momentum requires a momentum and zero '
+                             'dampening')
+        if t == 'Adagrad':
+            need(0.0 <= self.lr_decay, 'Invalid lr_decay value: %s',
+                 self.lr_decay)
+            need(0.0 <= self.init_acc,
+                 'Invalid initial_accumulator_value value: %s', self.init_acc)
+        if t == 'RMSprop':
+            need(0.0 <= self.momentum, 'Invalid momentum value: %s',
+                 self.momentum)
+            need(0.0 <= self.alpha, 'Invalid alpha value: %s', self.alpha)
 
     def _lr(self):
         if not self._annealing:

@@ -623,10 +623,23 @@ class B64Stager:
             device = torch.device('cuda', torch.cuda.current_device())
         self.device = device
         self.stream = stream
-        with torch.cuda.stream(stream):
-            self.status = torch.zeros(1, dtype=torch.int32,
-                                      device=self.device)
+        # one status word per upload since the last collect(): a rejected
+        # upload is reported by its tag (the sender / stack slot), not as a
+        # failure of the whole round
+        self._status = []
+        self.tags = []
         self.puts = 0
+
+    _BLOCK = 256
+
+    def _status_word(self, i):
+        b, j = divmod(i, self._BLOCK)
+        while len(self._status) <= b:
+            with torch.cuda.stream(self.stream):
+                self._status.append(torch.zeros(self._BLOCK,
+                                                dtype=torch.int32,
+                                                device=self.device))
+        return self._status[b].data_ptr() + 4 * j
 
     @staticmethod
     def plan(layout, model):
@@ -653,11 +666,12 @@ class B64Stager:
                 host.append(k)
         return dev, host
 
-    def put(self, layout, framings, dst_row, pinned, host=None):
+    def put(self, layout, framings, dst_row, pinned, host=None, tag=None):
         """Stage one upload (``framings`` from :meth:`plan`) into
         ``dst_row``; ``pinned(nbytes)`` returns a free pinned uint8 buffer.
         ``host``: {key: value} of the upload's keys :meth:`plan` left to the
-        host decode.  Returns the event of the DMA that reads it."""
+        host decode; ``tag`` names the upload in :meth:`collect`'s report.
+        Returns the event of the DMA that reads it."""
         host_keys = host or {}
         from ... import _lib as L
         from ...ops import WIRE_SEG_DTYPE, _stream
@@ -722,7 +736,7 @@ class B64Stager:
             L.check(L.load().fsagg_b64_unpack_f32(
                 dev.data_ptr() + sb, int(tb), dev.data_ptr(), len(segs),
                 int(max_len), dst_row.data_ptr(), int(layout.numel),
-                self.status.data_ptr(), _stream(self.device)),
+                self._status_word(self.puts), _stream(self.device)),
                 'fsagg_b64_unpack_f32')
             for k, v in host_keys.items():
                 # rare (a non-contiguous or non-fp32 key): decoded on the
@@ -731,23 +745,43 @@ class B64Stager:
                 o, m = layout.offsets[k], layout.numels[k]
                 dst_row[o:o + m].copy_(param2tensor(v).reshape(-1))
         self.puts += 1
+        self.tags.append(tag)
         STATS['device_puts'] += 1
         STATS['device_text_bytes'] += toff
         return ev
 
+    _REASON = {1: 'a character outside the base64 alphabet in the tensor '
+                  'data',
+               2: 'a segment outside the staged text or the row'}
+
+    def collect(self):
+        """[(tag, reason)] of the uploads since the last collect that the
+        device decode rejected (waits for their decodes); clears them."""
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        if not self.puts:
+            return []
+        words = torch.cat(self._status).cpu()[:self.puts].tolist()
+        bad = [(t, self._REASON.get(w, 'status %d' % w))
+               for t, w in zip(self.tags, words) if w]
+        if bad:
+            with torch.cuda.stream(self.stream):
+                for st in self._status:
+                    st.zero_()
+        self.puts = 0
+        self.tags = []
+        return bad
+
     def finish(self):
         """Order the consumer stream after every decode and raise if one of
-        them met a non-base64 character or an out-of-range segment."""
-        torch.cuda.current_stream(self.device).wait_stream(self.stream)
-        if self.puts:
-            st = int(self.status.item())
-            if st:
-                self.status.zero_()
-                raise FramingError(
-                    'base64 upload rejected on the device: %s' %
-                    ('a character outside the base64 alphabet in the '
-                     'tensor data' if st == 1 else
-                     'a segment outside the staged text or the row'))
+        them met a non-base64 character or an out-of-range segment (the
+        error's ``rejected`` lists the offending uploads' tags)."""
+        bad = self.collect()
+        if bad:
+            err = FramingError(
+                'base64 upload(s) rejected on the device: %s' % '; '.join(
+                    '%s: %s' % (t, r) for t, r in bad))
+            err.rejected = [t for t, _ in bad]
+            raise err
 
 
 _EXT = []

@@ -82,9 +82,26 @@ class DeviceIngress:
 
     def reset(self):
         """Start a new round: slots are reused (kernels of the previous round
-        are ordered before the next copies by HostStager)."""
+        are ordered before the next copies by HostStager).  A base64 upload
+        of the closing round whose device decode was rejected and never
+        reported (:meth:`rejected`, or an aggregation's sync) raises here
+        instead of being dropped silently."""
+        st = self._stager
         self.next_slot = 0
         self._stager = None
+        if st is not None:
+            st.finish()
+
+    def rejected(self):
+        """[(tag, reason)] of the uploads staged since the last check whose
+        device-side base64 decode was rejected — tag is the ``tag`` given to
+        :meth:`receive` (the sender) or else the stack slot.  Waits for the
+        staging; the rejected rows hold partial data and must not be
+        aggregated."""
+        st = self._stager
+        if st is None or not hasattr(st, 'rejected'):
+            return []
+        return st.rejected()
 
     def _slot(self, slot=None):
         """The stack row for the next upload: ``slot`` (a sender's earlier
@@ -124,9 +141,10 @@ class DeviceIngress:
                 return False
         return True
 
-    def receive(self, sample_size, model_para, slot=None):
+    def receive(self, sample_size, model_para, slot=None, tag=None):
         """Stage one upload; returns (sample_size, StagedUpdate).  ``slot``
-        reuses the row of the same sender's earlier upload this round.
+        reuses the row of the same sender's earlier upload this round;
+        ``tag`` (e.g. the sender) names it in :meth:`rejected`.
         fp32 keys go into the slot, keys of other dtypes to device copies
         of their own dtype (StagedUpdate.typed)."""
         if not self.accepts(model_para):
@@ -142,7 +160,8 @@ class DeviceIngress:
                 self._stager = HostStager(self.device)
             src = model_para if not self.as_float else {
                 k: as_float_upload(model_para[k]) for k in self.layout.keys}
-            self._stager.put(self.layout, src, self.stack.slab[slot])
+            self._stager.put(self.layout, src, self.stack.slab[slot],
+                             tag=slot if tag is None else tag)
             return sample_size, StagedUpdate(self, slot, model_para.keys(),
                                              typed)
         src = {k: (as_float_tensor(model_para[k]) if self.as_float else

@@ -60,6 +60,7 @@ class AggregationServer:
         self.msg_buffer = {'train': {}}
         self.staled_msg_buffer = []
         self.dropout_num = 0
+        self.rejected_uploads = []
         self.ingresses = [None] * self.model_num
         self.history = deque(maxlen=keep_history) if keep_history else None
         if online_aggr:
@@ -70,7 +71,7 @@ class AggregationServer:
         return self.ingresses[0]
 
     # -- server.py:929-988 ---------------------------------------------------
-    def _stage(self, idx, para, prev):
+    def _stage(self, idx, para, prev, sender=None):
         """Stage model ``idx``'s part of an upload on arrival (or keep it as
         it came when its layout differs from the round's)."""
         staged_quant = self.dequantize
@@ -87,7 +88,7 @@ class AggregationServer:
             return ing.receive_quantized(None, para, slot=slot)[1]
         if not ing.accepts(para):
             return para
-        return ing.receive(None, para, slot=slot)[1]
+        return ing.receive(None, para, slot=slot, tag=sender)[1]
 
     def callback_funcs_model_para(self, round, sender, content):
         staged_quant = self.dequantize and self.stage_on_arrival and \
@@ -106,9 +107,11 @@ class AggregationServer:
                 prev = self.msg_buffer['train'].get(round, {}).get(sender)
                 size, para = content
                 if self.model_num == 1:
-                    para = self._stage(0, para, prev[1] if prev else None)
+                    para = self._stage(0, para, prev[1] if prev else None,
+                                       sender)
                 else:
-                    para = [self._stage(i, p, prev[1][i] if prev else None)
+                    para = [self._stage(i, p, prev[1][i] if prev else None,
+                                        sender)
                             for i, p in enumerate(para)]
                 content = (size, para)
             self.msg_buffer['train'].setdefault(round, dict())[sender] = \
@@ -126,6 +129,8 @@ class AggregationServer:
         buf = self.msg_buffer['train'].get(self.state, {})
         if len(buf) < self.sample_client_num:
             return False
+        if self._drop_rejected(buf) and len(buf) < self.sample_client_num:
+            return False            # wait for uploads in their place
         self._perform_federated_aggregation()
         self.msg_buffer['train'].pop(self.state, None)
         self.state += 1
@@ -136,6 +141,24 @@ class AggregationServer:
         if self.online_aggr:
             self.aggregator.reset()
         return True
+
+    def _drop_rejected(self, buf):
+        """Uploads whose base64 text the device decode rejected (a character
+        outside the alphabet in the tensor data: DeviceIngress.rejected) are
+        removed from this round's buffer by sender and recorded in
+        ``rejected_uploads`` as (round, sender, reason) — the reference's
+        receive path raises on such a message before it is ever buffered.
+        Returns whether any was dropped."""
+        dropped = False
+        for ing in self.ingresses:
+            if ing is None:
+                continue
+            for sender, reason in ing.rejected():
+                if buf.pop(sender, None) is not None:
+                    self.rejected_uploads.append((self.state, sender,
+                                                  reason))
+                    dropped = True
+        return dropped
 
     # -- server.py:437-490 ----------------------------------------------------
     def _perform_federated_aggregation(self):

@@ -235,11 +235,13 @@ class HostStager:
         self.i = 0
         self._b64 = None
 
-    def put(self, layout, model, dst_row):
+    def put(self, layout, model, dst_row, tag=None):
+        """Stage one upload into ``dst_row``; ``tag`` names it when its
+        device-side base64 decode is rejected (:meth:`rejected`)."""
         slot = self.i % self.nbuf
         self.i += 1
         if isinstance(layout, BucketLayout) and self._put_b64(
-                layout, model, dst_row, slot):
+                layout, model, dst_row, slot, tag):
             return
         host = _pinned(layout.numel, slot)
         layout.pack_host(model, host)
@@ -250,7 +252,7 @@ class HostStager:
         _PINNED_EV[slot] = ev
         self.last = ev
 
-    def _put_b64(self, layout, model, dst_row, slot):
+    def _put_b64(self, layout, model, dst_row, slot, tag=None):
         """gRPC uploads (every fp32 key base64 text, core/compression/
         b64wire): the base64 characters cross PCIe and are decoded into the
         row on the device.  False when the upload is not of that form."""
@@ -265,7 +267,7 @@ class HostStager:
         ev = self._b64.put(layout, framings, dst_row,
                            lambda nb: _pinned(-(-nb // 4), slot).view(
                                torch.uint8),
-                           host={k: model[k] for k in host_keys})
+                           host={k: model[k] for k in host_keys}, tag=tag)
         if ev is not None:
             _PINNED_EV[slot] = ev
             self.last = ev
@@ -275,6 +277,12 @@ class HostStager:
         torch.cuda.current_stream(self.device).wait_stream(self.stream)
         if self._b64 is not None:
             self._b64.finish()
+
+    def rejected(self):
+        """[(tag, reason)] of the uploads whose device decode was rejected
+        since the last check (waits for the decodes; does not raise)."""
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        return self._b64.collect() if self._b64 is not None else []
 
 
 class ClientStack:

@@ -460,3 +460,54 @@ def test_b64_bad_character_in_data_raises():
     st.load_many([{'w': txt}])                 # the stager state is clean
     torch.cuda.synchronize()
     assert torch.equal(st.slab[0, :100_000].cpu(), t)
+
+
+def test_b64_rejected_upload_dropped_by_sender():
+    """One sender's base64 carries a character outside the alphabet inside
+    its tensor data: the server drops that sender's upload alone (recorded
+    in rejected_uploads with its reason), keeps waiting, and aggregates
+    once the sender re-uploads a clean one — bit-identical to the round
+    without the bad upload."""
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    from federatedscope_amd.core.workers.server import AggregationServer
+    meta, clients, out, _, _ = load_case('b64_fedavg_n5')
+    c = _cfg()
+
+    class M(torch.nn.Module):
+        def state_dict(self, *a, **kw):
+            return OrderedDict()
+
+        def load_state_dict(self, sd, strict=True):
+            self.loaded = sd
+
+    srv = AggregationServer(M(), ClientsAvgAggregator(device='cuda',
+                                                      config=c),
+                            sample_client_num=len(clients), keep_history=1)
+    bad_sender = 2
+    s2, d2 = clients[bad_sender]
+    k = max(d2, key=lambda key: len(d2[key]) if isinstance(d2[key], str)
+            else 0)
+    txt = d2[k]
+    mid = len(txt) // 2
+    corrupt = OrderedDict(d2)
+    corrupt[k] = txt[:mid] + '*' + txt[mid + 1:]
+    for sender, (s, d) in enumerate(clients):
+        moved = srv.callback_funcs_model_para(
+            0, sender, (s, corrupt if sender == bad_sender else
+                        OrderedDict(d)))
+    assert moved is False and srv.state == 0
+    assert [(r, snd) for r, snd, _ in srv.rejected_uploads] == \
+        [(0, bad_sender)]
+    assert 'alphabet' in srv.rejected_uploads[0][2]
+    assert bad_sender not in srv.msg_buffer['train'][0]
+    assert srv.callback_funcs_model_para(0, bad_sender, (s2, OrderedDict(d2)))
+    got = srv.history[-1]
+    # arrival order differs from the fixture's (the sender re-uploaded
+    # last): the reference's result for this order
+    order = [i for i in range(len(clients)) if i != bad_sender] + \
+        [bad_sender]
+    want = O.para_weighted_avg([(clients[i][0], OrderedDict(
+        (kk, O.b64_tensor(v) if isinstance(v, str) else v)
+        for kk, v in clients[i][1].items())) for i in order])
+    for kk in want:
+        _same_bits(got[kk], want[kk])

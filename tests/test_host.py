@@ -428,3 +428,48 @@ def test_b64_native_walk_matches_python_walk():
             B.parse_b64(x)
         with pytest.raises(B.FramingError):
             B.parse_b64_py(x)
+
+
+@pytest.mark.parametrize('opt', [
+    dict(type='SGD', lr=-0.1),
+    dict(type='SGD', lr=0.1, momentum=-0.5),
+    dict(type='SGD', lr=0.1, weight_decay=-1.0),
+    dict(type='SGD', lr=0.1, nesterov=True),
+    dict(type='SGD', lr=0.1, momentum=0.9, dampening=0.1, nesterov=True),
+    dict(type='Adam', lr=0.1, betas=(1.0, 0.999)),
+    dict(type='Adam', lr=0.1, betas=(0.9, -0.1)),
+    dict(type='Adam', lr=0.1, eps=-1e-8),
+    dict(type='AdamW', lr=0.1, weight_decay=-0.01),
+    dict(type='Adagrad', lr=0.1, lr_decay=-1.0),
+    dict(type='Adagrad', lr=0.1, initial_accumulator_value=-1.0),
+    dict(type='RMSprop', lr=0.1, alpha=-0.9),
+    dict(type='RMSprop', lr=0.1, momentum=-0.9),
+])
+def test_fedopt_rejects_what_torch_optim_rejects(opt):
+    """The FedOpt server optimizer's config is checked like the torch.optim
+    constructor the reference's get_optimizer builds
+    (optimizer_builder.py:53-56): same exception type and message."""
+    from types import SimpleNamespace
+    from federatedscope_amd.core.aggregators import FedOptAggregator
+    kw = {k: v for k, v in opt.items() if k != 'type'}
+    with pytest.raises(ValueError) as want:
+        getattr(torch.optim, opt['type'])(
+            [torch.zeros(1, requires_grad=True)], **kw)
+    cfg = SimpleNamespace(
+        federate=SimpleNamespace(ignore_weight=False, use_ss=False),
+        fedopt=SimpleNamespace(optimizer=dict(opt), annealing=False))
+    with pytest.raises(ValueError) as got:
+        FedOptAggregator(config=cfg, model=torch.nn.Linear(2, 2))
+    assert str(got.value) == str(want.value)
+
+
+def test_fedopt_keeps_its_config():
+    from types import SimpleNamespace
+    from federatedscope_amd.core.aggregators import FedOptAggregator
+    cfg = SimpleNamespace(
+        federate=SimpleNamespace(ignore_weight=False, use_ss=False),
+        fedopt=SimpleNamespace(optimizer=dict(type='SGD', lr=0.5,
+                                              momentum=0.9), annealing=False))
+    agg = FedOptAggregator(config=cfg, model=torch.nn.Linear(2, 2))
+    assert agg.opt_kwargs == {'momentum': 0.9}
+    assert agg.momentum == 0.9
