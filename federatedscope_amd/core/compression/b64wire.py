@@ -648,16 +648,24 @@ class B64Stager:
         shape (decoded on the device), and the other present keys (decoded
         on the host: param2tensor, which also raises on malformed text)."""
         dev, host = {}, []
-        for k in layout.keys:
-            if k not in model:
-                continue
-            v = model[k]
-            t = None
-            if is_b64(v):
+        keys = [k for k in layout.keys if k in model]
+        texts = [k for k in keys if is_b64(model[k])]
+        ext = _text_ext()
+        if ext is not None and hasattr(ext, 'b64_frame_many') and texts:
+            # every key's walk in one native call, over several threads
+            fr = ext.b64_frame_many([model[k] for k in texts])
+            parsed = {k: (None if f is None else _fill(
+                B64Tensor(), model[k], (_STORAGE_DTYPES[f[0]], ) + f[1:]))
+                      for k, f in zip(texts, fr)}
+        else:
+            parsed = {}
+            for k in texts:
                 try:
-                    t = parse_b64(v)
+                    parsed[k] = parse_b64(model[k])
                 except FramingError:
-                    t = None
+                    parsed[k] = None
+        for k in keys:
+            t = parsed.get(k)
             if t is not None and t.dtype == torch.float32 and \
                     tuple(t.shape) == tuple(layout.shapes[k]) and \
                     t.is_contiguous():
@@ -718,6 +726,11 @@ class B64Stager:
         buf[:32 * len(segs)].copy_(torch.from_numpy(arr.view(np.uint8)))
         base = buf.data_ptr() + sb
         ext = _text_ext()
+        if ext is not None and hasattr(ext, 'text_copy_many'):
+            # every key's characters in one call, the bytes split evenly
+            # over the threads whatever the key sizes
+            ext.text_copy_many(chunks, base)
+            chunks = []
         for text, c0, c1, off in chunks:
             if ext is not None:
                 ext.text_copy(text, c0, c1, base + off)

@@ -24,6 +24,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -449,7 +450,15 @@ V walk(Text &src, int64_t &pos, int64_t end, GlobalSet gs) {
 const unsigned char kMagic[10] = {0x6c, 0xfc, 0x9c, 0x46, 0xf9,
                                   0x20, 0x6a, 0xa8, 0x50, 0x19};
 
-PyObject *frame(Text &src) {
+// A walk's result (b64_frame's tuple, built once the GIL is held).
+struct FrameOut {
+  int si = -1;
+  std::vector<int64_t> size, stride;
+  int64_t offset = 0, numel = 0, data_pos = 0, nchars = 0;
+  bool rg = false;
+};
+
+FrameOut frame(Text &src) {
   int64_t pos = 0;
   V t = walk(src, pos, src.size, OUTER);
   if (pos != src.size) throw Fail{"bytes after the pickle"};
@@ -520,21 +529,68 @@ PyObject *frame(Text &src) {
     }
     if (last >= n) throw Fail{"tensor reaches past its storage"};
   }
-  PyObject *shape = PyTuple_New(Py_ssize_t(t->size.size()));
-  PyObject *stride = PyTuple_New(Py_ssize_t(t->size.size()));
+  FrameOut o;
+  o.si = si;
+  o.size = t->size;
+  o.stride = t->stride;
+  o.offset = t->i;
+  o.numel = n;
+  o.data_pos = p + 8;
+  o.rg = t->rg;
+  o.nchars = src.nchars;
+  return o;
+}
+
+PyObject *to_py(const FrameOut &o) {
+  PyObject *shape = PyTuple_New(Py_ssize_t(o.size.size()));
+  PyObject *stride = PyTuple_New(Py_ssize_t(o.size.size()));
   if (!shape || !stride) {
     Py_XDECREF(shape);
     Py_XDECREF(stride);
     return nullptr;
   }
-  for (size_t j = 0; j < t->size.size(); ++j) {
-    PyTuple_SET_ITEM(shape, Py_ssize_t(j), PyLong_FromLongLong(t->size[j]));
-    PyTuple_SET_ITEM(stride, Py_ssize_t(j),
-                     PyLong_FromLongLong(t->stride[j]));
+  for (size_t j = 0; j < o.size.size(); ++j) {
+    PyTuple_SET_ITEM(shape, Py_ssize_t(j), PyLong_FromLongLong(o.size[j]));
+    PyTuple_SET_ITEM(stride, Py_ssize_t(j), PyLong_FromLongLong(o.stride[j]));
   }
-  return Py_BuildValue("(sNNLLLOL)", kStorageClasses[si], shape, stride,
-                       (long long)t->i, (long long)n, (long long)(p + 8),
-                       t->rg ? Py_True : Py_False, (long long)src.nchars);
+  return Py_BuildValue("(sNNLLLOL)", kStorageClasses[o.si], shape, stride,
+                       (long long)o.offset, (long long)o.numel,
+                       (long long)o.data_pos, o.rg ? Py_True : Py_False,
+                       (long long)o.nchars);
+}
+
+// The characters of a str (compact ASCII, read in place) or bytes-like
+// object; false with a Python error set otherwise.
+bool text_of(PyObject *obj, Text &src, Py_buffer &view, bool &have_view) {
+  have_view = false;
+  if (PyUnicode_Check(obj)) {
+    if (PyUnicode_READY(obj) != 0) return false;
+    if (!PyUnicode_IS_COMPACT_ASCII(obj)) {
+      PyErr_SetString(PyExc_ValueError,
+                      "framing: invalid base64 in the tensor framing "
+                      "(non-ASCII text)");
+      return false;
+    }
+    src.c = static_cast<const unsigned char *>(PyUnicode_DATA(obj));
+    src.nchars = PyUnicode_GET_LENGTH(obj);
+    return true;
+  }
+  if (PyObject_GetBuffer(obj, &view, PyBUF_SIMPLE) != 0) return false;
+  have_view = true;
+  src.c = static_cast<const unsigned char *>(view.buf);
+  src.nchars = view.len;
+  return true;
+}
+
+// The walk of one text, no Python API (runs without the GIL).
+FrameOut frame_text(Text &src) {
+  if (src.nchars == 0 || src.nchars % 4)
+    throw Fail{"base64 text is not a whole number of 4-character groups"};
+  int pad = 0;
+  if (src.c[src.nchars - 1] == '=') ++pad;
+  if (src.c[src.nchars - 2] == '=') ++pad;
+  src.size = 3 * (src.nchars / 4) - pad;
+  return frame(src);
 }
 
 }  // namespace
@@ -545,31 +601,10 @@ PyObject *b64_frame(PyObject *, PyObject *args) {
   Text src;
   Py_buffer view{};
   bool have_view = false;
-  if (PyUnicode_Check(obj)) {
-    if (PyUnicode_READY(obj) != 0) return nullptr;
-    if (!PyUnicode_IS_COMPACT_ASCII(obj)) {
-      PyErr_SetString(PyExc_ValueError,
-                      "framing: invalid base64 in the tensor framing "
-                      "(non-ASCII text)");
-      return nullptr;
-    }
-    src.c = static_cast<const unsigned char *>(PyUnicode_DATA(obj));
-    src.nchars = PyUnicode_GET_LENGTH(obj);
-  } else {
-    if (PyObject_GetBuffer(obj, &view, PyBUF_SIMPLE) != 0) return nullptr;
-    have_view = true;
-    src.c = static_cast<const unsigned char *>(view.buf);
-    src.nchars = view.len;
-  }
+  if (!text_of(obj, src, view, have_view)) return nullptr;
   PyObject *res = nullptr;
   try {
-    if (src.nchars == 0 || src.nchars % 4)
-      throw Fail{"base64 text is not a whole number of 4-character groups"};
-    int pad = 0;
-    if (src.c[src.nchars - 1] == '=') ++pad;
-    if (src.c[src.nchars - 2] == '=') ++pad;
-    src.size = 3 * (src.nchars / 4) - pad;
-    res = frame(src);
+    res = to_py(frame_text(src));
   } catch (const Fail &f) {
     PyErr_SetString(PyExc_ValueError, ("framing: " + f.msg).c_str());
     res = nullptr;
@@ -578,5 +613,68 @@ PyObject *b64_frame(PyObject *, PyObject *args) {
     res = nullptr;
   }
   if (have_view) PyBuffer_Release(&view);
+  return res;
+}
+
+// b64_frame_many(texts[, threads]) -> [b64_frame(text) or None]: the walks
+// of every key of one upload, spread over `threads` threads with the GIL
+// released (a many-key model pays one call, not one walk per key in
+// series).  An entry is None when that text is not a tensor upload (its
+// b64_frame would raise); the caller decodes it on the host.
+PyObject *b64_frame_many(PyObject *, PyObject *args) {
+  PyObject *seq;
+  int threads = 8;
+  if (!PyArg_ParseTuple(args, "O|i", &seq, &threads)) return nullptr;
+  PyObject *fast = PySequence_Fast(seq, "b64_frame_many takes a sequence");
+  if (!fast) return nullptr;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(fast);
+  std::vector<Text> src(static_cast<size_t>(n));
+  std::vector<Py_buffer> views(static_cast<size_t>(n));
+  std::vector<char> have(static_cast<size_t>(n), 0), ok(static_cast<size_t>(n), 0);
+  std::vector<FrameOut> out(static_cast<size_t>(n));
+  bool fail = false;
+  for (Py_ssize_t i = 0; i < n && !fail; ++i) {
+    bool hv = false;
+    PyObject *o = PySequence_Fast_GET_ITEM(fast, i);
+    if (!text_of(o, src[size_t(i)], views[size_t(i)], hv)) {
+      PyErr_Clear();            // not text: left to the host decode
+      src[size_t(i)].c = nullptr;
+    }
+    have[size_t(i)] = hv;
+  }
+  Py_BEGIN_ALLOW_THREADS
+  auto work = [&](int t, int nt) {
+    for (Py_ssize_t i = t; i < n; i += nt) {
+      if (!src[size_t(i)].c) continue;
+      try {
+        out[size_t(i)] = frame_text(src[size_t(i)]);
+        ok[size_t(i)] = 1;
+      } catch (...) {
+        ok[size_t(i)] = 0;
+      }
+    }
+  };
+  int nt = threads < 1 ? 1 : threads;
+  if (Py_ssize_t(nt) > n / 4) nt = int(n / 4) < 1 ? 1 : int(n / 4);
+  if (nt == 1) {
+    work(0, 1);
+  } else {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; ++t) pool.emplace_back(work, t, nt);
+    for (auto &th : pool) th.join();
+  }
+  Py_END_ALLOW_THREADS
+  for (Py_ssize_t i = 0; i < n; ++i)
+    if (have[size_t(i)]) PyBuffer_Release(&views[size_t(i)]);
+  PyObject *res = PyList_New(n);
+  for (Py_ssize_t i = 0; res && i < n; ++i) {
+    PyObject *v = ok[size_t(i)] ? to_py(out[size_t(i)]) : Py_NewRef(Py_None);
+    if (!v) {
+      Py_CLEAR(res);
+      break;
+    }
+    PyList_SET_ITEM(res, i, v);
+  }
+  Py_DECREF(fast);
   return res;
 }

@@ -35,6 +35,7 @@
 
 // host/b64frame.cpp: the framing walk of one gRPC tensor upload
 PyObject *b64_frame(PyObject *, PyObject *args);
+PyObject *b64_frame_many(PyObject *, PyObject *args);
 
 namespace {
 
@@ -198,12 +199,123 @@ PyObject *text_copy(PyObject *, PyObject *args) {
   Py_RETURN_NONE;
 }
 
+// text_copy_many(items, dst_addr[, threads]) -> None: text_copy of every
+// (text, lo, hi, off) in `items` to dst_addr + off, the bytes of all items
+// split evenly over the threads (one call per upload: a model of many
+// small keys copies as fast as one large key).
+PyObject *text_copy_many(PyObject *, PyObject *args) {
+  PyObject *seq;
+  unsigned long long dst;
+  int threads = 8;
+  if (!PyArg_ParseTuple(args, "OK|i", &seq, &dst, &threads)) return nullptr;
+  if (dst == 0) {
+    PyErr_SetString(PyExc_ValueError, "text_copy_many: NULL destination");
+    return nullptr;
+  }
+  PyObject *fast = PySequence_Fast(seq, "text_copy_many takes a sequence");
+  if (!fast) return nullptr;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(fast);
+  struct Item {
+    const char *src;
+    char *out;
+    size_t n;
+  };
+  std::vector<Item> items;
+  std::vector<Py_buffer> views;
+  items.reserve(size_t(n));
+  views.reserve(size_t(n));
+  bool fail = false;
+  for (Py_ssize_t i = 0; i < n && !fail; ++i) {
+    PyObject *obj;
+    long long lo, hi, off;
+    if (!PyArg_ParseTuple(PySequence_Fast_GET_ITEM(fast, i), "OLLL", &obj,
+                          &lo, &hi, &off)) {
+      fail = true;
+      break;
+    }
+    const char *src = nullptr;
+    Py_ssize_t len = 0;
+    if (PyUnicode_Check(obj)) {
+      if (PyUnicode_READY(obj) != 0 || !PyUnicode_IS_COMPACT_ASCII(obj)) {
+        if (!PyErr_Occurred())
+          PyErr_SetString(PyExc_ValueError,
+                          "text_copy_many: base64 text must be ASCII");
+        fail = true;
+        break;
+      }
+      src = static_cast<const char *>(PyUnicode_DATA(obj));
+      len = PyUnicode_GET_LENGTH(obj);
+    } else {
+      Py_buffer v{};
+      if (PyObject_GetBuffer(obj, &v, PyBUF_SIMPLE) != 0) {
+        fail = true;
+        break;
+      }
+      views.push_back(v);
+      src = static_cast<const char *>(v.buf);
+      len = v.len;
+    }
+    if (lo < 0 || hi < lo || hi > len || off < 0) {
+      PyErr_SetString(PyExc_ValueError, "text_copy_many: range out of bounds");
+      fail = true;
+      break;
+    }
+    items.push_back({src + lo, reinterpret_cast<char *>(dst) + off,
+                     size_t(hi - lo)});
+  }
+  if (!fail) {
+    size_t total = 0;
+    for (const auto &it : items) total += it.n;
+    Py_BEGIN_ALLOW_THREADS
+    // thread t copies bytes [t·step, (t+1)·step) of the items laid end to
+    // end
+    auto work = [&](size_t a, size_t b) {
+      size_t base = 0;
+      for (const auto &it : items) {
+        const size_t e = base + it.n;
+        if (e > a && base < b) {
+          const size_t x = a > base ? a - base : 0;
+          const size_t y = (b < e ? b : e) - base;
+          std::memcpy(it.out + x, it.src + x, y - x);
+        }
+        base = e;
+        if (base >= b) break;
+      }
+    };
+    const size_t per_min = size_t(4) << 20;
+    int t = threads < 1 ? 1 : threads;
+    if (size_t(t) > total / per_min)
+      t = int(total / per_min) < 1 ? 1 : int(total / per_min);
+    if (t == 1) {
+      work(0, total);
+    } else {
+      const size_t step = ((total + t - 1) / t + 4095) & ~size_t(4095);
+      std::vector<std::thread> pool;
+      for (int i = 0; i < t; ++i) {
+        const size_t a = size_t(i) * step;
+        if (a >= total) break;
+        pool.emplace_back(work, a, a + step < total ? a + step : total);
+      }
+      for (auto &th : pool) th.join();
+    }
+    Py_END_ALLOW_THREADS
+  }
+  for (auto &v : views) PyBuffer_Release(&v);
+  Py_DECREF(fast);
+  if (fail) return nullptr;
+  Py_RETURN_NONE;
+}
+
 PyMethodDef kMethods[] = {
     {"device_tensor", device_tensor, METH_VARARGS,
      "device_tensor(ptr, numel, kind, device_index) -> Tensor (no ownership)"},
     {"b64_frame", b64_frame, METH_VARARGS,
      "b64_frame(text) -> (storage_class, shape, stride, storage_offset, "
      "storage_numel, data_pos, requires_grad, nchars)"},
+    {"b64_frame_many", b64_frame_many, METH_VARARGS,
+     "b64_frame_many(texts[, threads]) -> [b64_frame(text) or None]"},
+    {"text_copy_many", text_copy_many, METH_VARARGS,
+     "text_copy_many([(text, lo, hi, off)], dst_addr[, threads])"},
     {"text_copy", text_copy, METH_VARARGS,
      "text_copy(text, lo, hi, dst_addr[, threads]): copy chars [lo, hi)"},
     {"key_table", key_table, METH_VARARGS,
