@@ -171,6 +171,81 @@ def plugin_surface_leg(args, dev, slab, rows, sizes, w_dev, P, rounds=5,
     }
 
 
+def plugin_layout_b_leg(dev, sizes, w_dev, rounds=5, calls=10):
+    """configs[2] layout B: the same call on the ResNet-50 layout (161 keys,
+    tools/resnet50_layout.json) — 100 device-resident multi-key state_dicts
+    whose keys are views of one slab per client (read in place; the
+    multi-key row-set kernel), against the bare flat kernel over the same
+    slab rows, interleaved, every key compared bit for bit."""
+    import statistics
+    from collections import OrderedDict
+    from types import SimpleNamespace
+
+    import torch
+    from federatedscope_amd import ops
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    from federatedscope_amd.layout import BucketLayout
+    with open(os.path.join(ROOT, 'tools', 'resnet50_layout.json')) as f:
+        keys = [(k, tuple(s)) for k, s in json.load(f)['keys']]
+    lay = BucketLayout(OrderedDict((k, torch.empty(s, device='meta'))
+                                   for k, s in keys))
+    n, P = len(sizes), lay.numel
+    ld = ops.round_up(P, 64)
+    slab = torch.empty((n, ld), dtype=torch.float32, device=dev)
+    ops.fill_uniform(slab, ld, seed=SEED + 1)
+    clients = [(sizes[i], OrderedDict(
+        (k, slab[i, lay.offsets[k]:lay.offsets[k] + lay.numels[k]].view(
+            lay.shapes[k])) for k in lay.keys)) for i in range(n)]
+    cfg = SimpleNamespace(federate=SimpleNamespace(ignore_weight=False,
+                                                   use_ss=False))
+    agg = ClientsAvgAggregator(device=dev, config=cfg)
+    info = {'client_feedback': clients, 'recover_fun': None}
+    rows = ops.RowTable.from_slab(slab, numel=ld)
+    flat = torch.empty(ld, dtype=torch.float32, device=dev)
+
+    def run_agg():
+        return agg.aggregate(info)
+
+    def run_flat():
+        ops.weighted_sum(rows, w_dev, flat)
+
+    for _ in range(3):
+        res = run_agg()
+        run_flat()
+    torch.cuda.synchronize()
+    exact = all(torch.equal(res[k].reshape(-1), flat[
+        lay.offsets[k]:lay.offsets[k] + lay.numels[k]]) for k in lay.keys)
+    t_agg, t_flat = [], []
+    for _ in range(rounds):
+        for fn, acc in ((run_agg, t_agg), (run_flat, t_flat)):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(calls):
+                fn()
+            torch.cuda.synchronize()
+            acc.append((time.perf_counter() - t0) / calls * 1e3)
+    a, f = statistics.median(t_agg), statistics.median(t_flat)
+    log('layout B (%d keys, %d params): aggregate() %.4f ms/call, bare flat '
+        'kernel %.4f ms (ratio %.4f), bit-exact %s' %
+        (len(keys), P, a, f, a / f, exact))
+    del slab, rows
+    return {
+        'what': 'ClientsAvgAggregator.aggregate(agg_info) on %d device '
+                'dicts of the ResNet-50 layout (%d keys, %d fp32 params; '
+                'views of one slab row per client, read in place) against '
+                'the flat kernel over the same rows; median of %d '
+                'interleaved rounds of %d calls' % (n, len(keys), P, rounds,
+                                                    calls),
+        'keys': len(keys),
+        'params': P,
+        'ms_per_call': round(a, 4),
+        'GBps': round(4.0 * n * P / a / 1e6, 1),
+        'bare_flat_kernel_ms': round(f, 4),
+        'ratio_vs_bare_kernel': round(a / f, 4),
+        'bit_exact_vs_kernel': exact,
+    }
+
+
 def e2e_leg(args, dev, weights, sizes):
     """Host state_dicts in, host state_dict out, through the drop-in
     ClientsAvgAggregator (pinned double-buffered staging, H2D, kernel, D2H).
@@ -602,10 +677,11 @@ def main():
         (t_step * 1e3, kern_ms, t_sharded * 1e3, mean_launch_ms, achieved,
          ok))
 
-    plugin = None
+    plugin = plugin_b = None
     if world == 1 and not args.no_plugin:
         plugin = plugin_surface_leg(args, dev, pieces[0][0], pieces[0][1],
                                     sizes, w_dev, P)
+        plugin_b = plugin_layout_b_leg(dev, sizes, w_dev)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -700,6 +776,7 @@ def main():
                 'value': round(4.0 * n * P / t_sharded / 1e9, 2)},
             'weak_scaling': weak,
             'plugin_surface': plugin,
+            'plugin_surface_layout_b': plugin_b,
             'assembled_bit_exact': ok,
         }
         print(json.dumps(rec), flush=True)
