@@ -405,16 +405,28 @@ __device__ void centre_of(const double *G, int n, int *centre,
 
 // One arrival at a completion counter of `total` arrivals; true (on every
 // thread) for the last one, which then sees every other arrival's stores.
+// The split-K hand-off: every wave drains its own stores (a barrier does
+// not wait for them), one lane releases at agent scope (the XCD's L2
+// written back, whichever waves stored) and draws a ticket; the last
+// arriver's lane acquires at agent scope before the workgroup reads.  The
+// explicit vmcnt waits stay: the fences' own waits can be dropped.
 __device__ __forceinline__ bool arrive(int *cnt, int total, int *flag) {
-  __syncthreads();                 // the workgroup's stores are issued
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();               // release them device-wide
-    *flag = atomicAdd(cnt, 1) == total - 1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const bool last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) ==
+                      total - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
   }
   __syncthreads();
-  const bool last = *flag != 0;
-  if (last) __threadfence();       // acquire the others'
-  return last;
+  return *flag != 0;
 }
 
 // What runs after a chunk's partial is stored.  The last chunk of a group

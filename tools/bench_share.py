@@ -53,7 +53,15 @@ def main():
                     help='time the peer-assembly share instead: one bcast '
                          'launch over P/world writing `world` uncached local '
                          'buffers (stand-ins for the peers) + the barrier')
+    ap.add_argument('--aggregate', action='store_true',
+                    help='time rank 0\'s share of the plug-in path: '
+                         'ClientsAvgAggregator.aggregate() sharded by '
+                         'parameter range with the peer assembly (fused '
+                         'broadcast into world uncached buffers, barrier, '
+                         'copy-out of the assembled bucket, status check)')
     args = ap.parse_args()
+    if args.aggregate:
+        return aggregate_share(args)
     if args.p2p:
         return p2p_share(args)
 
@@ -177,6 +185,100 @@ def p2p_share(args):
     for p in fake:
         lib.fsagg_peer_free(0, p)
     pp.close()
+
+
+def aggregate_share(args):
+    """Rank 0 of ``world`` through Aggregator.aggregate() on one GPU: the
+    engine's sharded path (``aggregator.shard_by_param_range``) with a
+    PeerAssembly whose world - 1 peer copies are local uncached buffers and
+    whose barrier waits for this rank alone — everything rank 0 does on the
+    node (its row table over the 100 device dicts, the reduction of its
+    P/world range stored into every copy, the barrier, the copy-out of the
+    full result, the status check), without the xGMI link time."""
+    import ctypes
+    import statistics
+    from types import SimpleNamespace
+    from bench import sample_sizes
+    from federatedscope_amd import _lib as L, ops
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    from federatedscope_amd.core.sharding import Comm, PeerAssembly
+    dev = torch.device('cuda', 0)
+    n, P, W = args.clients, args.params, args.world
+    lib = L.load()
+
+    class EmuPeers(PeerAssembly):
+        def __init__(self, numel):
+            super().__init__(numel, comm=Comm(), device=dev)   # world 1
+            self.world = W
+            self.pc = max(-(-numel // W // 64) * 64, 64)
+            self.fake = []
+            for _ in range(W - 1):
+                q = ctypes.c_void_p()
+                L.check(lib.fsagg_peer_alloc(0, self.padded * 4,
+                                             ctypes.byref(q)))
+                self.fake.append(int(q.value))
+            own = self._ptr[0]
+            self._ptr = [own] + [[q] * len(own) for q in self.fake]
+
+        def _barrier(self):
+            saved = self.world
+            self.world = 1
+            try:
+                super()._barrier()
+            finally:
+                self.world = saved
+
+        def free(self):
+            for q in self.fake:
+                lib.fsagg_peer_free(0, q)
+            self.world = 1
+
+    sizes = sample_sizes(n)
+    slab = torch.empty((n, -(-P // 64) * 64), dtype=torch.float32,
+                       device=dev)
+    ops.fill_uniform(slab, P, seed=2026)
+    clients = [(sizes[i], {'w': slab[i, :P]}) for i in range(n)]
+    cfg = SimpleNamespace(federate=SimpleNamespace(ignore_weight=False,
+                                                   use_ss=False))
+    res = {}
+    for world in sorted({1, W}):
+        agg = ClientsAvgAggregator(device=dev, config=cfg)
+        info = {'client_feedback': clients, 'recover_fun': None}
+        emu = None
+        if world > 1:
+            emu = EmuPeers(P)
+            layout = agg._staged_rows(clients).layout
+            agg.cfg = SimpleNamespace(
+                federate=cfg.federate, aggregator=SimpleNamespace(
+                    shard_by_param_range=True, shard_chunks=1,
+                    shard_assembly='p2p'))
+            agg._shard = lambda: (emu.comm, 1)
+            agg._plans[(layout.signature(), 1, 'p2p')] = emu
+        for _ in range(args.warmup):
+            out = agg.aggregate(info)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(args.steps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = agg.aggregate(info)
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        res[world] = statistics.median(ts)
+        if world > 1:
+            lo, hi = emu.piece()
+            ref = torch.empty(-(-P // 64) * 64, dtype=torch.float32,
+                              device=dev)
+            ops.weighted_sum(ops.RowTable.from_slab(slab, numel=P),
+                             [s / sum(sizes) for s in sizes], ref)
+            ok = torch.equal(out['w'][lo:hi], ref[lo:hi])
+            emu.free()
+        print(json.dumps({
+            'mode': 'aggregate-share', 'world': world, 'clients': n,
+            'params': P, 'ms_per_call': round(res[world], 4),
+            'rank0_piece_bit_exact': ok if world > 1 else None,
+            'speedup_vs_world1': round(res[1] / res[world], 2)}),
+            flush=True)
 
 
 if __name__ == '__main__':
