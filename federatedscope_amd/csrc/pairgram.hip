@@ -239,6 +239,19 @@ struct Frags {
 };
 
 template <int NT, bool CENTRED>
+__device__ __forceinline__ void kstep_split_c(const float (&xb)[NT][8],
+                                              const float (&cb)[8],
+                                              const Neg &k, Frags<NT> &f) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = CENTRED ? xb[t][j] - cb[j] : xb[t][j];
+    split3(x, k, f.h[t], f.m[t], f.l[t]);
+  }
+}
+
+template <int NT, bool CENTRED>
 __device__ __forceinline__ void kstep_split(const float (&xb)[NT][8],
                                             const float *cs, const Neg &k,
                                             Frags<NT> &f) {
@@ -249,13 +262,7 @@ __device__ __forceinline__ void kstep_split(const float (&xb)[NT][8],
     cb[0] = x.x; cb[1] = x.y; cb[2] = x.z; cb[3] = x.w;
     cb[4] = y.x; cb[5] = y.y; cb[6] = y.z; cb[7] = y.w;
   }
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    float x[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = CENTRED ? xb[t][j] - cb[j] : xb[t][j];
-    split3(x, k, f.h[t], f.m[t], f.l[t]);
-  }
+  kstep_split_c<NT, CENTRED>(xb, cb, k, f);
 }
 
 // per tile pair: the six limb products in fp32 (the small ones first, so
@@ -515,13 +522,64 @@ __device__ void gram_tail(int chunk, int s, int n, int nseg,
   }
 }
 
+// Staged loads (kGramStaged): the chunk streams through LDS in stages of
+// kStage coordinates.  Each stage holds every row's kStage·4 = 512 B — the
+// 16·NT tile rows, then the centre's — written by global_load_lds_dwordx4
+// (one wave-instruction = 1 KiB = two rows) and read back in MFMA fragment
+// order.  A row's 512 B leave in one instruction: 50 rows that all start at
+// one offset within a 2 MiB page (separately allocated tensors) are read as
+// 512-B runs, not as the 128-B pieces each wave's own k-step loads take.
+// The LDS image is lane-linear per instruction, so the bank swizzle goes on
+// the SOURCE address: row r's 16-B chunk c sits in slot c ^ (r & 15), and
+// the 16 lanes of a fragment read (rows 16t .. 16t + 15, one chunk) hit 16
+// distinct bank quads.
+#ifdef FSAGG_GRAM_REGS   // probe builds only (tools/probe): the register path
+constexpr bool kGramStaged = false;
+#else
+constexpr bool kGramStaged = true;
+#endif
+constexpr int kStage = kKStep * kWaves;          // 128 coordinates
+constexpr int kStageRowBytes = kStage * 4;       // 512 B
+
+template <int NT, bool CENTRED>
+constexpr int stage_rows() { return 16 * NT + (CENTRED ? 1 : 0); }
+template <int NT, bool CENTRED>
+constexpr int stage_insts() { return (stage_rows<NT, CENTRED>() + 1) / 2; }
+// one stage buffer (rows rounded up to the instructions' row pairs)
+template <int NT, bool CENTRED>
+constexpr int stage_bytes() {
+  return 2 * stage_insts<NT, CENTRED>() * kStageRowBytes;
+}
+template <int NT, bool CENTRED>
+constexpr int chunk_smem() {
+  constexpr int red = 2 * ntp_of(NT) * 4 * kWave * 8;    // two waves' sums
+  constexpr int stg = kGramStaged ? 2 * stage_bytes<NT, CENTRED>()
+                                  : int(kMaxW) * 4;       // or the centre
+  constexpr int tail = (64 * 64 + 4 * 64) * 8;            // gram_tail
+  return red > stg ? (red > tail ? red : tail) : (stg > tail ? stg : tail);
+}
+
+// The 8 values of lane (row rr, group g) for k-step ks of a stage buffer.
+__device__ __forceinline__ void stage_read8(const char *buf, int rr, int ks,
+                                            int g, float (&v)[8]) {
+  typedef __attribute__((address_space(3))) const f32x4 lds_f32x4;
+  const int c0 = 8 * ks + g, c1 = c0 + 4;
+  const char *r = buf + rr * kStageRowBytes;
+  const f32x4 x = *(lds_f32x4 *)(uintptr_t)(r + 16 * (c0 ^ (rr & 15)));
+  const f32x4 y = *(lds_f32x4 *)(uintptr_t)(r + 16 * (c1 ^ (rr & 15)));
+  v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+}
+
 // One workgroup (4 waves) per chunk.  partial[chunk][tp][reg][lane] (fp64):
 // the chunk's (centred) Gram blocks in MFMA C-layout (row 4(lane>>4) + reg
 // of tile t, column lane & 15 of tile u).  !CENTRED: raw values (sample).
-// The centre's values of the chunk (<= kMaxW) are staged in LDS once and
-// read by every wave (registers go to the k-steps in flight).  Then
-// gram_tail: the reductions, d² and bounds, finish / centre — the last
-// workgroup to arrive at each level runs it, in the same launch.
+// The rows stream through LDS stages (kGramStaged, above; wave v takes
+// k-step v of every stage); without it each wave loads its own k-steps
+// straight into registers and the centre's values of the chunk are staged
+// in LDS once.  Then gram_tail: the reductions, d² and bounds, finish /
+// centre — the last workgroup to arrive at each level runs it, in the same
+// launch.
 template <int NT, bool CENTRED>
 __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n,
@@ -531,10 +589,7 @@ __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
     double *err, double tol, float *D, uint32_t *ill) {
   constexpr int NTP = ntp_of(NT);
   const int *__restrict__ prefix = ctl.prefix;
-  constexpr int kRedWords = 2 * NTP * 4 * kWave;   // two waves' sums
-  constexpr int kSmem = kRedWords * 8 > kMaxW * 4 ? kRedWords * 8
-                                                   : int(kMaxW) * 4;
-  __shared__ __attribute__((aligned(16))) char smem[kSmem];
+  __shared__ __attribute__((aligned(1024))) char smem[chunk_smem<NT, CENTRED>()];
   double(*red)[NTP * 4][kWave] =
       reinterpret_cast<double(*)[NTP * 4][kWave]>(smem);
   float *cs = reinterpret_cast<float *>(smem);
@@ -559,6 +614,7 @@ __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
     const int j = 16 * t + (lane & 15);
     row[t] = rows[j < n ? j : n - 1];
   }
+  const float *crow = CENTRED ? rows[*centre] : nullptr;
 
   double acc[NTP][4];
 #pragma unroll
@@ -575,74 +631,137 @@ __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
   bool ok = true;
 #pragma unroll
   for (int t = 0; t < NT; ++t) ok = ok && al16(row[t] + c0);
+  if (CENTRED) ok = ok && al16(crow + c0);
   const bool vec = __all(ok);
   int i = wv;   // this wave's next k-step: wv, wv + 4, ...
-  // one buffer: the next k-step's loads go out as soon as this one is split
-  // and fly while its products are formed (the load depth of a ping-pong
-  // pair of buffers measured the same); the first is issued
-  // before the centre staging
-  constexpr int64_t stp = int64_t(kWaves) * kKStep;
-  const float *a[NT];
-  float xa[NT][8];
-  if (vec) {
+  if constexpr (kGramStaged) {
+    const int nstage = vec ? int(len / kStage) : 0;
+    if (nstage > 0) {
+      // this wave's load instructions k = wv, wv + 4, ... of every stage:
+      // rows 2k (lanes 0-31) and 2k + 1 (lanes 32-63), each lane one 16-B
+      // chunk, its source swizzled (chunk (lane & 31) ^ (row & 15))
+      constexpr int NI = stage_insts<NT, CENTRED>();
+      constexpr int MY = (NI + kWaves - 1) / kWaves;
+      constexpr int NR = 16 * NT;
+      const float *src[MY];
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
-      a[t] = row[t] + c0 + int64_t(i) * kKStep + 4 * g;
-    if (i < nfull) {
+      for (int m = 0; m < MY; ++m) {
+        const int rr = 2 * (wv + kWaves * m) + (lane >> 5);
+        const float *rp = rr < NR ? rows[rr < n ? rr : n - 1]
+                                  : (CENTRED && rr == NR ? crow
+                                                         : rows[n - 1]);
+        src[m] = rp + c0 + 4 * ((lane & 31) ^ (rr & 15));
+      }
+      auto issue = [&](int st) {
+        char *buf = smem + (st & 1) * stage_bytes<NT, CENTRED>();
 #pragma unroll
-      for (int t = 0; t < NT; ++t) ld8(a[t], xa[t]);
-    }
-  }
-  if (CENTRED) {
-    const float *crow = rows[*centre] + c0;
-    if (al16(crow)) {
-      for (int e = 4 * int(threadIdx.x); e < len; e += 4 * kBlk) {
-        if (e + 4 <= len) {
-          *reinterpret_cast<f32x4 *>(cs + e) =
-              gld(reinterpret_cast<const f32x4 *>(crow + e));
-        } else {
-          for (int j = e; j < len; ++j) cs[j] = gload(crow + j);
+        for (int m = 0; m < MY; ++m) {
+          const int k = wv + kWaves * m;
+          if (k < NI)
+            __builtin_amdgcn_global_load_lds(
+                (__attribute__((address_space(1))) void *)(src[m] +
+                                                           st * kStage),
+                (__attribute__((address_space(3))) void *)(uintptr_t)(
+                    buf + k * 2 * kStageRowBytes),
+                16, 0, 0);
         }
-      }
-    } else {
-      for (int e = int(threadIdx.x); e < len; e += kBlk) cs[e] = gload(crow + e);
-    }
-    __syncthreads();
-  }
-  if (vec) {
-    for (; i < nfull; i += kWaves) {
-      Frags<NT> f;
-      kstep_split<NT, CENTRED>(xa, cs + i * kKStep + 4 * g, kn, f);
-      __builtin_amdgcn_sched_barrier(0);
-      // unconditional (the last k-step re-reads itself, from L2): a load
-      // under a branch would make the buffer a phi and cost a copy of it
-      const int64_t adv = i + kWaves < nfull ? stp : 0;
+      };
+      issue(0);
+      for (int st = 0; st < nstage; ++st) {
+        // this wave's stage-st loads have landed, every wave's (barrier),
+        // and every wave is done reading stage st − 1, whose buffer the
+        // next issue overwrites
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" :::
+                         "memory");
+        if (st + 1 < nstage) issue(st + 1);
+        const char *buf = smem + (st & 1) * stage_bytes<NT, CENTRED>();
+        float xb[NT][8], cb[8];
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        a[t] += adv;
-        ld8(a[t], xa[t]);
+        for (int t = 0; t < NT; ++t)
+          stage_read8(buf, 16 * t + (lane & 15), wv, g, xb[t]);
+        if (CENTRED) stage_read8(buf, NR, wv, g, cb);
+        Frags<NT> f;
+        kstep_split_c<NT, CENTRED>(xb, cb, kn, f);
+        kstep_mfma<NT>(f, acc);
       }
-      __builtin_amdgcn_sched_barrier(0);
-      kstep_mfma<NT>(f, acc);
+      i = nstage * kWaves + wv;
+      // the stage buffers are free again (the tail reads global memory)
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
-    i = nfull + ((wv - nfull) % kWaves + kWaves) % kWaves;
+  } else {
+    // one buffer: the next k-step's loads go out as soon as this one is
+    // split and fly while its products are formed; the first is issued
+    // before the centre staging
+    constexpr int64_t stp = int64_t(kWaves) * kKStep;
+    const float *a[NT];
+    float xa[NT][8];
+    if (vec) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        a[t] = row[t] + c0 + int64_t(i) * kKStep + 4 * g;
+      if (i < nfull) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) ld8(a[t], xa[t]);
+      }
+    }
+    if (CENTRED) {
+      const float *cr = crow + c0;
+      if (al16(cr)) {
+        for (int e = 4 * int(threadIdx.x); e < len; e += 4 * kBlk) {
+          if (e + 4 <= len) {
+            *reinterpret_cast<f32x4 *>(cs + e) =
+                gld(reinterpret_cast<const f32x4 *>(cr + e));
+          } else {
+            for (int j = e; j < len; ++j) cs[j] = gload(cr + j);
+          }
+        }
+      } else {
+        for (int e = int(threadIdx.x); e < len; e += kBlk)
+          cs[e] = gload(cr + e);
+      }
+      __syncthreads();
+    }
+    if (vec) {
+      for (; i < nfull; i += kWaves) {
+        Frags<NT> f;
+        kstep_split<NT, CENTRED>(xa, cs + i * kKStep + 4 * g, kn, f);
+        __builtin_amdgcn_sched_barrier(0);
+        // unconditional (the last k-step re-reads itself, from L2): a load
+        // under a branch would make the buffer a phi and cost a copy of it
+        const int64_t adv = i + kWaves < nfull ? stp : 0;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          a[t] += adv;
+          ld8(a[t], xa[t]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        kstep_mfma<NT>(f, acc);
+      }
+      i = nfull + ((wv - nfull) % kWaves + kWaves) % kWaves;
+    }
   }
-  // unaligned rows: every k-step; aligned: the partial last one (if any)
+  // unaligned rows: every k-step; aligned: the last partial stage (staged)
+  // or the partial last k-step (register loads)
   const int nall = int((len + kKStep - 1) / kKStep);
   for (; i < nall; i += kWaves) {
     const int64_t k0 = c0 + int64_t(i) * kKStep;
-    float xt[NT][8];
-    __attribute__((aligned(16))) float ct[32];
+    float xt[NT][8], cb[8];
 #pragma unroll
     for (int t = 0; t < NT; ++t) ld8_tail(row[t], k0, c1, g, xt[t]);
     if (CENTRED) {
+      if constexpr (kGramStaged) {
+        ld8_tail(crow, k0, c1, g, cb);
+      } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int o = kofs(g, j);
-        ct[o] = i * kKStep + o < len ? cs[i * kKStep + o] : 0.0f;
+        for (int j = 0; j < 8; ++j) {
+          const int o = kofs(g, j);
+          cb[j] = i * kKStep + o < len ? cs[i * kKStep + o] : 0.0f;
+        }
       }
     }
-    kstep<NT, CENTRED>(xt, ct + 4 * g, kn, acc);
+    Frags<NT> f;
+    kstep_split_c<NT, CENTRED>(xt, cb, kn, f);
+    kstep_mfma<NT>(f, acc);
   }
   // the four waves' sums in a fixed order, (w0 + w2) + (w1 + w3), through
   // two wave-slots of LDS (red overlays the centre)

@@ -79,12 +79,17 @@ def main():
                                           dev, keepalive=keep)
 
             def run():
-                sq2 = ops.pairgram_rows_segsq(rs)
-                return ops.pairgram_finish(sq2, _GRAM_TOL)
+                return ops.pairgram_rows_dist(rs, _GRAM_TOL)
+
+            def valu():
+                return ops.pairdist_finish(ops.pairdist_rows_segsq(rs))
             run()
             med, mn = timed(run)
-            print(json.dumps({'data': kind, 'form': form, 'ms_median': med,
-                              'ms_min': mn,
+            vmed, vmn = timed(valu)
+            print(json.dumps({'lib': os.environ.get('FSAGG_LIB', 'product'),
+                              'data': kind, 'form': form,
+                              'gram_ms_median': med, 'gram_ms_min': mn,
+                              'valu_ms_median': vmed,
                               'distinct_fc1_offsets_mod_2MiB': offs}),
                   flush=True)
 
