@@ -45,38 +45,6 @@ __device__ __forceinline__ int add_below(int c, uint32_t a, uint32_t b) {
   return c;
 }
 
-// One value of the trimmed mean's compaction over the key band [0, wb)
-// relative to A — [0, w1) bin 1, [w1, w1 + wm) the middle, then bin 2:
-// returns the value when it lies in the middle (the caller sums it), else 0,
-// and counts it into the LDS list when it lies in a bin.  rel = ukey(u) − A
-// = (u ^ s) + C0 with s = u >> 31 (arithmetic) — ukey's xor mask less its
-// top bit, which C0 = 2^31 − A absorbs — and rel − w1 likewise with C1 =
-// C0 − w1: one v_xad each instead of ukey + two subtractions.  The middle
-// lies inside the band, so "in a bin" = in band − in middle: both tests are
-// borrows carried straight into c (v_addc / v_subb), no 0/1 select.  The
-// middle test's borrow goes to an SGPR pair that the select reads three
-// instructions later (two VALU→SGPR-read wait states covered).
-__device__ __forceinline__ float trim_step(uint32_t u, uint32_t C0,
-                                           uint32_t C1, uint32_t wb,
-                                           uint32_t wm, int &c) {
-  uint32_t s, r;
-  uint64_t m;
-  float x;
-  asm("v_ashrrev_i32 %[s], 31, %[u]\n\t"
-      "v_xad_u32 %[r], %[u], %[s], %[C1]\n\t"
-      "v_sub_co_u32_e64 %[r], %[m], %[r], %[wm]\n\t"
-      "v_xad_u32 %[r], %[u], %[s], %[C0]\n\t"
-      "v_sub_co_u32 %[r], vcc, %[r], %[wb]\n\t"
-      "v_addc_co_u32 %[c], vcc, 0, %[c], vcc\n\t"
-      "v_cndmask_b32_e64 %[x], 0, %[u], %[m]\n\t"
-      "v_subb_co_u32_e64 %[c], vcc, %[c], 0, %[m]"
-      : [s] "=&v"(s), [r] "=&v"(r), [m] "=&s"(m), [x] "=&v"(x),
-        [c] "+v"(c)
-      : [u] "v"(u), [C0] "v"(C0), [C1] "v"(C1), [wb] "v"(wb), [wm] "v"(wm)
-      : "vcc");
-  return x;
-}
-
 // Opaque copy barrier: keeps the compiler from hoisting per-pass key math
 // (ukey of every value) out of a pass and holding N more registers live.
 template <int N>

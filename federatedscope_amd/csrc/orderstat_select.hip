@@ -167,13 +167,18 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
       const uint32_t w1 = list1 ? s1.hi - s1.lo + 1u : 0u;
       const uint32_t wm = shared ? 0u : s2.lo - (s1.hi + 1u);
       const uint32_t wb = w1 + wm + (list2 ? s2.hi - s2.lo + 1u : 0u);
-      // rel = ukey(u) − A = (u ^ (u >> 31)) + (2^31 − A), rel − w1 likewise
-      const uint32_t C0 = 0x80000000u - A, C1 = C0 - w1;
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         if (j >= N - kSelStep && j >= n) continue;
+        const uint32_t rel = ukey(u[j]) - A;
+        const bool inm = rel - w1 < wm;
+        // select in fp32, then widen: one v_cndmask, not a 64-bit pair (the
+        // empty asm keeps the compiler from sinking the select past the cvt)
+        float x = inm ? __uint_as_float(u[j]) : 0.0f;
+        asm("" : "+v"(x));
+        mid += double(x);
         *lds_at(hb | (uint32_t(c) << 8)) = u[j];  // a miss: overwritten
-        mid += double(trim_step(u[j], C0, C1, wb, wm, c));
+        c += (rel < wb) && !inm;
       }
     }
   }
