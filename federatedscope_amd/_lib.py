@@ -117,9 +117,9 @@ SIGNATURES['fsagg_pairgram_rows_segsq_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_sz, _c_p])
 SIGNATURES['fsagg_pairgram_rows_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i64, ctypes.c_double, _c_p, _c_p, _c_p, _c_p,
-           _c_p, _c_sz, _c_p])
+           _c_p, _c_p, _c_sz, _c_p])
 SIGNATURES['fsagg_pairgram_finish_f32'] = (
-    _c_i, [_c_p, _c_p, _c_i, _c_i, ctypes.c_double, _c_p, _c_p, _c_p])
+    _c_i, [_c_p, _c_p, _c_i, _c_i, ctypes.c_double, _c_p, _c_p, _c_p, _c_p])
 SIGNATURES['fsagg_pairdist_rows_segsq_f32'] = (
     _c_i, [_rows_p, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_sz, _c_p])
 

@@ -203,38 +203,50 @@ class DeviceEngine:
 
     def _pairdist(self, st):
         """Krum's distance matrix D (fp32 [n][n]) of a client set, as a
-        pending result whose ``.cpu()`` waits for it: for up to 64 clients
-        on the matrix cores (fsagg_pairgram_rows_segsq_f32 +
-        fsagg_pairgram_finish_f32, one copy of D and the flags back); the
-        pairs the Gram form cannot resolve to _GRAM_TOL of their distance
-        (near-duplicate clients far from every other, non-finite values)
-        are recomputed on the VALU kernel over the clients involved.  Above
-        64 clients, or when the clients' rows start at one offset within
-        a 2 MiB page (separately allocated device tensors, which the Gram
-        kernel's all-rows-at-once reads make camp on one HBM channel:
-        DESIGN §3.3): the VALU kernel."""
+        pending result whose ``.cpu()`` waits for it.  Up to 64 clients: on
+        the matrix cores (fsagg_pairgram_*: the Gram of the rows centred on a
+        central client, fp32 split exactly into bf16 limbs), every pair with
+        a worst-case bound on its error (``last_pair_bound``, host fp64
+        [n][n]) that the callers certify their selection with
+        (:meth:`_certified_order`); non-finite pairs are recomputed on the
+        VALU kernel.  Above 64 clients: the VALU kernel (direct differences,
+        ``last_pair_bound`` None)."""
         from ... import _lib
-        gram = 2 <= st.n <= _lib.FSAGG_PAIRGRAM_MAX_CLIENTS and \
-            _rows_spread(st)
-        if st.plan is not None and 2 <= st.n <= \
-                _lib.FSAGG_PAIRGRAM_MAX_CLIENTS:
-            # one path on every rank (the exchanged partials differ)
-            v = torch.tensor([1.0 if gram else 0.0],
-                             device=self.compute_device)
-            st.plan.comm.all_reduce_sum(v)
-            gram = int(v.item()) == st.plan.comm.world
-        if gram and st.plan is None:
-            buf, _, _, _ = ops.pairgram_rows_dist(st.rows(), _GRAM_TOL)
+        self.last_pair_bound = None
+        if not 2 <= st.n <= _lib.FSAGG_PAIRGRAM_MAX_CLIENTS:
+            return self._pairdist_valu(st)
+        if st.plan is None:
+            buf = ops.pairgram_rows_dist(st.rows(), _GRAM_TOL)[0]
             return _PendingD(self, st, buf=buf)
-        if gram:
-            sq2 = self._sum_pieces(
-                st, lambda rs, lo, hi: ops.pairgram_rows_segsq(rs, lo, hi))
-            buf, _, _ = ops.pairgram_finish(sq2, _GRAM_TOL)
-            return _PendingD(self, st, buf=buf)
+        sq2 = self._sum_pieces(
+            st, lambda rs, lo, hi: ops.pairgram_rows_segsq(rs, lo, hi))
+        return _PendingD(self, st, buf=ops.pairgram_finish(sq2, _GRAM_TOL)[0])
+
+    def _pairdist_valu(self, st):
+        """D on the VALU kernel (fsagg_pairdist_*)."""
         self.last_pairdist_path = 'valu'
+        self.last_pair_bound = None
         segsq = self._sum_pieces(
             st, lambda rs, lo, hi: ops.pairdist_rows_segsq(rs, lo, hi))
         return _PendingD(self, st, D=ops.pairdist_finish(segsq))
+
+    def _certified_order(self, st, D, f, m, ordered):
+        """(D, scores, order) for a Krum selection of ``m`` clients: from the
+        Gram path's D when its bounds certify the selection
+        (:func:`certified_selection`; ``ordered``: the order of the first
+        ``m`` as well, which fixes a multi-Krum average's summation order),
+        else from D recomputed on the VALU kernel."""
+        from .krum_aggregator import krum_scores
+        scores = krum_scores(D, f)
+        order = torch.sort(scores)[1]
+        B = self.last_pair_bound
+        if B is not None and not certified_selection(
+                D.numpy(), B, f, m, order.numpy(), ordered):
+            D = self._pairdist_valu(st).cpu()
+            self.last_pairdist_path = 'mfma, not certified: valu'
+            scores = krum_scores(D, f)
+            order = torch.sort(scores)[1]
+        return D, scores, order
 
     def _sqnorms(self, st):
         """[n][nseg] fp64 per-client, per-key squared norms."""
@@ -511,44 +523,48 @@ def _host_ext():
     return _HOST[0]
 
 
-# relative bound on a Krum distance's error from the Gram form above which
-# the pair is recomputed on the VALU kernel (the bound is 2-5x
-# the measured error; the Gram path measures 2.3e-7 at C4, the VALU kernel
-# 1.6e-7)
-_GRAM_TOL = 1e-6
+# fsagg_pairgram_finish_f32's flagging threshold: +inf, only non-finite
+# pairs are recomputed pair by pair — the Krum selection is certified with the
+# per-pair bounds instead
+_GRAM_TOL = float('inf')
 
 
-def _rows_spread(st):
-    """Whether the clients' rows of the largest key start at enough distinct
-    4-KiB offsets within a 2 MiB page for the Gram kernel, whose k-steps read
-    every row at the same coordinate at once: rows of one allocation (the
-    client stack, views of a slab) are spread; separately allocated device
-    tensors start 2 MiB-aligned, and the Gram path then measures 0.54 against
-    0.34 ms at C4 (the VALU kernel, which reads fewer rows at a time: 0.46)."""
+def certified_selection(D, B, f, m, order, ordered=True):
+    """Whether the Krum selection of the first ``m`` clients of ``order`` is
+    the one exact distances give, from D (host fp32 [n][n]) and per-pair
+    bounds B on |D − the exact distances' sum| (host fp64, D's own fp32
+    formation included).  Krum's score, the sum of a client's n − f − 2
+    smallest distances, is monotone in every distance: the exact score lies
+    in [lo, hi], the same sums over D − B and D + B.  The selected set holds
+    when the largest hi among the first m is below the smallest lo after
+    them; with ``ordered`` (a multi-Krum average sums its clients in that
+    order) every position i < m must clear every client after it."""
     import numpy as np
-    rs = None
-    for _, _, _, r in st.pieces:
-        if getattr(r, 'host', None) is not None:
-            rs = r
-            break
-    if rs is None:
-        return True
-    lay = rs.layout
-    if not lay.keys:
-        return True
-    s = max(range(len(lay.keys)), key=lambda i: lay.numels[lay.keys[i]])
-    col = rs.host[:, s if rs.host.shape[1] > 1 else 0]
-    col = col[col != 0] + 4 * int(lay.offsets[lay.keys[s]])
-    if col.size < 2:
-        return True
-    pages = np.unique((col >> 12) & 511).size
-    return pages >= max(2, col.size // 4)
+    D = np.asarray(D, dtype=np.float64)
+    n = D.shape[0]
+    k = n - f - 2
+    if k <= 0 or m <= 0:
+        return k > 0
+    B = np.asarray(B, dtype=np.float64)
+    lo = np.sort(np.maximum(D - B, 0.0), 1)[:, :k].sum(1) * (1 - 1e-12)
+    hi = np.sort(D + B, 1)[:, :k].sum(1) * (1 + 1e-12)
+    o = np.asarray(order)
+    lo_o, hi_o = lo[o], hi[o]
+    if m >= n:
+        return not ordered or all(
+            hi_o[i] < lo_o[i + 1:].min() for i in range(n - 1))
+    suf = np.minimum.accumulate(lo_o[::-1])[::-1]
+    if not ordered:
+        return bool(hi_o[:m].max() < suf[m])
+    return all(hi_o[i] < suf[i + 1] for i in range(m))
 
 
 class _PendingD:
     """Krum's distance matrix while its kernels run (``_pairdist``):
-    ``cpu()`` copies D (and the Gram path's flags) to the host, recomputes
-    the flagged pairs exactly and returns the host fp32 [n][n] matrix."""
+    ``cpu()`` copies D (and the Gram path's flags and bounds) to the host,
+    recomputes the flagged (non-finite) pairs exactly and returns the host
+    fp32 [n][n] matrix; the bounds go to ``last_pair_bound`` (0 for the
+    recomputed pairs)."""
 
     def __init__(self, eng, st, buf=None, D=None):
         self._eng, self._st, self._buf, self._D = eng, st, buf, D
@@ -562,6 +578,12 @@ class _PendingD:
         D = host[0].view(torch.float32).clone()
         flags = host[1].numpy()
         flags = (flags + flags.T) > 0
+        B = host[2].view(torch.float32).numpy().astype(np.float64)
+        # the kernel bounds the fp64 per-key distances' sum; D is its fp32
+        # formation (a rounded sqrt and an fp32 add per key)
+        nseg = max(1, len(st.layout.keys))
+        B = np.maximum(B, B.T) + (2 * nseg + 2) * 2.0 ** -24 * np.where(
+            np.isfinite(D.numpy()), D.numpy(), 0.0).astype(np.float64)
         eng.last_pairdist_path = 'mfma'
         if flags.any():
             # the flagged pairs exactly: the VALU kernel over the clients
@@ -573,8 +595,10 @@ class _PendingD:
             sub = ops.pairdist_finish(exact).cpu()
             idx = torch.tensor(sel)
             D[idx[:, None], idx[None, :]] = sub
+            B[np.ix_(sel, sel)] = 0.0
             eng.last_pairdist_path = 'mfma + exact %d of %d clients' % (
                 len(sel), st.n)
+        eng.last_pair_bound = B
         return D
 
 

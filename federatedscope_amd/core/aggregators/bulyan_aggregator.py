@@ -1,14 +1,11 @@
 """Bulyan (federatedscope/core/aggregators/bulyan_aggregator.py:6-106):
 multi-Krum selection of n - int(2·rate·f) clients (device distance matrix,
-host score/sort as the reference), then a coordinate-wise trimmed mean over
+certified as in krum_aggregator; host score/sort as the reference), then a coordinate-wise trimmed mean over
 the selected rows with k = int(rate·f), divided by gamma = |selected| - 2k,
 plus init — all on the GPU over the one staged client stack."""
-import torch
-
 from ... import ops
 from ._engine import _first_device
 from .clients_avg_aggregator import ClientsAvgAggregator
-from .krum_aggregator import krum_scores
 
 
 class BulyanAggregator(ClientsAvgAggregator):
@@ -27,10 +24,11 @@ class BulyanAggregator(ClientsAvgAggregator):
         D = self._pairdist(st)
         # the init model's table is built while the distance kernels run
         base = self._base(layout, self.model.state_dict(), as_float=True)
-        D = D.cpu()
-        scores = krum_scores(D, self.byzantine_node_num)
-        index_order = torch.sort(scores)[1].numpy()
         keep = n - int(2 * self.sample_client_rate * self.byzantine_node_num)
+        # the trimmed mean does not depend on the selected rows' order: the
+        # Gram path's bounds need only certify the selected set
+        _, _, index_order = self._certified_order(
+            st, D.cpu(), self.byzantine_node_num, max(keep, 0), ordered=False)
         sel = [int(i) for i in index_order[:max(keep, 0)]]
         self.last_selection = sel
         k = int(self.sample_client_rate * self.byzantine_node_num)

@@ -1,12 +1,22 @@
 """Krum / multi-Krum (federatedscope/core/aggregators/krum_aggregator.py:6-90).
 
 Device path: the client updates are read where they lie (a row set: the
-clients' own device tensors, or their staged stack rows);
-fsagg_pairdist_rows_segsq_f32 + fsagg_pairdist_finish_f64 compute the per-key L2 distances for every pair and the n×n matrix (sum over
-keys, +inf diagonal) in one pass over the stack; the n×n matrix (≤ 200² floats)
-comes back to the host where the score/sort/select logic runs with the same
-torch CPU ops as the reference (:75-87); the selected clients are then
-averaged in ascending-score order with init + avg fused into the kernel.
+clients' own device tensors, or their staged stack rows).  The n×n distance
+matrix (the per-key L2 distances summed over keys, +inf diagonal, :58-73):
+
+* up to 64 clients on the matrix cores (fsagg_pairgram_rows_f32: the Gram of
+  the rows centred on a central client, fp32 split exactly into three bf16
+  limbs, fp64 accumulation), with a worst-case error bound per pair — the
+  selection below is certified against those bounds, and recomputed from
+  the VALU kernel's matrix when the score gaps do not clear them
+  (_engine._certified_order);
+* above 64 clients on the VALU kernel (fsagg_pairdist_rows_segsq_f32 +
+  fsagg_pairdist_finish_f64: direct differences).
+
+The matrix (≤ 200² floats) comes back to the host where the score/sort/select
+logic runs with the same torch CPU ops as the reference (:75-87); the
+selected clients are then averaged in ascending-score order with init + avg
+fused into the kernel (fsagg_weighted_sum_rows_f32).
 """
 import torch
 
@@ -53,9 +63,8 @@ class KrumAggregator(ClientsAvgAggregator):
         # host work that does not need the selection runs while the
         # distance kernels do (the .cpu() below waits for them)
         base = self._base(layout, self.model.state_dict(), as_float=True)
-        D = D.cpu()
-        scores = krum_scores(D, self.byzantine_node_num)
-        index_order = torch.sort(scores)[1].numpy()
+        _, _, index_order = self._certified_order(
+            st, D.cpu(), self.byzantine_node_num, agg_num, ordered=True)
         sel = [int(i) for i in index_order[:agg_num]]
         self.last_selection = sel
         sizes = [models[i][0] for i in sel]

@@ -72,11 +72,14 @@ constexpr int64_t kSampleChunk = 512;
 //   significand, the residuals' signs absorbing the rounding), so the only
 //   product error is the three dropped limb products ml, lm, ll:
 //   <= (2·2^-24 + 2^-32)·(1 + 2^-8)²·|x·y|            -> kCoefLimb · u · S²
-// * MFMA accumulation: each v_mfma_f32_16x16x32_bf16 returns C + Σ of its
-//   32 exact products with an error <= kMfmaRound · u · (|C| + Σ|products|)
-//   (gfx950's rounding of the dot, tools/probe/mfma_numerics.py); over the
-//   chain mm, hl, lh, hm, mh, hh those sums total <= 1.035 · Σ|x·y|
-//                                                       -> 1.035·kMfmaRound
+// * MFMA accumulation: v_mfma_f32_16x16x32_bf16 aligns its 32 exact
+//   products (and C) to the largest and drops what lies below a window of
+//   about 26 bits under it, then rounds once (tools/probe/mfma_numerics.py,
+//   profiles/r04/mfma_numerics.jsonl: 31 terms just under 2^-26 of the
+//   largest vanish whole; the worst error over every family probed is
+//   7.5·u·max|term|): error <= (32·2^-26/u + 1)·u·max|term| <= 9·u·Σ|terms|
+//   per MFMA; over the chain mm, hl, lh, hm, mh, hh those sums total
+//   <= 1.035·Σ|x·y|                              -> 1.035·kMfmaRound
 // * fp64: the K k-step sums, four waves and two reduction levels add
 //   <= (K + 1024) · 2^-53 relative                     -> (K + 1024)·2^-29
 // * centring x' = fl32(x − x_c) perturbs the rows by <= u·|x'|: d² moves by
@@ -85,7 +88,7 @@ constexpr int64_t kSampleChunk = 512;
 //   <= 2^-126 · (12·sqrt(P)·S + 800·K) absolute
 constexpr double kU = 5.9604644775390625e-08;   // 2^-24
 constexpr double kCoefLimb = 2.02;
-constexpr double kMfmaRound = 1.0;
+constexpr double kMfmaRound = 9.0;
 constexpr double kMfmaChain = 1.035;
 constexpr double kTiny = 1.1754943508222875e-38;  // 2^-126
 
@@ -93,27 +96,20 @@ constexpr int ntp_of(int nt) { return nt * (nt + 1) / 2; }
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-// Per-pass control block (device workspace ints): chunk q of key s covers
+// Per-pass plan (device workspace ints): chunk q of key s covers
 // [seg_lo[s] + q·w, min(seg_lo[s] + (q+1)·w, cap_s)), cap_s = seg_end[s]
 // (or seg_lo[s] + cap for the sample pass); its chunks are prefix[s] ..
 // prefix[s+1] − 1 and its first-level groups (kRed chunks each)
-// gprefix[s] .. gprefix[s+1] − 1.  The completion counters let the last
-// workgroup of a group / key / pass run that level's reduction (fixed
-// summation order whichever workgroup arrives last: deterministic).
+// gprefix[s] .. gprefix[s+1] − 1.
 struct GramCtl {
   int *prefix;      // [nseg + 1]
   int *gprefix;     // [nseg + 1]
-  int *cnt_key;     // [nseg]
-  int *cnt_all;     // [1]
-  int *nonempty;    // [1]: keys with at least one chunk
-  int *cnt_group;   // [groups]
-  int groups;       // capacity of cnt_group
 };
 
 __device__ void plan_pass(const int64_t *__restrict__ seg_lo,
                           const int64_t *__restrict__ seg_end, int nseg,
                           int64_t w, int64_t cap, const GramCtl &c) {
-  int acc = 0, gacc = 0, ne = 0;
+  int acc = 0, gacc = 0;
   c.prefix[0] = 0;
   c.gprefix[0] = 0;
   for (int s = 0; s < nseg; ++s) {
@@ -123,41 +119,20 @@ __device__ void plan_pass(const int64_t *__restrict__ seg_lo,
     const int k = int((len + w - 1) / w);
     acc += k;
     gacc += (k + kRed - 1) / kRed;
-    ne += k > 0;
     c.prefix[s + 1] = acc;
     c.gprefix[s + 1] = gacc;
   }
-  *c.nonempty = ne;
 }
 
-// Both passes' plans in one launch; clears their completion counters and
-// zeroes what no workgroup writes: the per-key Gram, d² and bounds of empty
-// keys.
-__global__ __launch_bounds__(256) void gram_prefix_kernel(
-    const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
-    int nseg, int64_t w_sample, int64_t cap_sample, int64_t w_main,
-    GramCtl cs, GramCtl cm, double *g_key, double *segsq, double *err,
-    int n) {
-  if (threadIdx.x == 0) {
-    plan_pass(seg_lo, seg_end, nseg, w_sample, cap_sample, cs);
-    plan_pass(seg_lo, seg_end, nseg, w_main, 0, cm);
-  }
-  for (int i = threadIdx.x; i < nseg + 1 + cs.groups; i += 256) {
-    if (i < nseg) cs.cnt_key[i] = cm.cnt_key[i] = 0;
-    else if (i == nseg) *cs.cnt_all = *cm.cnt_all = 0;
-    else cs.cnt_group[i - nseg - 1] = 0;
-  }
-  for (int i = threadIdx.x; i < cm.groups; i += 256) cm.cnt_group[i] = 0;
-  __syncthreads();
-  const int nn = n * n;
-  for (int s = 0; s < nseg; ++s) {
-    if (cm.prefix[s + 1] > cm.prefix[s]) continue;
-    for (int i = threadIdx.x; i < 64 * 64; i += 256)
-      g_key[int64_t(s) * 64 * 64 + i] = 0.0;
-    if (segsq)
-      for (int i = threadIdx.x; i < nn; i += 256)
-        segsq[int64_t(s) * nn + i] = err[int64_t(s) * nn + i] = 0.0;
-  }
+// Both passes' plans in one launch.
+__global__ void gram_prefix_kernel(const int64_t *__restrict__ seg_lo,
+                                   const int64_t *__restrict__ seg_end,
+                                   int nseg, int64_t w_sample,
+                                   int64_t cap_sample, int64_t w_main,
+                                   GramCtl cs, GramCtl cm) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  plan_pass(seg_lo, seg_end, nseg, w_sample, cap_sample, cs);
+  plan_pass(seg_lo, seg_end, nseg, w_main, 0, cm);
 }
 
 __device__ __forceinline__ void tp_tiles(int tp, int nt, int &t, int &u) {
@@ -354,18 +329,20 @@ __device__ __forceinline__ void segsq_pair(const double *g, int a, int b,
 __device__ __forceinline__ void finish_pair(int q, const double *segsq,
                                             const double *err, int n,
                                             int nseg, double tol, float *D,
-                                            uint32_t *ill) {
+                                            uint32_t *ill, float *B) {
   if (q / n == q % n) {
     D[q] = __builtin_inff();
     ill[q] = 0u;
+    if (B) B[q] = 0.0f;
     return;
   }
   float dist = 0.0f;
   double sum_d = 0.0, bound = 0.0;
   bool inf = false;
   for (int s = 0; s < nseg; ++s) {
-    const double d2 = segsq[int64_t(s) * n * n + q];
-    const double e = err[int64_t(s) * n * n + q];
+    const int64_t at = int64_t(s) * n * n + q;
+    const double d2 = segsq[at];
+    const double e = err[at];
     const double d = sqrt(d2);
     dist = add_rn(dist, float(d));
     sum_d += d;
@@ -379,6 +356,8 @@ __device__ __forceinline__ void finish_pair(int q, const double *segsq,
   D[q] = dist;
   ill[q] = (!inf && bound <= tol * sum_d && dist < __builtin_inff()) ? 0u
                                                                       : 1u;
+  // the bound on |D − the exact per-key distances' sum|, rounded up to fp32
+  if (B) B[q] = inf ? __builtin_inff() : __double2float_ru(bound);
 }
 
 // The centre: argmin_a Σ_b sqrt(d²(a, b)) over a Gram matrix G (64 x 64 in
@@ -407,118 +386,6 @@ __device__ void centre_of(const double *G, int n, int *centre,
       }
     }
     *centre = best;
-  }
-}
-
-// One arrival at a completion counter of `total` arrivals; true (on every
-// thread) for the last one, which then sees every other arrival's stores.
-// The split-K hand-off: every wave drains its own stores (a barrier does
-// not wait for them), one lane releases at agent scope (the XCD's L2
-// written back, whichever waves stored) and draws a ticket; the last
-// arriver's lane acquires at agent scope before the workgroup reads.  The
-// explicit vmcnt waits stay: the fences' own waits can be dropped.
-__device__ __forceinline__ bool arrive(int *cnt, int total, int *flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const bool last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT) ==
-                      total - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  return *flag != 0;
-}
-
-// What runs after a chunk's partial is stored.  The last chunk of a group
-// sums the group's chunks in order into grp[b]; the last group of a key sums
-// the key's groups in order into the key's Gram matrix (LDS) and — main
-// pass — writes the key's d² and bounds; the last key of the pass runs the
-// finish (main pass, when D is given) or the centre choice (sample pass,
-// from the per-key matrices in g_key).  Every sum is in a fixed order,
-// whichever workgroup arrives last.
-template <int NT, bool CENTRED>
-__device__ void gram_tail(int chunk, int s, int n, int nseg,
-                          const int64_t *__restrict__ seg_lo,
-                          const int64_t *__restrict__ seg_end,
-                          const GramCtl &ctl, const double *partial,
-                          double *grp, double *g_key, int *centre,
-                          double *segsq, double *err, double tol, float *D,
-                          uint32_t *ill, double *lds, int *flag) {
-  constexpr int NTP = ntp_of(NT);
-  const int e = threadIdx.x;
-  const int q = chunk - ctl.prefix[s];
-  const int b = ctl.gprefix[s] + q / kRed;
-  const int qa = ctl.prefix[s] + (q / kRed) * kRed;
-  const int qb = min(qa + kRed, ctl.prefix[s + 1]);
-  if (!arrive(&ctl.cnt_group[b], qb - qa, flag)) return;
-#pragma unroll 1
-  for (int p = 0; p < NTP; ++p) {
-    double v[kRed];
-#pragma unroll
-    for (int j = 0; j < kRed; ++j)
-      v[j] = qa + j < qb ? partial[((int64_t(qa) + j) * NTP + p) * 256 + e]
-                         : 0.0;
-    double sum = 0.0;
-#pragma unroll
-    for (int j = 0; j < kRed; ++j) sum += v[j];
-    grp[(int64_t(b) * NTP + p) * 256 + e] = sum;
-  }
-  const int ga = ctl.gprefix[s], gb = ctl.gprefix[s + 1];
-  if (!arrive(&ctl.cnt_key[s], gb - ga, flag)) return;
-  const int r = e >> 6, ln = e & 63;
-#pragma unroll 1
-  for (int p = 0; p < NTP; ++p) {
-    constexpr int U = 8;
-    double sum = 0.0;
-    for (int c = ga; c < gb; c += U) {
-      double v[U];
-#pragma unroll
-      for (int j = 0; j < U; ++j)
-        v[j] = c + j < gb ? grp[(int64_t(c + j) * NTP + p) * 256 + e] : 0.0;
-#pragma unroll
-      for (int j = 0; j < U; ++j) sum += v[j];
-    }
-    int t, u;
-    tp_tiles(p, NT, t, u);
-    const int ra = 16 * t + 4 * (ln >> 4) + r, rc = 16 * u + (ln & 15);
-    lds[ra * 64 + rc] = sum;
-    if (t != u) lds[rc * 64 + ra] = sum;
-    if (!CENTRED) {
-      double *gk = g_key + int64_t(s) * 64 * 64;
-      gk[ra * 64 + rc] = sum;
-      if (t != u) gk[rc * 64 + ra] = sum;
-    }
-  }
-  __syncthreads();
-  const int nn = n * n;
-  if (CENTRED) {
-    const int64_t len = seg_end[s] - seg_lo[s];
-    for (int i = e; i < nn; i += 256)
-      segsq_pair(lds, i / n, i % n, len, segsq[int64_t(s) * nn + i],
-                 err[int64_t(s) * nn + i]);
-    if (!D) return;
-  }
-  if (!arrive(ctl.cnt_all, *ctl.nonempty, flag)) return;
-  if (CENTRED) {
-    for (int i = e; i < nn; i += 256)
-      finish_pair(i, segsq, err, n, nseg, tol, D, ill);
-  } else {
-    // Σ over keys (key order) of the per-key sample matrices
-    for (int i = e; i < 64 * 64; i += 256) {
-      double sum = 0.0;
-      for (int k = 0; k < nseg; ++k) sum += g_key[int64_t(k) * 64 * 64 + i];
-      lds[i] = sum;
-    }
-    __syncthreads();
-    centre_of(lds, n, centre,
-              reinterpret_cast<double(*)[64]>(lds + 64 * 64));
   }
 }
 
@@ -555,8 +422,7 @@ constexpr int chunk_smem() {
   constexpr int red = 2 * ntp_of(NT) * 4 * kWave * 8;    // two waves' sums
   constexpr int stg = kGramStaged ? 2 * stage_bytes<NT, CENTRED>()
                                   : int(kMaxW) * 4;       // or the centre
-  constexpr int tail = (64 * 64 + 4 * 64) * 8;            // gram_tail
-  return red > stg ? (red > tail ? red : tail) : (stg > tail ? stg : tail);
+  return red > stg ? red : stg;
 }
 
 // The 8 values of lane (row rr, group g) for k-step ks of a stage buffer.
@@ -577,16 +443,13 @@ __device__ __forceinline__ void stage_read8(const char *buf, int rr, int ks,
 // The rows stream through LDS stages (kGramStaged, above; wave v takes
 // k-step v of every stage); without it each wave loads its own k-steps
 // straight into registers and the centre's values of the chunk are staged
-// in LDS once.  Then gram_tail: the reductions, d² and bounds, finish /
-// centre — the last workgroup to arrive at each level runs it, in the same
-// launch.
+// in LDS once.
 template <int NT, bool CENTRED>
 __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n,
     const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
-    int nseg, GramCtl ctl, int64_t w, int64_t cap, int *centre,
-    double *__restrict__ partial, double *grp, double *g_key, double *segsq,
-    double *err, double tol, float *D, uint32_t *ill) {
+    int nseg, GramCtl ctl, int64_t w, int64_t cap,
+    const int *__restrict__ centre, double *__restrict__ partial) {
   constexpr int NTP = ntp_of(NT);
   const int *__restrict__ prefix = ctl.prefix;
   __shared__ __attribute__((aligned(1024))) char smem[chunk_smem<NT, CENTRED>()];
@@ -799,19 +662,95 @@ __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
         out[(p * 4 + r) * 64 + lane] = acc[p][r] + red[0][p * 4 + r][lane];
     }
   }
-  __shared__ int flag;
-  gram_tail<NT, CENTRED>(chunk, s, n, nseg, seg_lo, seg_end, ctl, partial,
-                         grp, g_key, centre, segsq, err, tol, D, ill,
-                         reinterpret_cast<double *>(smem), &flag);
+}
+
+// Level 1, grid (groups, NTP): group b (of key s) sums its <= kRed chunks
+// in order into red[b][p][256].
+template <int NT>
+__global__ __launch_bounds__(256) void gram_reduce1_kernel(
+    const double *__restrict__ partial, GramCtl ctl, int nseg,
+    double *__restrict__ red) {
+  constexpr int NTP = ntp_of(NT);
+  const int b = blockIdx.x, p = blockIdx.y, e = threadIdx.x;
+  if (b >= ctl.gprefix[nseg]) return;
+  int s = 0;
+  while (ctl.gprefix[s + 1] <= b) ++s;
+  const int q0 = ctl.prefix[s] + (b - ctl.gprefix[s]) * kRed;
+  const int q1 = min(q0 + kRed, ctl.prefix[s + 1]);
+  double v[kRed];
+#pragma unroll
+  for (int q = 0; q < kRed; ++q)
+    v[q] = q0 + q < q1 ? partial[((int64_t(q0) + q) * NTP + p) * 256 + e]
+                       : 0.0;
+  double sum = 0.0;
+#pragma unroll
+  for (int q = 0; q < kRed; ++q) sum += v[q];
+  red[(int64_t(b) * NTP + p) * 256 + e] = sum;
+}
+
+// Level 2 of groups [g0, g1) into a 64 x 64 Gram matrix in LDS (both
+// triangles of the tile pairs), groups summed in order.
+template <int NT>
+__device__ void gram_level2(const double *__restrict__ red, int g0, int g1,
+                            double *G) {
+  constexpr int NTP = ntp_of(NT);
+  constexpr int U = 8;
+  const int e = threadIdx.x, r = e >> 6, lane = e & 63;
+  for (int p = 0; p < NTP; ++p) {
+    double sum = 0.0;
+    for (int b = g0; b < g1; b += U) {
+      double v[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        v[j] = b + j < g1 ? red[(int64_t(b + j) * NTP + p) * 256 + e] : 0.0;
+#pragma unroll
+      for (int j = 0; j < U; ++j) sum += v[j];
+    }
+    int t, u;
+    tp_tiles(p, NT, t, u);
+    const int a = 16 * t + 4 * (lane >> 4) + r, c = 16 * u + (lane & 15);
+    G[a * 64 + c] = sum;
+    if (t != u) G[c * 64 + a] = sum;
+  }
+  __syncthreads();
+}
+
+// The sample pass's Gram (every group of every key) and the centre from it:
+// one workgroup.
+template <int NT>
+__global__ __launch_bounds__(256) void gram_centre_kernel(
+    const double *__restrict__ red, GramCtl ctl, int nseg, int n,
+    int *__restrict__ centre) {
+  __shared__ double G[64 * 64 + 4 * 64];
+  gram_level2<NT>(red, 0, ctl.gprefix[nseg], G);
+  centre_of(G, n, centre, reinterpret_cast<double(*)[64]>(G + 64 * 64));
+}
+
+// Per key (grid nseg): its groups into its Gram matrix, then every pair's d²
+// and worst-case bound (segsq_pair).
+template <int NT>
+__global__ __launch_bounds__(256) void gram_key_kernel(
+    const double *__restrict__ red, GramCtl ctl, int n,
+    const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
+    double *__restrict__ segsq, double *__restrict__ err) {
+  __shared__ double G[64 * 64];
+  const int s = blockIdx.x;
+  gram_level2<NT>(red, ctl.gprefix[s], ctl.gprefix[s + 1], G);
+  const int64_t len = seg_end[s] - seg_lo[s];
+  const int nn = n * n;
+  for (int i = threadIdx.x; i < nn; i += 256)
+    segsq_pair(G, i / n, i % n, len, segsq[int64_t(s) * nn + i],
+               err[int64_t(s) * nn + i]);
 }
 
 // The finish of a sharded call, after the ranks' d² and bounds were summed
 // (fsagg_pairgram_finish_f32): finish_pair on every pair.
 __global__ __launch_bounds__(256) void gram_finish_kernel(
     const double *__restrict__ segsq, const double *__restrict__ err, int n,
-    int nseg, double tol, float *__restrict__ D, uint32_t *__restrict__ ill) {
+    int nseg, double tol, float *__restrict__ D, uint32_t *__restrict__ ill,
+    float *__restrict__ B) {
   const int q = blockIdx.x * 256 + threadIdx.x;
-  if (q < n * n) finish_pair(q, segsq, err, n, nseg, tol, D, ill);
+  if (q < n * n) finish_pair(q, segsq, err, n, nseg, tol, D, ill, B);
 }
 
 struct GramPlan {
@@ -840,9 +779,9 @@ GramPlan gram_plan(int n, int64_t numel, int nseg) {
 }
 
 struct GramWs {
-  GramCtl cs, cm;          // sample and main pass control blocks
+  GramCtl cs, cm;          // sample and main pass plans
   int *centre;
-  double *partial, *g_key, *grp;
+  double *partial, *red;
 };
 
 size_t gram_ws_layout(int n, int64_t numel, int nseg, void *ws, GramWs *w) {
@@ -860,64 +799,66 @@ size_t gram_ws_layout(int n, int64_t numel, int nseg, void *ws, GramWs *w) {
     off += align256(bytes);
     return static_cast<char *>(ws) + o;
   };
-  auto ctl = [&](int g) {
-    // prefix, gprefix, cnt_key, cnt_all, nonempty, cnt_group
-    const size_t k = size_t(nseg);
-    int *p = reinterpret_cast<int *>(
-        take(sizeof(int) * (3 * k + 4 + size_t(g))));
+  auto ctl = [&]() {
+    int *p = reinterpret_cast<int *>(take(sizeof(int) * 2 * size_t(nseg + 1)));
     GramCtl c;
     c.prefix = p;
-    c.gprefix = p + (k + 1);
-    c.cnt_key = p + 2 * (k + 1);
-    c.cnt_all = c.cnt_key + k;
-    c.nonempty = c.cnt_all + 1;
-    c.cnt_group = c.nonempty + 1;
-    c.groups = g;
+    c.gprefix = p + (nseg + 1);
     return c;
   };
-  const GramCtl cs = ctl(pl.sample_groups), cm = ctl(pl.main_groups);
+  const GramCtl cs = ctl(), cm = ctl();
   char *p_c = take(256),
-       *p_gk = take(sizeof(double) * 64 * 64 * size_t(nseg)),
-       *p_grp = take(sizeof(double) * groups * ntp * 256),
+       *p_red = take(sizeof(double) * groups * ntp * 256),
        *p_part = take(sizeof(double) * chunks * ntp * 256);
   if (w) {
     w->cs = cs;
     w->cm = cm;
     w->centre = reinterpret_cast<int *>(p_c);
-    w->g_key = reinterpret_cast<double *>(p_gk);
-    w->grp = reinterpret_cast<double *>(p_grp);
+    w->red = reinterpret_cast<double *>(p_red);
     w->partial = reinterpret_cast<double *>(p_part);
   }
   return off;
 }
 
-// Three launches: the plans (and counters), the sample pass (its tail picks
-// the centre), the centred main pass (its tail writes every key's d² and
-// bounds, and with D the finish).
+// Seven launches (eight with the finish): both plans; the sample pass, its
+// group sums and the centre; the centred main pass, its group sums, and per
+// key the Gram matrix, every pair's d² and bound.
 template <int NT>
 void gram_launch(const float *const *tab, int64_t ss, int n,
                  const int64_t *seg_lo, const int64_t *seg_end, int nseg,
                  const GramPlan &pl, const GramWs &w, double *segsq,
-                 double *err, double tol, float *D, uint32_t *ill,
+                 double *err, double tol, float *D, uint32_t *ill, float *B,
                  hipStream_t st) {
-  hipLaunchKernelGGL(gram_prefix_kernel, dim3(1), dim3(256), 0, st, seg_lo,
+  constexpr int NTP = ntp_of(NT);
+  hipLaunchKernelGGL(gram_prefix_kernel, dim3(1), dim3(1), 0, st, seg_lo,
                      seg_end, nseg, kSampleChunk, kSampleCoords, pl.w, w.cs,
-                     w.cm, w.g_key, segsq, err, n);
+                     w.cm);
   // 1. the centre: Gram of the first kSampleCoords of every key, raw
   hipLaunchKernelGGL((gram_chunk_kernel<NT, false>),
                      dim3(unsigned(pl.sample_chunks)), dim3(kBlk), 0, st,
                      tab, ss, n, seg_lo, seg_end, nseg, w.cs, kSampleChunk,
-                     kSampleCoords, w.centre, w.partial, w.grp, w.g_key,
-                     static_cast<double *>(nullptr),
-                     static_cast<double *>(nullptr), 0.0,
-                     static_cast<float *>(nullptr),
-                     static_cast<uint32_t *>(nullptr));
-  // 2. the centred Gram of every key, its d² and bounds (and D)
+                     kSampleCoords, static_cast<const int *>(nullptr),
+                     w.partial);
+  hipLaunchKernelGGL((gram_reduce1_kernel<NT>),
+                     dim3(unsigned(pl.sample_groups), unsigned(NTP)),
+                     dim3(256), 0, st, w.partial, w.cs, nseg, w.red);
+  hipLaunchKernelGGL((gram_centre_kernel<NT>), dim3(1), dim3(256), 0, st,
+                     w.red, w.cs, nseg, n, w.centre);
+  // 2. the centred Gram of every key, its d² and bounds
   hipLaunchKernelGGL((gram_chunk_kernel<NT, true>),
                      dim3(unsigned(pl.main_chunks)), dim3(kBlk), 0, st, tab,
                      ss, n, seg_lo, seg_end, nseg, w.cm, pl.w, int64_t(0),
-                     w.centre, w.partial, w.grp, w.g_key, segsq, err, tol, D,
-                     ill);
+                     static_cast<const int *>(w.centre), w.partial);
+  hipLaunchKernelGGL((gram_reduce1_kernel<NT>),
+                     dim3(unsigned(pl.main_groups), unsigned(NTP)),
+                     dim3(256), 0, st, w.partial, w.cm, nseg, w.red);
+  hipLaunchKernelGGL((gram_key_kernel<NT>), dim3(unsigned(nseg)), dim3(256),
+                     0, st, w.red, w.cm, n, seg_lo, seg_end, segsq, err);
+  if (D)
+    hipLaunchKernelGGL(gram_finish_kernel,
+                       dim3(unsigned((int64_t(n) * n + 255) / 256)),
+                       dim3(256), 0, st, segsq, err, n, nseg, tol, D, ill,
+                       B);
 }
 
 }  // namespace
@@ -935,7 +876,7 @@ namespace {
 int pairgram_rows(const char *what, const fsagg_rows *rows,
                   const int64_t *seg_lo, const int64_t *seg_end,
                   int64_t numel, double *segsq, double *err, double tol,
-                  float *D, uint32_t *ill, void *workspace,
+                  float *D, uint32_t *ill, float *B, void *workspace,
                   size_t workspace_bytes, fsagg_stream_t stream) {
   if (!rows || !rows->tab || !seg_lo || !seg_end || !segsq || !err ||
       rows->n < 2 || rows->n > 16 * kGramMaxTiles || rows->nseg < 1 ||
@@ -957,13 +898,13 @@ int pairgram_rows(const char *what, const fsagg_rows *rows,
   hipStream_t st = as_stream(stream);
   switch (pl.nt) {
     case 1: gram_launch<1>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg, pl,
-                           w, segsq, err, tol, D, ill, st); break;
+                           w, segsq, err, tol, D, ill, B, st); break;
     case 2: gram_launch<2>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg, pl,
-                           w, segsq, err, tol, D, ill, st); break;
+                           w, segsq, err, tol, D, ill, B, st); break;
     case 3: gram_launch<3>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg, pl,
-                           w, segsq, err, tol, D, ill, st); break;
+                           w, segsq, err, tol, D, ill, B, st); break;
     default: gram_launch<4>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg, pl,
-                            w, segsq, err, tol, D, ill, st); break;
+                            w, segsq, err, tol, D, ill, B, st); break;
   }
   return check_launch(what);
 }
@@ -978,7 +919,7 @@ extern "C" int fsagg_pairgram_rows_segsq_f32(const fsagg_rows *rows,
                                              fsagg_stream_t stream) {
   return pairgram_rows("fsagg_pairgram_rows_segsq_f32", rows, seg_lo,
                        seg_end, numel, segsq, err, 0.0, nullptr, nullptr,
-                       workspace, workspace_bytes, stream);
+                       nullptr, workspace, workspace_bytes, stream);
 }
 
 extern "C" int fsagg_pairgram_rows_f32(const fsagg_rows *rows,
@@ -986,7 +927,7 @@ extern "C" int fsagg_pairgram_rows_f32(const fsagg_rows *rows,
                                        const int64_t *seg_end, int64_t numel,
                                        double tol, double *segsq,
                                        double *err, float *D, uint32_t *ill,
-                                       void *workspace,
+                                       float *bound, void *workspace,
                                        size_t workspace_bytes,
                                        fsagg_stream_t stream) {
   if (!D) {
@@ -994,13 +935,14 @@ extern "C" int fsagg_pairgram_rows_f32(const fsagg_rows *rows,
     return FSAGG_EINVAL;
   }
   return pairgram_rows("fsagg_pairgram_rows_f32", rows, seg_lo, seg_end,
-                       numel, segsq, err, tol, D, ill, workspace,
+                       numel, segsq, err, tol, D, ill, bound, workspace,
                        workspace_bytes, stream);
 }
 
 extern "C" int fsagg_pairgram_finish_f32(const double *segsq,
                                          const double *err, int n, int nseg,
                                          double tol, float *D, uint32_t *ill,
+                                         float *bound,
                                          fsagg_stream_t stream) {
   if (!segsq || !err || !D || !ill || n < 2 || nseg < 1 || !(tol >= 0.0)) {
     set_error("fsagg_pairgram_finish_f32: invalid argument (n=%d nseg=%d)",
@@ -1009,6 +951,7 @@ extern "C" int fsagg_pairgram_finish_f32(const double *segsq,
   }
   hipLaunchKernelGGL(gram_finish_kernel,
                      dim3(unsigned((int64_t(n) * n + 255) / 256)), dim3(256),
-                     0, as_stream(stream), segsq, err, n, nseg, tol, D, ill);
+                     0, as_stream(stream), segsq, err, n, nseg, tol, D, ill,
+                     bound);
   return check_launch("fsagg_pairgram_finish_f32");
 }

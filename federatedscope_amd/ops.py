@@ -1051,28 +1051,29 @@ def pairgram_rows_segsq(rs, lo=0, hi=None, workspace=None, keep=None):
 
 
 def pairgram_finish(sq2, tol):
-    """D (fp32 [n][n], device, as :func:`pairdist_finish`) and ill (int32
-    [n][n]: the pairs whose error bound exceeds ``tol``·D) from
-    :func:`pairgram_rows_segsq`'s output, both in one int32 [2][n][n]
-    device tensor (one copy to the host): returns (buf, D view, ill view)."""
+    """D (fp32 [n][n], device, as :func:`pairdist_finish`), ill (int32
+    [n][n]: the pairs whose bound exceeds ``tol``·D, or non-finite) and B
+    (fp32 [n][n]: each pair's worst-case bound on |D − the exact
+    distance|) from :func:`pairgram_rows_segsq`'s output, in one int32
+    [3][n][n] device tensor (one copy to the host): returns (buf, D view,
+    ill view, B view)."""
     if sq2.dim() != 4 or sq2.shape[0] != 2 or sq2.dtype != torch.float64 \
             or not sq2.is_contiguous():
         raise ValueError('sq2 must be a contiguous fp64 [2][nseg][n][n] '
                          'tensor')
     nseg, n = int(sq2.shape[1]), int(sq2.shape[2])
-    buf = torch.empty((2, n, n), dtype=torch.int32, device=sq2.device)
-    D = buf[0].view(torch.float32)
+    buf = torch.empty((3, n, n), dtype=torch.int32, device=sq2.device)
     L.check(L.load().fsagg_pairgram_finish_f32(
         sq2[0].data_ptr(), sq2[1].data_ptr(), n, nseg, float(tol),
-        buf[0].data_ptr(), buf[1].data_ptr(), _stream(sq2.device)),
-        'fsagg_pairgram_finish_f32')
-    return buf, D, buf[1]
+        buf[0].data_ptr(), buf[1].data_ptr(), buf[2].data_ptr(),
+        _stream(sq2.device)), 'fsagg_pairgram_finish_f32')
+    return buf, buf[0].view(torch.float32), buf[1], buf[2].view(torch.float32)
 
 
 def pairgram_rows_dist(rs, tol, workspace=None):
     """:func:`pairgram_rows_segsq` and :func:`pairgram_finish` in one call
-    (fsagg_pairgram_rows_f32: the finish runs in the main pass's last
-    workgroup).  Returns (buf, D view, ill view, sq2) as those two."""
+    (fsagg_pairgram_rows_f32).  Returns (buf, D view, ill view, B view, sq2)
+    as those two."""
     _require_all(rs, 'Krum')
     if not 2 <= rs.n <= L.FSAGG_PAIRGRAM_MAX_CLIENTS:
         raise ValueError('the Gram path takes 2..%d clients' %
@@ -1085,13 +1086,14 @@ def pairgram_rows_dist(rs, tol, workspace=None):
     ws = (workspace or _WS).get(rs.device, need)
     sq2 = torch.empty((2, rs.nseg, rs.n, rs.n), dtype=torch.float64,
                       device=rs.device)
-    buf = torch.empty((2, rs.n, rs.n), dtype=torch.int32, device=rs.device)
+    buf = torch.empty((3, rs.n, rs.n), dtype=torch.int32, device=rs.device)
     L.check(lib.fsagg_pairgram_rows_f32(
         rs.ptr(), seg_lo.data_ptr(), seg_end.data_ptr(), extent, float(tol),
         sq2[0].data_ptr(), sq2[1].data_ptr(), buf[0].data_ptr(),
-        buf[1].data_ptr(), ws.data_ptr(), ws.numel(), _stream(rs.device)),
-        'fsagg_pairgram_rows_f32')
-    return buf, buf[0].view(torch.float32), buf[1], sq2
+        buf[1].data_ptr(), buf[2].data_ptr(), ws.data_ptr(), ws.numel(),
+        _stream(rs.device)), 'fsagg_pairgram_rows_f32')
+    return buf, buf[0].view(torch.float32), buf[1], \
+        buf[2].view(torch.float32), sq2
 
 
 def pairdist_rows(rs, workspace=None):

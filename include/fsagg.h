@@ -466,11 +466,10 @@ int fsagg_pairdist_rows_segsq_f32(const fsagg_rows *rows,
  * Sums of segsq and err over disjoint coordinate ranges (ranks) stay
  * valid.  Replaces the same torch.dist loop (krum_aggregator.py:41-73) as
  * fsagg_pairdist_f32, with fsagg_pairgram_finish_f32 in place of
- * fsagg_pairdist_finish_f64.  Three launches (plans; the sample pass, whose
- * last workgroup picks the centre; the main pass, whose last workgroup of
- * each chunk group / key runs that level's fixed-order reduction and the
- * key's d² and bounds).  Workspace: fsagg_pairgram_workspace_bytes(n,
- * numel, nseg) (0 when n is outside 2..64). */
+ * fsagg_pairdist_finish_f64.  The rows stream through LDS in 512-B runs
+ * per row (global_load_lds), whatever their placement.  Workspace:
+ * fsagg_pairgram_workspace_bytes(n, numel, nseg) (0 when n is outside
+ * 2..64). */
 size_t fsagg_pairgram_workspace_bytes(int n, int64_t numel, int nseg);
 int fsagg_pairgram_rows_segsq_f32(const fsagg_rows *rows,
                                   const int64_t *seg_lo,
@@ -482,22 +481,24 @@ int fsagg_pairgram_rows_segsq_f32(const fsagg_rows *rows,
 /* Krum's n×n distance matrix from fsagg_pairgram_rows_segsq_f32's output:
  * D[a][b] = Σ_s fl32(sqrt(segsq[s][a][b])) in key order (fp32, as
  * fsagg_pairdist_finish_f64 and the reference's `distance +=
- * torch.dist(...)`, krum_aggregator.py:45-56), D[a][a] = +inf, and
- * ill[a*n + b] = 1 for a pair whose per-key distances the bounds do not
- * certify to tol (Σ_s worst move of sqrt(d²_s) over [d²_s ± err_s] >
- * tol · Σ_s sqrt(d²_s)), or whose D is not finite — the caller recomputes
- * those pairs with fsagg_pairdist_rows_segsq_f32 on the clients involved. */
+ * torch.dist(...)`, krum_aggregator.py:45-56), D[a][a] = +inf;
+ * bound[a][b] (fp32, rounded up; may be NULL) a worst-case bound on
+ * |Σ_s sqrt(segsq_s) − Σ_s (exact per-key distance)| — Σ_s of the worst
+ * move of sqrt over [segsq_s ± err_s] — that the caller certifies its Krum
+ * selection with; ill[a*n + b] = 1 where that bound exceeds tol · Σ_s d_s,
+ * or d² came out negative beyond its bound, or D is not finite — the
+ * caller recomputes those pairs with fsagg_pairdist_rows_segsq_f32 on the
+ * clients involved (tol = +inf: only the non-finite ones). */
 int fsagg_pairgram_finish_f32(const double *segsq, const double *err, int n,
                               int nseg, double tol, float *D, uint32_t *ill,
-                              fsagg_stream_t stream);
+                              float *bound, fsagg_stream_t stream);
 
-/* fsagg_pairgram_rows_segsq_f32 and fsagg_pairgram_finish_f32 in the same
- * three launches (the finish runs in the last workgroup of the main pass):
- * the unsharded call. */
+/* fsagg_pairgram_rows_segsq_f32 and fsagg_pairgram_finish_f32 in one call
+ * (the unsharded path). */
 int fsagg_pairgram_rows_f32(const fsagg_rows *rows, const int64_t *seg_lo,
                             const int64_t *seg_end, int64_t numel, double tol,
                             double *segsq, double *err, float *D,
-                            uint32_t *ill, void *workspace,
+                            uint32_t *ill, float *bound, void *workspace,
                             size_t workspace_bytes, fsagg_stream_t stream);
 
 /* Per-(client, key segment) squared L2 norms over a row set in fp64:

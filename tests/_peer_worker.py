@@ -65,8 +65,13 @@ def aggregate_mode(rank, world):
     one = [('w', (1_000_003, ))]
     multi = [('a', (300_001, )), ('b', (64, 70)), ('c', (1, )),
              ('d', (70_000, ))]
-    init1 = OrderedDict((k, torch.randn(s, device='cuda')) for k, s in one)
-    initm = OrderedDict((k, torch.randn(s, device='cuda')) for k, s in multi)
+    # the same init model on every rank (each rank reduces its piece of
+    # init + update)
+    g = torch.Generator(device='cuda').manual_seed(99)
+    init1 = OrderedDict((k, torch.randn(s, device='cuda', generator=g))
+                        for k, s in one)
+    initm = OrderedDict((k, torch.randn(s, device='cuda', generator=g))
+                        for k, s in multi)
     cases = [
         ('fedavg_one_key', ClientsAvgAggregator, one, None, {}, 20),
         ('fedavg_multi_key', ClientsAvgAggregator, multi, None, {}, 20),
@@ -84,7 +89,18 @@ def aggregate_mode(rank, world):
             got = a.aggregate(info)
             want = b.aggregate(info)
             for k in want:
-                assert torch.equal(got[k], want[k]), (name, k, rnd)
+                if not torch.equal(got[k], want[k]):
+                    bad = (got[k] != want[k]).reshape(-1).nonzero()
+                    pa = next(iter(a._plans.values()))
+                    lay = next(iter(a._layouts.values()), None)
+                    off = lay.offsets[k] if lay is not None else None
+                    raise AssertionError(
+                        (name, k, rnd, 'rank', rank, 'bad', bad.numel(),
+                         'first', bad[:4].reshape(-1).tolist(),
+                         'key offset', off, 'pieces',
+                         [pa.piece(r) for r in range(world)],
+                         got[k].reshape(-1)[bad[:2].reshape(-1)].tolist(),
+                         want[k].reshape(-1)[bad[:2].reshape(-1)].tolist()))
         assert all(isinstance(p, PeerAssembly) for p in a._plans.values())
         if name == 'krum':
             assert a.last_selection == b.last_selection

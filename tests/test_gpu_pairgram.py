@@ -1,26 +1,27 @@
 """Krum distances on the matrix cores (fsagg_pairgram_rows_segsq_f32 +
-fsagg_pairgram_finish_f32).
+fsagg_pairgram_finish_f32, fsagg_pairgram_rows_f32).
 
-The Gram form d² = G_aa + G_bb − 2·G_ab (centred on a central client, bf16
-limbs, fp32 within a k-step / fp64 beyond) against an fp64 restatement of
-every per-key squared distance, and against the VALU kernel (pairdist.hip):
+The Gram form d² = G_aa + G_bb − 2·G_ab (centred on a central client, fp32
+split exactly into three bf16 limbs, fp32 within an MFMA k-step / fp64
+beyond) against an fp64 restatement of every per-key squared distance, and
+against the VALU kernel (pairdist.hip):
 * n = 2 … 64 (1–4 MFMA tiles, ragged last tile), keys of 0, 1, 3, 5 … 300k
   elements (partial k-steps, chunk tails), keyed and stacked row sets;
 * rows that are not 16-B aligned (the per-element load path);
 * a common component 1000× the spread (cancellation without centring),
   with a far Byzantine client;
-* identical and near-duplicate clients far from the others (their pair
-  flagged; the engine recomputes the flagged clients' pairs exactly on the
-  VALU kernel), and non-finite values (flagged, VALU semantics).
+* identical and near-duplicate clients far from the others, and non-finite
+  values (flagged, recomputed with the VALU kernel's semantics);
 * structured data where the k-steps' roundings do not cancel (DESIGN
   §3.3): dequantised int8-grid uploads, Student-t (ν = 3) tails, a
   colluding group shifted by one sign-biased offset away from the centre,
   half-zero sparse updates — keys of >= 1M coordinates.
 Contract checked: every per-key |d²_got − d²_fp64| is within the kernel's
-worst-case bound err; the unflagged pairs' per-key distances are within
-_GRAM_TOL (1e-6) of fp64 (Σ_s |d_s − d̂_s| <= 1e-6 · Σ_s d_s), and D — the
-reference's fp32 formation of them — within 1e-6 plus the fp32 rounding of
-that formation."""
+worst-case bound err; every finite pair's D is within its bound B (plus the
+fp32 rounding of D's formation) of the fp64 distances' D; and the engine's
+Krum selection — certified against B, else recomputed on the VALU kernel —
+is the fp64 distances' selection wherever the fp64 scores separate it by
+more than their own fp32 formation."""
 from collections import OrderedDict
 
 import numpy as np
@@ -46,8 +47,7 @@ def _clients(n, sizes=SIZES, seed=9, fn=None):
 
 def _as_slab(clients):
     """The same clients as views of one allocation (each client's keys
-    contiguous, as in the client stack): rows at spread offsets, the layout
-    the engine gives the matrix cores (_engine._rows_spread)."""
+    contiguous, as in the client stack)."""
     keys = list(clients[0].keys())
     sizes = [clients[0][k].numel() for k in keys]
     total = sum(sizes) + 16 * len(keys)
@@ -89,14 +89,16 @@ def _fp64_segsq(clients, lay):
 
 
 def _gram(rs):
-    """The Gram path over every key: (segsq, err, D, flags) on the host."""
+    """The Gram path over every key: (segsq, err, D, flags, B) on the host."""
     from federatedscope_amd import ops
     from federatedscope_amd.core.aggregators._engine import _GRAM_TOL
     sq2 = ops.pairgram_rows_segsq(rs)
-    _, D, ill = ops.pairgram_finish(sq2, _GRAM_TOL)
+    _, D, ill, B = ops.pairgram_finish(sq2, _GRAM_TOL)
     flags = ill.cpu().numpy()
     sq2 = sq2.cpu().numpy()
-    return sq2[0], sq2[1], D.cpu().numpy(), (flags + flags.T) > 0
+    B = B.cpu().numpy().astype(np.float64)
+    return sq2[0], sq2[1], D.cpu().numpy(), (flags + flags.T) > 0, \
+        np.maximum(B, B.T)
 
 
 def _fp64_D(want):
@@ -117,27 +119,37 @@ def _formation(nseg):
     return 2.0 * (nseg + 1) * 2.0 ** -24
 
 
-def _check(got, err, D, flags, want, rtol=1e-6):
-    """Returns max |d²_got − d²_fp64| / err over the keys and pairs."""
+def _check(got, err, D, flags, B, want):
+    """Returns (max |d²_got − d²_fp64| / err, max |D − D_fp64| / B)."""
     # the worst-case bound holds on every key and pair
     dev = np.abs(got - want)
     assert np.all(dev <= err), np.max(dev / np.maximum(err, 1e-300))
     ratio = float(np.max(np.where(err > 0, dev / np.maximum(err, 1e-300),
                                   0.0)))
-    # identical d² = 0 rows stay 0
+    # identical rows: d² = 0 exactly
     Dw = _fp64_D(want)
     off = ~np.eye(D.shape[0], dtype=bool) & ~flags
-    pos = off & (Dw > 0)
     assert np.all(D[off & (Dw == 0)] == 0.0)
-    if pos.any():
-        # the certified per-key distances
-        dk = np.abs(np.sqrt(got) - np.sqrt(want)).sum(0)
-        sk = np.sqrt(want).sum(0)
-        assert np.all(dk[pos] <= rtol * sk[pos] + 1e-300), \
-            (dk[pos] / sk[pos]).max()
-        e = np.abs(D[pos].astype(np.float64) - Dw[pos]) / Dw[pos]
-        assert e.max() <= rtol + _formation(got.shape[0]), e.max()
-    return ratio
+    # the per-pair bound on D (a sum of per-key distances)
+    dk = np.abs(np.sqrt(got) - np.sqrt(want)).sum(0)
+    assert np.all(dk[off] <= B[off] * (1 + 1e-6) + 1e-300), \
+        (dk[off] / np.maximum(B[off], 1e-300)).max()
+    e = np.abs(D[off].astype(np.float64) - Dw[off].astype(np.float64))
+    slack = _formation(got.shape[0]) * Dw[off].astype(np.float64)
+    assert np.all(e <= B[off] + slack), (e - B[off] - slack).max()
+    bratio = float(np.max(np.where(B[off] > 0, dk[off] / np.maximum(
+        B[off], 1e-300), 0.0))) if off.any() else 0.0
+    return ratio, bratio
+
+
+def _separated(s, m, ordered, n):
+    """Whether fp64-derived scores s fix the selection of m (and with
+    ``ordered`` its order) beyond their own fp32 formation."""
+    o = np.argsort(s, kind='stable')
+    ss = s[o]
+    gaps = range(min(m, len(s) - 1)) if ordered else [m - 1]
+    return all(ss[i + 1] - ss[i] > 4 * n * 2.0 ** -23 * ss[i + 1]
+               for i in gaps)
 
 
 @pytest.mark.parametrize('n', [2, 5, 16, 17, 33, 50, 64])
@@ -147,9 +159,9 @@ def test_pairgram_vs_fp64_and_valu(n):
     lay, _, keyed, stacked = _sets(clients)
     want = _fp64_segsq(clients, lay)
     for rs in (keyed, stacked):
-        got, err, D, flags = _gram(rs)
-        assert flags.sum() <= 2, flags.sum()
-        _check(got, err, D, flags, want)
+        got, err, D, flags, B = _gram(rs)
+        assert not flags.any()
+        _check(got, err, D, flags, B, want)
     valu = ops.pairdist_rows_segsq(keyed).cpu().numpy()
     d_got, d_want = np.sqrt(valu), np.sqrt(want)
     pos = d_want > 0
@@ -172,9 +184,9 @@ def test_pairgram_unaligned_rows():
                     dtype=np.int64)
     rs = ops.RowSet.from_pointers(lay, ptrs, 'cuda', keepalive=clients,
                                   aligned16=False)
-    got, err, D, flags = _gram(rs)
+    got, err, D, flags, B = _gram(rs)
     assert not flags.any()
-    _check(got, err, D, flags, _fp64_segsq(clients, lay))
+    _check(got, err, D, flags, B, _fp64_segsq(clients, lay))
 
 
 def test_pairgram_common_component_and_byzantine():
@@ -191,12 +203,12 @@ def test_pairgram_common_component_and_byzantine():
 
     clients = _clients(n, sizes=[300_001, 4097, 9], seed=12, fn=fn)
     lay, _, keyed, _ = _sets(clients)
-    got, err, D, flags = _gram(keyed)
+    got, err, D, flags, B = _gram(keyed)
     assert not flags.any()
-    _check(got, err, D, flags, _fp64_segsq(clients, lay))
+    _check(got, err, D, flags, B, _fp64_segsq(clients, lay))
 
 
-def _krum(clients, f=2):
+def _krum(clients, f=2, m=1):
     from types import SimpleNamespace
     from federatedscope_amd.core.aggregators import KrumAggregator
     cfg = SimpleNamespace(
@@ -204,12 +216,45 @@ def _krum(clients, f=2):
                                  client_num=1000, sample_client_rate=1.0),
         aggregator=SimpleNamespace(
             byzantine_node_num=f,
-            BFT_args=SimpleNamespace(krum_agg_num=1)))
+            BFT_args=SimpleNamespace(krum_agg_num=m)))
     return KrumAggregator(device='cuda', config=cfg)
+
+
+class _DictModel(torch.nn.Module):
+    def __init__(self, sd):
+        super().__init__()
+        self.sd = sd
+
+    def state_dict(self, *a, **kw):
+        return self.sd
+
+
+def _select(clients, f, m):
+    """The engine's Krum selection (KrumAggregator.aggregate on the clients
+    as slab views, a zero init model) and its distance path."""
+    agg = _krum(clients, f=f, m=m)
+    agg.model = _DictModel(OrderedDict(
+        (k, torch.zeros_like(v)) for k, v in clients[0].items()))
+    agg.aggregate({'client_feedback': [(1, c) for c in _as_slab(clients)],
+                   'recover_fun': None})
+    return agg.last_selection, agg.last_pairdist_path
+
+
+def _fp64_selection(want, f, m):
+    from federatedscope_amd.core.aggregators.krum_aggregator import \
+        krum_scores
+    Dw = _fp64_D(want)
+    n = Dw.shape[0]
+    s = krum_scores(torch.from_numpy(Dw), f).double().numpy()
+    return [int(i) for i in np.argsort(s, kind='stable')[:m]], \
+        _separated(s, m, True, n)
 
 
 @pytest.mark.parametrize('case', ['identical', 'near', 'nonfinite'])
 def test_pairgram_flags_and_exact_repair(case):
+    """Identical / near-duplicate clients far from the rest: bounded like
+    every pair, no recomputation; a non-finite value: its client's pairs
+    flagged and recomputed on the VALU kernel (its ±inf semantics)."""
     n = 24
 
     def fn(i, j, z):
@@ -224,54 +269,59 @@ def test_pairgram_flags_and_exact_repair(case):
 
     clients = _clients(n, sizes=[10_000, 33], seed=6, fn=fn)
     lay, _, keyed, _ = _sets(clients)
-    got, err, D, flags = _gram(keyed)
+    got, err, D, flags, B = _gram(keyed)
     want = _fp64_segsq(clients, lay)
-    if case == 'nonfinite':
-        assert flags[9].sum() == n - 1
-    else:
-        assert flags[3, 4]
-        assert flags.sum() <= 2 * (2 * n - 3)
-        assert got[:, 3, 4].max() == 0.0 or case == 'near'
-        _check(got, err, D, flags, want)
     agg = _krum(clients)
     De, _ = agg.distance_matrix([(1, c) for c in _as_slab(clients)])
-    assert agg.last_pairdist_path.startswith('mfma + exact')
-    # the recomputed pairs are the VALU kernel's (its semantics for ±inf)
-    from federatedscope_amd import ops
-    Dv = ops.pairdist_finish(ops.pairdist_rows_segsq(keyed)).cpu().numpy()
-    sel = sorted(set(np.nonzero(flags)[0].tolist()))
-    ix = np.ix_(sel, sel)
-    assert np.allclose(De.numpy()[ix], Dv[ix], rtol=2e-7, atol=0,
-                       equal_nan=True)
-    if case != 'nonfinite':
-        Dw = _fp64_D(want)
-        off = ~np.eye(n, dtype=bool)
-        pos = off & (Dw > 0)
-        e = np.abs(De.numpy()[pos] - Dw[pos]) / Dw[pos]
-        assert e.max() <= 1e-6 + _formation(len(lay.keys))
-        assert De.numpy()[3, 4] == Dw[3, 4] or case == 'near'
+    if case == 'nonfinite':
+        assert flags[9].sum() == n - 1
+        assert agg.last_pairdist_path.startswith('mfma + exact')
+        from federatedscope_amd import ops
+        Dv = ops.pairdist_finish(ops.pairdist_rows_segsq(keyed)).cpu().numpy()
+        sel = sorted(set(np.nonzero(flags)[0].tolist()))
+        ix = np.ix_(sel, sel)
+        assert np.allclose(De.numpy()[ix], Dv[ix], rtol=2e-7, atol=0,
+                           equal_nan=True)
+        assert np.all(agg.last_pair_bound[ix] == 0.0)
+        return
+    assert not flags.any()
+    assert agg.last_pairdist_path == 'mfma'
+    _check(got, err, D, flags, B, want)
+    if case == 'identical':
+        assert got[:, 3, 4].max() == 0.0 and De.numpy()[3, 4] == 0.0
+    sel, path = _select(clients, f=2, m=3)
+    want_sel, sep = _fp64_selection(want, 2, 3)
+    if sep:
+        assert sel == want_sel, (sel, want_sel, path)
 
 
 @pytest.mark.parametrize('n', [7, 50])
 def test_krum_distance_matrix_engine(n):
-    """Through the engine: every key on the matrix cores, one distance
-    matrix within 1e-6 of fp64 (summed over keys in fp32 like the
-    reference), no pair recomputed."""
+    """Through the engine: every key on the matrix cores, D within its
+    per-pair bound of the fp64 distances, no pair recomputed, and the
+    multi-Krum selection the fp64 one."""
     clients = _clients(n, seed=40 + n)
     lay = _sets(clients)[0]
     agg = _krum(clients, f=1)
     D, _ = agg.distance_matrix([(1, c) for c in _as_slab(clients)])
     assert agg.last_pairdist_path == 'mfma'
-    Dw = _fp64_D(_fp64_segsq(clients, lay))
+    want = _fp64_segsq(clients, lay)
+    Dw = _fp64_D(want)
     off = ~np.eye(n, dtype=bool)
-    err = np.abs(D.numpy()[off] - Dw[off]) / Dw[off]
-    assert err.max() <= 1e-6 + _formation(len(lay.keys))
+    B = agg.last_pair_bound
+    e = np.abs(D.numpy()[off].astype(np.float64) - Dw[off])
+    assert np.all(e <= B[off] + _formation(len(lay.keys)) * Dw[off])
+    m = max(1, n // 3)
+    sel, path = _select(clients, f=1, m=m)
+    want_sel, sep = _fp64_selection(want, 1, m)
+    if sep:
+        assert sel == want_sel, (sel, want_sel, path)
 
 
 def test_krum_distance_path_by_row_placement():
-    """Rows that all start at one offset within a 2 MiB page (separately
-    allocated 2 MiB-aligned tensors) take the VALU kernel, rows of one
-    allocation the matrix cores; both within 1e-6 of fp64."""
+    """Rows of separately allocated 2 MiB-aligned tensors (the Gram kernel
+    stages them through LDS) and rows of one allocation: both on the matrix
+    cores, within their bounds of fp64."""
     n = 12
     m = 600_000
     stride = 1 << 20                 # floats: rows 4 MiB apart
@@ -282,12 +332,13 @@ def test_krum_distance_path_by_row_placement():
     lay = _sets(sep)[0]
     Dw = _fp64_D(_fp64_segsq(sep, lay))
     off = ~np.eye(n, dtype=bool)
-    for clients, path in ((sep, 'valu'), (_as_slab(sep), 'mfma')):
+    for clients in (sep, _as_slab(sep)):
         agg = _krum(clients, f=1)
         D, _ = agg.distance_matrix([(1, c) for c in clients])
-        assert agg.last_pairdist_path == path
-        err = np.abs(D.numpy()[off] - Dw[off]) / Dw[off]
-        assert err.max() <= 1e-6 + _formation(1)
+        assert agg.last_pairdist_path == 'mfma'
+        B = agg.last_pair_bound
+        e = np.abs(D.numpy()[off].astype(np.float64) - Dw[off])
+        assert np.all(e <= B[off] + _formation(1) * Dw[off])
 
 
 def _fp64_segsq_dev(clients, lay):
@@ -347,37 +398,33 @@ def _stress_clients(family, n=50, seed=123):
                                     'sparse'])
 def test_pairgram_stress_families(family):
     """Structured data, 50 clients, keys of 1M / 4097 / 33: the worst-case
-    per-key bound holds on every pair, the pairs it leaves unflagged are
-    certified to 1e-6, and the engine's D (flagged pairs recomputed on the
-    VALU kernel) is within 1e-6 of fp64 with the fp64 selection."""
+    per-key bound and the per-pair bound on D hold on every pair, nothing is
+    flagged, and the engine's multi-Krum selection (certified, else
+    recomputed on the VALU kernel) is the fp64 one."""
     import json
     import os
-    from federatedscope_amd.core.aggregators.krum_aggregator import \
-        krum_scores
     clients = _stress_clients(family)
     n = len(clients)
+    f, m = 10, 5
     lay, _, _, stacked = _sets(clients)
     want = _fp64_segsq_dev(clients, lay)
-    got, err, D, flags = _gram(stacked)
-    ratio = _check(got, err, D, flags, want)
-    agg = _krum(clients, f=10)
-    De, _ = agg.distance_matrix([(1, c) for c in _as_slab(clients)])
-    assert agg.last_pairdist_path.startswith('mfma'), agg.last_pairdist_path
+    got, err, D, flags, B = _gram(stacked)
+    assert not flags.any()
+    ratio, bratio = _check(got, err, D, flags, B, want)
+    sel, path = _select(clients, f=f, m=m)
+    assert path.startswith('mfma'), path
+    want_sel, sep = _fp64_selection(want, f, m)
+    if sep:
+        assert sel == want_sel, (sel, want_sel, path)
     Dw = _fp64_D(want)
     off = ~np.eye(n, dtype=bool)
-    pos = off & (Dw > 0)
-    rel = float((np.abs(De.numpy()[pos] - Dw[pos]) / Dw[pos]).max())
-    assert rel <= 1e-6 + _formation(len(lay.keys)), rel
-    s_ref = np.sort(Dw, axis=1)[:, :n - 10 - 2].sum(-1)
-    order = np.argsort(s_ref, kind='stable')
-    s_got = krum_scores(De, 10).numpy()
-    srt = np.sort(s_ref)
-    if (srt[1] - srt[0]) / srt[0] >= 1e-5:
-        assert int(np.argmin(s_got)) == int(order[0])
-    rec = {'family': family, 'max_abserr_over_bound': ratio,
-           'flagged_pairs': int(flags.sum()) // 2,
-           'engine_path': agg.last_pairdist_path,
-           'engine_max_rel_err_vs_fp64': rel}
+    rel = float((np.abs(D[off].astype(np.float64) - Dw[off]) /
+                 Dw[off]).max())
+    brel = float((B[off] / Dw[off]).max())
+    rec = {'family': family, 'max_abserr_over_bound_per_key': ratio,
+           'max_D_err_over_pair_bound': bratio,
+           'max_rel_err_D_vs_fp64': rel, 'max_rel_pair_bound': brel,
+           'engine_path': path, 'fp64_selection_separated': sep}
     log = os.environ.get('FSAGG_TEST_LOG')
     if log:
         with open(log, 'a') as fh:

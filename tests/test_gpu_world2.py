@@ -37,7 +37,11 @@ def _run2(args, timeout=110, nproc=2):
     env = dict(os.environ, OMP_NUM_THREADS='4')
     p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True,
                        timeout=timeout, env=env)
-    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    # the ranks' own tracebacks (torchrun prefixes them with [rankN])
+    tb = '\n'.join(ln for ln in p.stderr.splitlines()
+                   if ln.startswith('[rank'))
+    assert p.returncode == 0, (p.stdout[-2000:], tb[-6000:] or
+                               p.stderr[-4000:])
     # every JSON object in the output (the two ranks' lines can interleave)
     dec, out, i = json.JSONDecoder(), [], p.stdout.find('{')
     while i >= 0:

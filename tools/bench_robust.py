@@ -113,19 +113,25 @@ def krum_c4(dev, n=50, f=10):
     sel_gpu = torch.sort(s_gpu)[1][:5].tolist()
     sel_ref = torch.sort(s_ref)[1][:5].tolist()
     # the matrix-core path the aggregators take for n <= 64
-    # (fsagg_pairgram_rows_segsq_f32 over every key + fsagg_pairgram_finish)
+    # (fsagg_pairgram_rows_f32: every key, D, flags and per-pair bounds)
     import numpy as np
-    from federatedscope_amd.core.aggregators._engine import _GRAM_TOL
+    from federatedscope_amd.core.aggregators._engine import (
+        _GRAM_TOL, certified_selection)
     rs = ops.RowSet(lay, np.array([[slab[i].data_ptr()] for i in range(n)],
                                   dtype=np.int64), dev, keepalive=(slab, ))
 
     def gram_D():
-        sq2 = ops.pairgram_rows_segsq(rs)
-        buf, D_, ill_ = ops.pairgram_finish(sq2, _GRAM_TOL)
-        return sq2, D_, ill_
+        buf, D_, ill_, B_, sq2_ = ops.pairgram_rows_dist(rs, _GRAM_TOL)
+        return sq2_, D_, ill_, B_
 
-    sq2, Dg, ill = gram_D()
+    sq2, Dg, ill, Bg = gram_D()
     Dg, flags = Dg.cpu(), ill.cpu().numpy()
+    Bg = Bg.cpu().numpy().astype(np.float64)
+    Bg = np.maximum(Bg, Bg.T) + (2 * len(lay.keys) + 2) * 2.0 ** -24 * \
+        np.where(np.isfinite(Dg.numpy()), Dg.numpy(), 0.0)
+    sg = krum_scores(Dg, f)
+    certified = certified_selection(Dg.numpy(), Bg, f, 5,
+                                    torch.sort(sg)[1].numpy(), True)
     # per key: the Gram path's worst relative distance error, the predicted
     # bound at that pair and the conditioning (Σ|x'|² / d², centred on the
     # medoid) of the worst-conditioned pair
@@ -192,6 +198,8 @@ def krum_c4(dev, n=50, f=10):
         'gram_GBps': nbytes / gmed / 1e6,
         'gram_max_rel_err_vs_fp64': grel,
         'gram_flagged_pairs': int((flags > 0).sum()),
+        'gram_max_rel_pair_bound': float((Bg / ref.numpy())[off.numpy()].max()),
+        'gram_selection5_certified': bool(certified),
         'gram_per_key': per_key,
         'gram_selection_exact': sel_gram == sel_ref,
         'kernel': 'fsagg_pairdist_f32', 'config': 'C4 Krum n=%d P=%d f=%d' %

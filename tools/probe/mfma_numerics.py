@@ -84,6 +84,14 @@ def raw_cases(fam, rng, nc):
         A[:, :, 0] = 2.0 ** -12
         t = rng.integers(1, 4, size=(nc, 16))
         B[:, 0, :] = t * 2.0 ** -12
+    elif fam.startswith('window'):      # 1 + 31 terms of ±1.99·2^-k
+        # window<k>[n]: the alignment window below the largest term
+        neg = fam.endswith('n')
+        k = int(fam[6:].rstrip('n'))
+        A[:, :, 0] = 1.0
+        B[:, 0, :] = 1.0
+        A[:, :, 1:] = 2.0 ** -12
+        B[:, 1:, :] = (-1.0 if neg else 1.0) * 1.9921875 * 2.0 ** (12 - k)
     elif fam == 'mixed_sign_same_mag':   # Σ of ±1·(1+m) terms, cancellation
         A[:] = rand_bf16(rng, A.shape, 0, 0)
         B[:] = rand_bf16(rng, B.shape, 0, 0)
@@ -142,7 +150,7 @@ def run_raw(L, fam, nc=256, seed=0):
     P = A.astype(np.float64)[:, :, None, :] * \
         B.astype(np.float64).transpose(0, 2, 1)[:, None, :, :]
     n_rne = n_rtz = n = 0
-    worst_ulp = worst_rel = 0.0
+    worst_ulp = worst_rel = worst_max = 0.0
     for c in range(nc):
         for i in range(16):
             for j in range(16):
@@ -157,7 +165,10 @@ def run_raw(L, fam, nc=256, seed=0):
                 tot = math.fsum(abs(x) for x in t)
                 if tot > 0:
                     worst_rel = max(worst_rel, e / (U * tot))
+                    worst_max = max(worst_max, e / (U * max(abs(x)
+                                                             for x in t)))
     return {'probe': 'raw', 'family': fam, 'outputs': n,
+            'max_err_over_u_max_abs_term': worst_max,
             'frac_equal_rne_of_exact': n_rne / n,
             'frac_equal_rtz_of_exact': n_rtz / n,
             'max_err_ulps_of_result': worst_ulp,
@@ -231,10 +242,17 @@ def run_kstep(L, fam, nc=256, seed=1):
 def main():
     L = lib()
     which = sys.argv[1:] or ['raw', 'kstep']
+    if 'window' in which:
+        which = ['raw', 'window']
     if 'raw' in which:
-        for fam in ('int', 'wide', 'one_plus_tiny', 'cancel', 'c_dominant',
-                    'ties', 'mixed_sign_same_mag'):
-            print(json.dumps(run_raw(L, fam)), flush=True)
+        fams = ['int', 'wide', 'one_plus_tiny', 'cancel', 'c_dominant',
+                'ties', 'mixed_sign_same_mag']
+        if 'window' in which:
+            fams = ['window%d%s' % (k, sg) for k in range(22, 33)
+                    for sg in ('', 'n')]
+        for fam in fams:
+            print(json.dumps(run_raw(L, fam, nc=16 if fam.startswith(
+                'window') else 256)), flush=True)
     if 'kstep' in which:
         for fam in ('gaussian', 'int8_grid', 'student_t3', 'offset',
                     'sparse', 'wide_exp', 'same_row'):
