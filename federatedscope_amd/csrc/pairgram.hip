@@ -28,20 +28,20 @@
 //   so (G'_aa + G'_bb) / d² stays O(1) for every pair near the centre.
 //   Every per-key d² leaves with a worst-case error bound err (limb
 //   products, the MFMA's rounding, fp64 sums, centring, underflow: see
-//   kCoefLimb below), and fsagg_pairgram_finish_f32 flags the pairs whose
-//   per-key distances that bound does not certify to the tolerance — a
-//   cluster far from the centre (near-duplicate or colluding clients), or a
-//   non-finite value; the caller recomputes those pairs exactly on the VALU
-//   kernel.
+//   kCoefLimb below); fsagg_pairgram_finish_f32 sums those into a bound B
+//   on every pair's D, which the caller certifies its Krum selection with
+//   (core/aggregators/_engine.certified_selection), recomputing D on the
+//   VALU kernel when the score gaps do not clear it.  Non-finite pairs are
+//   flagged and recomputed on the VALU kernel (its ±inf / NaN semantics).
 //
 // Work: a workgroup of 4 waves per chunk of one key; wave v takes the
-// chunk's k-steps v, v + 4, ...  A lane loads its 16-client tile rows
-// straight into MFMA fragment order (lane l: client 16t + (l & 15); fragment
-// slots 0-3 = coordinates 4(l>>4) .. +3 and slots 4-7 = 16 + 4(l>>4) .. +3
-// of the k-step — any permutation of k is a valid contraction as long as
-// both operands use it), so each load instruction reads 64 contiguous bytes
-// of 16 rows, every value is read from HBM once and nothing goes through
-// LDS on the way in.
+// chunk's k-steps v, v + 4, ...  The chunk's rows stream through LDS in
+// stages (global_load_lds_dwordx4, 512-B runs per row: see kGramStaged) and
+// are read back in MFMA fragment order (lane l: client 16t + (l & 15);
+// fragment slots 0-3 = coordinates 4(l>>4) .. +3 and slots 4-7 =
+// 16 + 4(l>>4) .. +3 of the k-step — any permutation of k is a valid
+// contraction as long as both operands use it); every value is read from
+// HBM once.
 #include "common.h"
 
 namespace fsagg {
@@ -63,8 +63,9 @@ constexpr int kMainChunks = 1024;         // ~2 rounds at 2 blocks per CU
 constexpr int64_t kMaxW = 16384;          // chunk length cap (LDS centre)
 constexpr int64_t kSampleCoords = 2048;   // per key, for the centre choice
 constexpr int64_t kSampleChunk = 512;
+constexpr int kL2 = 1024;                 // threads of the level-2 kernels
 
-// Worst-case error bound of a key's d²(a, b) (gram_segsq_kernel; DESIGN
+// Worst-case error bound of a key's d²(a, b) (segsq_pair; DESIGN
 // §3.3 derives each term).  u = 2^-24; S = sqrt(G'aa) + sqrt(G'bb), so
 // Σ_p |x'_a[p]·x'_b[p]| <= sqrt(G'aa·G'bb) and G'aa + G'bb + 2·sqrt(G'aa·G'bb)
 // = S² bound every Gram entry's magnitude sum (Cauchy-Schwarz):
@@ -354,26 +355,28 @@ __device__ __forceinline__ void finish_pair(int q, const double *segsq,
     }
   }
   D[q] = dist;
-  ill[q] = (!inf && bound <= tol * sum_d && dist < __builtin_inff()) ? 0u
-                                                                      : 1u;
+  // tol = +inf: only non-finite pairs are flagged (inf · 0 is NaN, so the
+  // relative test is skipped rather than evaluated)
+  const bool close = !(tol < __builtin_inf()) || bound <= tol * sum_d;
+  ill[q] = (!inf && close && dist < __builtin_inff()) ? 0u : 1u;
   // the bound on |D − the exact per-key distances' sum|, rounded up to fp32
   if (B) B[q] = inf ? __builtin_inff() : __double2float_ru(bound);
 }
 
 // The centre: argmin_a Σ_b sqrt(d²(a, b)) over a Gram matrix G (64 x 64 in
-// LDS; 256 threads; part: 4 x 64 doubles of LDS).
+// LDS; the first 256 threads; part: 4 x 64 doubles of LDS).
 __device__ void centre_of(const double *G, int n, int *centre,
                           double (*part)[64]) {
   const int a = threadIdx.x & 63, h = threadIdx.x >> 6;
   double sum = 0.0;
-  if (a < n) {
+  if (a < n && h < 4) {
     const double gaa = G[a * 64 + a];
     for (int b = h; b < n; b += 4) {
       const double d2 = gaa + G[b * 64 + b] - 2.0 * G[a * 64 + b];
       sum += d2 > 0.0 ? sqrt(d2) : 0.0;
     }
   }
-  part[h][a] = sum;
+  if (h < 4) part[h][a] = sum;
   __syncthreads();
   if (threadIdx.x == 0) {
     int best = 0;
@@ -689,56 +692,80 @@ __global__ __launch_bounds__(256) void gram_reduce1_kernel(
 }
 
 // Level 2 of groups [g0, g1) into a 64 x 64 Gram matrix in LDS (both
-// triangles of the tile pairs), groups summed in order.
+// triangles of the tile pairs), kL2 threads: thread quarter h sums groups
+// g0 + h, g0 + h + 4, ... in order, every tile pair's loads of U groups
+// issued together, and the four quarters are added in a fixed order (one
+// thread per element at a time made the group loop a chain of dependent HBM
+// round trips: 27 us for the key kernel at C4).  part: 4·NTP·256 doubles.
 template <int NT>
 __device__ void gram_level2(const double *__restrict__ red, int g0, int g1,
-                            double *G) {
+                            double *G, double *part) {
   constexpr int NTP = ntp_of(NT);
-  constexpr int U = 8;
-  const int e = threadIdx.x, r = e >> 6, lane = e & 63;
-  for (int p = 0; p < NTP; ++p) {
-    double sum = 0.0;
-    for (int b = g0; b < g1; b += U) {
-      double v[U];
+  constexpr int U = 4;
+  const int e = threadIdx.x & 255, h = threadIdx.x >> 8;
+  double sum[NTP];
 #pragma unroll
-      for (int j = 0; j < U; ++j)
-        v[j] = b + j < g1 ? red[(int64_t(b + j) * NTP + p) * 256 + e] : 0.0;
+  for (int p = 0; p < NTP; ++p) sum[p] = 0.0;
+  for (int b = g0 + h; b < g1; b += 4 * U) {
+    double v[U][NTP];
 #pragma unroll
-      for (int j = 0; j < U; ++j) sum += v[j];
+    for (int j = 0; j < U; ++j)
+#pragma unroll
+      for (int p = 0; p < NTP; ++p)
+        v[j][p] = b + 4 * j < g1
+                      ? red[(int64_t(b + 4 * j) * NTP + p) * 256 + e]
+                      : 0.0;
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+#pragma unroll
+      for (int p = 0; p < NTP; ++p) sum[p] += v[j][p];
+  }
+#pragma unroll
+  for (int p = 0; p < NTP; ++p) part[(h * NTP + p) * 256 + e] = sum[p];
+  __syncthreads();
+  if (h == 0) {
+    const int r = e >> 6, lane = e & 63;
+#pragma unroll
+    for (int p = 0; p < NTP; ++p) {
+      const double t4 = ((part[p * 256 + e] + part[(NTP + p) * 256 + e]) +
+                         part[(2 * NTP + p) * 256 + e]) +
+                        part[(3 * NTP + p) * 256 + e];
+      int t, u;
+      tp_tiles(p, NT, t, u);
+      const int a = 16 * t + 4 * (lane >> 4) + r, c = 16 * u + (lane & 15);
+      G[a * 64 + c] = t4;
+      if (t != u) G[c * 64 + a] = t4;
     }
-    int t, u;
-    tp_tiles(p, NT, t, u);
-    const int a = 16 * t + 4 * (lane >> 4) + r, c = 16 * u + (lane & 15);
-    G[a * 64 + c] = sum;
-    if (t != u) G[c * 64 + a] = sum;
   }
   __syncthreads();
 }
 
-// The sample pass's Gram (every group of every key) and the centre from it:
-// one workgroup.
+// The sample pass's Gram (its chunk partials, summed as level 2 sums
+// groups) and the centre from it: one workgroup of kL2 threads.
 template <int NT>
-__global__ __launch_bounds__(256) void gram_centre_kernel(
-    const double *__restrict__ red, GramCtl ctl, int nseg, int n,
+__global__ __launch_bounds__(kL2) void gram_centre_kernel(
+    const double *__restrict__ partial, GramCtl ctl, int nseg, int n,
     int *__restrict__ centre) {
-  __shared__ double G[64 * 64 + 4 * 64];
-  gram_level2<NT>(red, 0, ctl.gprefix[nseg], G);
-  centre_of(G, n, centre, reinterpret_cast<double(*)[64]>(G + 64 * 64));
+  __shared__ double G[64 * 64];
+  __shared__ double part[4 * ntp_of(NT) * 256];
+  gram_level2<NT>(partial, 0, ctl.prefix[nseg], G, part);
+  centre_of(G, n, centre, reinterpret_cast<double(*)[64]>(part));
 }
 
-// Per key (grid nseg): its groups into its Gram matrix, then every pair's d²
-// and worst-case bound (segsq_pair).
+// Per key (grid nseg, kL2 threads): its groups into its Gram matrix, then
+// every pair's d² and worst-case bound (segsq_pair).
 template <int NT>
-__global__ __launch_bounds__(256) void gram_key_kernel(
+__global__ __launch_bounds__(kL2) void gram_key_kernel(
     const double *__restrict__ red, GramCtl ctl, int n,
     const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
     double *__restrict__ segsq, double *__restrict__ err) {
   __shared__ double G[64 * 64];
+  __shared__ double part[4 * ntp_of(NT) * 256];
   const int s = blockIdx.x;
-  gram_level2<NT>(red, ctl.gprefix[s], ctl.gprefix[s + 1], G);
+  gram_level2<NT>(red, ctl.gprefix[s], ctl.gprefix[s + 1], G, part);
   const int64_t len = seg_end[s] - seg_lo[s];
   const int nn = n * n;
-  for (int i = threadIdx.x; i < nn; i += 256)
+  for (int i = threadIdx.x; i < nn; i += kL2)
     segsq_pair(G, i / n, i % n, len, segsq[int64_t(s) * nn + i],
                err[int64_t(s) * nn + i]);
 }
@@ -820,8 +847,8 @@ size_t gram_ws_layout(int n, int64_t numel, int nseg, void *ws, GramWs *w) {
   return off;
 }
 
-// Seven launches (eight with the finish): both plans; the sample pass, its
-// group sums and the centre; the centred main pass, its group sums, and per
+// Six launches (seven with the finish): both plans; the sample pass and the
+// centre from its chunk partials; the centred main pass, its group sums, and per
 // key the Gram matrix, every pair's d² and bound.
 template <int NT>
 void gram_launch(const float *const *tab, int64_t ss, int n,
@@ -839,11 +866,8 @@ void gram_launch(const float *const *tab, int64_t ss, int n,
                      tab, ss, n, seg_lo, seg_end, nseg, w.cs, kSampleChunk,
                      kSampleCoords, static_cast<const int *>(nullptr),
                      w.partial);
-  hipLaunchKernelGGL((gram_reduce1_kernel<NT>),
-                     dim3(unsigned(pl.sample_groups), unsigned(NTP)),
-                     dim3(256), 0, st, w.partial, w.cs, nseg, w.red);
-  hipLaunchKernelGGL((gram_centre_kernel<NT>), dim3(1), dim3(256), 0, st,
-                     w.red, w.cs, nseg, n, w.centre);
+  hipLaunchKernelGGL((gram_centre_kernel<NT>), dim3(1), dim3(kL2), 0, st,
+                     w.partial, w.cs, nseg, n, w.centre);
   // 2. the centred Gram of every key, its d² and bounds
   hipLaunchKernelGGL((gram_chunk_kernel<NT, true>),
                      dim3(unsigned(pl.main_chunks)), dim3(kBlk), 0, st, tab,
@@ -852,7 +876,7 @@ void gram_launch(const float *const *tab, int64_t ss, int n,
   hipLaunchKernelGGL((gram_reduce1_kernel<NT>),
                      dim3(unsigned(pl.main_groups), unsigned(NTP)),
                      dim3(256), 0, st, w.partial, w.cm, nseg, w.red);
-  hipLaunchKernelGGL((gram_key_kernel<NT>), dim3(unsigned(nseg)), dim3(256),
+  hipLaunchKernelGGL((gram_key_kernel<NT>), dim3(unsigned(nseg)), dim3(kL2),
                      0, st, w.red, w.cm, n, seg_lo, seg_end, segsq, err);
   if (D)
     hipLaunchKernelGGL(gram_finish_kernel,
