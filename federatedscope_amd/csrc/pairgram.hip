@@ -74,13 +74,16 @@ constexpr int kL2 = 1024;                 // threads of the level-2 kernels
 //   product error is the three dropped limb products ml, lm, ll:
 //   <= (2·2^-24 + 2^-32)·(1 + 2^-8)²·|x·y|            -> kCoefLimb · u · S²
 // * MFMA accumulation: v_mfma_f32_16x16x32_bf16 aligns its 32 exact
-//   products (and C) to the largest and drops what lies below a window of
-//   about 26 bits under it, then rounds once (tools/probe/mfma_numerics.py,
-//   profiles/r04/mfma_numerics.jsonl: 31 terms just under 2^-26 of the
-//   largest vanish whole; the worst error over every family probed is
-//   7.5·u·max|term|): error <= (32·2^-26/u + 1)·u·max|term| <= 9·u·Σ|terms|
-//   per MFMA; over the chain mm, hl, lh, hm, mh, hh those sums total
-//   <= 1.035·Σ|x·y|                              -> 1.035·kMfmaRound
+//   products and C to the largest and truncates what lies below a window
+//   of about 26 bits under its leading bit, then rounds once
+//   (tools/probe/mfma_numerics.py, profiles/r04/mfma_numerics.jsonl and
+//   mfma_window.jsonl: 31 same-sign terms below 2^-27 of the largest vanish
+//   whole; the worst error over every family probed is 7.5·u·Σ|terms|, and
+//   9.4·u·max|term| where the terms cancel): each of the 33 terms loses
+//   < 2^-26·max|term|, the rounding <= u·|result|, so the error is
+//   <= (33·2^-26/u)·u·max|term| + u·|result| <= 9.25·u·Σ|terms| per MFMA
+//   (bound used: 10); over the chain mm, hl, lh, hm, mh, hh those sums
+//   total <= 1.035·Σ|x·y|                        -> 1.035·kMfmaRound
 // * fp64: the K k-step sums, four waves and two reduction levels add
 //   <= (K + 1024) · 2^-53 relative                     -> (K + 1024)·2^-29
 // * centring x' = fl32(x − x_c) perturbs the rows by <= u·|x'|: d² moves by
@@ -89,7 +92,7 @@ constexpr int kL2 = 1024;                 // threads of the level-2 kernels
 //   <= 2^-126 · (12·sqrt(P)·S + 800·K) absolute
 constexpr double kU = 5.9604644775390625e-08;   // 2^-24
 constexpr double kCoefLimb = 2.02;
-constexpr double kMfmaRound = 9.0;
+constexpr double kMfmaRound = 10.0;
 constexpr double kMfmaChain = 1.035;
 constexpr double kTiny = 1.1754943508222875e-38;  // 2^-126
 
