@@ -132,7 +132,7 @@ SIGNATURES['fsagg_normbound_prescale_f32'] = (
     _c_i, [_c_p, _c_i, _c_i, ctypes.c_float, _c_p, _c_p])
 
 FSAGG_MAX_PEERS = 8
-FSAGG_PAIRGRAM_MAX_CLIENTS = 64
+FSAGG_PAIRGRAM_MAX_CLIENTS = 208
 _c_u32 = ctypes.c_uint32
 SIGNATURES['fsagg_peer_handle_bytes'] = (_c_sz, [])
 SIGNATURES['fsagg_peer_alloc'] = (_c_i, [_c_i, _c_sz, ctypes.POINTER(_c_p)])

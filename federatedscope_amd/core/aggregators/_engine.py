@@ -203,13 +203,13 @@ class DeviceEngine:
 
     def _pairdist(self, st):
         """Krum's distance matrix D (fp32 [n][n]) of a client set, as a
-        pending result whose ``.cpu()`` waits for it.  Up to 64 clients: on
+        pending result whose ``.cpu()`` waits for it.  Up to 208 clients: on
         the matrix cores (fsagg_pairgram_*: the Gram of the rows centred on a
         central client, fp32 split exactly into bf16 limbs), every pair with
         a worst-case bound on its error (``last_pair_bound``, host fp64
         [n][n]) that the callers certify their selection with
         (:meth:`_certified_order`); non-finite pairs are recomputed on the
-        VALU kernel.  Above 64 clients: the VALU kernel (direct differences,
+        VALU kernel.  Above 208 clients: the VALU kernel (direct differences,
         ``last_pair_bound`` None)."""
         from ... import _lib
         self.last_pair_bound = None

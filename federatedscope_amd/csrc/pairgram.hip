@@ -53,7 +53,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int kGramMaxTiles = 4;          // n <= 64
+constexpr int kGramMaxTiles = 13;         // n <= 208
+constexpr int kFullTiles = 4;             // one workgroup forms every pair
 constexpr int kKStep = 32;                // coordinates per MFMA k-step
 constexpr int kWaves = 4;                 // waves per workgroup (chunk)
 constexpr int kBlk = kWaves * kWave;
@@ -63,7 +64,7 @@ constexpr int kMainChunks = 1024;         // ~2 rounds at 2 blocks per CU
 constexpr int64_t kMaxW = 16384;          // chunk length cap (LDS centre)
 constexpr int64_t kSampleCoords = 2048;   // per key, for the centre choice
 constexpr int64_t kSampleChunk = 512;
-constexpr int kL2 = 1024;                 // threads of the level-2 kernels
+constexpr int kLineBlocks = 8192;         // n > 64: ~workgroups per pass
 
 // Worst-case error bound of a key's d²(a, b) (segsq_pair; DESIGN
 // §3.3 derives each term).  u = 2^-24; S = sqrt(G'aa) + sqrt(G'bb), so
@@ -244,6 +245,28 @@ __device__ __forceinline__ void kstep_split(const float (&xb)[NT][8],
   kstep_split_c<NT, CENTRED>(xb, cb, k, f);
 }
 
+// n > 64 (T > 4 tiles of 16 clients): every workgroup forms every pair of
+// its NT tiles, and the tile sets are the lines of a finite projective
+// plane, which hold every pair of points exactly once — PG(2, 3): 13 points,
+// 13 lines of 4 (T <= 13, the difference set {0, 1, 3, 9} mod 13); PG(2, 2)
+// (Fano): 7 points, 7 lines of 3 (T <= 7, {0, 1, 3} mod 7).  Each tile is
+// loaded and split 4 (3) times per chunk, not once per super-tile pair; a
+// point's diagonal block is stored by the line it generates.  Points >= T
+// are absent (their rows clamp to the last client, their pairs are not
+// stored).  Lines sorted, so t < u within a line maps to tile t < tile u.
+__constant__ int8_t kPlane13[13][4] = {
+    {0, 1, 3, 9},  {1, 2, 4, 10}, {2, 3, 5, 11}, {3, 4, 6, 12}, {0, 4, 5, 7},
+    {1, 5, 6, 8},  {2, 6, 7, 9},  {3, 7, 8, 10}, {4, 8, 9, 11}, {5, 9, 10, 12},
+    {0, 6, 10, 11}, {1, 7, 11, 12}, {0, 2, 8, 12}};
+__constant__ int8_t kPlane7[7][3] = {{0, 1, 3}, {1, 2, 4}, {2, 3, 5},
+                                     {3, 4, 6}, {0, 4, 5}, {1, 5, 6},
+                                     {0, 2, 6}};
+
+// index of tile pair (t, u), t <= u, among the T(T+1)/2 (tp_tiles' order)
+__device__ __forceinline__ int pair_index(int t, int u, int T) {
+  return t * T - (t * (t - 1)) / 2 + (u - t);
+}
+
 // per tile pair: the six limb products in fp32 (the small ones first, so
 // their roundings happen at their own magnitude), then into fp64
 template <int NT>
@@ -265,15 +288,6 @@ __device__ __forceinline__ void kstep_mfma(const Frags<NT> &f,
   }
 }
 
-template <int NT, bool CENTRED>
-__device__ __forceinline__ void kstep(const float (&xb)[NT][8],
-                                      const float *cs, const Neg &k,
-                                      double (&acc)[ntp_of(NT)][4]) {
-  Frags<NT> f;
-  kstep_split<NT, CENTRED>(xb, cs, k, f);
-  kstep_mfma<NT>(f, acc);
-}
-
 // 16-B loads of one full k-step: slots 0-3 at a, 4-7 at a + 16
 __device__ __forceinline__ void ld8(const float *a, float (&v)[8]) {
   const f32x4 x = gld_nt(reinterpret_cast<const f32x4 *>(a));
@@ -292,19 +306,18 @@ __device__ __forceinline__ void ld8_tail(const float *row, int64_t k0,
   }
 }
 
-// d²(a, b) of one key from its Gram matrix g (64 x 64, both triangles) and
-// its worst-case error bound (the terms at kCoefLimb); +inf when d² came out
+// d²(a, b) of one key from its Gram entries G'aa, G'bb, G'ab and its
+// worst-case error bound (the terms at kCoefLimb); +inf when d² came out
 // negative beyond that bound or is not finite (the pair is recomputed).
-__device__ __forceinline__ void segsq_pair(const double *g, int a, int b,
-                                           int64_t len, double &d2o,
-                                           double &eo) {
-  if (a == b) {
+__device__ __forceinline__ void segsq_pair(double gaa, double gbb, double gab,
+                                           bool same, int64_t len,
+                                           double &d2o, double &eo) {
+  if (same) {
     d2o = 0.0;
     eo = 0.0;
     return;
   }
-  const double gaa = g[a * 64 + a], gbb = g[b * 64 + b];
-  const double d2 = gaa + gbb - 2.0 * g[a * 64 + b];
+  const double d2 = gaa + gbb - 2.0 * gab;
   const double K = double((len + kKStep - 1) / kKStep);
   // S from the computed diagonal, inflated for its own error (the relative
   // bound below is < 1e-5 of it)
@@ -366,35 +379,6 @@ __device__ __forceinline__ void finish_pair(int q, const double *segsq,
   if (B) B[q] = inf ? __builtin_inff() : __double2float_ru(bound);
 }
 
-// The centre: argmin_a Σ_b sqrt(d²(a, b)) over a Gram matrix G (64 x 64 in
-// LDS; the first 256 threads; part: 4 x 64 doubles of LDS).
-__device__ void centre_of(const double *G, int n, int *centre,
-                          double (*part)[64]) {
-  const int a = threadIdx.x & 63, h = threadIdx.x >> 6;
-  double sum = 0.0;
-  if (a < n && h < 4) {
-    const double gaa = G[a * 64 + a];
-    for (int b = h; b < n; b += 4) {
-      const double d2 = gaa + G[b * 64 + b] - 2.0 * G[a * 64 + b];
-      sum += d2 > 0.0 ? sqrt(d2) : 0.0;
-    }
-  }
-  if (h < 4) part[h][a] = sum;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int best = 0;
-    double bv = 0.0;
-    for (int b = 0; b < n; ++b) {
-      const double v = ((part[0][b] + part[1][b]) + part[2][b]) + part[3][b];
-      if (b == 0 || v < bv) {
-        bv = v;
-        best = b;
-      }
-    }
-    *centre = best;
-  }
-}
-
 // Staged loads (kGramStaged): the chunk streams through LDS in stages of
 // kStage coordinates.  Each stage holds every row's kStage·4 = 512 B — the
 // 16·NT tile rows, then the centre's — written by global_load_lds_dwordx4
@@ -443,26 +427,43 @@ __device__ __forceinline__ void stage_read8(const char *buf, int rr, int ks,
   v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
 }
 
-// One workgroup (4 waves) per chunk.  partial[chunk][tp][reg][lane] (fp64):
-// the chunk's (centred) Gram blocks in MFMA C-layout (row 4(lane>>4) + reg
-// of tile t, column lane & 15 of tile u).  !CENTRED: raw values (sample).
-// The rows stream through LDS stages (kGramStaged, above; wave v takes
-// k-step v of every stage); without it each wave loads its own k-steps
-// straight into registers and the centre's values of the chunk are staged
-// in LDS once.
-template <int NT, bool CENTRED>
+// One workgroup (4 waves) per chunk (n <= 64: its NT tiles are all the
+// tiles) or per chunk and plane line (LINES, n > 64).  partial[chunk][tp]
+// [reg][lane] (fp64, tp over the T(T+1)/2 tile pairs): the chunk's
+// (centred) Gram blocks in MFMA C-layout (row 4(lane>>4) + reg of tile t,
+// column lane & 15 of tile u).  !CENTRED: raw values (sample).  The rows
+// stream through LDS stages (kGramStaged, above; wave v takes k-step v of
+// every stage); without it each wave loads its own k-steps straight into
+// registers and the centre's values of the chunk are staged in LDS once.
+// LINES: block b takes chunk 8·(k / lines) + b % 8 and line k % lines
+// (k = b / 8): blocks b and b + 8 share an XCD, so one chunk's workgroups
+// run on one XCD together and read its rows from that XCD's L2 after the
+// first.
+template <int NT, bool CENTRED, bool LINES>
 __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
-    const float *const *__restrict__ tab, int64_t ss, int n,
+    const float *const *__restrict__ tab, int64_t ss, int n, int T,
     const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
     int nseg, GramCtl ctl, int64_t w, int64_t cap,
     const int *__restrict__ centre, double *__restrict__ partial) {
+  static_assert(!LINES || NT == 3 || NT == 4, "plane lines hold 3 or 4");
   constexpr int NTP = ntp_of(NT);
+  constexpr int kLines = NT == 4 ? 13 : 7;
   const int *__restrict__ prefix = ctl.prefix;
   __shared__ __attribute__((aligned(1024))) char smem[chunk_smem<NT, CENTRED>()];
   double(*red)[NTP * 4][kWave] =
       reinterpret_cast<double(*)[NTP * 4][kWave]>(smem);
   float *cs = reinterpret_cast<float *>(smem);
-  const int chunk = blockIdx.x;
+  int chunk = blockIdx.x, line = 0;
+  if constexpr (LINES) {
+    const int k = int(blockIdx.x >> 3);
+    chunk = (k / kLines) * 8 + int(blockIdx.x & 7);
+    line = k % kLines;
+  }
+  // global tile of local tile lt
+  auto gtile = [&](int lt) {
+    return LINES ? int(NT == 4 ? kPlane13[line][lt] : kPlane7[line][lt])
+                 : lt;
+  };
   if (chunk >= prefix[nseg]) return;   // whole workgroup
   int s = 0;
   while (prefix[s + 1] <= chunk) ++s;
@@ -480,7 +481,7 @@ __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
   const float *row[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const int j = 16 * t + (lane & 15);
+    const int j = 16 * gtile(t) + (lane & 15);
     row[t] = rows[j < n ? j : n - 1];
   }
   const float *crow = CENTRED ? rows[*centre] : nullptr;
@@ -516,7 +517,8 @@ __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
 #pragma unroll
       for (int m = 0; m < MY; ++m) {
         const int rr = 2 * (wv + kWaves * m) + (lane >> 5);
-        const float *rp = rr < NR ? rows[rr < n ? rr : n - 1]
+        const int cr = 16 * gtile(rr >> 4) + (rr & 15);
+        const float *rp = rr < NR ? rows[cr < n ? cr : n - 1]
                                   : (CENTRED && rr == NR ? crow
                                                          : rows[n - 1]);
         src[m] = rp + c0 + 4 * ((lane & 31) ^ (rr & 15));
@@ -660,23 +662,29 @@ __global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
   }
   __syncthreads();
   if (wv == 0) {
-    double *out = partial + int64_t(chunk) * NTP * 256;
+    const int ntpg = T * (T + 1) / 2;
+    double *out = partial + int64_t(chunk) * ntpg * 256;
 #pragma unroll
     for (int p = 0; p < NTP; ++p) {
+      int t, u;
+      tp_tiles(p, NT, t, u);
+      const int gt = gtile(t), gu = gtile(u);
+      // absent points; a diagonal block belongs to the line its point
+      // generates (every point lies on NT lines)
+      if (LINES && (gu >= T || (gt == gu && gt != line))) continue;
+      double *o = out + int64_t(LINES ? pair_index(gt, gu, T) : p) * 256;
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        out[(p * 4 + r) * 64 + lane] = acc[p][r] + red[0][p * 4 + r][lane];
+        o[r * 64 + lane] = acc[p][r] + red[0][p * 4 + r][lane];
     }
   }
 }
 
-// Level 1, grid (groups, NTP): group b (of key s) sums its <= kRed chunks
+// Level 1, grid (groups, ntpg): group b (of key s) sums its <= kRed chunks
 // in order into red[b][p][256].
-template <int NT>
 __global__ __launch_bounds__(256) void gram_reduce1_kernel(
-    const double *__restrict__ partial, GramCtl ctl, int nseg,
+    const double *__restrict__ partial, GramCtl ctl, int nseg, int ntpg,
     double *__restrict__ red) {
-  constexpr int NTP = ntp_of(NT);
   const int b = blockIdx.x, p = blockIdx.y, e = threadIdx.x;
   if (b >= ctl.gprefix[nseg]) return;
   int s = 0;
@@ -686,91 +694,130 @@ __global__ __launch_bounds__(256) void gram_reduce1_kernel(
   double v[kRed];
 #pragma unroll
   for (int q = 0; q < kRed; ++q)
-    v[q] = q0 + q < q1 ? partial[((int64_t(q0) + q) * NTP + p) * 256 + e]
+    v[q] = q0 + q < q1 ? partial[((int64_t(q0) + q) * ntpg + p) * 256 + e]
                        : 0.0;
   double sum = 0.0;
 #pragma unroll
   for (int q = 0; q < kRed; ++q) sum += v[q];
-  red[(int64_t(b) * NTP + p) * 256 + e] = sum;
+  red[(int64_t(b) * ntpg + p) * 256 + e] = sum;
 }
 
-// Level 2 of groups [g0, g1) into a 64 x 64 Gram matrix in LDS (both
-// triangles of the tile pairs), kL2 threads: thread quarter h sums groups
-// g0 + h, g0 + h + 4, ... in order, every tile pair's loads of U groups
-// issued together, and the four quarters are added in a fixed order (one
-// thread per element at a time made the group loop a chain of dependent HBM
-// round trips: 27 us for the key kernel at C4).  part: 4·NTP·256 doubles.
-template <int NT>
-__device__ void gram_level2(const double *__restrict__ red, int g0, int g1,
-                            double *G, double *part) {
-  constexpr int NTP = ntp_of(NT);
-  constexpr int U = 4;
-  const int e = threadIdx.x & 255, h = threadIdx.x >> 8;
-  double sum[NTP];
+// Σ over items [g0, g1) of entry e of tile pair p (items = groups or chunks,
+// laid out [item][ntpg][256]), in order; eight loads in flight.
+__device__ __forceinline__ double sum_items(const double *__restrict__ v,
+                                            int g0, int g1, int ntpg, int p,
+                                            int e) {
+  double s = 0.0;
+  for (int b = g0; b < g1; b += 8) {
+    double x[8];
 #pragma unroll
-  for (int p = 0; p < NTP; ++p) sum[p] = 0.0;
-  for (int b = g0 + h; b < g1; b += 4 * U) {
-    double v[U][NTP];
+    for (int j = 0; j < 8; ++j)
+      x[j] = b + j < g1 ? v[(int64_t(b + j) * ntpg + p) * 256 + e] : 0.0;
 #pragma unroll
-    for (int j = 0; j < U; ++j)
-#pragma unroll
-      for (int p = 0; p < NTP; ++p)
-        v[j][p] = b + 4 * j < g1
-                      ? red[(int64_t(b + 4 * j) * NTP + p) * 256 + e]
-                      : 0.0;
-#pragma unroll
-    for (int j = 0; j < U; ++j)
-#pragma unroll
-      for (int p = 0; p < NTP; ++p) sum[p] += v[j][p];
+    for (int j = 0; j < 8; ++j) s += x[j];
   }
-#pragma unroll
-  for (int p = 0; p < NTP; ++p) part[(h * NTP + p) * 256 + e] = sum[p];
-  __syncthreads();
-  if (h == 0) {
-    const int r = e >> 6, lane = e & 63;
-#pragma unroll
-    for (int p = 0; p < NTP; ++p) {
-      const double t4 = ((part[p * 256 + e] + part[(NTP + p) * 256 + e]) +
-                         part[(2 * NTP + p) * 256 + e]) +
-                        part[(3 * NTP + p) * 256 + e];
-      int t, u;
-      tp_tiles(p, NT, t, u);
-      const int a = 16 * t + 4 * (lane >> 4) + r, c = 16 * u + (lane & 15);
-      G[a * 64 + c] = t4;
-      if (t != u) G[c * 64 + a] = t4;
-    }
+  return s;
+}
+
+// C-layout entry of diagonal element i of a tile (row = column = i)
+__device__ __forceinline__ int diag_entry(int i) {
+  return (i & 3) * 64 + 16 * (i >> 2) + i;
+}
+
+// One tile pair (t, u) of one Gram matrix from items [g0, g1): thread e's
+// entry G'[16t + ia][16u + ib] into gab, and the two tiles' diagonals into
+// dg[0..15] (tile t) and dg[16..31] (tile u), each summed as the (t, t) and
+// (u, u) blocks sum them.
+__device__ __forceinline__ double pair_block(const double *__restrict__ v,
+                                             int g0, int g1, int T, int p,
+                                             int t, int u, double *dg) {
+  const int e = threadIdx.x, ntpg = T * (T + 1) / 2;
+  const double gab = sum_items(v, g0, g1, ntpg, p, e);
+  if (e < 32) {
+    const int tt = e < 16 ? t : u;
+    dg[e] = sum_items(v, g0, g1, ntpg, pair_index(tt, tt, T),
+                      diag_entry(e & 15));
   }
   __syncthreads();
+  return gab;
 }
 
-// The sample pass's Gram (its chunk partials, summed as level 2 sums
-// groups) and the centre from it: one workgroup of kL2 threads.
-template <int NT>
-__global__ __launch_bounds__(kL2) void gram_centre_kernel(
-    const double *__restrict__ partial, GramCtl ctl, int nseg, int n,
-    int *__restrict__ centre) {
-  __shared__ double G[64 * 64];
-  __shared__ double part[4 * ntp_of(NT) * 256];
-  gram_level2<NT>(partial, 0, ctl.prefix[nseg], G, part);
-  centre_of(G, n, centre, reinterpret_cast<double(*)[64]>(part));
+// The sample pass's Gram (every key's sample chunks, in order), per tile
+// pair (grid ntpg): the distances of its 256 entries, their sums along each
+// row (the rows of tile t) and each column (the rows of tile u) into
+// rsum[p][32].
+__global__ __launch_bounds__(256) void gram_centre_pairs_kernel(
+    const double *__restrict__ partial, GramCtl ctl, int nseg, int n, int T,
+    double *__restrict__ rsum) {
+  __shared__ double dg[32];
+  __shared__ double dd[16][17];
+  const int p = blockIdx.x, e = threadIdx.x;
+  int t, u;
+  tp_tiles(p, T, t, u);
+  const double gab = pair_block(partial, 0, ctl.prefix[nseg], T, p, t, u, dg);
+  const int l = e & 63, r = e >> 6, ia = 4 * (l >> 4) + r, ib = l & 15;
+  double d = 0.0;
+  if (16 * t + ia < n && 16 * u + ib < n) {
+    const double d2 = dg[ia] + dg[16 + ib] - 2.0 * gab;
+    d = d2 > 0.0 ? sqrt(d2) : 0.0;
+  }
+  dd[ia][ib] = d;
+  __syncthreads();
+  if (e < 32) {
+    double sum = 0.0;
+    for (int j = 0; j < 16; ++j) sum += e < 16 ? dd[e][j] : dd[j][e - 16];
+    rsum[p * 32 + e] = sum;
+  }
 }
 
-// Per key (grid nseg, kL2 threads): its groups into its Gram matrix, then
-// every pair's d² and worst-case bound (segsq_pair).
-template <int NT>
-__global__ __launch_bounds__(kL2) void gram_key_kernel(
-    const double *__restrict__ red, GramCtl ctl, int n,
+// The centre: argmin_a Σ_b d(a, b) from the tile pairs' row sums (one
+// workgroup; n <= 256), tiles summed in order, the first minimum wins.
+__global__ __launch_bounds__(256) void gram_centre_pick_kernel(
+    const double *__restrict__ rsum, int n, int T, int *__restrict__ centre) {
+  __shared__ double tot[256];
+  const int a = threadIdx.x;
+  double sum = 0.0;
+  if (a < n) {
+    const int t = a >> 4, i = a & 15;
+    for (int u = 0; u < T; ++u)
+      sum += t <= u ? rsum[pair_index(t, u, T) * 32 + i]
+                    : rsum[pair_index(u, t, T) * 32 + 16 + i];
+  }
+  tot[a] = sum;
+  __syncthreads();
+  if (a == 0) {
+    int best = 0;
+    for (int b = 1; b < n; ++b)
+      if (tot[b] < tot[best]) best = b;
+    *centre = best;
+  }
+}
+
+// Per key and tile pair (grid nseg x ntpg): the pair's Gram block summed
+// over the key's groups, then every entry's d² and worst-case bound
+// (segsq_pair), stored at (a, b) and (b, a) — a diagonal block keeps its
+// a <= b entries, so D is exactly symmetric.
+__global__ __launch_bounds__(256) void gram_key_kernel(
+    const double *__restrict__ red, GramCtl ctl, int n, int T,
     const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
     double *__restrict__ segsq, double *__restrict__ err) {
-  __shared__ double G[64 * 64];
-  __shared__ double part[4 * ntp_of(NT) * 256];
-  const int s = blockIdx.x;
-  gram_level2<NT>(red, ctl.gprefix[s], ctl.gprefix[s + 1], G, part);
-  const int64_t len = seg_end[s] - seg_lo[s];
-  const int nn = n * n;
-  for (int i = threadIdx.x; i < nn; i += kL2)
-    segsq_pair(G, i / n, i % n, len, segsq[int64_t(s) * nn + i],
-               err[int64_t(s) * nn + i]);
+  __shared__ double dg[32];
+  const int s = blockIdx.x, p = blockIdx.y, e = threadIdx.x;
+  int t, u;
+  tp_tiles(p, T, t, u);
+  const double gab = pair_block(red, ctl.gprefix[s], ctl.gprefix[s + 1], T,
+                                p, t, u, dg);
+  const int l = e & 63, r = e >> 6, ia = 4 * (l >> 4) + r, ib = l & 15;
+  const int a = 16 * t + ia, b = 16 * u + ib;
+  if (a >= n || b >= n || (t == u && ia > ib)) return;
+  double d2, er;
+  segsq_pair(dg[ia], dg[16 + ib], gab, a == b, seg_end[s] - seg_lo[s], d2,
+             er);
+  const int64_t o = int64_t(s) * n * n;
+  segsq[o + int64_t(a) * n + b] = d2;
+  err[o + int64_t(a) * n + b] = er;
+  segsq[o + int64_t(b) * n + a] = d2;
+  err[o + int64_t(b) * n + a] = er;
 }
 
 // The finish of a sharded call, after the ranks' d² and bounds were summed
@@ -784,18 +831,28 @@ __global__ __launch_bounds__(256) void gram_finish_kernel(
 }
 
 struct GramPlan {
-  int nt;
+  int nt;              // tiles of 16 clients
+  bool lines;          // nt > kFullTiles: one workgroup per plane line
+  int nlines;          // 13 (PG(2,3)) or 7 (Fano)
+  int ntpg;            // tile pairs
   int64_t w;           // main chunk length (multiple of kUnit)
   int main_chunks;     // upper bounds
   int sample_chunks;
   int main_groups;
-  int sample_groups;
 };
 
 GramPlan gram_plan(int n, int64_t numel, int nseg) {
   GramPlan pl;
   pl.nt = (n + 15) / 16;
-  int64_t w = (numel + kMainChunks - 1) / kMainChunks;
+  pl.lines = pl.nt > kFullTiles;
+  pl.nlines = pl.lines ? (pl.nt <= 7 ? 7 : 13) : 1;
+  pl.ntpg = ntp_of(pl.nt);
+  // ~kMainChunks workgroups; LINES: ~kLineBlocks over all the lines
+  // (fewer, longer chunks: less partial traffic)
+  const int64_t target =
+      pl.lines ? (kLineBlocks / pl.nlines > 64 ? kLineBlocks / pl.nlines : 64)
+               : kMainChunks;
+  int64_t w = (numel + target - 1) / target;
   w = (w + kUnit - 1) / kUnit * kUnit;
   if (w < kUnit) w = kUnit;
   if (w > kMaxW) w = kMaxW;
@@ -804,25 +861,29 @@ GramPlan gram_plan(int n, int64_t numel, int nseg) {
   pl.main_groups = pl.main_chunks / kRed + nseg + 1;
   const int per_key = int((kSampleCoords + kSampleChunk - 1) / kSampleChunk);
   pl.sample_chunks = nseg * per_key;
-  pl.sample_groups = nseg * ((per_key + kRed - 1) / kRed);
   return pl;
+}
+
+// chunk-kernel grid: one workgroup per chunk, or per chunk and plane line
+// with the chunks rounded up to the 8 XCDs (LINES)
+unsigned chunk_grid(const GramPlan &pl, int chunks) {
+  return pl.lines ? unsigned((chunks + 7) / 8 * 8 * pl.nlines)
+                  : unsigned(chunks);
 }
 
 struct GramWs {
   GramCtl cs, cm;          // sample and main pass plans
   int *centre;
-  double *partial, *red;
+  double *partial, *red, *rsum;
 };
 
 size_t gram_ws_layout(int n, int64_t numel, int nseg, void *ws, GramWs *w) {
   const GramPlan pl = gram_plan(n, numel, nseg);
-  const size_t ntp = size_t(ntp_of(pl.nt));
+  const size_t ntp = size_t(pl.ntpg);
   const size_t chunks = size_t(pl.main_chunks > pl.sample_chunks
                                    ? pl.main_chunks
                                    : pl.sample_chunks);
-  const size_t groups = size_t(pl.main_groups > pl.sample_groups
-                                   ? pl.main_groups
-                                   : pl.sample_groups);
+  const size_t groups = size_t(pl.main_groups);
   size_t off = 0;
   auto take = [&](size_t bytes) {
     const size_t o = off;
@@ -838,49 +899,55 @@ size_t gram_ws_layout(int n, int64_t numel, int nseg, void *ws, GramWs *w) {
   };
   const GramCtl cs = ctl(), cm = ctl();
   char *p_c = take(256),
+       *p_rs = take(sizeof(double) * ntp * 32),
        *p_red = take(sizeof(double) * groups * ntp * 256),
        *p_part = take(sizeof(double) * chunks * ntp * 256);
   if (w) {
     w->cs = cs;
     w->cm = cm;
     w->centre = reinterpret_cast<int *>(p_c);
+    w->rsum = reinterpret_cast<double *>(p_rs);
     w->red = reinterpret_cast<double *>(p_red);
     w->partial = reinterpret_cast<double *>(p_part);
   }
   return off;
 }
 
-// Six launches (seven with the finish): both plans; the sample pass and the
-// centre from its chunk partials; the centred main pass, its group sums, and per
-// key the Gram matrix, every pair's d² and bound.
-template <int NT>
+// Seven launches (eight with the finish): both plans; the sample pass, the
+// tile pairs' distance sums and the centre; the centred main pass, its group
+// sums, and per key and tile pair the Gram block, d² and bounds.
+template <int NT, bool LINES>
 void gram_launch(const float *const *tab, int64_t ss, int n,
                  const int64_t *seg_lo, const int64_t *seg_end, int nseg,
                  const GramPlan &pl, const GramWs &w, double *segsq,
                  double *err, double tol, float *D, uint32_t *ill, float *B,
                  hipStream_t st) {
-  constexpr int NTP = ntp_of(NT);
+  const int T = pl.nt;
   hipLaunchKernelGGL(gram_prefix_kernel, dim3(1), dim3(1), 0, st, seg_lo,
                      seg_end, nseg, kSampleChunk, kSampleCoords, pl.w, w.cs,
                      w.cm);
   // 1. the centre: Gram of the first kSampleCoords of every key, raw
-  hipLaunchKernelGGL((gram_chunk_kernel<NT, false>),
-                     dim3(unsigned(pl.sample_chunks)), dim3(kBlk), 0, st,
-                     tab, ss, n, seg_lo, seg_end, nseg, w.cs, kSampleChunk,
-                     kSampleCoords, static_cast<const int *>(nullptr),
-                     w.partial);
-  hipLaunchKernelGGL((gram_centre_kernel<NT>), dim3(1), dim3(kL2), 0, st,
-                     w.partial, w.cs, nseg, n, w.centre);
+  hipLaunchKernelGGL((gram_chunk_kernel<NT, false, LINES>),
+                     dim3(chunk_grid(pl, pl.sample_chunks)), dim3(kBlk), 0,
+                     st, tab, ss, n, T, seg_lo, seg_end, nseg, w.cs,
+                     kSampleChunk, kSampleCoords,
+                     static_cast<const int *>(nullptr), w.partial);
+  hipLaunchKernelGGL(gram_centre_pairs_kernel, dim3(unsigned(pl.ntpg)),
+                     dim3(256), 0, st, w.partial, w.cs, nseg, n, T, w.rsum);
+  hipLaunchKernelGGL(gram_centre_pick_kernel, dim3(1), dim3(256), 0, st,
+                     w.rsum, n, T, w.centre);
   // 2. the centred Gram of every key, its d² and bounds
-  hipLaunchKernelGGL((gram_chunk_kernel<NT, true>),
-                     dim3(unsigned(pl.main_chunks)), dim3(kBlk), 0, st, tab,
-                     ss, n, seg_lo, seg_end, nseg, w.cm, pl.w, int64_t(0),
-                     static_cast<const int *>(w.centre), w.partial);
-  hipLaunchKernelGGL((gram_reduce1_kernel<NT>),
-                     dim3(unsigned(pl.main_groups), unsigned(NTP)),
-                     dim3(256), 0, st, w.partial, w.cm, nseg, w.red);
-  hipLaunchKernelGGL((gram_key_kernel<NT>), dim3(unsigned(nseg)), dim3(kL2),
-                     0, st, w.red, w.cm, n, seg_lo, seg_end, segsq, err);
+  hipLaunchKernelGGL((gram_chunk_kernel<NT, true, LINES>),
+                     dim3(chunk_grid(pl, pl.main_chunks)), dim3(kBlk), 0, st,
+                     tab, ss, n, T, seg_lo, seg_end, nseg, w.cm, pl.w,
+                     int64_t(0), static_cast<const int *>(w.centre),
+                     w.partial);
+  hipLaunchKernelGGL(gram_reduce1_kernel,
+                     dim3(unsigned(pl.main_groups), unsigned(pl.ntpg)),
+                     dim3(256), 0, st, w.partial, w.cm, nseg, pl.ntpg, w.red);
+  hipLaunchKernelGGL(gram_key_kernel,
+                     dim3(unsigned(nseg), unsigned(pl.ntpg)), dim3(256), 0,
+                     st, w.red, w.cm, n, T, seg_lo, seg_end, segsq, err);
   if (D)
     hipLaunchKernelGGL(gram_finish_kernel,
                        dim3(unsigned((int64_t(n) * n + 255) / 256)),
@@ -924,14 +991,26 @@ int pairgram_rows(const char *what, const fsagg_rows *rows,
   gram_ws_layout(n, numel, nseg, workspace, &w);
   hipStream_t st = as_stream(stream);
   switch (pl.nt) {
-    case 1: gram_launch<1>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg, pl,
-                           w, segsq, err, tol, D, ill, B, st); break;
-    case 2: gram_launch<2>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg, pl,
-                           w, segsq, err, tol, D, ill, B, st); break;
-    case 3: gram_launch<3>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg, pl,
-                           w, segsq, err, tol, D, ill, B, st); break;
-    default: gram_launch<4>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg, pl,
-                            w, segsq, err, tol, D, ill, B, st); break;
+    case 1: gram_launch<1, false>(rows->tab, rows->ss, n, seg_lo, seg_end,
+                                  nseg, pl, w, segsq, err, tol, D, ill, B,
+                                  st); break;
+    case 2: gram_launch<2, false>(rows->tab, rows->ss, n, seg_lo, seg_end,
+                                  nseg, pl, w, segsq, err, tol, D, ill, B,
+                                  st); break;
+    case 3: gram_launch<3, false>(rows->tab, rows->ss, n, seg_lo, seg_end,
+                                  nseg, pl, w, segsq, err, tol, D, ill, B,
+                                  st); break;
+    case 4: gram_launch<4, false>(rows->tab, rows->ss, n, seg_lo, seg_end,
+                                  nseg, pl, w, segsq, err, tol, D, ill, B,
+                                  st); break;
+    default:
+      if (pl.nlines == 7)
+        gram_launch<3, true>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg,
+                             pl, w, segsq, err, tol, D, ill, B, st);
+      else
+        gram_launch<4, true>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg,
+                             pl, w, segsq, err, tol, D, ill, B, st);
+      break;
   }
   return check_launch(what);
 }

@@ -1025,7 +1025,7 @@ def pairdist_rows_segsq(rs, lo=0, hi=None, workspace=None, keep=None,
 
 
 def pairgram_rows_segsq(rs, lo=0, hi=None, workspace=None, keep=None):
-    """As :func:`pairdist_rows_segsq`, on the matrix cores (n <= 64,
+    """As :func:`pairdist_rows_segsq`, on the matrix cores (n <= 208,
     fsagg_pairgram_rows_segsq_f32): returns ``[2][nseg][n][n]`` fp64 —
     [0] the per-key squared distances, [1] their predicted absolute error
     bounds (both may be summed over ranks); :func:`pairgram_finish` turns

@@ -451,7 +451,7 @@ int fsagg_pairdist_rows_segsq_f32(const fsagg_rows *rows,
                                   size_t workspace_bytes,
                                   fsagg_stream_t stream);
 
-/* Krum per-key squared distances on the matrix cores (n <= 64; segsq as
+/* Krum per-key squared distances on the matrix cores (n <= 208; segsq as
  * fsagg_pairdist_rows_segsq_f32).  d²(a, b) = G_aa + G_bb − 2·G_ab from a
  * Gram matrix of the rows centred on a central client (the argmin of the
  * summed distances over the first 2048 coordinates of every key), every
@@ -467,9 +467,13 @@ int fsagg_pairdist_rows_segsq_f32(const fsagg_rows *rows,
  * valid.  Replaces the same torch.dist loop (krum_aggregator.py:41-73) as
  * fsagg_pairdist_f32, with fsagg_pairgram_finish_f32 in place of
  * fsagg_pairdist_finish_f64.  The rows stream through LDS in 512-B runs
- * per row (global_load_lds), whatever their placement.  Workspace:
+ * per row (global_load_lds), whatever their placement.  Up to 64 clients
+ * one workgroup per chunk forms every 16x16 tile pair; above, the tiles
+ * form super tiles of two and one workgroup per chunk and super-tile pair
+ * forms the pairs across (XCD-grouped, so a chunk's rows are read from
+ * HBM once and from L2 after).  Workspace:
  * fsagg_pairgram_workspace_bytes(n, numel, nseg) (0 when n is outside
- * 2..64). */
+ * 2..208). */
 size_t fsagg_pairgram_workspace_bytes(int n, int64_t numel, int nseg);
 int fsagg_pairgram_rows_segsq_f32(const fsagg_rows *rows,
                                   const int64_t *seg_lo,

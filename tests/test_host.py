@@ -473,3 +473,31 @@ def test_fedopt_keeps_its_config():
     agg = FedOptAggregator(config=cfg, model=torch.nn.Linear(2, 2))
     assert agg.opt_kwargs == {'momentum': 0.9}
     assert agg.momentum == 0.9
+
+
+# -- row-set chunk plan (layout.plan_row_chunks) ------------------------------
+@pytest.mark.parametrize('unit', [1024, 4096, 16384, 24576])
+def test_plan_row_chunks_covers_keys(unit):
+    """Every key span is cut into whole-tile pieces from its start (the last
+    one shorter) that tile it exactly and never straddle a key."""
+    import json
+    import os
+    import numpy as np
+    from federatedscope_amd.layout import plan_row_chunks
+    from federatedscope_amd.ops import CHUNK_DTYPE
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, 'tools', 'resnet50_layout.json')) as f:
+        keys = [tuple(s) for _, s in json.load(f)['keys']]
+    spans, off = [], 0
+    for i, s in enumerate(keys):
+        m = int(np.prod(s))
+        spans.append((i, off, off + m))
+        off = (off + m + 63) // 64 * 64
+    arr = plan_row_chunks(spans, unit, CHUNK_DTYPE)
+    assert arr['len'].max() <= unit and arr['len'].min() >= 1
+    for s, a, b in spans:
+        sel = arr[arr['seg'] == s]
+        assert sel['lo'][0] == a and sel['lo'][-1] + sel['len'][-1] == b
+        assert np.all(sel['lo'][1:] == sel['lo'][:-1] + sel['len'][:-1])
+        assert np.all(sel['len'][:-1] == unit)
+    assert plan_row_chunks([], unit, CHUNK_DTYPE).size == 0

@@ -356,6 +356,14 @@ def main():
         print(json.dumps(krum_c4(dev)), flush=True)
         log('krum done in %.1fs' % (time.time() - t0))
         torch.cuda.empty_cache()
+    if 'krum_large' in which:
+        # n > 64: the Gram path's super-tile pairs, C4's layout and byte
+        # count per client
+        for n in (100, 200):
+            t0 = time.time()
+            print(json.dumps(krum_c4(dev, n=n, f=n // 5)), flush=True)
+            log('krum n=%d done in %.1fs' % (n, time.time() - t0))
+            torch.cuda.empty_cache()
     if 'orderstat' in which:
         for r in orderstat_c5(dev):
             print(json.dumps(r), flush=True)
