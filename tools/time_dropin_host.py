@@ -1,8 +1,12 @@
 #!/usr/bin/env python3
 """Host-side phases of the drop-in ClientsAvgAggregator.aggregate() on
-device-resident ConvNet2-h2048 dicts (200 clients): each phase wrapped with
-perf_counter (no device synchronisation inside), mean microseconds per call,
-plus the call's return time and its synchronised wall time.  GPU only."""
+device-resident ConvNet2-h2048 dicts (200 clients), or with --layout
+resnet50 the configs[2] layout B dicts (100 clients, 161 keys, views of one
+slab row per client, as bench.py's plugin_surface_layout_b): each phase
+wrapped with perf_counter (no device synchronisation inside), mean
+microseconds per call, plus the call's return time and its synchronised
+wall time.  GPU only."""
+import argparse
 import functools
 import json
 import os
@@ -41,6 +45,10 @@ def main():
     from federatedscope_amd import ops
     from federatedscope_amd.core.aggregators import ClientsAvgAggregator
     from federatedscope_amd.core.aggregators import _engine
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--layout', default='convnet2',
+                    choices=['convnet2', 'resnet50'])
+    args = ap.parse_args()
     dev = torch.device('cuda', 0)
     g = torch.Generator(device=dev).manual_seed(7)
     cfg = SimpleNamespace(
@@ -48,9 +56,22 @@ def main():
                                  client_num=1000, sample_client_rate=1.0),
         aggregator=SimpleNamespace(byzantine_node_num=0, BFT_args=None))
     agg = ClientsAvgAggregator(device=dev, config=cfg)
-    fb = [(1 + i, OrderedDict((k, torch.randn(s, device=dev, generator=g))
-                              for k, s in CONVNET2_H2048))
-          for i in range(200)]
+    if args.layout == 'convnet2':
+        fb = [(1 + i, OrderedDict((k, torch.randn(s, device=dev,
+                                                  generator=g))
+                                  for k, s in CONVNET2_H2048))
+              for i in range(200)]
+    else:
+        from federatedscope_amd.layout import BucketLayout
+        with open(os.path.join(ROOT, 'tools', 'resnet50_layout.json')) as f:
+            keys = [(k, tuple(s)) for k, s in json.load(f)['keys']]
+        lay = BucketLayout(OrderedDict((k, torch.empty(s, device='meta'))
+                                       for k, s in keys))
+        slab = torch.randn((100, ops.round_up(lay.numel, 64)), device=dev,
+                           generator=g)
+        fb = [(1 + i, OrderedDict(
+            (k, slab[i, lay.offsets[k]:lay.offsets[k] + lay.numels[k]].view(
+                lay.shapes[k])) for k in lay.keys)) for i in range(100)]
     info = {'client_feedback': fb, 'recover_fun': None}
     for _ in range(3):
         agg.aggregate(info)
