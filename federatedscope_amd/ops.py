@@ -20,9 +20,14 @@ class _PinnedRing:
     (row pointers, weights, chunk lists): NSLOT slots of SLOT bytes, used
     round robin; a slot is refilled only after the copy that last read it
     has run (its event).  torch's pin_memory() per table cost ~10-20 µs of
-    host time per upload in the drop-in path."""
-    SLOT = 1 << 16
-    NSLOT = 64
+    host time per upload in the drop-in path, and a fresh pinned allocation
+    waits for the device: with 64-KiB slots the 129-KB key table of 100
+    clients x 161 keys (the ResNet-50 layout) took that path, and every
+    aggregate() then waited for the previous call's kernel before launching
+    its own (a 33 µs gap between back-to-back calls, profiles/r04).  Slots
+    of 1 MiB hold the key table of up to ~800 clients of that layout."""
+    SLOT = 1 << 20
+    NSLOT = 32
 
     def __init__(self):
         self.buf = None

@@ -12,4 +12,7 @@ bash tools/gpu_job.sh \
   "timeout -k 10 200 python -u tools/probe_layout_b.py --plan short_first >> gpurun_out/layout_b.jsonl" \
   "timeout -k 10 200 python -u tools/probe_layout_b.py >> gpurun_out/layout_b.jsonl" \
   "timeout -k 10 200 python -u tools/time_dropin_host.py --layout resnet50 > gpurun_out/host_lb.json" \
-  "timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_lb -o run --output-format csv -- python tools/probe_layout_b.py --rounds 2"
+  "timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_lb -o run --output-format csv -- python tools/probe_layout_b.py --rounds 2" || exit $?
+bash tools/pmc.sh krum r04 > gpurun_out/pmc_krum.log 2>&1 || exit 1
+bash tools/pmc.sh orderstat r04 > gpurun_out/pmc_os.log 2>&1 || exit 1
+bash tools/gpu_job.sh "timeout -k 10 300 python -u tools/bench_robust.py dropin > gpurun_out/dropin.jsonl"
