@@ -357,7 +357,7 @@ def main():
         log('krum done in %.1fs' % (time.time() - t0))
         torch.cuda.empty_cache()
     if 'krum_large' in which:
-        # n > 64: the Gram path's super-tile pairs, C4's layout and byte
+        # n > 64: the Gram path on projective-plane lines, C4's layout and byte
         # count per client
         for n in (100, 200):
             t0 = time.time()
