@@ -24,11 +24,12 @@ KEY_ALIGN = 16  # elements
 def plan_row_chunks(spans, unit, dtype):
     """The chunk list of key spans [(seg, lo, hi)]: pieces of exactly
     ``unit`` coordinates (a whole tile of the row-set kernel) from each
-    key's start, its last piece shorter, in key order.  (Balanced pieces —
-    equal lengths per key, short keys first — measured slower at the
-    ResNet-50 layout: 1.612 against 1.534 ms, since nearly every piece then
-    takes the kernel's guarded partial-tile path; tools/probe_layout_b.py,
-    profiles/r04/layout_b.jsonl.)"""
+    key's start, its last piece shorter, in key order.  Measured and not
+    kept at the ResNet-50 layout (tools/probe_layout_b.py, profiles/r04/):
+    balanced equal pieces (slower: nearly every piece then takes the
+    kernel's guarded partial-tile path), short pieces first (no change) and
+    longest first (2.5 % slower than key order, whose row-set kernel runs
+    at the flat kernel's time on that box)."""
     import numpy as np
     parts = []
     for s, a, b in spans:

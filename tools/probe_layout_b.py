@@ -35,21 +35,7 @@ def main():
     ap.add_argument('--clients', type=int, default=100)
     ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--calls', type=int, default=10)
-    ap.add_argument('--plan', default='product',
-                    choices=['product', 'short_first'],
-                    help="row-set chunk plan: the product's (whole-unit "
-                         "pieces in key order) or 'short_first' (the same "
-                         "pieces, every key's short last piece first)")
     args = ap.parse_args()
-    if args.plan == 'short_first':
-        from federatedscope_amd import layout as _layout
-        _cut = _layout.plan_row_chunks
-
-        def short_first(spans, unit, dtype):
-            arr = _cut(spans, unit, dtype)
-            short = arr['len'] < unit
-            return np.concatenate([arr[short], arr[~short]])
-        _layout.plan_row_chunks = short_first
     from federatedscope_amd import ops
     from federatedscope_amd.core.aggregators import ClientsAvgAggregator
     from federatedscope_amd.layout import BucketLayout
@@ -105,8 +91,7 @@ def main():
             torch.cuda.synchronize()
             ts[k].append((time.perf_counter() - t0) / args.calls * 1e3)
     med = {k: statistics.median(v) for k, v in ts.items()}
-    rec = {'plan': args.plan, 'keys': len(keys), 'params': P,
-           'clients': n}
+    rec = {'keys': len(keys), 'params': P, 'clients': n}
     rec.update({k + '_ms': round(v, 4) for k, v in med.items()})
     rec.update({k + '_over_flat': round(v / med['flat'], 4)
                 for k, v in med.items() if k != 'flat'})

@@ -1,17 +1,10 @@
 #!/bin/bash
-# Layout B A/B on one box: the row-set kernel with short keys' clients
-# loaded eight at a time (product) against the previous form
-# (tools/probe/nb), interleaved.
+# Layout B: kernel trace of the probe (gaps between back-to-back
+# aggregate() calls) and the host phases of aggregate().
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-NB=tools/probe/nb/libfsagg.so
 bash tools/gpu_job.sh \
-  "timeout -k 10 200 python -u tools/probe_layout_b.py > gpurun_out/lb_ab.jsonl" \
-  "FSAGG_LIB=$NB timeout -k 10 200 python -u tools/probe_layout_b.py >> gpurun_out/lb_ab.jsonl" \
-  "timeout -k 10 200 python -u tools/probe_layout_b.py >> gpurun_out/lb_ab.jsonl" \
-  "FSAGG_LIB=$NB timeout -k 10 200 python -u tools/probe_layout_b.py >> gpurun_out/lb_ab.jsonl" \
-  "timeout -k 10 200 python -u tools/probe_layout_b.py >> gpurun_out/lb_ab.jsonl" \
-  "FSAGG_LIB=$NB timeout -k 10 200 python -u tools/probe_layout_b.py >> gpurun_out/lb_ab.jsonl" || exit $?
-bash tools/r04_final.sh
+  "timeout -k 10 200 python -u tools/time_dropin_host.py --layout resnet50 > gpurun_out/host_lb.json" \
+  "timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_lb -o run --output-format csv -- python tools/probe_layout_b.py --rounds 2"
