@@ -33,9 +33,25 @@ class _PinnedRing:
         self.buf = None
         self.events = [None] * self.NSLOT
         self.i = 0
+        self.streams = {}
+
+    def _copy_stream(self, device):
+        s = self.streams.get(device.index)
+        if s is None:
+            s = self.streams[device.index] = torch.cuda.Stream(device=device)
+        return s
 
     def upload(self, arr, device):
-        """numpy array -> device tensor of its dtype and shape (async)."""
+        """numpy array -> device tensor of its dtype and shape (async).
+
+        The copy runs on a side stream of the device and the caller's
+        stream waits for it: enqueued on the caller's stream, a table's
+        copy sat behind the previous call's kernel and held back the next
+        launch by its own latency (~34 µs between back-to-back aggregate()
+        calls at the ResNet-50 layout).  The device tensor is allocated on
+        the side stream and marked used by the caller's stream, so the
+        allocator never hands its block to a copy while a kernel may still
+        read it."""
         import numpy as np
         arr = np.ascontiguousarray(arr)
         raw = arr.reshape(-1).view(np.uint8)
@@ -55,11 +71,16 @@ class _PinnedRing:
             ev.synchronize()            # the copy that last read slot k
         lo = k * self.SLOT
         self.np[lo:lo + nb] = raw
-        dev = torch.empty(nb, dtype=torch.uint8, device=device)
-        dev.copy_(self.buf[lo:lo + nb], non_blocking=True)
         if ev is None:
             ev = self.events[k] = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(device))
+        cur = torch.cuda.current_stream(device)
+        side = self._copy_stream(device)
+        with torch.cuda.stream(side):
+            dev = torch.empty(nb, dtype=torch.uint8, device=device)
+            dev.copy_(self.buf[lo:lo + nb], non_blocking=True)
+            ev.record(side)
+        dev.record_stream(cur)
+        cur.wait_event(ev)
         return dev.view(_TORCH_OF[arr.dtype.str]).reshape(arr.shape)
 
 

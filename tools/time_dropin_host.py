@@ -48,6 +48,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--layout', default='convnet2',
                     choices=['convnet2', 'resnet50'])
+    ap.add_argument('--pipelined', action='store_true',
+                    help='back-to-back calls without synchronising: a '
+                         'phase that waits for the GPU shows the wait')
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
     g = torch.Generator(device=dev).manual_seed(7)
@@ -84,15 +87,21 @@ def main():
     wrap(ops, 'absent', 'absent')
     wrap(ops, 'weighted_sum_rows', 'weighted_sum_rows')
     wrap(_engine, 'fedavg_weights', 'fedavg_weights')
+    wrap(ops._PinnedRing, 'upload', 'pinned ring upload')
+    wrap(ops.RowSet, 'from_virtual', 'RowSet.from_virtual')
+    wrap(ops, '_fp32_dev', '_fp32_dev')
+    wrap(_engine.DeviceEngine, '_staged_rows', 'staged_rows')
     reps = 20
     ret = 0.0
     wall = 0.0
     for _ in range(reps):
-        torch.cuda.synchronize()
+        if not args.pipelined:
+            torch.cuda.synchronize()
         t0 = time.perf_counter()
         agg.aggregate(info)
         t1 = time.perf_counter()
-        torch.cuda.synchronize()
+        if not args.pipelined:
+            torch.cuda.synchronize()
         t2 = time.perf_counter()
         ret += t1 - t0
         wall += t2 - t0
