@@ -343,20 +343,47 @@ __device__ __forceinline__ void wsum_rows_chunk(
 #pragma unroll
     for (int v = 0; v < V; ++v) acc[v] = f4{0.0f, 0.0f, 0.0f, 0.0f};
   }
-  for (int i = i0 + 1; i < n; ++i) {
-    const float *row = rows[i];
-    if (row == nullptr) continue;
+  // the other clients two at a time, the next one's loads in flight while
+  // the current one is added (ping-pong buffers, V <= 16; an absent client
+  // loads and adds nothing).  One client in flight measured 0.8–1.1 % slower at
+  // the ResNet-50 layout (tools/probe_layout_b.py): the row
+  // pointer and buffer descriptor of each client are scalar work the
+  // wave otherwise waits behind.
+  auto load = [&](f4 (&x)[V], int c) {
+    const float *row = rows[c];
+    if (row == nullptr) return;
     const __amdgpu_buffer_rsrc_t r = row_rsrc(row + lo, cbytes);
-    f4 x[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) x[v] = ld4_rowv<GUARD>(r, loff, v);
-    const float wi = w[i];
-    const float s = PRE ? pre[i] : 1.0f;
+  };
+  auto add = [&](const f4 (&x)[V], int c) {
+    if (rows[c] == nullptr) return;
+    const float wc = w[c];
+    const float sc = PRE ? pre[c] : 1.0f;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       f4 t = x[v];
-      if (PRE) t = mul4(t, s);
-      acc[v] = add4(acc[v], mul4(t, wi));
+      if (PRE) t = mul4(t, sc);
+      acc[v] = add4(acc[v], mul4(t, wc));
+    }
+  };
+  if constexpr (V <= 16) {
+    f4 xa[V], xb[V];
+    int i = i0 + 1;
+    if (i < n) load(xa, i);
+    for (; i + 1 < n; i += 2) {
+      load(xb, i + 1);
+      add(xa, i);
+      if (i + 2 < n) load(xa, i + 2);
+      add(xb, i + 1);
+    }
+    if (i < n) add(xa, i);
+  } else {
+    // V = 24: two buffers would not fit 256 VGPRs
+    for (int i = i0 + 1; i < n; ++i) {
+      f4 x[V];
+      load(x, i);
+      add(x, i);
     }
   }
   f4 *o = reinterpret_cast<f4 *>(out + lo);

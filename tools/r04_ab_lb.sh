@@ -1,12 +1,12 @@
 #!/bin/bash
-# Host-table uploads on a side stream: every GPU test, the layout-B probe,
-# its kernel trace, and the bench line (plugin surfaces).
+# Row-set weighted sum with two clients' loads in flight: row-set and
+# golden parity, the layout-B probe, the bench line.
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-bash tools/gpu_job.sh pytestall \
+bash tools/gpu_job.sh \
+  "timeout -k 10 300 python -u -m pytest tests/test_gpu_rows.py tests/test_gpu_golden.py tests/test_gpu_server.py tests/test_gpu_world2.py -q --timeout 200 --timeout-method thread > gpurun_out/rows.log 2>&1" \
   "timeout -k 10 200 python -u tools/probe_layout_b.py > gpurun_out/layout_b.jsonl" \
   "timeout -k 10 200 python -u tools/probe_layout_b.py >> gpurun_out/layout_b.jsonl" \
-  "timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_lb -o run --output-format csv -- python tools/probe_layout_b.py --rounds 2" \
   bench
