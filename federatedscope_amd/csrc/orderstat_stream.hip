@@ -163,6 +163,31 @@ __device__ __forceinline__ void stream_column(const float *const *rows, int n,
   }
 }
 
+// stream_column from the last row down: the pass after a forward pass
+// starts on the rows that pass read last, which the XCD's L2 may still hold
+template <int U, typename F>
+__device__ __forceinline__ void stream_column_rev(const float *const *rows,
+                                                  int n, uint32_t off,
+                                                  F &&f) {
+  int j = n;
+#pragma unroll 1
+  for (; j - U >= 0; j -= U) {
+    uint32_t u[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) u[i] = col_at(rows, j - 1 - i, off);
+#pragma unroll
+    for (int i = 0; i < U; ++i) f(u[i]);
+  }
+  if (j > 0) {
+    uint32_t u[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) u[i] = col_at(rows, max(j - 1 - i, 0), off);
+#pragma unroll
+    for (int i = 0; i < U; ++i)
+      if (j - 1 - i >= 0) f(u[i]);
+  }
+}
+
 template <int MODE, int U>
 __global__ __launch_bounds__(kBlock) void orderstat_stream_kernel(
     RowSrc rs, int n, int kk, float divisor, float *__restrict__ out) {
@@ -238,7 +263,8 @@ __global__ __launch_bounds__(kBlock) void orderstat_stream_kernel(
     shared = same_bin(s1, s2);
   }
 
-  // 4. compaction: the listed bins' values in row order (at most kList)
+  // 4. compaction: the listed bins' values (at most kList), the rows read
+  // last first (stream_column_rev; the list is sorted afterwards)
   const bool list1 = !resolved(s1);
   const bool list2 = !shared && !resolved(s2);
   double mid = 0.0;
@@ -250,7 +276,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_stream_kernel(
       const uint32_t lo = list1 ? s1.lo : s2.lo;
       const uint32_t w =
           (list1 || list2) ? (list2 ? s2.hi : s1.hi) - lo + 1u : 0u;
-      stream_column<U>(rows, n, off, [&](uint32_t u) {
+      stream_column_rev<U>(rows, n, off, [&](uint32_t u) {
         *lds_at(hb | (uint32_t(c) << 8)) = u;  // a miss: overwritten
         c = add_below(c, ukey(u) - lo, w);
       });
@@ -259,7 +285,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_stream_kernel(
       const uint32_t w1 = list1 ? s1.hi - s1.lo + 1u : 0u;
       const uint32_t wm = shared ? 0u : s2.lo - (s1.hi + 1u);
       const uint32_t wb = w1 + wm + (list2 ? s2.hi - s2.lo + 1u : 0u);
-      stream_column<U>(rows, n, off, [&](uint32_t u) {
+      stream_column_rev<U>(rows, n, off, [&](uint32_t u) {
         const uint32_t rel = ukey(u) - A;
         const bool inm = rel - w1 < wm;
         float x = inm ? __uint_as_float(u) : 0.0f;
