@@ -259,3 +259,38 @@ def test_dropin_device_dicts_read_in_place():
         {'client_feedback': host, 'recover_fun': None})
     for k in want:
         assert torch.equal(got[k].cpu(), want[k]), k
+
+
+def test_back_to_back_aggregates_without_sync():
+    """Twenty aggregate() calls issued back to back with no host
+    synchronisation, alternating two multi-key layouts and client sets of
+    different sizes (so the row tables, weights and chunk lists the pinned
+    ring copies on its side stream differ every call and their device
+    blocks are freed and reused while earlier kernels may still run): every
+    result equals the same call made alone, bit for bit."""
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    layouts = [[(513, 3), (7, ), (70_001, ), (64, 64)],
+               [(5, ), (1000, 33), (4096, ), (3, 3, 3)]]
+    sets = []
+    g = torch.Generator(device='cuda').manual_seed(77)
+    for j in range(4):
+        shapes = layouts[j % 2]
+        n = 9 + 7 * j
+        sets.append([(1 + (5 * i + j) % 17, OrderedDict(
+            ('w%d' % k, torch.randn(s, device='cuda', generator=g))
+            for k, s in enumerate(shapes))) for i in range(n)])
+    agg = ClientsAvgAggregator(device='cuda', config=_cfg())
+    want = []
+    for fb in sets:
+        r = agg.aggregate({'client_feedback': fb, 'recover_fun': None})
+        torch.cuda.synchronize()
+        want.append({k: v.clone() for k, v in r.items()})
+    got = []
+    torch.cuda.synchronize()
+    for c in range(20):
+        got.append(agg.aggregate({'client_feedback': sets[c % 4],
+                                  'recover_fun': None}))
+    torch.cuda.synchronize()
+    for c, r in enumerate(got):
+        for k, v in want[c % 4].items():
+            assert torch.equal(r[k], v), (c, k)

@@ -1,8 +1,8 @@
 #!/bin/bash
-# Host phases of Krum's distance matrix + certified selection at C4.
+# Row-set tests incl. back-to-back aggregate() calls without host sync.
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 bash tools/gpu_job.sh \
-  "timeout -k 10 200 python -u tools/time_krum_host.py > gpurun_out/krum_host.json"
+  "timeout -k 10 300 python -u -m pytest tests/test_gpu_rows.py -q --timeout 200 --timeout-method thread > gpurun_out/rows.log 2>&1"
