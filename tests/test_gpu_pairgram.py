@@ -152,11 +152,13 @@ def _separated(s, m, ordered, n):
                for i in gaps)
 
 
-@pytest.mark.parametrize('n', [2, 5, 16, 17, 33, 50, 64, 65, 80, 100, 129,
-                               200, 208])
+@pytest.mark.parametrize('n', [2, 5, 16, 17, 33, 50, 64, 65, 80, 100, 112,
+                               120, 129, 200, 208])
 def test_pairgram_vs_fp64_and_valu(n):
-    """n <= 64: one workgroup forms every tile pair; n > 64: super-tile pairs
-    (odd and even tile counts, a last tile of 1 client at 65 and 129)."""
+    """n <= 64: one workgroup forms every tile pair; n > 64: the lines of a
+    projective plane — Fano for 5..7 tiles (65, 80, 100, 112: every point
+    present), PG(2, 3) for 8..13 tiles (120: 5 points absent; 129; 200;
+    208: all 13) — with a last tile of 1 client at 65 and 129."""
     from federatedscope_amd import ops
     clients = _clients(n, seed=n)
     lay, _, keyed, stacked = _sets(clients)
