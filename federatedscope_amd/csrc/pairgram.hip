@@ -111,33 +111,55 @@ struct GramCtl {
   int *gprefix;     // [nseg + 1]
 };
 
+// One wave: lane l takes keys l, l + 64, ...; the chunk and group counts
+// are prefix-summed across the wave (one 64-bit division per lane instead
+// of nseg in a row: 6.1 us for both plans from one thread at C4).
 __device__ void plan_pass(const int64_t *__restrict__ seg_lo,
                           const int64_t *__restrict__ seg_end, int nseg,
                           int64_t w, int64_t cap, const GramCtl &c) {
-  int acc = 0, gacc = 0;
-  c.prefix[0] = 0;
-  c.gprefix[0] = 0;
-  for (int s = 0; s < nseg; ++s) {
-    int64_t len = seg_end[s] - seg_lo[s];
-    if (cap > 0 && len > cap) len = cap;
-    if (len < 0) len = 0;
-    const int k = int((len + w - 1) / w);
-    acc += k;
-    gacc += (k + kRed - 1) / kRed;
-    c.prefix[s + 1] = acc;
-    c.gprefix[s + 1] = gacc;
+  const int lane = int(threadIdx.x) & (kWave - 1);
+  if (lane == 0) {
+    c.prefix[0] = 0;
+    c.gprefix[0] = 0;
+  }
+  int base = 0, gbase = 0;
+  for (int s0 = 0; s0 < nseg; s0 += kWave) {
+    const int s = s0 + lane;
+    int k = 0, g = 0;
+    if (s < nseg) {
+      int64_t len = seg_end[s] - seg_lo[s];
+      if (cap > 0 && len > cap) len = cap;
+      if (len < 0) len = 0;
+      k = int((len + w - 1) / w);
+      g = (k + kRed - 1) / kRed;
+    }
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const int kk = __shfl_up(k, d, kWave), gg = __shfl_up(g, d, kWave);
+      if (lane >= d) {
+        k += kk;
+        g += gg;
+      }
+    }
+    if (s < nseg) {
+      c.prefix[s + 1] = base + k;
+      c.gprefix[s + 1] = gbase + g;
+    }
+    base += __shfl(k, kWave - 1, kWave);
+    gbase += __shfl(g, kWave - 1, kWave);
   }
 }
 
-// Both passes' plans in one launch.
-__global__ void gram_prefix_kernel(const int64_t *__restrict__ seg_lo,
-                                   const int64_t *__restrict__ seg_end,
-                                   int nseg, int64_t w_sample,
-                                   int64_t cap_sample, int64_t w_main,
-                                   GramCtl cs, GramCtl cm) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  plan_pass(seg_lo, seg_end, nseg, w_sample, cap_sample, cs);
-  plan_pass(seg_lo, seg_end, nseg, w_main, 0, cm);
+// Both passes' plans in one launch: wave 0 the sample pass, wave 1 the
+// main pass.
+__global__ __launch_bounds__(2 * kWave) void gram_prefix_kernel(
+    const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
+    int nseg, int64_t w_sample, int64_t cap_sample, int64_t w_main,
+    GramCtl cs, GramCtl cm) {
+  if (threadIdx.x < kWave)
+    plan_pass(seg_lo, seg_end, nseg, w_sample, cap_sample, cs);
+  else
+    plan_pass(seg_lo, seg_end, nseg, w_main, 0, cm);
 }
 
 __device__ __forceinline__ void tp_tiles(int tp, int nt, int &t, int &u) {
@@ -923,9 +945,9 @@ void gram_launch(const float *const *tab, int64_t ss, int n,
                  double *err, double tol, float *D, uint32_t *ill, float *B,
                  hipStream_t st) {
   const int T = pl.nt;
-  hipLaunchKernelGGL(gram_prefix_kernel, dim3(1), dim3(1), 0, st, seg_lo,
-                     seg_end, nseg, kSampleChunk, kSampleCoords, pl.w, w.cs,
-                     w.cm);
+  hipLaunchKernelGGL(gram_prefix_kernel, dim3(1), dim3(2 * kWave), 0, st,
+                     seg_lo, seg_end, nseg, kSampleChunk, kSampleCoords, pl.w,
+                     w.cs, w.cm);
   // 1. the centre: Gram of the first kSampleCoords of every key, raw
   hipLaunchKernelGGL((gram_chunk_kernel<NT, false, LINES>),
                      dim3(chunk_grid(pl, pl.sample_chunks)), dim3(kBlk), 0,
