@@ -58,6 +58,11 @@ def main():
     wrap(ops, 'pairgram_rows_dist', 'pairgram_rows_dist (launches)')
     wrap(_engine._PendingD, 'cpu', 'pending.cpu (wait + copy)')
     wrap(_engine, 'certified_selection', 'certified_selection')
+    wrap(_engine.DeviceEngine, '_key_table', 'key_table (C++ walk)')
+    wrap(ops.RowSet, 'from_virtual', 'RowSet.from_virtual')
+    wrap(ops._PinnedRing, 'upload', 'pinned ring upload')
+    wrap(ops, 'absent', 'absent')
+    wrap(_engine.DeviceEngine, '_staged_rows', 'staged_rows')
     reps = 50
     walls, gpus = [], []
     # the selection too (krum_scores + the certificate), as aggregate()
