@@ -36,6 +36,11 @@ def main():
     pinned = ring.buf[:arr.nbytes]
     d0 = torch.empty(arr.nbytes, dtype=torch.uint8, device=dev)
     ev = torch.cuda.Event()
+
+    def ctx():
+        with torch.cuda.stream(side):
+            pass
+
     res = {
         'upload (whole)': t(lambda: ring.upload(arr, dev)),
         'ops._h2d_np': t(lambda: ops._h2d_np(arr, dev)),
@@ -45,9 +50,7 @@ def main():
             lambda: ring.np.__setitem__(slice(0, arr.nbytes),
                                         arr.view(np.uint8))),
         'torch.cuda.current_stream': t(lambda: torch.cuda.current_stream(dev)),
-        'with torch.cuda.stream(side)': t(
-            lambda: torch.cuda.stream(side).__enter__() or
-            torch.cuda.stream(side).__exit__(None, None, None)),
+        'with torch.cuda.stream(side)': t(ctx),
         'torch.empty (device)': t(
             lambda: torch.empty(arr.nbytes, dtype=torch.uint8, device=dev)),
         'copy_ pinned->device non_blocking': t(
