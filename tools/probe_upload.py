@@ -2,6 +2,7 @@
 """Host cost of one pinned-ring upload (ops._PinnedRing.upload), statement
 by statement: the same calls timed in isolation over many repetitions of a
 4.8-KB table (Krum's row table at C4).  GPU only."""
+import ctypes
 import json
 import os
 import sys
@@ -41,7 +42,21 @@ def main():
         with torch.cuda.stream(side):
             pass
 
+    hip = ctypes.CDLL('libamdhip64.so')
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_size_t, ctypes.c_int,
+                                   ctypes.c_void_p]
+    hip.hipMemcpyAsync.restype = ctypes.c_int
+    dst, src, nb = d0.data_ptr(), pinned.data_ptr(), arr.nbytes
+    sh = side.cuda_stream
+
+    def raw():
+        # hipMemcpyHostToDevice = 1; the copy a native ring would issue
+        rc = hip.hipMemcpyAsync(dst, src, nb, 1, sh)
+        assert rc == 0, rc
+
     res = {
+        'hipMemcpyAsync via ctypes (side stream)': t(raw),
         'upload (whole)': t(lambda: ring.upload(arr, dev)),
         'ops._h2d_np': t(lambda: ops._h2d_np(arr, dev)),
         'np.ascontiguousarray + view': t(
