@@ -6,12 +6,15 @@ BASELINE.json — 100 clients x 25,000,000 fp32 parameters, synthetic updates
 already resident in HBM — whose FULL result ends up on every GPU.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py
---gpus N ...) is STRONG scaling of that fixed model: the parameter range is
-cut into ``chunks`` rounds of N block-cyclic pieces (core/sharding.py
-PipelinedAssembly), rank r holds piece (j, r) of every client and runs the
-full client loop over it (bit-identical to one GPU: no arithmetic crosses
-GPUs), and round j's pieces are all-gathered in place over RCCL/xGMI while
-round j+1 computes.  value = 4·n·P bytes / max-over-ranks step time.
+--gpus N ..., or a bare ``bench.py --gpus N``, which starts its own N rank
+processes) is STRONG scaling of that fixed model: rank r owns parameter
+range r of every client and runs the full client loop over it
+(bit-identical to one GPU: no arithmetic crosses GPUs).  By default (RCCL
+group) the reducing kernel stores each output tile into every GPU's copy
+over xGMI, then a flag barrier (core/sharding.py PeerAssembly); the
+fallback cuts the range into ``chunks`` rounds of N block-cyclic pieces
+whose all-gathers overlap the next round (PipelinedAssembly).
+value = 4·n·P bytes / max-over-ranks step time.
 Secondary fields: the same sharded compute with the output left sharded
 (no collective), and the weak-scaling rate (every rank its own 100 x 25M).
 
@@ -314,8 +317,9 @@ class Dist:
         self.rank = int(os.environ.get('RANK', '0'))
         self.local = int(os.environ.get('LOCAL_RANK', '0'))
         if self.world != gpus:
-            log('note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE' %
-                (gpus, self.world))
+            # a line must never claim a GPU count other than the one run
+            log('error: --gpus %d but WORLD_SIZE %d' % (gpus, self.world))
+            sys.exit(2)
         if backend == 'gloo':
             self.local %= max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(self.local)
@@ -460,6 +464,79 @@ def live_traffic(args, kernel='wsum_f32_vec_kernel'):
         'reads) + write %.4g B per launch' % (kernel, read_b, write_b))
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(args, argv):
+    """``--gpus N`` (N > 1) started without a launcher: start the N rank
+    processes ourselves — one per GPU, RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* set as torch.distributed.run sets them — the way the
+    reference's parallel runner starts its own ranks
+    (core/parallel/parallel_runner.py:89-96).  Runs before this process
+    touches the GPU (torch.cuda.device_count() does not initialise HIP on
+    this image) and never execs: the children are started, rank 0's JSON
+    line reaches our stdout through the inherited descriptor, and we exit
+    with the first failing rank's status.  With RCCL a rank per GPU is
+    required: fewer visible GPUs than N is an error, never a smaller-N
+    line."""
+    import signal
+    import subprocess
+    import torch
+    n = args.gpus
+    visible = torch.cuda.device_count()
+    if args.backend == 'nccl' and visible < n:
+        log('error: --gpus %d needs %d visible GPUs, found %d' %
+            (n, n, visible))
+        return 3
+    port = free_port()
+    log('starting %d rank processes (%s, MASTER 127.0.0.1:%d)' %
+        (n, args.backend, port))
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r),
+                   WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK='0', MASTER_ADDR='127.0.0.1',
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.abspath(__file__)] + argv, env=env))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+    old = signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    log('rank %d exited %d; stopping the others' %
+                        (procs.index(p), code))
+                    stop()
+            time.sleep(0.05)
+    finally:
+        stop()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        signal.signal(signal.SIGTERM, old)
+    return rc
+
+
 def default_split(world):
     """Rounds' relative sizes of the strong-scaling pipeline (None: equal
     rounds).  DESIGN §7."""
@@ -531,6 +608,10 @@ def main():
                     help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        ap.error('--gpus must be >= 1')
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(spawn_ranks(args, sys.argv[1:]))
     import torch
     if args.pmc_child:
         return pmc_child(args)
@@ -642,6 +723,9 @@ def main():
     mean_launch_ms = sum(t for t, _ in launches) / len(launches)
     mean_launch_p = sum(m for _, m in launches) / len(launches)
     kern_ms = D.max(kern_ms)
+    # every rank's launch covers the same share (equal pieces): the slowest
+    # rank's mean launch sets the job's kernel rate
+    mean_launch_ms = D.max(mean_launch_ms)
     t_sharded = timed_steps(D, sharded_only, args.steps, args.warmup) \
         if world > 1 else t_step
 
@@ -670,7 +754,10 @@ def main():
     ok = D.max(0.0 if ok else 1.0) == 0.0
 
     algo_launch = 4.0 * n * mean_launch_p + 4.0 * mean_launch_p + 4.0 * n
-    achieved = algo_launch / (mean_launch_ms / 1e3) / 1e9
+    # N > 1: all ranks' launches together against N x the HBM peak (the
+    # per-rank fraction is the same number)
+    achieved = world * algo_launch / (mean_launch_ms / 1e3) / 1e9
+    peak = world * HBM_PEAK_GBS
     value = 4.0 * n * P / t_step / 1e9
     log('step %.3f ms (kernels %.3f ms/rank, sharded-output step %.3f ms), '
         'launch %.3f ms -> %.0f GB/s, assembled result bit-exact: %s' %
@@ -760,9 +847,10 @@ def main():
             'roofline': {
                 'bound': 'hbm',
                 'achieved': round(achieved, 1),
-                'peak': HBM_PEAK_GBS,
+                'peak': peak,
                 'unit': 'GB/s',
-                'frac': round(achieved / HBM_PEAK_GBS, 4),
+                'frac': round(achieved / peak, 4),
+                'per_rank_launch_ms': round(mean_launch_ms, 4),
                 'traffic': traffic,
                 'traffic_over_algorithmic': round(traffic / algo_launch, 5)
                 if traffic and world == 1 else None,

@@ -24,6 +24,12 @@ from ..auxiliaries.utils import (as_float_tensor, as_float_upload,
                                  param2tensor, param_meta)
 
 
+# the peer assembly's flag-barrier bound on the aggregate() path when
+# aggregator.shard_peer_timeout_s is unset (torch.distributed's default
+# process-group timeout is 10 min for RCCL)
+PEER_TIMEOUT_DEFAULT_S = 300.0
+
+
 def compute_device(device=None):
     if not torch.cuda.is_available():
         raise RuntimeError(
@@ -141,12 +147,20 @@ class DeviceEngine:
         if pa is not None:
             return pa
         if mode != 'rccl':
+            # no collective precedes the flag barrier on this path, so any
+            # host-side skew between the ranks (uneven staging, gRPC ingest
+            # on one rank before it calls aggregate()) counts against the
+            # bound: by default it is on the order of a process group's
+            # timeout, not the bench's 10 s
+            tmo = getattr(agg, 'shard_peer_timeout_s', None)
+            if tmo is None:
+                tmo = PEER_TIMEOUT_DEFAULT_S
             try:
                 # collective: every rank takes the same branch (the
                 # constructor agrees on success or failure across ranks)
                 pa = PeerAssembly(
                     layout.numel, comm=comm, device=self.compute_device,
-                    timeout_s=getattr(agg, 'shard_peer_timeout_s', None))
+                    timeout_s=tmo)
             except Exception:  # noqa: BLE001 (agreed by every rank)
                 if mode == 'p2p':
                     raise
@@ -420,7 +434,9 @@ class DeviceEngine:
         if as_float:
             dicts = [OrderedDict((k, as_float_tensor(v))
                                  for k, v in m.items()) for m in dicts]
-        key = ('range', st.layout.signature(), chunks)
+        # the spans differ between assemblies (one piece per rank for the
+        # peer assembly, ``chunks`` for the pipelined one)
+        key = ('range', st.layout.signature(), tuple(spans))
         rst = self._stacks.get(key)
         if rst is None or rst.capacity < len(dicts):
             rst = RangeStack(st.layout, spans, len(dicts),
@@ -563,8 +579,8 @@ class _PendingD:
     """Krum's distance matrix while its kernels run (``_pairdist``):
     ``cpu()`` copies D (and the Gram path's flags and bounds) to the host,
     recomputes the flagged (non-finite) pairs exactly and returns the host
-    fp32 [n][n] matrix; the bounds go to ``last_pair_bound`` (0 for the
-    recomputed pairs)."""
+    fp32 [n][n] matrix; the bounds go to ``last_pair_bound`` (for the
+    recomputed pairs only D's own fp32 formation)."""
 
     def __init__(self, eng, st, buf=None, D=None):
         self._eng, self._st, self._buf, self._D = eng, st, buf, D
@@ -595,7 +611,11 @@ class _PendingD:
             sub = ops.pairdist_finish(exact).cpu()
             idx = torch.tensor(sel)
             D[idx[:, None], idx[None, :]] = sub
-            B[np.ix_(sel, sel)] = 0.0
+            # exact per-key sums, but D is still their fp32 formation (a
+            # rounded sqrt and an fp32 add per key)
+            s = sub.numpy().astype(np.float64)
+            B[np.ix_(sel, sel)] = (2 * nseg + 2) * 2.0 ** -24 * np.where(
+                np.isfinite(s), s, 0.0)
             eng.last_pairdist_path = 'mfma + exact %d of %d clients' % (
                 len(sel), st.n)
         eng.last_pair_bound = B

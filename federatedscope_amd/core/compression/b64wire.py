@@ -774,8 +774,15 @@ class B64Stager:
         if not self.puts:
             return []
         words = torch.cat(self._status).cpu()[:self.puts].tolist()
+        # a later put under the same tag (a sender's retry into the same
+        # slot, ordered after the failed one on the staging stream) rewrites
+        # the whole row: only each tag's latest put decides
+        last = {}
+        for t, w in zip(self.tags, words):
+            last.pop(t, None)
+            last[t] = w
         bad = [(t, self._REASON.get(w, 'status %d' % w))
-               for t, w in zip(self.tags, words) if w]
+               for t, w in last.items() if w]
         if bad:
             with torch.cuda.stream(self.stream):
                 for st in self._status:

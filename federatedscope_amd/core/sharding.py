@@ -541,9 +541,15 @@ class PeerAssembly:
             'fsagg_peer_barrier')
 
     def check(self):
-        """Raise if a barrier gave up waiting for a peer (synchronises)."""
+        """Raise if a barrier gave up waiting for a peer (synchronises).
+        The status word is cleared before raising: a peer that arrives late
+        runs the round it missed against flags that are already up, and the
+        ranks' epochs meet again at the next round, which then succeeds (the
+        plan stays cached — rebuilding it would be a collective the late
+        peer is not in)."""
         v = int(self.ctrl[self.STATUS].item())
         if v:
+            self.ctrl[self.STATUS].zero_()
             raise RuntimeError('peer barrier timed out waiting for rank %d'
                                % (v - 1))
 

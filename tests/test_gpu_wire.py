@@ -511,3 +511,52 @@ def test_b64_rejected_upload_dropped_by_sender():
         for kk, v in clients[i][1].items())) for i in order])
     for kk in want:
         _same_bits(got[kk], want[kk])
+
+
+def test_b64_rejected_then_retried_before_round_fills():
+    """A sender's corrupt upload followed, in the same round and before the
+    buffer fills, by a clean retry into the same slot: only the sender's
+    latest put decides, so nothing is dropped and the round aggregates the
+    retry (rejections were matched by sender tag alone)."""
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    from federatedscope_amd.core.workers.server import AggregationServer
+    meta, clients, out, _, _ = load_case('b64_fedavg_n5')
+    c = _cfg()
+
+    class M(torch.nn.Module):
+        def state_dict(self, *a, **kw):
+            return OrderedDict()
+
+        def load_state_dict(self, sd, strict=True):
+            self.loaded = sd
+
+    srv = AggregationServer(M(), ClientsAvgAggregator(device='cuda',
+                                                      config=c),
+                            sample_client_num=len(clients), keep_history=1)
+    bad_sender = 2
+    s2, d2 = clients[bad_sender]
+    k = max(d2, key=lambda key: len(d2[key]) if isinstance(d2[key], str)
+            else 0)
+    txt = d2[k]
+    mid = len(txt) // 2
+    corrupt = OrderedDict(d2)
+    corrupt[k] = txt[:mid] + '*' + txt[mid + 1:]
+    assert srv.callback_funcs_model_para(0, bad_sender,
+                                         (s2, corrupt)) is False
+    assert srv.callback_funcs_model_para(0, bad_sender,
+                                         (s2, OrderedDict(d2))) is False
+    moved = False
+    for sender, (s, d) in enumerate(clients):
+        if sender != bad_sender:
+            moved = srv.callback_funcs_model_para(0, sender,
+                                                  (s, OrderedDict(d)))
+    assert moved is True and srv.rejected_uploads == []
+    got = srv.history[-1]
+    # the buffer keeps the sender's first arrival position
+    order = [bad_sender] + [i for i in range(len(clients))
+                            if i != bad_sender]
+    want = O.para_weighted_avg([(clients[i][0], OrderedDict(
+        (kk, O.b64_tensor(v) if isinstance(v, str) else v)
+        for kk, v in clients[i][1].items())) for i in order])
+    for kk in want:
+        _same_bits(got[kk], want[kk])

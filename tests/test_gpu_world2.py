@@ -66,6 +66,37 @@ def test_bench_strong_scaling_world2():
     assert r['config']['params'] == 1000003
 
 
+def test_bench_self_launch():
+    """A bare ``bench.py --gpus 2`` (no torchrun) starts its own two rank
+    processes and prints ONE n_gpus 2 line, bit-exact after the assembly;
+    with RCCL on a box with fewer GPUs than ranks it refuses (non-zero exit,
+    no line)."""
+    import torch
+    env = dict(os.environ, OMP_NUM_THREADS='4')
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK'):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, 'bench.py', '--gpus', '2',
+                        '--backend', 'gloo', '--assembly', 'p2p',
+                        '--clients', '10', '--params', '1000003', '--steps',
+                        '3', '--warmup', '1', '--no-cpu-baseline',
+                        '--no-weak'], cwd=ROOT, capture_output=True,
+                       text=True, timeout=110, env=env)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, p.stdout
+    r = json.loads(lines[0])
+    assert r['n_gpus'] == 2 and r['assembled_bit_exact'] is True
+    assert r['roofline']['peak'] == 2 * 8000.0
+    if torch.cuda.device_count() < 2:
+        q = subprocess.run([sys.executable, 'bench.py', '--gpus', '2',
+                            '--steps', '1', '--warmup', '0'], cwd=ROOT,
+                           capture_output=True, text=True, timeout=110,
+                           env=env)
+        assert q.returncode != 0
+        assert not [ln for ln in q.stdout.splitlines()
+                    if ln.startswith('{')]
+
+
 @pytest.mark.parametrize('world,clients,params', [
     (2, 100, 25_000_000),       # configs[2] itself: 5 GB per rank
     (4, 10, 1_000_003)])
@@ -122,3 +153,6 @@ def test_peer_assembly_lost_rank():
     assert by[1]['raised'] is None
     assert 'rank 1' in (by[0]['raised'] or ''), by[0]
     assert 0.9 <= by[0]['waited_s'] <= 30.0, by[0]
+    # once the late rank has caught up, the next round succeeds everywhere
+    assert by[0]['second_round_ok'] is True, by[0]
+    assert by[1]['second_round_ok'] is True, by[1]
