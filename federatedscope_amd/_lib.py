@@ -109,6 +109,7 @@ SIGNATURES['fsagg_weighted_sum_rows_f32'] = (
     _c_i, [_rows_p, _c_p, _c_i, _c_i64, _c_p, _c_p, _c_p, _c_i64, _c_p, _c_p])
 SIGNATURES['fsagg_coord_median_rows_f32'] = (
     _c_i, [_rows_p, _c_p, _c_i, _c_i64, _c_p, _c_i64, _c_p, _c_p])
+SIGNATURES['fsagg_orderstat_set_pair_min'] = (_c_i, [_c_i])
 SIGNATURES['fsagg_trimmed_mean_rows_f32'] = (
     _c_i, [_rows_p, _c_p, _c_i, _c_i64, _c_i, _c_f, _c_p, _c_i64, _c_p,
            _c_p])
@@ -137,6 +138,9 @@ _c_u32 = ctypes.c_uint32
 SIGNATURES['fsagg_peer_handle_bytes'] = (_c_sz, [])
 SIGNATURES['fsagg_peer_alloc'] = (_c_i, [_c_i, _c_sz, ctypes.POINTER(_c_p)])
 SIGNATURES['fsagg_peer_free'] = (_c_i, [_c_i, _c_p])
+SIGNATURES['fsagg_peer_status_alloc'] = (
+    _c_i, [ctypes.POINTER(_c_p), ctypes.POINTER(_c_p)])
+SIGNATURES['fsagg_peer_status_free'] = (_c_i, [_c_p])
 SIGNATURES['fsagg_peer_handle'] = (_c_i, [_c_p, _c_p])
 SIGNATURES['fsagg_peer_open'] = (_c_i, [_c_i, _c_p, ctypes.POINTER(_c_p)])
 SIGNATURES['fsagg_peer_close'] = (_c_i, [_c_i, _c_p])

@@ -348,9 +348,7 @@ class PeerAssembly:
     uploads arrive on the ranks' GPUs, parallel_runner.py:243-302)."""
 
     TIMEOUT_S = 10.0       # a lost peer ends the barrier with an error
-    CTRL_WORDS = 64        # flags [0, world), status word STATUS
-
-    STATUS = 32
+    CTRL_WORDS = 64        # flag words [0, world)
 
     def __init__(self, numel, comm=None, device=None, align=ALIGN,
                  group=None, buffers=2, timeout_s=None):
@@ -444,6 +442,17 @@ class PeerAssembly:
                                        idx)
         self._flags = (ctypes.c_void_p * W)(
             *[self._ptr[k][-1] for k in range(W)])
+        # the barrier's status word lives in mapped pinned host memory: the
+        # host reads it once the barrier has run (an event), with no
+        # device-to-host copy on the stream
+        hs, ds = ctypes.c_void_p(), ctypes.c_void_p()
+        self._L.check(self._lib.fsagg_peer_status_alloc(ctypes.byref(hs),
+                                                        ctypes.byref(ds)),
+                      'fsagg_peer_status_alloc')
+        self._st_host, self._st_dev = int(hs.value), int(ds.value)
+        self._status = ctypes.c_uint32.from_address(self._st_host)
+        self._ev = torch.cuda.Event()
+        self._pending = None       # a views-mode round not yet checked
 
     # -- allocation plumbing ------------------------------------------------
     def _alloc(self, nbytes):
@@ -468,6 +477,9 @@ class PeerAssembly:
         return int(p.value)
 
     def _release(self):
+        if getattr(self, '_st_host', None):
+            self._lib.fsagg_peer_status_free(self._st_host)
+            self._st_host = None
         for p in self._opened:
             self._lib.fsagg_peer_close(self.device.index, p)
         for p in self._own:
@@ -502,7 +514,7 @@ class PeerAssembly:
         self._barrier()
         return self.buffers[b][:self.numel]
 
-    def run_bucket(self, compute):
+    def run_bucket(self, compute, copy=True):
         """The Aggregator.aggregate() form.  ``compute(lo, hi, own, peers)``
         reduces this rank's piece [lo, hi) of the bucket into ``own`` (this
         GPU's copy, a [padded] fp32 tensor in bucket coordinates) on the
@@ -510,10 +522,18 @@ class PeerAssembly:
         GPUs' copies (same coordinates).  It returns True when its kernel
         stored the piece into the peers' copies itself (the fused broadcast
         epilogue of FedAvg), else the piece is pushed to them here
-        (fsagg_peer_push_f32).  After the flag barrier the assembled bucket
-        is copied into a fresh tensor — the caller owns it, the rotating
-        copies are reused — and the barrier's status is checked (raises if
-        a peer never arrived)."""
+        (fsagg_peer_push_f32).
+
+        ``copy`` (default): after the flag barrier the assembled bucket is
+        copied into a fresh tensor the caller owns, and the barrier's status
+        is checked before returning (raises if a peer never arrived).
+        ``copy=False``: the result is a view of this round's copy, valid for
+        work enqueued on the current stream before this rank's next-but-one
+        run_bucket (a peer writes that copy again only in round epoch +
+        len(buffers), which it starts after this rank's barrier of round
+        epoch + len(buffers) − 1); nothing waits here — the round's status
+        is checked at the end of the next run_bucket (after its launches)
+        or by :meth:`check`."""
         from .. import ops
         b = self.epoch % len(self.buffers)
         self.epoch += 1
@@ -527,31 +547,45 @@ class PeerAssembly:
                               [p + 4 * lo for p in peers], hi - lo,
                               self.device)
         self._barrier()
-        res = torch.empty(self.numel, dtype=torch.float32, device=self.device)
-        res.copy_(own[:self.numel])
-        self.check()
-        return res
+        if copy:
+            res = torch.empty(self.numel, dtype=torch.float32,
+                              device=self.device)
+            res.copy_(own[:self.numel])
+            self.check()
+            return res
+        prev = self._pending
+        self._pending = ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        if prev is not None:
+            prev.synchronize()
+            self._raise_status()
+        return own[:self.numel]
 
     def _barrier(self):
         st = torch.cuda.current_stream(self.device).cuda_stream
         ticks = int(self.TIMEOUT_S * 1e8)
         self._L.check(self._lib.fsagg_peer_barrier(
             self._flags, self.world, self.rank, self.epoch & 0xFFFFFFFF,
-            ticks, self.ctrl.data_ptr() + 4 * self.STATUS, st or None),
-            'fsagg_peer_barrier')
+            ticks, self._st_dev, st or None), 'fsagg_peer_barrier')
+        self._ev.record(torch.cuda.current_stream(self.device))
 
-    def check(self):
-        """Raise if a barrier gave up waiting for a peer (synchronises).
-        The status word is cleared before raising: a peer that arrives late
-        runs the round it missed against flags that are already up, and the
-        ranks' epochs meet again at the next round, which then succeeds (the
-        plan stays cached — rebuilding it would be a collective the late
-        peer is not in)."""
-        v = int(self.ctrl[self.STATUS].item())
+    def _raise_status(self):
+        v = int(self._status.value)
         if v:
-            self.ctrl[self.STATUS].zero_()
+            self._status.value = 0
             raise RuntimeError('peer barrier timed out waiting for rank %d'
                                % (v - 1))
+
+    def check(self):
+        """Raise if a barrier gave up waiting for a peer (waits for this
+        rank's last barrier).  The status word is cleared before raising: a
+        peer that arrives late runs the round it missed against flags that
+        are already up, and the ranks' epochs meet again at the next round,
+        which then succeeds (the plan stays cached — rebuilding it would be
+        a collective the late peer is not in)."""
+        self._ev.synchronize()
+        self._pending = None
+        self._raise_status()
 
     def close(self):
         """Collective: unmap the peers' buffers and free this rank's."""

@@ -227,6 +227,16 @@ template <int N, int MODE>
 void launch_select(const RowSrc &rs, unsigned grid, int n, int kk,
                    float divisor, float *out, hipStream_t s);
 
+// Default client count from which 64 < n <= 255 runs the two-wave kernel.
+constexpr int kPairMinDefault = 129;
+
+// Launch the two-wave select kernel for 2H - 8 < n <= 2H (orderstat_pair.h,
+// built in orderstat_select.hip's translation unit for SEL_N = 2H); its grid
+// is one 128-thread block per 64 coordinates.
+template <int H, int MODE>
+void launch_pair(const RowSrc &rs, unsigned grid, int n, int kk, float divisor,
+                 float *out, hipStream_t s);
+
 // Launch the streaming select kernel for 255 < n <= 65535
 // (orderstat_stream.hip).
 template <int MODE>

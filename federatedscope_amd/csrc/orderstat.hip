@@ -18,6 +18,8 @@
 //    re-reads the column 64 times.
 //
 // Algorithmic bytes per coordinate: 4·n read + 4 (base) read + 4 written.
+#include <atomic>
+
 #include "orderstat.h"
 
 namespace fsagg {
@@ -161,6 +163,10 @@ __global__ __launch_bounds__(kBlock) void orderstat_generic_kernel(
   out[p] = r;
 }
 
+// Clients from which 64 < n <= 255 takes the two-wave kernel;
+// fsagg_orderstat_set_pair_min() moves it for A/B measurements.
+std::atomic<int> g_pair_min{kPairMinDefault};
+
 template <int MODE>
 int launch(const RowSrc &rs, int nchunk, int n, int kk, float divisor,
            float *out, hipStream_t s) {
@@ -176,36 +182,44 @@ int launch(const RowSrc &rs, int nchunk, int n, int kk, float divisor,
   // the 64-key sort); 57..64 the sort (n = 64: equal or 4 % faster)
   else if (n <= 64 && (n > 56 || rs.numel > (int64_t(1) << 30)))
     FSAGG_OS(64);
-#define FSAGG_RX(NN) launch_select<NN, MODE>(rs, grid, n, kk, divisor, out, s)
+#define FSAGG_SEL(NN)                                                       \
+  if (pair)                                                                \
+    launch_pair<NN / 2, MODE>(rs, pgrid, n, kk, divisor, out, s);          \
+  else                                                                     \
+    launch_select<NN, MODE>(rs, grid, n, kk, divisor, out, s)
   else if (n <= 255 && rs.numel <= (int64_t(1) << 30)) {
+    // the two-wave form from g_pair_min clients up (orderstat_pair.h)
+    const bool pair = n >= g_pair_min.load(std::memory_order_relaxed);
+    const unsigned pgrid = rs.chunks ? unsigned(nchunk) * 4u
+                                     : unsigned((rs.numel + kWave - 1) / kWave);
     switch ((n + kSelStep - 1) / kSelStep * kSelStep) {
-    case 40: FSAGG_RX(40); break;
-    case 48: FSAGG_RX(48); break;
-    case 56: FSAGG_RX(56); break;
-    case 72: FSAGG_RX(72); break;
-    case 80: FSAGG_RX(80); break;
-    case 88: FSAGG_RX(88); break;
-    case 96: FSAGG_RX(96); break;
-    case 104: FSAGG_RX(104); break;
-    case 112: FSAGG_RX(112); break;
-    case 120: FSAGG_RX(120); break;
-    case 128: FSAGG_RX(128); break;
-    case 136: FSAGG_RX(136); break;
-    case 144: FSAGG_RX(144); break;
-    case 152: FSAGG_RX(152); break;
-    case 160: FSAGG_RX(160); break;
-    case 168: FSAGG_RX(168); break;
-    case 176: FSAGG_RX(176); break;
-    case 184: FSAGG_RX(184); break;
-    case 192: FSAGG_RX(192); break;
-    case 200: FSAGG_RX(200); break;
-    case 208: FSAGG_RX(208); break;
-    case 216: FSAGG_RX(216); break;
-    case 224: FSAGG_RX(224); break;
-    case 232: FSAGG_RX(232); break;
-    case 240: FSAGG_RX(240); break;
-    case 248: FSAGG_RX(248); break;
-    case 256: FSAGG_RX(256); break;
+    case 40: FSAGG_SEL(40); break;
+    case 48: FSAGG_SEL(48); break;
+    case 56: FSAGG_SEL(56); break;
+    case 72: FSAGG_SEL(72); break;
+    case 80: FSAGG_SEL(80); break;
+    case 88: FSAGG_SEL(88); break;
+    case 96: FSAGG_SEL(96); break;
+    case 104: FSAGG_SEL(104); break;
+    case 112: FSAGG_SEL(112); break;
+    case 120: FSAGG_SEL(120); break;
+    case 128: FSAGG_SEL(128); break;
+    case 136: FSAGG_SEL(136); break;
+    case 144: FSAGG_SEL(144); break;
+    case 152: FSAGG_SEL(152); break;
+    case 160: FSAGG_SEL(160); break;
+    case 168: FSAGG_SEL(168); break;
+    case 176: FSAGG_SEL(176); break;
+    case 184: FSAGG_SEL(184); break;
+    case 192: FSAGG_SEL(192); break;
+    case 200: FSAGG_SEL(200); break;
+    case 208: FSAGG_SEL(208); break;
+    case 216: FSAGG_SEL(216); break;
+    case 224: FSAGG_SEL(224); break;
+    case 232: FSAGG_SEL(232); break;
+    case 240: FSAGG_SEL(240); break;
+    case 248: FSAGG_SEL(248); break;
+    case 256: FSAGG_SEL(256); break;
     }
   } else if (n <= 65535 && rs.numel <= (int64_t(1) << 30)) {
     launch_stream<MODE>(rs, grid, n, kk, divisor, out, s);
@@ -214,7 +228,7 @@ int launch(const RowSrc &rs, int nchunk, int n, int kk, float divisor,
                        dim3(kBlock), 0, s, rs, n, kk, divisor, out);
   }
 #undef FSAGG_OS
-#undef FSAGG_RX
+#undef FSAGG_SEL
   return check_launch(MODE == kMedian ? "coordinate median"
                                       : "trimmed mean");
 }
@@ -303,4 +317,8 @@ extern "C" int fsagg_trimmed_mean_rows_f32(const fsagg_rows *rows,
                   base_ss};
   return launch<kTrimmed>(rs, nchunk, rows->n, k, divisor, out,
                           as_stream(stream));
+}
+
+extern "C" int fsagg_orderstat_set_pair_min(int n) {
+  return g_pair_min.exchange(n < 0 ? kPairMinDefault : n);
 }

@@ -30,6 +30,7 @@
 //     (and the kept partial sums) read off.
 // Register budget: SEL_N values + ~40 within 256 VGPRs (2 waves per SIMD).
 #include "orderstat_sel.h"
+#include "orderstat_pair.h"
 
 #ifndef SEL_N
 #error "compile with -DSEL_N=<keys per lane>"
@@ -254,6 +255,21 @@ template void launch_select<SEL_N, kMedian>(const RowSrc &, unsigned, int,
 template void launch_select<SEL_N, kTrimmed>(const RowSrc &, unsigned, int,
                                              int, float, float *,
                                              hipStream_t);
+
+// the two-wave form (orderstat_pair.h): H = SEL_N / 2 values per wave
+template <int H, int MODE>
+void launch_pair(const RowSrc &rs, unsigned grid, int n, int kk,
+                 float divisor, float *out, hipStream_t s) {
+  hipLaunchKernelGGL((orderstat_pair_kernel<H, MODE>), dim3(grid),
+                     dim3(kPairBlock), 0, s, rs, n, kk, divisor, out);
+}
+
+template void launch_pair<SEL_N / 2, kMedian>(const RowSrc &, unsigned, int,
+                                              int, float, float *,
+                                              hipStream_t);
+template void launch_pair<SEL_N / 2, kTrimmed>(const RowSrc &, unsigned, int,
+                                               int, float, float *,
+                                               hipStream_t);
 
 }  // namespace os
 }  // namespace fsagg

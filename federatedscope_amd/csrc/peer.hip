@@ -115,6 +115,32 @@ extern "C" int fsagg_peer_free(int device, void *ptr) {
   return FSAGG_OK;
 }
 
+extern "C" int fsagg_peer_status_alloc(void **host, void **dev) {
+  if (!host || !dev) {
+    set_error("fsagg_peer_status_alloc: invalid argument");
+    return FSAGG_EINVAL;
+  }
+  *host = *dev = nullptr;
+  hipError_t e = hipHostMalloc(host, 64, hipHostMallocMapped);
+  if (e != hipSuccess)
+    return hip_fail("fsagg_peer_status_alloc: hipHostMalloc", e);
+  std::memset(*host, 0, 64);
+  e = hipHostGetDevicePointer(dev, *host, 0);
+  if (e != hipSuccess) {
+    (void)hipHostFree(*host);
+    *host = nullptr;
+    return hip_fail("fsagg_peer_status_alloc: hipHostGetDevicePointer", e);
+  }
+  return FSAGG_OK;
+}
+
+extern "C" int fsagg_peer_status_free(void *host) {
+  if (!host) return FSAGG_OK;
+  hipError_t e = hipHostFree(host);
+  if (e != hipSuccess) return hip_fail("fsagg_peer_status_free", e);
+  return FSAGG_OK;
+}
+
 extern "C" int fsagg_peer_handle(void *ptr, void *handle) {
   if (!ptr || !handle) {
     set_error("fsagg_peer_handle: invalid argument");

@@ -28,12 +28,42 @@ class _PinnedRing:
     of 1 MiB hold the key table of up to ~800 clients of that layout."""
     SLOT = 1 << 20
     NSLOT = 32
+    # Content-addressed cache of the uploaded tables (the kernels only read
+    # them): a table whose bytes were uploaded before is handed out again
+    # without a copy.  Row tables hold the clients' tensor addresses, which
+    # stay the same from call to call whenever the clients' tensors do (the
+    # standalone simulator's persistent client models, a server's stack
+    # slots, and every repeated aggregate() over the same dicts); weights,
+    # chunk lists and selections repeat likewise.  Entries are immutable
+    # device tensors; each is marked used (record_stream) by every stream
+    # it is handed to, so the caching allocator recycles an evicted entry's
+    # block only after the work that read it.
+    CACHE_MAX_BYTES = 64 << 10
+    CACHE_ENTRIES = 512
 
     def __init__(self):
+        from collections import OrderedDict
         self.buf = None
         self.events = [None] * self.NSLOT
         self.i = 0
         self.streams = {}
+        self.cache = OrderedDict()
+        self.cache_on = True
+        self.hits = 0
+        self.misses = 0
+
+    def _cached(self, key, device):
+        hit = self.cache.get(key)
+        if hit is None:
+            return None
+        self.cache.move_to_end(key)
+        t, seen = hit
+        s = torch._C._cuda_getCurrentRawStream(device.index)
+        if s not in seen:
+            t.record_stream(torch.cuda.current_stream(device))
+            seen.add(s)
+        self.hits += 1
+        return t
 
     def _copy_stream(self, device):
         s = self.streams.get(device.index)
@@ -53,9 +83,28 @@ class _PinnedRing:
         allocator never hands its block to a copy while a kernel may still
         read it."""
         import numpy as np
+        if device.index is None:
+            device = torch.device('cuda', torch.cuda.current_device())
         arr = np.ascontiguousarray(arr)
         raw = arr.reshape(-1).view(np.uint8)
         nb = raw.size
+        key = None
+        if self.cache_on and 0 < nb <= self.CACHE_MAX_BYTES:
+            key = (device.index, arr.dtype.str, arr.shape, raw.tobytes())
+            t = self._cached(key, device)
+            if t is not None:
+                return t
+            self.misses += 1
+        t = self._upload(arr, raw, nb, device)
+        if key is not None:
+            self.cache[key] = (t, {torch._C._cuda_getCurrentRawStream(
+                device.index)})
+            if len(self.cache) > self.CACHE_ENTRIES:
+                self.cache.popitem(last=False)
+        return t
+
+    def _upload(self, arr, raw, nb, device):
+        import numpy as np
         if nb == 0 or nb > self.SLOT:
             host = torch.from_numpy(raw.copy())
             return host.pin_memory().to(device, non_blocking=True).view(
@@ -120,7 +169,11 @@ def _h2d_np(arr, device):
 
 
 def _stream(device):
-    return ctypes_ptr(torch.cuda.current_stream(device).cuda_stream)
+    """The raw current stream of ``device`` (an int, 0 = the null stream),
+    without building a torch Stream object (~2 us each)."""
+    idx = device.index if device.index is not None else \
+        torch.cuda.current_device()
+    return ctypes_ptr(torch._C._cuda_getCurrentRawStream(idx))
 
 
 def ctypes_ptr(x):

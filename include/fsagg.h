@@ -439,6 +439,14 @@ int fsagg_trimmed_mean_rows_f32(const fsagg_rows *rows,
                                 const float *const *base, int64_t base_ss,
                                 float *out, fsagg_stream_t stream);
 
+/* Tuning hook of the order statistics above (no reference counterpart):
+ * the client count from which 64 < n <= 255 runs the two-wave select
+ * kernel (each column's rows split over two waves of one workgroup) instead
+ * of the one-wave kernel; both give identical medians and trimmed means
+ * within the stated tolerance.  n < 0 restores the default; returns the
+ * previous value.  Process-wide; for A/B measurements. */
+int fsagg_orderstat_set_pair_min(int n);
+
 /* Krum per-key squared distances over a row set: segment s covers
  * [seg_lo[s], seg_end[s]) (device int64 arrays; keys may leave gaps between
  * them, which are never read); numel = the bucket extent (for planning).
@@ -566,13 +574,21 @@ int fsagg_normbound_prescale_f32(const double *sq, int n, int nseg,
  *                    rank's array reached `epoch` (epochs increase by one
  *                    per call; compared modulo 2^32).  A wait longer than
  *                    `timeout_ticks` of the 100 MHz constant clock stores
- *                    1 + the missing rank into *status (device) and ends
- *                    instead of hanging.
+ *                    1 + the missing rank into *status (device-visible:
+ *                    device memory, or the mapped host word of
+ *                    fsagg_peer_status_alloc) and ends instead of hanging.
+ * fsagg_peer_status_alloc  a zeroed 64-byte word block in pinned, mapped
+ *                    host memory: *host for the host to read once the
+ *                    barrier's stream has passed it (no device-to-host
+ *                    copy), *dev for fsagg_peer_barrier's `status`; free
+ *                    with fsagg_peer_status_free.
  */
 #define FSAGG_MAX_PEERS 8
 size_t fsagg_peer_handle_bytes(void);
 int fsagg_peer_alloc(int device, size_t bytes, void **ptr);
 int fsagg_peer_free(int device, void *ptr);
+int fsagg_peer_status_alloc(void **host, void **dev);
+int fsagg_peer_status_free(void *host);
 int fsagg_peer_handle(void *ptr, void *handle);
 int fsagg_peer_open(int device, const void *handle, void **ptr);
 int fsagg_peer_close(int device, void *ptr);

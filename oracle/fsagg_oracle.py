@@ -21,6 +21,7 @@ from collections import OrderedDict
 import numpy as np
 
 __all__ = [
+    'trimmed_group_bound',
     'BF16', 'fedavg_weights', 'para_weighted_avg', 'asyn_weighted_avg',
     'asyn_aggregate', 'online_aggregate', 'krum_distance', 'krum_distance_matrix',
     'krum_scores', 'krum_select', 'krum_aggregate', 'median_update',
@@ -394,6 +395,29 @@ def trimmed_tolerance(models, excluded_num, divisor=None):
         n = T.shape[0]
         div = (n - 2 * excluded_num) if divisor is None else divisor
         out[k] = 8 * eps * (2 * np.abs(T).sum(0)) / div + 1e-30
+    return out
+
+
+def trimmed_group_bound(models, excluded_num, divisor=None):
+    """Elementwise abs bound on the device trimmed mean against this
+    oracle's fp64 middle sum (test infrastructure): the device
+    kernel sums the values strictly between the two rank bins in fp32 groups
+    of at most 12 terms before widening each group to fp64, so its sum is
+    off by at most 11·u·Σ|kept| (u = 2^-24); divided by the divisor.  The
+    final cast, division and init add round once each and are covered by
+    the callers' ε·|result| terms.  Far inside the reference's own bound
+    (:func:`trimmed_tolerance`, 16ε·Σ|x|/div)."""
+    first = models[0][1]
+    out = OrderedDict()
+    u = 2.0 ** -24
+    for k in first:
+        T = np.sort(np.stack([_to_float(d[k]) for _, d in models], 0).astype(
+            np.float64), 0)
+        n = T.shape[0]
+        div = (n - 2 * excluded_num) if divisor is None else divisor
+        kept = np.abs(np.where(np.isfinite(T), T, 0.0)[
+            excluded_num:n - excluded_num]).sum(0)
+        out[k] = 11 * u * kept / div
     return out
 
 

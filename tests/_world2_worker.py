@@ -68,10 +68,11 @@ def main():
             cfg(f=1, ratio=0.2))).aggregate(
                 {'client_feedback': feedback(clients)})
         want = O.add_init(init, O.trimmed_mean_update(clients, k))
+        grp = O.trimmed_group_bound(clients, k)
         eps = np.finfo(np.float32).eps
         for key in got:
             g, o = to_np(got[key]).astype(np.float64), np.asarray(want[key])
-            assert (np.abs(g - o) <= 4 * eps * (np.abs(o) + np.abs(
+            assert (np.abs(g - o) <= grp[key] + 4 * eps * (np.abs(o) + np.abs(
                 np.asarray(init[key])))).all(), (name, key)
         done.append(name)
     for name in ('krum_n50_f10_a5', 'krum_n12_f2_a3', 'krum_n10_f10_a1'):

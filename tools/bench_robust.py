@@ -246,8 +246,9 @@ def orderstat_c5(dev, n=200, ratio=0.2, P=None, tag='C5'):
                                    oracle.trimmed_mean_update(models, k))['w']
             eps = np.finfo(np.float32).eps
             err = float(np.max(np.abs(got - want)))
-            ok = bool((np.abs(got.astype(np.float64) - want) <= 4 * eps *
-                       (np.abs(want) + np.abs(hbase) + 1e-30)).all())
+            grp = oracle.trimmed_group_bound(models, k)['w']
+            ok = bool((np.abs(got.astype(np.float64) - want) <= grp + 4 * eps
+                       * (np.abs(want) + np.abs(hbase) + 1e-30)).all())
         med, mn = timed(fn)
         nbytes = 4.0 * n * P + 8.0 * P
         res.append({

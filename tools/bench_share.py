@@ -188,13 +188,23 @@ def p2p_share(args):
 
 
 def aggregate_share(args):
-    """Rank 0 of ``world`` through Aggregator.aggregate() on one GPU: the
-    engine's sharded path (``aggregator.shard_by_param_range``) with a
-    PeerAssembly whose world - 1 peer copies are local uncached buffers and
-    whose barrier waits for this rank alone — everything rank 0 does on the
-    node (its row table over the 100 device dicts, the reduction of its
-    P/world range stored into every copy, the barrier, the copy-out of the
-    full result, the status check), without the xGMI link time."""
+    """Rank ``--rank`` of ``world`` through Aggregator.aggregate() on one
+    GPU: the engine's sharded path (``aggregator.shard_by_param_range``)
+    with a PeerAssembly whose world - 1 peer copies are local uncached
+    buffers and whose barrier waits for this rank alone — everything that
+    rank does on the node (its row table over the 100 device dicts, the
+    reduction of its P/world range stored into every copy, the barrier, the
+    result, the status check), without the xGMI link time.
+
+    Per mode one JSON line:
+      latency   — synchronize, one aggregate(), synchronize (median);
+      pipelined — 10 back-to-back calls between synchronizes (per call);
+    for the default result (a fresh copy of the assembled bucket, status
+    checked before returning) and ``shard_result_views`` (views of the
+    rotating copies, status checked at the next call); with the upload
+    cache on (the same client tensors every call, as a persistent client
+    model gives) and off (every table uploaded, as new client tensors
+    would need)."""
     import ctypes
     import statistics
     from types import SimpleNamespace
@@ -203,13 +213,15 @@ def aggregate_share(args):
     from federatedscope_amd.core.aggregators import ClientsAvgAggregator
     from federatedscope_amd.core.sharding import Comm, PeerAssembly
     dev = torch.device('cuda', 0)
-    n, P, W = args.clients, args.params, args.world
+    n, P, W, R = args.clients, args.params, args.world, args.rank
     lib = L.load()
 
     class EmuPeers(PeerAssembly):
-        def __init__(self, numel):
-            super().__init__(numel, comm=Comm(), device=dev)   # world 1
+        def __init__(self, numel, buffers):
+            super().__init__(numel, comm=Comm(), device=dev,
+                             buffers=buffers)   # world 1
             self.world = W
+            self.rank = R
             self.pc = max(-(-numel // W // 64) * 64, 64)
             self.fake = []
             for _ in range(W - 1):
@@ -218,15 +230,19 @@ def aggregate_share(args):
                                              ctypes.byref(q)))
                 self.fake.append(int(q.value))
             own = self._ptr[0]
-            self._ptr = [own] + [[q] * len(own) for q in self.fake]
+            self._ptr = [[q] * len(own) for q in self.fake[:R]] + [own] + \
+                [[q] * len(own) for q in self.fake[R:]]
 
         def _barrier(self):
-            saved = self.world
-            self.world = 1
+            saved, sr = self.world, self.rank
+            self.world, self.rank = 1, 0
+            saved_flags = self._flags
+            self._flags = (ctypes.c_void_p * 1)(self._ptr[sr][-1])
             try:
                 super()._barrier()
             finally:
-                self.world = saved
+                self.world, self.rank = saved, sr
+                self._flags = saved_flags
 
         def free(self):
             for q in self.fake:
@@ -240,45 +256,67 @@ def aggregate_share(args):
     clients = [(sizes[i], {'w': slab[i, :P]}) for i in range(n)]
     cfg = SimpleNamespace(federate=SimpleNamespace(ignore_weight=False,
                                                    use_ss=False))
-    res = {}
-    for world in sorted({1, W}):
-        agg = ClientsAvgAggregator(device=dev, config=cfg)
-        info = {'client_feedback': clients, 'recover_fun': None}
-        emu = None
-        if world > 1:
-            emu = EmuPeers(P)
-            layout = agg._staged_rows(clients).layout
-            agg.cfg = SimpleNamespace(
-                federate=cfg.federate, aggregator=SimpleNamespace(
-                    shard_by_param_range=True, shard_chunks=1,
-                    shard_assembly='p2p'))
-            agg._shard = lambda: (emu.comm, 1)
-            agg._plans[(layout.signature(), 1, 'p2p')] = emu
+    ref = torch.empty(-(-P // 64) * 64, dtype=torch.float32, device=dev)
+    ops.weighted_sum(ops.RowTable.from_slab(slab, numel=P),
+                     [s / sum(sizes) for s in sizes], ref)
+    info = {'client_feedback': clients, 'recover_fun': None}
+
+    def measure(agg):
         for _ in range(args.warmup):
-            out = agg.aggregate(info)
+            agg.aggregate(info)
         torch.cuda.synchronize()
-        ts = []
+        lat = []
         for _ in range(args.steps):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             out = agg.aggregate(info)
             torch.cuda.synchronize()
-            ts.append((time.perf_counter() - t0) * 1e3)
-        res[world] = statistics.median(ts)
-        if world > 1:
-            lo, hi = emu.piece()
-            ref = torch.empty(-(-P // 64) * 64, dtype=torch.float32,
-                              device=dev)
-            ops.weighted_sum(ops.RowTable.from_slab(slab, numel=P),
-                             [s / sum(sizes) for s in sizes], ref)
-            ok = torch.equal(out['w'][lo:hi], ref[lo:hi])
-            emu.free()
-        print(json.dumps({
-            'mode': 'aggregate-share', 'world': world, 'clients': n,
-            'params': P, 'ms_per_call': round(res[world], 4),
-            'rank0_piece_bit_exact': ok if world > 1 else None,
-            'speedup_vs_world1': round(res[1] / res[world], 2)}),
-            flush=True)
+            lat.append((time.perf_counter() - t0) * 1e3)
+        pipe = []
+        for _ in range(5):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(10):
+                out = agg.aggregate(info)
+            torch.cuda.synchronize()
+            pipe.append((time.perf_counter() - t0) * 1e3 / 10)
+        return statistics.median(lat), statistics.median(pipe), out
+
+    base = None
+    for world, views in [(1, False)] + [(W, v) for v in (False, True)]:
+        for cache in ((True, ) if world == 1 else (True, False)):
+            ops._RING.cache_on = cache
+            ops._RING.cache.clear()
+            agg = ClientsAvgAggregator(device=dev, config=cfg)
+            emu = None
+            if world > 1:
+                emu = EmuPeers(P, 3 if views else 2)
+                layout = agg._staged_rows(clients).layout
+                agg.cfg = SimpleNamespace(
+                    federate=cfg.federate, aggregator=SimpleNamespace(
+                        shard_by_param_range=True, shard_chunks=1,
+                        shard_assembly='p2p', shard_result_views=views))
+                agg._shard = lambda: (emu.comm, 1)
+                agg._plans[(layout.signature(), 1, 'p2p', views)] = emu
+            lat, pipe, out = measure(agg)
+            ok = None
+            if world > 1:
+                lo, hi = emu.piece()
+                ok = bool(torch.equal(out['w'][lo:hi], ref[lo:hi]))
+                emu.check()
+                emu.free()
+            else:
+                base = lat
+            print(json.dumps({
+                'mode': 'aggregate-share', 'world': world, 'rank': R,
+                'clients': n, 'params': P,
+                'result': ('views' if views else 'copy') if world > 1
+                else 'unsharded', 'upload_cache': cache,
+                'ms_latency': round(lat, 4), 'ms_pipelined': round(pipe, 4),
+                'piece_bit_exact': ok,
+                'speedup_latency_vs_world1': round(base / lat, 2)}),
+                flush=True)
+    ops._RING.cache_on = True
 
 
 if __name__ == '__main__':
