@@ -107,15 +107,9 @@ __device__ __forceinline__ void pair_list_select(uint32_t hb, int c0, int cnt,
   sum = acc;
 }
 
-// Strictly-middle sum of the trimmed mean: fp32 over groups of kMidGroup
-// values (a select and an add per value), each group widened into fp64.
-// A group's error is at most (kMidGroup − 1)·u·Σ|group| (u = 2^-24), i.e.
-// 7u·Σ|x| over the kept values in all — inside the reference's own fp32
-// cascade bound 8ε·2Σ|x|.
-constexpr int kMidGroup = 8;
-
 template <int H, int MODE>
 __device__ __forceinline__ void pair_compact(const uint32_t (&u)[H], int nw,
+                                             int n, bool first,
                                              uint32_t start, int step,
                                              const RankSel &s1,
                                              const RankSel &s2, bool shared,
@@ -145,30 +139,20 @@ __device__ __forceinline__ void pair_compact(const uint32_t (&u)[H], int nw,
       }
     }
   } else {
-    const uint32_t A = list1 ? s1.lo : s1.hi + 1u;
-    const uint32_t w1 = list1 ? s1.hi - s1.lo + 1u : 0u;
-    const uint32_t wm = shared ? 0u : s2.lo - (s1.hi + 1u);
-    const uint32_t wb = w1 + wm + (list2 ? s2.hi - s2.lo + 1u : 0u);
+    // the trimmed mean's bins and middle (orderstat_sel.h TrimBounds); the
+    // correction of the clamped sum is taken once, by wave 0
+    const TrimBounds tb = trim_bounds(s1, s2, shared, list1, list2, n);
     float g = 0.0f;
 #pragma unroll
     for (int j = 0; j < H; ++j) {
       if (j >= H - 4 && j >= nw) continue;
-      const uint32_t rel = ukey(u[j]) - A;
-      const bool inm = rel - w1 < wm;
-      float x = inm ? __uint_as_float(u[j]) : 0.0f;
-      g = add_rn(g, x);
-      // in place: left to itself the compiler sinks the selects and adds
-      // below the barrier (only wave 0 reads the sum after it), holding H
-      // lane masks in SGPRs that then spill into VGPR lanes
-      asm volatile("" : "+v"(g));
+      trim_step(u[j], tb, g, c, slot_addr(c, step, start));
       if (j % kMidGroup == kMidGroup - 1) {
         mid += double(g);
         g = 0.0f;
       }
-      *lds_at(slot_addr(c, step, start)) = u[j];  // a miss: overwritten
-      c += (rel < wb) && !inm;
     }
-    mid += double(g);
+    mid += double(g) - (first ? tb.corr : 0.0);
   }
 }
 
@@ -201,8 +185,7 @@ __global__ __launch_bounds__(kPairBlock) void orderstat_pair_kernel(
     for (int j = 0; j < H; ++j)
       u[j] = __float_as_uint(ld_nt(row_at(rows, j < nw ? j : nw - 1), off));
     if (base && wv == 0) bval = ld_nt(base, off);
-#pragma unroll
-    for (int j = 0; j < H; ++j) amax = max(amax, u[j] & 0x7FFFFFFFu);
+    amax = abs_max_bits<H>(u);
   }
   xch[wv * kWave + lane] = amax;
   // the histogram clear, half per wave
@@ -280,7 +263,8 @@ __global__ __launch_bounds__(kPairBlock) void orderstat_pair_kernel(
   fence_regs<H>(u);
   __syncthreads();
   if (__any(list1 || list2) || MODE == kTrimmed)
-    pair_compact<H, MODE>(u, nw, wv ? hb | (kPairTop << 8) : hb,
+    pair_compact<H, MODE>(u, nw, n, wv == 0,
+                          wv ? hb | (kPairTop << 8) : hb,
                           wv ? -256 : 256, s1, s2, shared, list1, list2, c,
                           mid);
   if (MODE == kTrimmed && wv == 1) {

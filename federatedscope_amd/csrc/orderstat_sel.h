@@ -45,6 +45,25 @@ __device__ __forceinline__ int add_below(int c, uint32_t a, uint32_t b) {
   return c;
 }
 
+// |x|max of a lane's values as float bits (NaN flagged: > 0x7F800000), from
+// a signed and an unsigned max chain (v_max3_i32 / v_max3_u32: one op per
+// value in all, against an and + half a max3 for max(u & 0x7FFFFFFF)): the
+// signed max is the largest non-negative value's bits, the unsigned max the
+// largest negative one's magnitude with the sign bit on top.
+template <int N>
+__device__ __forceinline__ uint32_t abs_max_bits(const uint32_t (&u)[N]) {
+  int32_t smax = int32_t(0x80000000u);
+  uint32_t umax = 0u;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    smax = max(smax, int32_t(u[j]));
+    umax = max(umax, u[j]);
+  }
+  const uint32_t pos = smax >= 0 ? uint32_t(smax) : 0u;
+  const uint32_t neg = umax >= 0x80000000u ? umax & 0x7FFFFFFFu : 0u;
+  return max(pos, neg);
+}
+
 // Opaque copy barrier: keeps the compiler from hoisting per-pass key math
 // (ukey of every value) out of a pass and holding N more registers live.
 template <int N>
@@ -259,6 +278,67 @@ __device__ __forceinline__ uint32_t tree_pick(const uint32_t (&a)[S],
     for (int k = 0; k < w; ++k) t[k] = up ? t[2 * k + 1] : t[2 * k];
   }
   return t[0];
+}
+
+// The trimmed mean's compaction bounds.  Each listed bin as an
+// interval of RAW float bits [lo, lo + w) — a bin never holds both signs, and
+// positive keys k are the bits k − 2^31, negative ones ~k (order reversed) —
+// so membership is one subtract and one borrow, no key transform per value
+// (w = 0: the bin is not listed).  The values strictly between the bins are
+// summed as Σ med3(x, L, U) over every value, L = the largest value of bin 1
+// and U = the smallest of bin 2: a value at or below L adds L, one at or
+// above U adds U, so Σmiddle = Σmed3 − L·#(key <= bin 1) − U·#(key >= bin 2),
+// the counts known from the histogram (corr below; exact in fp64).  ±0 may
+// land on either side of a zero bound, where it adds 0 either way.
+// The clamped middle terms are summed in fp32 over groups of kMidGroup
+// values, each group widened into the fp64 total: a group of m terms is off
+// by at most (m − 1)·u·Σ|terms| (u = 2^-24; m <= 12 where pad rows fold into
+// the last group), inside the reference's own fp32 cascade bound.
+constexpr int kMidGroup = 8;
+
+struct TrimBounds {
+  uint32_t lo1, w1, lo2, w2;
+  float L, U;
+  double corr;
+};
+
+__device__ __forceinline__ void raw_bin(const RankSel &s, bool listed,
+                                        uint32_t &lo, uint32_t &w) {
+  w = listed ? s.hi - s.lo + 1u : 0u;
+  lo = s.lo >= 0x80000000u ? s.lo - 0x80000000u : ~s.hi;
+}
+
+__device__ __forceinline__ TrimBounds trim_bounds(const RankSel &s1,
+                                                  const RankSel &s2,
+                                                  bool shared, bool list1,
+                                                  bool list2, int n) {
+  TrimBounds b;
+  raw_bin(s1, list1, b.lo1, b.w1);
+  raw_bin(s2, list2, b.lo2, b.w2);
+  if (shared) {  // both ranks in one bin: no middle
+    b.L = b.U = 0.0f;
+    b.corr = 0.0;
+  } else {
+    b.L = key2f(s1.hi);
+    b.U = key2f(s2.lo);
+    b.corr = double(b.L) * double(s1.below + s1.cnt) +
+             double(b.U) * double(n - s2.below);
+  }
+  return b;
+}
+
+// One value of the trimmed compaction: its clamped middle term into the
+// fp32 group sum g, its bits into list slot c (a miss is overwritten by the
+// next value), c advanced when it lies in a listed bin.
+__device__ __forceinline__ void trim_step(uint32_t u, const TrimBounds &b,
+                                          float &g, int &c, uint32_t addr) {
+  g = add_rn(g, __builtin_amdgcn_fmed3f(__uint_as_float(u), b.L, b.U));
+  // in place: left to itself the compiler sinks the med3s and adds to the
+  // end of the pass and holds every value's term live
+  asm volatile("" : "+v"(g));
+  *lds_at(addr) = u;
+  c = add_below(c, u - b.lo1, b.w1);
+  c = add_below(c, u - b.lo2, b.w2);
 }
 
 // Sort the lane's list of `cnt` values (float bits) at LDS slots [0, cnt) by

@@ -68,8 +68,7 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
     // with the rows, not at the end: a load issued as the wave's last act
     // exposes one full HBM round trip per wave (0.14 ms at C5)
     if (base) bval = ld_nt(base, off);
-#pragma unroll
-    for (int j = 0; j < N; ++j) amax = max(amax, u[j] & 0x7FFFFFFFu);
+    amax = abs_max_bits<N>(u);
   }
   const bool nan = amax > 0x7F800000u;
   const bool nonfinite = amax >= 0x7F800000u;
@@ -161,26 +160,20 @@ __global__ __launch_bounds__(kBlock) void orderstat_select_kernel(
         }
       }
     } else {
-      // the band from bin 1 to bin 2 relative to A: [0, w1) bin 1 listed,
-      // [w1, w1 + wm) strictly between the bins (summed), then bin 2 listed
-      // up to wb
-      const uint32_t A = list1 ? s1.lo : s1.hi + 1u;
-      const uint32_t w1 = list1 ? s1.hi - s1.lo + 1u : 0u;
-      const uint32_t wm = shared ? 0u : s2.lo - (s1.hi + 1u);
-      const uint32_t wb = w1 + wm + (list2 ? s2.hi - s2.lo + 1u : 0u);
+      // the listed bins as raw-bit intervals, the middle as Σ med3(x, L, U)
+      // in fp32 groups of kMidGroup (orderstat_sel.h TrimBounds)
+      const TrimBounds tb = trim_bounds(s1, s2, shared, list1, list2, n);
+      float g = 0.0f;
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         if (j >= N - kSelStep && j >= n) continue;
-        const uint32_t rel = ukey(u[j]) - A;
-        const bool inm = rel - w1 < wm;
-        // select in fp32, then widen: one v_cndmask, not a 64-bit pair (the
-        // empty asm keeps the compiler from sinking the select past the cvt)
-        float x = inm ? __uint_as_float(u[j]) : 0.0f;
-        asm("" : "+v"(x));
-        mid += double(x);
-        *lds_at(hb | (uint32_t(c) << 8)) = u[j];  // a miss: overwritten
-        c += (rel < wb) && !inm;
+        trim_step(u[j], tb, g, c, hb | (uint32_t(c) << 8));
+        if (j % kMidGroup == kMidGroup - 1) {
+          mid += double(g);
+          g = 0.0f;
+        }
       }
+      mid += double(g) - tb.corr;
     }
   }
 

@@ -400,13 +400,17 @@ def trimmed_tolerance(models, excluded_num, divisor=None):
 
 def trimmed_group_bound(models, excluded_num, divisor=None):
     """Elementwise abs bound on the device trimmed mean against this
-    oracle's fp64 middle sum (test infrastructure): the device
-    kernel sums the values strictly between the two rank bins in fp32 groups
-    of at most 12 terms before widening each group to fp64, so its sum is
-    off by at most 11·u·Σ|kept| (u = 2^-24); divided by the divisor.  The
-    final cast, division and init add round once each and are covered by
-    the callers' ε·|result| terms.  Far inside the reference's own bound
-    (:func:`trimmed_tolerance`, 16ε·Σ|x|/div)."""
+    oracle's fp64 middle sum (test infrastructure).  The device
+    kernel sums Σ med3(x, L, U) over every value — L the top of the bin
+    holding rank k, U the bottom of the bin holding rank n − k − 1, so each
+    term is |x| of a kept value or at most max(|L|, |U|) — in fp32 groups
+    of at most 12 terms widened to fp64, then removes L·#(≤ L) + U·#(≥ U)
+    exactly: its sum is off by at most 11·u·Σ|terms| (u = 2^-24).  |L| and
+    |U| are at most 1.125·max(|x_(k)|, |x_(n−k−1)|) (a bin spans 1/8 octave)
+    or, for the bin of magnitudes below the digit base, |x|max·2^-15.
+    Divided by the divisor; the final cast, division and init add round
+    once each and are covered by the callers' ε·|result| terms.  Far inside
+    the reference's own bound (:func:`trimmed_tolerance`, 16ε·Σ|x|/div)."""
     first = models[0][1]
     out = OrderedDict()
     u = 2.0 ** -24
@@ -415,9 +419,12 @@ def trimmed_group_bound(models, excluded_num, divisor=None):
             np.float64), 0)
         n = T.shape[0]
         div = (n - 2 * excluded_num) if divisor is None else divisor
-        kept = np.abs(np.where(np.isfinite(T), T, 0.0)[
-            excluded_num:n - excluded_num]).sum(0)
-        out[k] = 11 * u * kept / div
+        F = np.where(np.isfinite(T), T, 0.0)
+        kept = np.abs(F[excluded_num:n - excluded_num]).sum(0)
+        edge = np.maximum(np.abs(F[excluded_num]),
+                          np.abs(F[n - excluded_num - 1]))
+        amax = np.abs(F).max(0)
+        out[k] = 11 * u * (kept + n * (1.125 * edge + amax * 2.0 ** -15)) / div
     return out
 
 

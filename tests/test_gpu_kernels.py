@@ -137,11 +137,10 @@ def test_median_trimmed_all_kernels(n):
         ops.trimmed_mean(rows, k, out)
         want = O.trimmed_mean_update(models, k)['w']
         eps = np.finfo(np.float32).eps
-        mag = np.abs(np.sort(X, 0)[k:n - k]).sum(0) / (n - 2 * k)
+        grp = O.trimmed_group_bound(models, k)['w']
         err = np.abs(out.cpu().numpy().astype(np.float64) - want)
-        # fp32 group sums of the middle (O.trimmed_group_bound): 5.5ε·mag
-        assert (err <= 5.5 * eps * mag + 2 * eps * np.abs(want)).all(), (
-            n, k, err.max())
+        # the kernel's fp32 group sums of the clamped middle
+        assert (err <= grp + 2 * eps * np.abs(want)).all(), (n, k, err.max())
 
 
 def test_orderstat_nonfinite_columns():
@@ -307,10 +306,9 @@ def test_orderstat_refinement_stress(n):
     for k in (1, n // 5, n // 2 - 1):
         ops.trimmed_mean(rows, k, out)
         want = O.trimmed_mean_update(models, k)['w']
-        mag = np.abs(np.sort(X, 0)[k:n - k]).sum(0) / (n - 2 * k)
+        grp = O.trimmed_group_bound(models, k)['w']
         err = np.abs(out.cpu().numpy().astype(np.float64) - want)
-        assert (err <= 5.5 * eps * mag + 2 * eps * np.abs(want)).all(), (
-            k, err.max())
+        assert (err <= grp + 2 * eps * np.abs(want)).all(), (k, err.max())
 
 
 @pytest.mark.parametrize('n', [12, 50, 130, 255, 256, 300])

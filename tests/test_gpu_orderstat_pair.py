@@ -30,14 +30,10 @@ def pair_min(n):
 
 
 def trimmed_tol(X, k, want):
-    """|ours − oracle| bound: the strictly-middle values are summed in fp32
-    groups of at most 12 terms (8, plus up to 4 pad-skipped rows folded into
-    the last group) → 11u·Σ|kept| = 5.5ε·mean|kept|; the fp64 list sums and
-    the group adds are exact to far below that; the cast and the division
-    round once each (ε|want|)."""
-    n = X.shape[0]
-    mag = np.abs(np.sort(X, 0)[k:n - k]).sum(0) / (n - 2 * k)
-    return 5.5 * EPS * mag + 2 * EPS * np.abs(want)
+    """|ours − oracle|: the kernel's fp32 group sums of the clamped middle
+    (O.trimmed_group_bound) plus the final roundings (ε|want|)."""
+    models = [(1, {'w': X[i]}) for i in range(X.shape[0])]
+    return O.trimmed_group_bound(models, k)['w'] + 2 * EPS * np.abs(want)
 
 
 def columns(n, P, seed):

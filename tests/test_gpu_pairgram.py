@@ -291,7 +291,12 @@ def test_pairgram_flags_and_exact_repair(case):
         ix = np.ix_(sel, sel)
         assert np.allclose(De.numpy()[ix], Dv[ix], rtol=2e-7, atol=0,
                            equal_nan=True)
-        assert np.all(agg.last_pair_bound[ix] == 0.0)
+        # the recomputed pairs carry only D's own fp32 formation bound
+        Dr = De.numpy()[ix].astype(np.float64)
+        nseg = len(lay.keys)
+        want_b = (2 * nseg + 2) * 2.0 ** -24 * np.where(np.isfinite(Dr), Dr,
+                                                        0.0)
+        assert np.array_equal(agg.last_pair_bound[ix], want_b)
         return
     assert not flags.any()
     assert agg.last_pairdist_path == 'mfma'

@@ -341,6 +341,8 @@ def dropin_rules(dev):
             ts.append(time.perf_counter() - t0)
         t = statistics.median(ts)
         out.append({'rule': name, 'clients': n, 'params': P,
+                    'pairdist_path': getattr(agg, 'last_pairdist_path',
+                                             None),
                     'ms_aggregate': round(t * 1e3, 3),
                     'GBps_algorithmic': round(4.0 * n * P / t / 1e9, 1),
                     'what': 'aggregate() on device-resident dicts read in '
