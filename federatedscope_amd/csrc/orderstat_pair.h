@@ -20,11 +20,12 @@
 //  1. each wave loads its rows and takes |x|max of them; the two maxima meet
 //     in LDS (barrier);
 //  2. both waves add their values' octave digits into the shared histogram
-//     (barrier) and both scan it — they compute identical bins, so every
-//     later wave-level decision (refinement rounds, network size) agrees;
-//  3. refinement rounds (rare) likewise, a barrier before each clear;
+//     (barrier); wave 0 scans it and hands both ranks' bins to wave 1
+//     through LDS (barrier), so every later wave-level decision (refinement
+//     rounds, network size) agrees;
+//  3. refinement rounds (rare) likewise;
 //  4. compaction: wave 0 lists its bin values from slot 0 up, wave 1 from
-//     slot kPairList - 1... down (slots [0, 62]); each wave's misses land
+//     slot kPairTop = 62 down (slots [0, 62]); each wave's misses land
 //     on its next free slot, which lies in the gap between the two fills
 //     (stored <= 62), so no valid entry is ever overwritten.  Trimmed mean:
 //     each wave sums its strictly-middle values; wave 1 leaves its partial
@@ -156,6 +157,32 @@ __device__ __forceinline__ void pair_compact(const uint32_t (&u)[H], int nw,
   }
 }
 
+// Wave 0 scans the shared histogram and hands both ranks' bins to wave 1
+// through LDS (8 words per lane) instead of both waves scanning it.
+__device__ __forceinline__ void sel_put(uint32_t *X, int lane, const RankSel &a,
+                                        const RankSel &b) {
+  X[0 * kWave + lane] = a.lo;
+  X[1 * kWave + lane] = a.hi;
+  X[2 * kWave + lane] = uint32_t(a.below);
+  X[3 * kWave + lane] = uint32_t(a.cnt);
+  X[4 * kWave + lane] = b.lo;
+  X[5 * kWave + lane] = b.hi;
+  X[6 * kWave + lane] = uint32_t(b.below);
+  X[7 * kWave + lane] = uint32_t(b.cnt);
+}
+
+__device__ __forceinline__ void sel_get(const uint32_t *X, int lane,
+                                        RankSel &a, RankSel &b) {
+  a.lo = X[0 * kWave + lane];
+  a.hi = X[1 * kWave + lane];
+  a.below = int(X[2 * kWave + lane]);
+  a.cnt = int(X[3 * kWave + lane]);
+  b.lo = X[4 * kWave + lane];
+  b.hi = X[5 * kWave + lane];
+  b.below = int(X[6 * kWave + lane]);
+  b.cnt = int(X[7 * kWave + lane]);
+}
+
 template <int H, int MODE>
 __global__ __launch_bounds__(kPairBlock) void orderstat_pair_kernel(
     RowSrc rs, int n, int kk, float divisor, float *__restrict__ out) {
@@ -163,6 +190,7 @@ __global__ __launch_bounds__(kPairBlock) void orderstat_pair_kernel(
   // 16 KiB-aligned so a lane's word addresses are hb | (w << 8)
   __shared__ __attribute__((aligned(16384))) uint32_t lds[kSelWords * kWave];
   __shared__ uint32_t xch[2 * kWave];
+  __shared__ uint32_t xsel[8 * kWave];
   const int wv = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
   const int lane = int(threadIdx.x) & (kWave - 1);
   uint32_t *Hs = lds + lane;
@@ -199,15 +227,15 @@ __global__ __launch_bounds__(kPairBlock) void orderstat_pair_kernel(
   const int r1 = MODE == kMedian ? (n - 1) / 2 : kk;
   const int r2 = MODE == kMedian ? n / 2 : n - kk - 1;
 
-  // 2. the shared octave-digit histogram: both ranks' bins
+  // 2. the shared octave-digit histogram: both ranks' bins, found by wave 0
   RankSel s1, s2;
-  {
 #pragma unroll
-    for (int j = 0; j < H; ++j) {
-      if (j >= H - 4 && j >= nw) continue;  // pads
-      hist_inc(hb, octave_digit(u[j], obase));
-    }
-    __syncthreads();
+  for (int j = 0; j < H; ++j) {
+    if (j >= H - 4 && j >= nw) continue;  // pads
+    hist_inc(hb, octave_digit(u[j], obase));
+  }
+  __syncthreads();
+  if (wv == 0) {
     uint32_t d1, d2;
     int b1, c1, b2, c2;
     hist_scan<true, 64>(Hs, r1, r2, d1, b1, c1, d2, b2, c2);
@@ -217,7 +245,12 @@ __global__ __launch_bounds__(kPairBlock) void orderstat_pair_kernel(
     s1.cnt = c1;
     s2.below = b2;
     s2.cnt = c2;
+    sel_put(xsel, lane, s1, s2);
   }
+  // after this barrier wave 0 is done reading the histogram (the list may
+  // overwrite it) and wave 1 holds the same bins
+  __syncthreads();
+  if (wv == 1) sel_get(xsel, lane, s1, s2);
 
   // 3. refine while the two bins would overflow the list (rare); both waves
   // hold the same bins, so they take the same number of rounds
@@ -231,7 +264,6 @@ __global__ __launch_bounds__(kPairBlock) void orderstat_pair_kernel(
     const bool pick2 = list2 && (!list1 || s2.cnt > s1.cnt);
     fence_regs<H>(u);
     const Refine f = refine_plan(pick2 ? s2 : s1);
-    __syncthreads();  // both waves have scanned the previous histogram
 #pragma unroll
     for (int w = 0; w < 17; ++w)
       if (wv * 17 + w < 33) Hs[(wv * 17 + w) * kWave] = 0u;
@@ -243,13 +275,18 @@ __global__ __launch_bounds__(kPairBlock) void orderstat_pair_kernel(
       hist_inc(hb, (rel + f.pad) >> f.sh);
     }
     __syncthreads();
-    uint32_t da, db;
-    int ba, ca, bb, cb;
-    const int ra = pick2 ? r2 - s2.below : r1 - s1.below;
-    hist_scan<true, 32>(Hs, ra, r2 - s2.below, da, ba, ca, db, bb, cb);
-    refine_apply(s2, f, need && shared, db, bb, cb);
-    refine_apply(s2, f, need && pick2, da, ba, ca);
-    refine_apply(s1, f, need && !pick2, da, ba, ca);
+    if (wv == 0) {
+      uint32_t da, db;
+      int ba, ca, bb, cb;
+      const int ra = pick2 ? r2 - s2.below : r1 - s1.below;
+      hist_scan<true, 32>(Hs, ra, r2 - s2.below, da, ba, ca, db, bb, cb);
+      refine_apply(s2, f, need && shared, db, bb, cb);
+      refine_apply(s2, f, need && pick2, da, ba, ca);
+      refine_apply(s1, f, need && !pick2, da, ba, ca);
+      sel_put(xsel, lane, s1, s2);
+    }
+    __syncthreads();
+    if (wv == 1) sel_get(xsel, lane, s1, s2);
     shared = same_bin(s1, s2);
   }
 
@@ -261,7 +298,6 @@ __global__ __launch_bounds__(kPairBlock) void orderstat_pair_kernel(
   double mid = 0.0;
   int c = 0;
   fence_regs<H>(u);
-  __syncthreads();
   if (__any(list1 || list2) || MODE == kTrimmed)
     pair_compact<H, MODE>(u, nw, n, wv == 0,
                           wv ? hb | (kPairTop << 8) : hb,
