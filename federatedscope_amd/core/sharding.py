@@ -451,7 +451,7 @@ class PeerAssembly:
                       'fsagg_peer_status_alloc')
         self._st_host, self._st_dev = int(hs.value), int(ds.value)
         self._status = ctypes.c_uint32.from_address(self._st_host)
-        self._ev = torch.cuda.Event()
+        self._done = ctypes.c_uint32.from_address(self._st_host + 4)
         self._pending = None       # a views-mode round not yet checked
 
     # -- allocation plumbing ------------------------------------------------
@@ -553,21 +553,41 @@ class PeerAssembly:
             res.copy_(own[:self.numel])
             self.check()
             return res
-        prev = self._pending
-        self._pending = ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
+        prev, self._pending = self._pending, self.epoch
         if prev is not None:
-            prev.synchronize()
+            self._wait_done(prev)
             self._raise_status()
         return own[:self.numel]
 
     def _barrier(self):
-        st = torch.cuda.current_stream(self.device).cuda_stream
         ticks = int(self.TIMEOUT_S * 1e8)
         self._L.check(self._lib.fsagg_peer_barrier(
             self._flags, self.world, self.rank, self.epoch & 0xFFFFFFFF,
-            ticks, self._st_dev, st or None), 'fsagg_peer_barrier')
-        self._ev.record(torch.cuda.current_stream(self.device))
+            ticks, self._st_dev, ops._stream(self.device)),
+            'fsagg_peer_barrier')
+        self._issued = self.epoch
+
+    def _wait_done(self, epoch):
+        """Spin until the barrier of ``epoch`` has run (its status[1] word
+        in pinned host memory), bounded by the barrier's own timeout plus a
+        margin for the work queued before it."""
+        import time
+        want = epoch & 0xFFFFFFFF
+        if ((self._done.value - want) & 0xFFFFFFFF) < 0x80000000:
+            return
+        t0 = time.perf_counter()
+        limit = self.TIMEOUT_S + 60.0
+        spins = 0
+        while ((self._done.value - want) & 0xFFFFFFFF) >= 0x80000000:
+            spins += 1
+            if spins & 0xFFF:
+                continue        # a plain spin first: a sleep costs ~60 us
+            t = time.perf_counter() - t0
+            if t > limit:
+                raise RuntimeError('peer barrier of round %d never ran' %
+                                   epoch)
+            if t > 0.05:
+                time.sleep(1e-4)
 
     def _raise_status(self):
         v = int(self._status.value)
@@ -583,7 +603,8 @@ class PeerAssembly:
         are already up, and the ranks' epochs meet again at the next round,
         which then succeeds (the plan stays cached — rebuilding it would be
         a collective the late peer is not in)."""
-        self._ev.synchronize()
+        if getattr(self, '_issued', None) is not None:
+            self._wait_done(self._issued)
         self._pending = None
         self._raise_status()
 

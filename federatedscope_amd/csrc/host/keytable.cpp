@@ -136,6 +136,51 @@ PyObject *device_tensor(PyObject *, PyObject *args) {
   return THPVariable_Wrap(t);
 }
 
+// views(flat, spec) -> list[Tensor]
+// Views of a flat device bucket in one call: spec is bytes of int64 records
+// [ndim, shape[ndim], stride[ndim], offset] (BucketLayout.unpack's per-key
+// shape, contiguous strides and bucket offset).  The drop-in's result
+// emission made one as_strided call per key from Python (~0.7 us each: 110
+// us for the 161 keys of ResNet-50).
+PyObject *views(PyObject *, PyObject *args) {
+  PyObject *obj;
+  Py_buffer spec{};
+  if (!PyArg_ParseTuple(args, "Oy*", &obj, &spec)) return nullptr;
+  if (!THPVariable_Check(obj)) {
+    PyBuffer_Release(&spec);
+    PyErr_SetString(PyExc_TypeError, "views: flat must be a tensor");
+    return nullptr;
+  }
+  const at::Tensor &flat = THPVariable_Unpack(obj);
+  const auto *r = static_cast<const int64_t *>(spec.buf);
+  const size_t nw = size_t(spec.len) / sizeof(int64_t);
+  const int64_t base = flat.storage_offset();
+  PyObject *out = PyList_New(0);
+  size_t i = 0;
+  bool ok = out != nullptr;
+  while (ok && i < nw) {
+    const int64_t nd = r[i];
+    if (nd < 0 || i + 2 + 2 * size_t(nd) > nw) {
+      PyErr_SetString(PyExc_ValueError, "views: malformed spec");
+      ok = false;
+      break;
+    }
+    std::vector<int64_t> shape(r + i + 1, r + i + 1 + nd);
+    std::vector<int64_t> stride(r + i + 1 + nd, r + i + 1 + 2 * nd);
+    const int64_t off = r[i + 1 + 2 * nd];
+    i += 2 + 2 * size_t(nd);
+    PyObject *t = THPVariable_Wrap(flat.as_strided(shape, stride, base + off));
+    if (!t || PyList_Append(out, t) != 0) ok = false;
+    Py_XDECREF(t);
+  }
+  PyBuffer_Release(&spec);
+  if (!ok) {
+    Py_XDECREF(out);
+    return nullptr;
+  }
+  return out;
+}
+
 // text_copy(text, lo, hi, dst_addr[, threads]) -> None
 // Copy characters [lo, hi) of a base64 upload into host memory at dst_addr
 // (a pinned staging buffer; core/compression/b64wire.B64Stager).  `text` is
@@ -318,6 +363,8 @@ PyMethodDef kMethods[] = {
      "text_copy_many([(text, lo, hi, off)], dst_addr[, threads])"},
     {"text_copy", text_copy, METH_VARARGS,
      "text_copy(text, lo, hi, dst_addr[, threads]): copy chars [lo, hi)"},
+    {"views", views, METH_VARARGS,
+     "views(flat, spec_bytes) -> [Tensor]: as_strided views per record"},
     {"key_table", key_table, METH_VARARGS,
      "key_table(dicts, keys, shapes, device_index[, offs4]) -> (bytes, "
      "missing, aligned16) or None"},

@@ -27,8 +27,10 @@ struct Flags {
 // this rank, then waits until this rank's word for rank t reaches `epoch`.
 // The flag words are uncached; the stores are release and the loads acquire
 // at system scope.  The spin is bounded: after `timeout` ticks of the
-// 100 MHz constant clock the lane sets *status and gives up, so the grid
+// 100 MHz constant clock the lane sets status[0] and gives up, so the grid
 // always drains (a lost peer becomes an error the host reads, not a hang).
+// Last, lane 0 stores `epoch` into status[1]: the host (status in mapped
+// pinned memory) sees the barrier done without an event or a copy.
 __global__ void peer_barrier_kernel(Flags f, int world, int rank,
                                     uint32_t epoch, uint64_t timeout,
                                     uint32_t *status) {
@@ -49,6 +51,9 @@ __global__ void peer_barrier_kernel(Flags f, int world, int rank,
       __builtin_amdgcn_s_sleep(2);
     }
   }
+  if (t == 0)
+    __hip_atomic_store(status + 1, epoch, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 struct Dsts {

@@ -204,11 +204,40 @@ class BucketLayout:
                     acc *= d
                 spec[k] = (shp, tuple(reversed(st)), self.offsets[k])
             self.__dict__['_view_spec'] = spec
+        ks = self.keys if keys is None else keys
+        if len(ks) > 8:
+            # many keys: every view in one native call
+            packed = self.__dict__.get('_view_pack')
+            if packed is None or packed[0] is not ks and packed[0] != ks:
+                import numpy as np
+                rec = []
+                for k in ks:
+                    shp, st, off = spec[k]
+                    rec += [len(shp)] + list(shp) + list(st) + [off]
+                packed = (list(ks), np.asarray(rec, np.int64).tobytes())
+                self.__dict__['_view_pack'] = packed
+            host = _views_ext()
+            if host is not None:
+                return OrderedDict(zip(ks, host.views(flat, packed[1])))
         view = flat.as_strided
         base = flat.storage_offset()
         return OrderedDict([(k, view(spec[k][0], spec[k][1],
-                                     base + spec[k][2]))
-                            for k in (self.keys if keys is None else keys)])
+                                     base + spec[k][2])) for k in ks])
+
+
+_VIEWS = []
+
+
+def _views_ext():
+    """_fsagg_host (its ``views``), or None when it was not built."""
+    if not _VIEWS:
+        try:
+            from . import _lib
+            h = _lib.host()
+            _VIEWS.append(h if hasattr(h, 'views') else None)
+        except Exception:  # noqa: BLE001 (no extension: per-key views)
+            _VIEWS.append(None)
+    return _VIEWS[0]
 
 
 # Pinned staging buffers are shared by every HostStager of the process, so

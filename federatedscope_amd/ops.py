@@ -38,7 +38,7 @@ class _PinnedRing:
     # device tensors; each is marked used (record_stream) by every stream
     # it is handed to, so the caching allocator recycles an evicted entry's
     # block only after the work that read it.
-    CACHE_MAX_BYTES = 64 << 10
+    CACHE_MAX_BYTES = 1 << 20      # = SLOT: the ResNet-50 key table fits
     CACHE_ENTRIES = 512
 
     def __init__(self):

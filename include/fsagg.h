@@ -574,9 +574,11 @@ int fsagg_normbound_prescale_f32(const double *sq, int n, int nseg,
  *                    rank's array reached `epoch` (epochs increase by one
  *                    per call; compared modulo 2^32).  A wait longer than
  *                    `timeout_ticks` of the 100 MHz constant clock stores
- *                    1 + the missing rank into *status (device-visible:
- *                    device memory, or the mapped host word of
- *                    fsagg_peer_status_alloc) and ends instead of hanging.
+ *                    1 + the missing rank into status[0] and ends instead
+ *                    of hanging; on exit the barrier stores `epoch` into
+ *                    status[1].  status: two device-visible words (the
+ *                    mapped host block of fsagg_peer_status_alloc, which the
+ *                    host reads without a copy, or device memory).
  * fsagg_peer_status_alloc  a zeroed 64-byte word block in pinned, mapped
  *                    host memory: *host for the host to read once the
  *                    barrier's stream has passed it (no device-to-host
