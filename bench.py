@@ -174,12 +174,16 @@ def plugin_surface_leg(args, dev, slab, rows, sizes, w_dev, P, rounds=5,
     }
 
 
-def plugin_layout_b_leg(dev, sizes, w_dev, rounds=5, calls=10):
+def plugin_layout_b_leg(dev, sizes, w_dev, rounds=5, calls=10,
+                        separate=False):
     """configs[2] layout B: the same call on the ResNet-50 layout (161 keys,
     tools/resnet50_layout.json) — 100 device-resident multi-key state_dicts
-    whose keys are views of one slab per client (read in place; the
-    multi-key row-set kernel), against the bare flat kernel over the same
-    slab rows, interleaved, every key compared bit for bit."""
+    whose keys are views of one slab row per client laid out as the bucket
+    (read in place; a uniform row set: the flat kernel over each client's
+    range), or with ``separate`` every key its own allocation (a per-module
+    state_dict: the multi-key row-set kernel) — against the bare flat
+    kernel over the same slab rows, interleaved, every key compared bit for
+    bit."""
     import statistics
     from collections import OrderedDict
     from types import SimpleNamespace
@@ -199,6 +203,9 @@ def plugin_layout_b_leg(dev, sizes, w_dev, rounds=5, calls=10):
     clients = [(sizes[i], OrderedDict(
         (k, slab[i, lay.offsets[k]:lay.offsets[k] + lay.numels[k]].view(
             lay.shapes[k])) for k in lay.keys)) for i in range(n)]
+    if separate:
+        clients = [(s, OrderedDict((k, v.clone()) for k, v in d.items()))
+                   for s, d in clients]
     cfg = SimpleNamespace(federate=SimpleNamespace(ignore_weight=False,
                                                    use_ss=False))
     agg = ClientsAvgAggregator(device=dev, config=cfg)
@@ -228,17 +235,22 @@ def plugin_layout_b_leg(dev, sizes, w_dev, rounds=5, calls=10):
             torch.cuda.synchronize()
             acc.append((time.perf_counter() - t0) / calls * 1e3)
     a, f = statistics.median(t_agg), statistics.median(t_flat)
-    log('layout B (%d keys, %d params): aggregate() %.4f ms/call, bare flat '
-        'kernel %.4f ms (ratio %.4f), bit-exact %s' %
-        (len(keys), P, a, f, a / f, exact))
-    del slab, rows
+    log('layout B (%d keys, %d params, %s): aggregate() %.4f ms/call, bare '
+        'flat kernel %.4f ms (ratio %.4f), bit-exact %s' %
+        (len(keys), P, 'separate tensors' if separate else 'slab views', a,
+         f, a / f, exact))
+    del slab, rows, clients, info
+    torch.cuda.empty_cache()
     return {
         'what': 'ClientsAvgAggregator.aggregate(agg_info) on %d device '
-                'dicts of the ResNet-50 layout (%d keys, %d fp32 params; '
-                'views of one slab row per client, read in place) against '
-                'the flat kernel over the same rows; median of %d '
-                'interleaved rounds of %d calls' % (n, len(keys), P, rounds,
-                                                    calls),
+                'dicts of the ResNet-50 layout (%d keys, %d fp32 params; %s, '
+                'read in place) against the flat kernel over the same '
+                'values; median of %d interleaved rounds of %d calls' % (
+                    n, len(keys), P,
+                    'every key a separate allocation (row-set kernel)'
+                    if separate else 'views of one slab row per client laid '
+                    'out as the bucket (uniform row set: flat kernel)',
+                    rounds, calls),
         'keys': len(keys),
         'params': P,
         'ms_per_call': round(a, 4),
@@ -764,11 +776,12 @@ def main():
         (t_step * 1e3, kern_ms, t_sharded * 1e3, mean_launch_ms, achieved,
          ok))
 
-    plugin = plugin_b = None
+    plugin = plugin_b = plugin_bs = None
     if world == 1 and not args.no_plugin:
         plugin = plugin_surface_leg(args, dev, pieces[0][0], pieces[0][1],
                                     sizes, w_dev, P)
         plugin_b = plugin_layout_b_leg(dev, sizes, w_dev)
+        plugin_bs = plugin_layout_b_leg(dev, sizes, w_dev, separate=True)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -865,6 +878,7 @@ def main():
             'weak_scaling': weak,
             'plugin_surface': plugin,
             'plugin_surface_layout_b': plugin_b,
+            'plugin_surface_layout_b_separate': plugin_bs,
             'assembled_bit_exact': ok,
         }
         print(json.dumps(rec), flush=True)

@@ -348,11 +348,13 @@ class DeviceEngine:
             res = host.key_table(dicts, kl[0], kl[1], dev.index)
         if res is None:
             return None
-        raw, missing, aligned = res
+        raw, missing, aligned = res[:3]
         shape = (len(kl[0]), len(dicts)) if virtual else (len(dicts),
                                                             len(kl[0]))
-        return np.frombuffer(raw, dtype=np.int64).reshape(shape), aligned, \
-            missing
+        tab = np.frombuffer(raw, dtype=np.int64).reshape(shape)
+        if virtual:
+            return tab, aligned, missing, bool(res[3])
+        return tab, aligned, missing
 
     def _base(self, layout, model, as_float=False):
         """The server model as the kernels' ``base`` operand: its own device
@@ -499,7 +501,7 @@ class DeviceEngine:
         if not layout.other:
             kt = self._key_table(layout, dicts, virtual=True)
             if kt is not None and kt[1]:
-                virt, _, nmiss = kt
+                virt, _, nmiss, uniform = kt
                 gone = 0
                 if nmiss:        # absent keys (an empty key never counts)
                     absent = ops.absent(layout, virt.T)
@@ -510,7 +512,7 @@ class DeviceEngine:
                     gone = int(absent.sum())
                 return StagedSet(layout, ops.RowSet.from_virtual(
                     layout, virt, self.compute_device, keepalive=(dicts, ),
-                    missing=gone))
+                    missing=gone, uniform=uniform))
         # staged through a device stack
         layout = self._layout(d0, as_float=as_float)
         present = [[k in d for k in layout.keys] for d in dicts]

@@ -22,7 +22,10 @@
 // error: the caller then stages the dicts instead.
 // With offs4 the table is the device row table itself (include/fsagg.h
 // fsagg_rows): segment-major [key][client] virtual bases ptr - offs4[key]
-// (0 stays 0), so the caller uploads it as is.
+// (0 stays 0), so the caller uploads it as is; the result then carries a
+// fourth item, uniform: no key is missing and every client's keys are views
+// of one storage at their bucket offsets (one virtual base per client — the
+// client's whole bucket is a contiguous range of that storage).
 #include <ATen/ATen.h>
 #include <Python.h>
 #include <torch/csrc/autograd/python_variable.h>
@@ -81,9 +84,15 @@ PyObject *key_table(PyObject *, PyObject *args) {
   auto *out = reinterpret_cast<int64_t *>(&buf[0]);
   Py_ssize_t missing = 0;
   bool aligned = true;
+  // uniform (virtual mode): every client's keys are views of ONE storage at
+  // exactly their bucket offsets (one virtual base per client), so the
+  // client's bucket is that storage's contiguous range
+  bool uniform = offs != nullptr;
   for (Py_ssize_t i = 0; i < n; ++i) {
     PyObject *d = PyList_GET_ITEM(dicts, i);
     if (!PyDict_Check(d)) Py_RETURN_NONE;
+    int64_t vb0 = 0;
+    const void *st0 = nullptr;
     for (Py_ssize_t s = 0; s < nk; ++s) {
       PyObject *v = PyDict_GetItemWithError(d, PyList_GET_ITEM(keys, s));
       // [client][key], or segment-major [key][client] with offsets
@@ -95,22 +104,45 @@ PyObject *key_table(PyObject *, PyObject *args) {
         continue;
       }
       if (!THPVariable_Check(v)) Py_RETURN_NONE;
-      const at::Tensor &t = THPVariable_Unpack(v);
-      if (t.scalar_type() != at::kFloat || !t.is_cuda() ||
-          t.get_device() != device_index || !t.is_contiguous())
+      // the TensorImpl directly: no Tensor / Storage handles (and their
+      // refcount traffic) per key — 16,100 keys at 100 x ResNet-50
+      const c10::TensorImpl *t =
+          THPVariable_Unpack(v).unsafeGetTensorImpl();
+      const c10::Device dv = t->device();
+      if (t->dtype() != caffe2::TypeMeta::Make<float>() || !dv.is_cuda() ||
+          dv.index() != device_index || !t->is_contiguous())
         Py_RETURN_NONE;
-      const auto sz = t.sizes();
+      const auto sz = t->sizes();
       if (sz.size() != shp[s].size()) Py_RETURN_NONE;
       for (size_t j = 0; j < sz.size(); ++j)
         if (sz[j] != shp[s][j]) Py_RETURN_NONE;
-      const auto p = reinterpret_cast<uintptr_t>(t.data_ptr());
-      if (p == 0 && t.numel() > 0) Py_RETURN_NONE;
+      const int64_t numel = t->numel();
+      const void *data = t->storage().data();
+      const auto p = data == nullptr ? uintptr_t(0)
+                                     : reinterpret_cast<uintptr_t>(data) +
+                                           uintptr_t(t->storage_offset()) * 4u;
+      if (p == 0 && numel > 0) Py_RETURN_NONE;
       aligned = aligned && (p & 15u) == 0;
       slot = p ? int64_t(p) - off4[s] : 0;
+      if (uniform) {
+        const void *st = data;
+        if (numel == 0 || st == nullptr) {
+          uniform = false;
+        } else if (s == 0) {
+          vb0 = slot;
+          st0 = st;
+        } else if (slot != vb0 || st != st0) {
+          uniform = false;
+        }
+      }
     }
   }
   PyObject *bytes = PyBytes_FromStringAndSize(buf.data(), Py_ssize_t(buf.size()));
   if (!bytes) return nullptr;
+  if (offs)
+    return Py_BuildValue("(NnOO)", bytes, missing, aligned ? Py_True : Py_False,
+                         (uniform && missing == 0 && nk > 0) ? Py_True
+                                                             : Py_False);
   return Py_BuildValue("(NnO)", bytes, missing, aligned ? Py_True : Py_False);
 }
 

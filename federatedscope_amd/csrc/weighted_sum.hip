@@ -213,24 +213,47 @@ __device__ __forceinline__ void put1(float *out, int64_t p, float a) {
 __device__ __forceinline__ void put1(const Bcast &o, int64_t p, float a) {
   for (int k = 0; k < o.n; ++k) o.p[k][p] = a;
 }
+// The < 4 elements past the last float4 column.  One block: the n client
+// values of each tail element are loaded 256 clients at a time by all the
+// threads together (one memory latency per 256 clients, where a single
+// thread walking the clients waited out n dependent loads: 45 us at n =
+// 100), then thread e adds them up for element e in client order from LDS.
+constexpr int kTailBlock = 256;
 template <class O = float *>
-__global__ void wsum_f32_tail_kernel(const float *const *__restrict__ rows,
-                                     const float *__restrict__ w,
-                                     const float *__restrict__ pre, int n,
-                                     int64_t start, int64_t numel,
-                                     const float *__restrict__ base, O out) {
-  const int64_t p = start + threadIdx.x;
-  if (p >= numel) return;
-  float x = gld(rows[0] + p);
-  if (pre) x = mul_rn(x, pre[0]);
-  float acc = mul_rn(x, w[0]);
-  for (int i = 1; i < n; ++i) {
-    float t = gld(rows[i] + p);
-    if (pre) t = mul_rn(t, pre[i]);
-    acc = add_rn(acc, mul_rn(t, w[i]));
+__global__ __launch_bounds__(kTailBlock) void wsum_f32_tail_kernel(
+    const float *const *__restrict__ rows, const float *__restrict__ w,
+    const float *__restrict__ pre, int n, int64_t start, int64_t numel,
+    const float *__restrict__ base, O out) {
+  __shared__ float xs[3][kTailBlock];
+  const int m = int(numel - start);  // 1..3
+  const int e = threadIdx.x;
+  float acc = 0.0f;
+  for (int c0 = 0; c0 < n; c0 += kTailBlock) {
+    const int c = c0 + threadIdx.x;
+    if (c < n) {
+      const float *r = rows[c];
+      const float s = pre ? pre[c] : 1.0f;
+      for (int k = 0; k < m; ++k) {
+        float x = gld(r + start + k);
+        if (pre) x = mul_rn(x, s);
+        xs[k][threadIdx.x] = x;
+      }
+    }
+    __syncthreads();
+    if (e < m) {
+      const int cn = n - c0 < kTailBlock ? n - c0 : kTailBlock;
+      for (int j = 0; j < cn; ++j) {
+        const float t = mul_rn(xs[e][j], w[c0 + j]);
+        acc = c0 + j == 0 ? t : add_rn(acc, t);
+      }
+    }
+    __syncthreads();
   }
-  if (base) acc = add_rn(base[p], acc);
-  put1(out, p, acc);
+  if (e < m) {
+    const int64_t p = start + e;
+    if (base) acc = add_rn(base[p], acc);
+    put1(out, p, acc);
+  }
 }
 
 // Launch shape of the streaming kernel, from interleaved timing on MI355X
@@ -296,8 +319,9 @@ void launch_wsum_any(const float *const *rows, const float *weights,
     }
   }
   if (numel > nvec * 4) {
-    hipLaunchKernelGGL((wsum_f32_tail_kernel<O>), dim3(1), dim3(kWave), 0, s,
-                       rows, weights, prescale, n, nvec * 4, numel, base, out);
+    hipLaunchKernelGGL((wsum_f32_tail_kernel<O>), dim3(1), dim3(kTailBlock),
+                       0, s, rows, weights, prescale, n, nvec * 4, numel, base,
+                       out);
   }
 }
 

@@ -805,7 +805,7 @@ class RowSet:
     copy ([n][1] for a stack without absent keys, else [n][nseg])."""
 
     def __init__(self, layout, table, device, keepalive=(), aligned16=True,
-                 missing=None, segmajor=None):
+                 missing=None, segmajor=None, uniform=False):
         if segmajor is not None:
             # the device layout built by the caller ([nseg][n]); the host
             # copy is its transposed view
@@ -838,6 +838,11 @@ class RowSet:
         self.struct = L.Rows(self.tab.data_ptr(), self.ss, self.n,
                              self.nseg)
         self._keep = tuple(keepalive)
+        # uniform: every client's keys lie in ONE storage at their bucket
+        # offsets (csrc/host/keytable.cpp), so client i's bucket is the
+        # contiguous range at its virtual base — the flat kernels apply
+        self.uniform = bool(uniform) and self.missing == 0 and \
+            self.host.shape[1] == self.nseg
 
     @classmethod
     def from_stack(cls, stack, slots, present=None, offset=0):
@@ -872,11 +877,14 @@ class RowSet:
 
     @classmethod
     def from_virtual(cls, layout, segmajor, device, keepalive=(),
-                     aligned16=True, missing=None):
+                     aligned16=True, missing=None, uniform=False):
         """[nseg][n] virtual bases (0: absent), i.e. the device table as
-        csrc/host/keytable.cpp builds it with offsets."""
+        csrc/host/keytable.cpp builds it with offsets (``uniform``: its
+        report that each client's keys are views of one storage at their
+        bucket offsets)."""
         return cls(layout, None, device, keepalive=keepalive,
-                   aligned16=aligned16, missing=missing, segmajor=segmajor)
+                   aligned16=aligned16, missing=missing, segmajor=segmajor,
+                   uniform=uniform)
 
     def subset(self, sel):
         """The clients ``sel`` (indices, in the new reduction order)."""
@@ -967,10 +975,13 @@ def weighted_sum_rows(rs, weights, out, prescale=None, base=None, lo=0,
 
 
 def _flat_rows(rs, base):
-    """Whether a row set runs the flat streaming kernel (one key, every
-    client holding it)."""
-    return rs.nseg == 1 and not rs.missing and bool(rs.layout.keys) and (
-        base is None or base.host is not None)
+    """Whether a row set runs the flat streaming kernel: one key every
+    client holds, or a uniform row set (each client's keys laid out in one
+    storage exactly as the bucket: its bucket is one contiguous range, the
+    padding between keys included, which lies inside that storage)."""
+    return (rs.nseg == 1 or getattr(rs, 'uniform', False)) and \
+        not rs.missing and bool(rs.layout.keys) and (
+            base is None or (base.host is not None and len(base.host) == 1))
 
 
 def weighted_sum_rows_bcast(rs, weights, out, peers, prescale=None,
@@ -994,8 +1005,13 @@ def weighted_sum_rows_bcast(rs, weights, out, peers, prescale=None,
 
 def _weighted_sum_rows_flat(rs, weights, out, prescale, base, lo, hi, lib,
                             peers=None):
-    k = rs.layout.keys[0]
-    o, m = rs.layout.offsets[k], rs.layout.numels[k]
+    if rs.nseg == 1:
+        k = rs.layout.keys[0]
+        o, m = rs.layout.offsets[k], rs.layout.numels[k]
+    else:          # uniform: the bucket up to the last key's end (the
+        # storage holds every key, so everything before it too)
+        last = rs.layout.keys[-1]
+        o, m = 0, rs.layout.offsets[last] + rs.layout.numels[last]
     a = max(int(lo), o)
     b = min(int(hi) if hi is not None else rs.layout.numel, o + m)
     if b <= a:

@@ -76,8 +76,8 @@ def test_host_extension_key_table_without_gpu():
         h.key_table(d, ['a'], [], 0)
     # the device-table form (per-key byte offsets): same checks
     assert h.key_table(d, ['a', 'b'], [(3, ), (2, 2)], 0, [0, 64]) is None
-    raw, missing, aligned = h.key_table(d, [], [], 0, [])
-    assert raw == b'' and missing == 0 and aligned
+    raw, missing, aligned, uniform = h.key_table(d, [], [], 0, [])
+    assert raw == b'' and missing == 0 and aligned and not uniform
     with pytest.raises(ValueError):
         h.key_table(d, ['a', 'b'], [(3, ), (2, 2)], 0, [0])
 
