@@ -237,6 +237,13 @@ template <int H, int MODE>
 void launch_pair(const RowSrc &rs, unsigned grid, int n, int kk, float divisor,
                  float *out, hipStream_t s);
 
+// Launch the K-wave select kernel (orderstat_group.h) for 255 < n <= 512;
+// false when n is outside its range (the caller streams instead).  Its grid
+// is one block of K·64 threads per 64 coordinates, as launch_pair's.
+template <int MODE>
+bool launch_group(const RowSrc &rs, unsigned grid, int n, int kk,
+                  float divisor, float *out, hipStream_t s);
+
 // Launch the streaming select kernel for 255 < n <= 65535
 // (orderstat_stream.hip).
 template <int MODE>

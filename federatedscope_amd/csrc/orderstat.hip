@@ -166,6 +166,9 @@ __global__ __launch_bounds__(kBlock) void orderstat_generic_kernel(
 // Clients from which 64 < n <= 255 takes the two-wave kernel;
 // fsagg_orderstat_set_pair_min() moves it for A/B measurements.
 std::atomic<int> g_pair_min{kPairMinDefault};
+// Clients up to which 255 < n takes the K-wave kernel (orderstat_group.h);
+// fsagg_orderstat_set_group_max() moves it for A/B measurements.
+std::atomic<int> g_group_max{512};
 
 template <int MODE>
 int launch(const RowSrc &rs, int nchunk, int n, int kk, float divisor,
@@ -222,7 +225,13 @@ int launch(const RowSrc &rs, int nchunk, int n, int kk, float divisor,
     case 256: FSAGG_SEL(256); break;
     }
   } else if (n <= 65535 && rs.numel <= (int64_t(1) << 30)) {
-    launch_stream<MODE>(rs, grid, n, kk, divisor, out, s);
+    // one HBM pass with the column split over a workgroup's waves, up to
+    // n = 512 (g_group_max moves it for A/B); the streaming kernel above
+    const unsigned ggrid = rs.chunks ? unsigned(nchunk) * 4u
+                                     : unsigned((rs.numel + kWave - 1) / kWave);
+    if (n > g_group_max.load(std::memory_order_relaxed) ||
+        !launch_group<MODE>(rs, ggrid, n, kk, divisor, out, s))
+      launch_stream<MODE>(rs, grid, n, kk, divisor, out, s);
   } else {
     hipLaunchKernelGGL((orderstat_generic_kernel<MODE>), dim3(grid),
                        dim3(kBlock), 0, s, rs, n, kk, divisor, out);
@@ -321,4 +330,8 @@ extern "C" int fsagg_trimmed_mean_rows_f32(const fsagg_rows *rows,
 
 extern "C" int fsagg_orderstat_set_pair_min(int n) {
   return g_pair_min.exchange(n < 0 ? kPairMinDefault : n);
+}
+
+extern "C" int fsagg_orderstat_set_group_max(int n) {
+  return g_group_max.exchange(n < 0 ? 512 : n);
 }

@@ -446,6 +446,10 @@ int fsagg_trimmed_mean_rows_f32(const fsagg_rows *rows,
  * within the stated tolerance.  n < 0 restores the default; returns the
  * previous value.  Process-wide; for A/B measurements. */
 int fsagg_orderstat_set_pair_min(int n);
+/* The same for 255 < n: up to this many clients (at most 512, the default)
+ * the K-wave kernel reads each column once, the rows split over a
+ * workgroup's waves; above it the one-lane streaming kernel (two passes). */
+int fsagg_orderstat_set_group_max(int n);
 
 /* Krum per-key squared distances over a row set: segment s covers
  * [seg_lo[s], seg_end[s]) (device int64 arrays; keys may leave gaps between

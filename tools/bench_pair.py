@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""A/B of the order-statistic kernels for 64 < n <= 255: the two-wave form
-(csrc/orderstat_pair.h) against the one-wave register select, interleaved
+"""A/B of the order-statistic kernels: for 64 < n <= 255 the two-wave form
+(csrc/orderstat_pair.h) against the one-wave register select, for
+255 < n <= 512 the K-wave form (csrc/orderstat_group.h, "two_wave" in the
+output) against the two-pass streaming kernel ("one_wave"), interleaved
 call by call in one process (fsagg_orderstat_set_pair_min moves the
 dispatch), on C5-style data (N(0,1), 10 % of clients x100) at a fixed
 4·n·P ≈ 5.3 GB (C5 itself at n = 200).  One JSON line per (n, rule).
@@ -67,6 +69,10 @@ def main():
             def run(thr, rule=rule):
                 def fn():
                     lib.fsagg_orderstat_set_pair_min(thr)
+                    # n > 255: the K-wave kernel (thr 65) against the
+                    # two-pass streaming kernel (thr 256)
+                    lib.fsagg_orderstat_set_group_max(512 if thr == 65
+                                                      else 255)
                     if rule == 'median':
                         ops.coord_median(rows, out, base=base)
                     else:
@@ -83,6 +89,7 @@ def main():
                 'one_wave_hbm_frac': round(nbytes / one / 1e6 / 8000.0, 4)}),
                 flush=True)
         lib.fsagg_orderstat_set_pair_min(-1)
+        lib.fsagg_orderstat_set_group_max(-1)
         del slab, rows, base, out
         torch.cuda.empty_cache()
 
