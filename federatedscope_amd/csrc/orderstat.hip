@@ -166,9 +166,19 @@ __global__ __launch_bounds__(kBlock) void orderstat_generic_kernel(
 // Clients from which 64 < n <= 255 takes the two-wave kernel;
 // fsagg_orderstat_set_pair_min() moves it for A/B measurements.
 std::atomic<int> g_pair_min{kPairMinDefault};
-// Clients up to which 255 < n takes the K-wave kernel (orderstat_group.h);
-// fsagg_orderstat_set_group_max() moves it for A/B measurements.
-std::atomic<int> g_group_max{512};
+// The client range [lo, hi] of 255 < n that takes the K-wave kernel
+// (orderstat_group.h), per mode (median, trimmed mean), from interleaved
+// A/B against the two-pass streaming kernel at 5.3 GB
+// (profiles/r05/orderstat_group_ab.jsonl): the median gains from n = 384
+// (n = 500: 1.21 against 1.50 ms) and loses at n = 300 (1.56 / 1.47); the
+// trimmed mean's serial list tail in wave 0 keeps it behind (n = 500:
+// 1.94 / 1.88), so it streams.  fsagg_orderstat_set_group_max() opens the
+// whole range to both modes for tests and A/B.
+constexpr int kGroupDefault[2][2] = {{384, 512}, {513, 512}};
+std::atomic<int> g_group[2][2] = {{{kGroupDefault[0][0]},
+                                   {kGroupDefault[0][1]}},
+                                  {{kGroupDefault[1][0]},
+                                   {kGroupDefault[1][1]}}};
 
 template <int MODE>
 int launch(const RowSrc &rs, int nchunk, int n, int kk, float divisor,
@@ -229,7 +239,9 @@ int launch(const RowSrc &rs, int nchunk, int n, int kk, float divisor,
     // n = 512 (g_group_max moves it for A/B); the streaming kernel above
     const unsigned ggrid = rs.chunks ? unsigned(nchunk) * 4u
                                      : unsigned((rs.numel + kWave - 1) / kWave);
-    if (n > g_group_max.load(std::memory_order_relaxed) ||
+    const std::atomic<int> *rg = g_group[MODE == kMedian ? 0 : 1];
+    if (n < rg[0].load(std::memory_order_relaxed) ||
+        n > rg[1].load(std::memory_order_relaxed) ||
         !launch_group<MODE>(rs, ggrid, n, kk, divisor, out, s))
       launch_stream<MODE>(rs, grid, n, kk, divisor, out, s);
   } else {
@@ -333,5 +345,10 @@ extern "C" int fsagg_orderstat_set_pair_min(int n) {
 }
 
 extern "C" int fsagg_orderstat_set_group_max(int n) {
-  return g_group_max.exchange(n < 0 ? 512 : n);
+  const int prev = g_group[0][1].load();
+  for (int m = 0; m < 2; ++m) {
+    g_group[m][0] = n < 0 ? kGroupDefault[m][0] : 256;
+    g_group[m][1] = n < 0 ? kGroupDefault[m][1] : n;
+  }
+  return prev;
 }

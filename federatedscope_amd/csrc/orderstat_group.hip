@@ -15,10 +15,15 @@ void launch_group_h(const RowSrc &rs, unsigned grid, int n, int kk,
 template <int MODE>
 bool launch_group(const RowSrc &rs, unsigned grid, int n, int kk,
                   float divisor, float *out, hipStream_t s) {
-  const int K = (n + kGroupRows - 1) / kGroupRows;
-  if (n <= 255 || K > kGroupMaxWaves) return false;
+  // eight waves per block whatever n: two blocks (the LDS they take) fill a
+  // CU's 16 wave slots — five waves per block at n = 300 left 10 of 16 and
+  // ran slower than the two-pass streaming kernel
+  const int K = kGroupMaxWaves;
+  if (n <= 255 || n > K * kGroupRows) return false;
   const int per = (n + K - 1) / K;
   switch ((per + 7) / 8 * 8) {
+    case 32: launch_group_h<32, MODE>(rs, grid, n, kk, divisor, out, K, s); break;
+    case 40: launch_group_h<40, MODE>(rs, grid, n, kk, divisor, out, K, s); break;
     case 48: launch_group_h<48, MODE>(rs, grid, n, kk, divisor, out, K, s); break;
     case 56: launch_group_h<56, MODE>(rs, grid, n, kk, divisor, out, K, s); break;
     case 64: launch_group_h<64, MODE>(rs, grid, n, kk, divisor, out, K, s); break;

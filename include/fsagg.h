@@ -446,9 +446,12 @@ int fsagg_trimmed_mean_rows_f32(const fsagg_rows *rows,
  * within the stated tolerance.  n < 0 restores the default; returns the
  * previous value.  Process-wide; for A/B measurements. */
 int fsagg_orderstat_set_pair_min(int n);
-/* The same for 255 < n: up to this many clients (at most 512, the default)
- * the K-wave kernel reads each column once, the rows split over a
- * workgroup's waves; above it the one-lane streaming kernel (two passes). */
+/* The same for 255 < n: with n >= 0, every n in (255, n] (n <= 512) takes
+ * the K-wave kernel, which reads each column once with its rows split over
+ * a workgroup's waves, for both statistics; n < 0 restores the default
+ * (the median for 384 <= n <= 512, where it measured faster; otherwise the
+ * one-lane streaming kernel, two passes).  Returns the previous median
+ * upper bound.  For tests and A/B measurements. */
 int fsagg_orderstat_set_group_max(int n);
 
 /* Krum per-key squared distances over a row set: segment s covers
