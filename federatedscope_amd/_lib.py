@@ -119,11 +119,20 @@ SIGNATURES['fsagg_pairgram_rows_segsq_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_sz, _c_p])
 SIGNATURES['fsagg_pairgram_rows_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i64, ctypes.c_double, _c_p, _c_p, _c_p, _c_p,
-           _c_p, _c_p, _c_sz, _c_p])
+           _c_p, _c_p, _c_p, _c_sz, _c_p])
 SIGNATURES['fsagg_pairgram_finish_f32'] = (
-    _c_i, [_c_p, _c_p, _c_i, _c_i, ctypes.c_double, _c_p, _c_p, _c_p, _c_p])
+    _c_i, [_c_p, _c_p, _c_i, _c_i, ctypes.c_double, _c_p, _c_p, _c_p, _c_p,
+           _c_p])
 SIGNATURES['fsagg_pairdist_rows_segsq_f32'] = (
     _c_i, [_rows_p, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_sz, _c_p])
+SIGNATURES['fsagg_pairsel_workspace_bytes'] = (_c_sz, [_c_i, _c_i, _c_i])
+SIGNATURES['fsagg_pairsel_rows_segsq_f64'] = (
+    _c_i, [_rows_p, _c_p, _c_i, _c_p, _c_i, _c_p, _c_p, _c_sz, _c_p])
+SIGNATURES['fsagg_pairsel_finish_f64'] = (
+    _c_i, [_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_p])
+FSAGG_PAIRSEL_MAX_SEL = 32
+FSAGG_PAIRSEL_MAX_CLIENTS = 256
+FSAGG_PAIRSEL_CHUNK = 4096
 
 SIGNATURES['fsagg_online_inc_typed'] = (
     _c_i, [_c_p, _c_i, _c_p, _c_i, _c_p, _c_i, _c_i64, _c_i64, _c_i64, _c_p])

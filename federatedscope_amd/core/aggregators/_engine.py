@@ -236,6 +236,7 @@ class DeviceEngine:
         ``last_pair_bound`` None)."""
         from ... import _lib
         self.last_pair_bound = None
+        self.last_pair_cert = None
         if not 2 <= st.n <= _lib.FSAGG_PAIRGRAM_MAX_CLIENTS:
             return self._pairdist_valu(st)
         if st.plan is None:
@@ -249,27 +250,72 @@ class DeviceEngine:
         """D on the VALU kernel (fsagg_pairdist_*)."""
         self.last_pairdist_path = 'valu'
         self.last_pair_bound = None
+        self.last_pair_cert = None
         segsq = self._sum_pieces(
             st, lambda rs, lo, hi: ops.pairdist_rows_segsq(rs, lo, hi))
         return _PendingD(self, st, D=ops.pairdist_finish(segsq))
 
     def _certified_order(self, st, D, f, m, ordered):
         """(D, scores, order) for a Krum selection of ``m`` clients: from the
-        Gram path's D when its bounds certify the selection
+        Gram path's fp64 sums when their bounds certify the selection
         (:func:`certified_selection`; ``ordered``: the order of the first
-        ``m`` as well, which fixes a multi-Krum average's summation order),
-        else from D recomputed on the VALU kernel."""
+        ``m`` as well, which fixes a multi-Krum average's summation order);
+        else with the ambiguous clients' rows recomputed in fp64
+        (:meth:`_refine_selection`); else from D recomputed on the VALU
+        kernel."""
+        import numpy as np
         from .krum_aggregator import krum_scores
+        cert = self.last_pair_cert if self.last_pair_bound is not None \
+            else None
+        if cert is None:
+            scores = krum_scores(D, f)
+            return D, scores, torch.sort(scores)[1]
+        D64, B64 = cert
+        n = D64.shape[0]
+        k = n - f - 2
+        sc = np.sort(D64, 1)[:, :max(k, 0)].sum(1)
+        order = np.argsort(sc, kind='stable')
+        amb = ambiguous_clients(D64, B64, f, m, order, ordered)
+        if amb is not None and not amb:
+            return D, torch.from_numpy(sc), torch.from_numpy(order)
+        got = self._refine_selection(st, D64, B64, f, m, ordered, amb)
+        if got is not None:
+            sc, o, nrows = got
+            self.last_pairdist_path = 'mfma + exact rows %d of %d' % (
+                nrows, st.n)
+            return D, torch.from_numpy(sc), torch.from_numpy(o)
+        D = self._pairdist_valu(st).cpu()
+        self.last_pairdist_path = 'mfma, not certified: valu'
         scores = krum_scores(D, f)
         order = torch.sort(scores)[1]
-        B = self.last_pair_bound
-        if B is not None and not certified_selection(
-                D.numpy(), B, f, m, order.numpy(), ordered):
-            D = self._pairdist_valu(st).cpu()
-            self.last_pairdist_path = 'mfma, not certified: valu'
-            scores = krum_scores(D, f)
-            order = torch.sort(scores)[1]
         return D, scores, order
+
+    def _refine_selection(self, st, D, B, f, m, ordered, amb):
+        """:func:`refine_selection` with the ambiguous clients' rows from
+        the fp64 kernel (fsagg_pairsel_*, summed across ranks when
+        sharded); None when the client count is outside its range."""
+        from ... import _lib
+        if st.n > _lib.FSAGG_PAIRSEL_MAX_CLIENTS:
+            return None
+        nseg = max(1, len(st.layout.keys))
+        big = max([st.layout.numels[key] for key in st.layout.keys] or [1])
+        world = st.plan.comm.world if st.plan is not None else 1
+        # fp64 differences and squares, sums of at most `big` terms per key
+        # (+ slices, chunks and ranks), a sqrt and nseg adds per pair
+        rel = ((big + 64 + world) / 2 + nseg + 8) * 2.0 ** -53
+        return refine_selection(D, B, f, m, ordered, amb,
+                                lambda sel: self._exact_rows(st, sel), rel,
+                                _lib.FSAGG_PAIRSEL_MAX_SEL)
+
+    def _exact_rows(self, st, sel):
+        """fp64 host [len(sel)][n]: the selected clients' rows of D in fp64
+        (summed across ranks when sharded)."""
+        import numpy as np
+        dev = self.compute_device
+        sel_t = torch.from_numpy(np.asarray(sel, dtype=np.int32)).to(dev)
+        sq = self._sum_pieces(
+            st, lambda rs, lo, hi: ops.pairsel_rows_segsq(rs, sel_t, lo, hi))
+        return ops.pairsel_finish(sq, sel_t).cpu().numpy()
 
     def _sqnorms(self, st):
         """[n][nseg] fp64 per-client, per-key squared norms."""
@@ -568,32 +614,104 @@ def certified_selection(D, B, f, m, order, ordered=True):
     when the largest hi among the first m is below the smallest lo after
     them; with ``ordered`` (a multi-Krum average sums its clients in that
     order) every position i < m must clear every client after it."""
+    amb = ambiguous_clients(D, B, f, m, order, ordered)
+    return amb is not None and not amb
+
+
+def ambiguous_clients(D, B, f, m, order, ordered=True):
+    """The clients whose score intervals keep :func:`certified_selection`
+    from holding — an empty list when it holds; None when no interval
+    argument applies (no distances in a score: n − f − 2 <= 0).  Unordered: the first m whose hi reaches the smallest lo
+    after them, and the others whose lo reaches the largest hi among the
+    first m.  Ordered: every position i < m whose hi reaches a lo after it,
+    with the clients after it whose lo it reaches."""
     import numpy as np
     D = np.asarray(D, dtype=np.float64)
     n = D.shape[0]
     k = n - f - 2
-    if k <= 0 or m <= 0:
-        return k > 0
+    if k <= 0:
+        return None
+    if m <= 0:
+        return []
     B = np.asarray(B, dtype=np.float64)
     lo = np.sort(np.maximum(D - B, 0.0), 1)[:, :k].sum(1) * (1 - 1e-12)
     hi = np.sort(D + B, 1)[:, :k].sum(1) * (1 + 1e-12)
     o = np.asarray(order)
     lo_o, hi_o = lo[o], hi[o]
     if m >= n:
-        return not ordered or all(
-            hi_o[i] < lo_o[i + 1:].min() for i in range(n - 1))
+        if not ordered:
+            return []
+        m = n - 1
     suf = np.minimum.accumulate(lo_o[::-1])[::-1]
+    amb = set()
     if not ordered:
-        return bool(hi_o[:m].max() < suf[m])
-    return all(hi_o[i] < suf[i + 1] for i in range(m))
+        top = hi_o[:m].max()
+        if top < suf[m]:
+            return []
+        amb.update(o[:m][hi_o[:m] >= suf[m]].tolist())
+        amb.update(o[m:][lo_o[m:] <= top].tolist())
+        return sorted(amb)
+    for i in range(m):
+        if hi_o[i] >= suf[i + 1]:
+            amb.add(int(o[i]))
+            amb.update(o[i + 1:][lo_o[i + 1:] <= hi_o[i]].tolist())
+    return sorted(amb)
+
+
+def refine_selection(D, B, f, m, ordered, amb, exact_rows, rel, max_rows):
+    """A Krum selection from D (host [n][n]: the Gram path's fp64 sums) and
+    its bounds B with the ambiguous clients' rows recomputed: ``exact_rows(sel)`` returns their
+    rows of D (fp64 host [len(sel)][n], +inf at their own column) within
+    ``rel``·D of the exact distances.  Those clients' scores — sums over
+    their own rows — become near points, the others keep their intervals
+    (their entries against the recomputed clients tightened too).  Two
+    rounds at most (a round's points may overlap clients the first left
+    alone), at most ``max_rows`` rows in all.  Returns (fp64 scores, order,
+    rows recomputed), or None when the selection stays uncertified or a
+    recomputed distance is not finite (the caller recomputes all of D)."""
+    import numpy as np
+    n = D.shape[0]
+    k = n - f - 2
+    if amb is None or k <= 0:
+        return None
+    Dx = np.asarray(D, dtype=np.float64).copy()
+    Bx = np.asarray(B, dtype=np.float64).copy()
+    done = set()
+    for _ in range(2):
+        new = sorted(set(int(i) for i in amb) - done)
+        if not new or len(done) + len(new) > max_rows:
+            return None
+        rows = np.asarray(exact_rows(new), dtype=np.float64)
+        own = np.zeros(rows.shape, dtype=bool)
+        own[np.arange(len(new)), new] = True
+        if not np.isfinite(rows[~own]).all():
+            return None
+        Dx[new, :] = rows
+        Dx[:, new] = rows.T
+        bnd = rel * np.where(own, 0.0, rows)
+        Bx[new, :] = bnd
+        Bx[:, new] = bnd.T
+        done.update(new)
+        sc = np.sort(Dx, 1)[:, :k].sum(1)
+        order = np.argsort(sc, kind='stable')
+        amb = ambiguous_clients(Dx, Bx, f, m, order, ordered)
+        if amb is None:
+            return None
+        if not amb:
+            return sc, order, len(done)
+    return None
 
 
 class _PendingD:
     """Krum's distance matrix while its kernels run (``_pairdist``):
-    ``cpu()`` copies D (and the Gram path's flags and bounds) to the host,
-    recomputes the flagged (non-finite) pairs exactly and returns the host
-    fp32 [n][n] matrix; the bounds go to ``last_pair_bound`` (for the
-    recomputed pairs only D's own fp32 formation)."""
+    ``cpu()`` copies D (and the Gram path's flags, bounds and fp64 sums) to
+    the host, recomputes the flagged (non-finite) pairs exactly and returns
+    the host fp32 [n][n] matrix.  ``last_pair_bound``: the bounds on D (the
+    kernel's bound on the fp64 per-key sum plus D's own fp32 formation; for
+    the recomputed pairs the formation alone); ``last_pair_cert``: (D64,
+    B64), the fp64 sums and the kernel's bounds on them alone — what the
+    selection is certified with (D's fp32 rounding, about half of the
+    first bound on i.i.d. data, is no part of the exact distances)."""
 
     def __init__(self, eng, st, buf=None, D=None):
         self._eng, self._st, self._buf, self._D = eng, st, buf, D
@@ -603,15 +721,20 @@ class _PendingD:
             return self._D.cpu()
         import numpy as np
         eng, st = self._eng, self._st
-        host = self._buf.cpu()
-        D = host[0].view(torch.float32).clone()
-        flags = host[1].numpy()
+        D, flags, B64, D64 = ops.gram_views(self._buf.cpu())
+        D = D.clone()
+        flags = flags.numpy()
         flags = (flags + flags.T) > 0
-        B = host[2].view(torch.float32).numpy().astype(np.float64)
-        # the kernel bounds the fp64 per-key distances' sum; D is its fp32
-        # formation (a rounded sqrt and an fp32 add per key)
+        B64 = B64.numpy().astype(np.float64)
+        B64 = np.maximum(B64, B64.T)
+        D64 = D64.numpy().copy()
+        # D64's own fp64 sum over the keys (relative 2^-53 per add)
         nseg = max(1, len(st.layout.keys))
-        B = np.maximum(B, B.T) + (2 * nseg + 2) * 2.0 ** -24 * np.where(
+        fin64 = np.where(np.isfinite(D64), D64, 0.0)
+        B64 = B64 + (nseg + 2) * 2.0 ** -52 * fin64
+        # D is the fp32 formation of the fp64 per-key distances (a rounded
+        # sqrt and an fp32 add per key)
+        B = B64 + (2 * nseg + 2) * 2.0 ** -24 * np.where(
             np.isfinite(D.numpy()), D.numpy(), 0.0).astype(np.float64)
         eng.last_pairdist_path = 'mfma'
         if flags.any():
@@ -627,11 +750,15 @@ class _PendingD:
             # exact per-key sums, but D is still their fp32 formation (a
             # rounded sqrt and an fp32 add per key)
             s = sub.numpy().astype(np.float64)
-            B[np.ix_(sel, sel)] = (2 * nseg + 2) * 2.0 ** -24 * np.where(
-                np.isfinite(s), s, 0.0)
+            form = (2 * nseg + 2) * 2.0 ** -24 * np.where(np.isfinite(s), s,
+                                                           0.0)
+            B[np.ix_(sel, sel)] = form
+            D64[np.ix_(sel, sel)] = s
+            B64[np.ix_(sel, sel)] = form
             eng.last_pairdist_path = 'mfma + exact %d of %d clients' % (
                 len(sel), st.n)
         eng.last_pair_bound = B
+        eng.last_pair_cert = (D64, B64)
         return D
 
 

@@ -364,15 +364,19 @@ __device__ __forceinline__ void segsq_pair(double gaa, double gbb, double gab,
 // of the exact ones: Σ_s δ_s <= tol · Σ_s d_s, where δ_s is the worst move
 // of d = sqrt(d²) over the d² interval [d² − e, d² + e] (at most
 // e / (sqrt(d²) + sqrt(d² − e)) and sqrt(e)), summed linearly over the keys.
-// D itself is the reference's fp32 formation of those per-key distances.
+// D itself is the reference's fp32 formation of those per-key distances;
+// D64 (optional) the same sum in fp64, Σ_s sqrt(d²_s), which B bounds
+// without D's own fp32 rounding.
 __device__ __forceinline__ void finish_pair(int q, const double *segsq,
                                             const double *err, int n,
                                             int nseg, double tol, float *D,
-                                            uint32_t *ill, float *B) {
+                                            uint32_t *ill, float *B,
+                                            double *D64) {
   if (q / n == q % n) {
     D[q] = __builtin_inff();
     ill[q] = 0u;
     if (B) B[q] = 0.0f;
+    if (D64) D64[q] = __builtin_inf();
     return;
   }
   float dist = 0.0f;
@@ -393,6 +397,7 @@ __device__ __forceinline__ void finish_pair(int q, const double *segsq,
     }
   }
   D[q] = dist;
+  if (D64) D64[q] = sum_d;
   // tol = +inf: only non-finite pairs are flagged (inf · 0 is NaN, so the
   // relative test is skipped rather than evaluated)
   const bool close = !(tol < __builtin_inf()) || bound <= tol * sum_d;
@@ -847,9 +852,9 @@ __global__ __launch_bounds__(256) void gram_key_kernel(
 __global__ __launch_bounds__(256) void gram_finish_kernel(
     const double *__restrict__ segsq, const double *__restrict__ err, int n,
     int nseg, double tol, float *__restrict__ D, uint32_t *__restrict__ ill,
-    float *__restrict__ B) {
+    float *__restrict__ B, double *__restrict__ D64) {
   const int q = blockIdx.x * 256 + threadIdx.x;
-  if (q < n * n) finish_pair(q, segsq, err, n, nseg, tol, D, ill, B);
+  if (q < n * n) finish_pair(q, segsq, err, n, nseg, tol, D, ill, B, D64);
 }
 
 struct GramPlan {
@@ -943,7 +948,7 @@ void gram_launch(const float *const *tab, int64_t ss, int n,
                  const int64_t *seg_lo, const int64_t *seg_end, int nseg,
                  const GramPlan &pl, const GramWs &w, double *segsq,
                  double *err, double tol, float *D, uint32_t *ill, float *B,
-                 hipStream_t st) {
+                 double *D64, hipStream_t st) {
   const int T = pl.nt;
   hipLaunchKernelGGL(gram_prefix_kernel, dim3(1), dim3(2 * kWave), 0, st,
                      seg_lo, seg_end, nseg, kSampleChunk, kSampleCoords, pl.w,
@@ -974,7 +979,7 @@ void gram_launch(const float *const *tab, int64_t ss, int n,
     hipLaunchKernelGGL(gram_finish_kernel,
                        dim3(unsigned((int64_t(n) * n + 255) / 256)),
                        dim3(256), 0, st, segsq, err, n, nseg, tol, D, ill,
-                       B);
+                       B, D64);
 }
 
 }  // namespace
@@ -992,8 +997,9 @@ namespace {
 int pairgram_rows(const char *what, const fsagg_rows *rows,
                   const int64_t *seg_lo, const int64_t *seg_end,
                   int64_t numel, double *segsq, double *err, double tol,
-                  float *D, uint32_t *ill, float *B, void *workspace,
-                  size_t workspace_bytes, fsagg_stream_t stream) {
+                  float *D, uint32_t *ill, float *B, double *D64,
+                  void *workspace, size_t workspace_bytes,
+                  fsagg_stream_t stream) {
   if (!rows || !rows->tab || !seg_lo || !seg_end || !segsq || !err ||
       rows->n < 2 || rows->n > 16 * kGramMaxTiles || rows->nseg < 1 ||
       numel < 0 || (rows->ss != 0 && rows->ss < rows->n) ||
@@ -1015,23 +1021,23 @@ int pairgram_rows(const char *what, const fsagg_rows *rows,
   switch (pl.nt) {
     case 1: gram_launch<1, false>(rows->tab, rows->ss, n, seg_lo, seg_end,
                                   nseg, pl, w, segsq, err, tol, D, ill, B,
-                                  st); break;
+                                  D64, st); break;
     case 2: gram_launch<2, false>(rows->tab, rows->ss, n, seg_lo, seg_end,
                                   nseg, pl, w, segsq, err, tol, D, ill, B,
-                                  st); break;
+                                  D64, st); break;
     case 3: gram_launch<3, false>(rows->tab, rows->ss, n, seg_lo, seg_end,
                                   nseg, pl, w, segsq, err, tol, D, ill, B,
-                                  st); break;
+                                  D64, st); break;
     case 4: gram_launch<4, false>(rows->tab, rows->ss, n, seg_lo, seg_end,
                                   nseg, pl, w, segsq, err, tol, D, ill, B,
-                                  st); break;
+                                  D64, st); break;
     default:
       if (pl.nlines == 7)
         gram_launch<3, true>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg,
-                             pl, w, segsq, err, tol, D, ill, B, st);
+                             pl, w, segsq, err, tol, D, ill, B, D64, st);
       else
         gram_launch<4, true>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg,
-                             pl, w, segsq, err, tol, D, ill, B, st);
+                             pl, w, segsq, err, tol, D, ill, B, D64, st);
       break;
   }
   return check_launch(what);
@@ -1047,7 +1053,7 @@ extern "C" int fsagg_pairgram_rows_segsq_f32(const fsagg_rows *rows,
                                              fsagg_stream_t stream) {
   return pairgram_rows("fsagg_pairgram_rows_segsq_f32", rows, seg_lo,
                        seg_end, numel, segsq, err, 0.0, nullptr, nullptr,
-                       nullptr, workspace, workspace_bytes, stream);
+                       nullptr, nullptr, workspace, workspace_bytes, stream);
 }
 
 extern "C" int fsagg_pairgram_rows_f32(const fsagg_rows *rows,
@@ -1055,7 +1061,8 @@ extern "C" int fsagg_pairgram_rows_f32(const fsagg_rows *rows,
                                        const int64_t *seg_end, int64_t numel,
                                        double tol, double *segsq,
                                        double *err, float *D, uint32_t *ill,
-                                       float *bound, void *workspace,
+                                       float *bound, double *dist64,
+                                       void *workspace,
                                        size_t workspace_bytes,
                                        fsagg_stream_t stream) {
   if (!D) {
@@ -1063,14 +1070,14 @@ extern "C" int fsagg_pairgram_rows_f32(const fsagg_rows *rows,
     return FSAGG_EINVAL;
   }
   return pairgram_rows("fsagg_pairgram_rows_f32", rows, seg_lo, seg_end,
-                       numel, segsq, err, tol, D, ill, bound, workspace,
-                       workspace_bytes, stream);
+                       numel, segsq, err, tol, D, ill, bound, dist64,
+                       workspace, workspace_bytes, stream);
 }
 
 extern "C" int fsagg_pairgram_finish_f32(const double *segsq,
                                          const double *err, int n, int nseg,
                                          double tol, float *D, uint32_t *ill,
-                                         float *bound,
+                                         float *bound, double *dist64,
                                          fsagg_stream_t stream) {
   if (!segsq || !err || !D || !ill || n < 2 || nseg < 1 || !(tol >= 0.0)) {
     set_error("fsagg_pairgram_finish_f32: invalid argument (n=%d nseg=%d)",
@@ -1080,6 +1087,6 @@ extern "C" int fsagg_pairgram_finish_f32(const double *segsq,
   hipLaunchKernelGGL(gram_finish_kernel,
                      dim3(unsigned((int64_t(n) * n + 255) / 256)), dim3(256),
                      0, as_stream(stream), segsq, err, n, nseg, tol, D, ill,
-                     bound);
+                     bound, dist64);
   return check_launch("fsagg_pairgram_finish_f32");
 }

@@ -1145,30 +1145,47 @@ def pairgram_rows_segsq(rs, lo=0, hi=None, workspace=None, keep=None):
     return out
 
 
+def _gram_buf(n, device):
+    """The finish's outputs in one int32 [5][n][n] device tensor (one copy
+    to the host): planes 0-1 D64 (fp64 [n][n], first so that it is 8-byte
+    aligned for any n), planes 2-4 D (fp32), ill, B (fp32).  Returns (buf,
+    D, ill, B, D64) views (:func:`gram_views` of a host copy)."""
+    buf = torch.empty((5, n, n), dtype=torch.int32, device=device)
+    return (buf,) + gram_views(buf)
+
+
+def gram_views(buf):
+    """(D, ill, B, D64) views of a :func:`_gram_buf` buffer (device or a
+    host copy)."""
+    n = int(buf.shape[1])
+    return buf[2].view(torch.float32), buf[3], buf[4].view(torch.float32), \
+        buf[0:2].reshape(-1).view(torch.float64).view(n, n)
+
+
 def pairgram_finish(sq2, tol):
     """D (fp32 [n][n], device, as :func:`pairdist_finish`), ill (int32
-    [n][n]: the pairs whose bound exceeds ``tol``·D, or non-finite) and B
-    (fp32 [n][n]: each pair's worst-case bound on |D − the exact
-    distance|) from :func:`pairgram_rows_segsq`'s output, in one int32
-    [3][n][n] device tensor (one copy to the host): returns (buf, D view,
-    ill view, B view)."""
+    [n][n]: the pairs whose bound exceeds ``tol``·D, or non-finite), B
+    (fp32 [n][n]: each pair's worst-case bound on |Σ_key d_key − the exact
+    distance|) and D64 (fp64 [n][n]: Σ_key d_key in fp64, what B bounds
+    without D's own fp32 rounding) from :func:`pairgram_rows_segsq`'s
+    output: returns (buf, D, ill, B, D64) as :func:`_gram_buf`."""
     if sq2.dim() != 4 or sq2.shape[0] != 2 or sq2.dtype != torch.float64 \
             or not sq2.is_contiguous():
         raise ValueError('sq2 must be a contiguous fp64 [2][nseg][n][n] '
                          'tensor')
     nseg, n = int(sq2.shape[1]), int(sq2.shape[2])
-    buf = torch.empty((3, n, n), dtype=torch.int32, device=sq2.device)
+    buf, D, ill, B, D64 = _gram_buf(n, sq2.device)
     L.check(L.load().fsagg_pairgram_finish_f32(
         sq2[0].data_ptr(), sq2[1].data_ptr(), n, nseg, float(tol),
-        buf[0].data_ptr(), buf[1].data_ptr(), buf[2].data_ptr(),
+        D.data_ptr(), ill.data_ptr(), B.data_ptr(), D64.data_ptr(),
         _stream(sq2.device)), 'fsagg_pairgram_finish_f32')
-    return buf, buf[0].view(torch.float32), buf[1], buf[2].view(torch.float32)
+    return buf, D, ill, B, D64
 
 
 def pairgram_rows_dist(rs, tol, workspace=None):
     """:func:`pairgram_rows_segsq` and :func:`pairgram_finish` in one call
-    (fsagg_pairgram_rows_f32).  Returns (buf, D view, ill view, B view, sq2)
-    as those two."""
+    (fsagg_pairgram_rows_f32).  Returns (buf, D, ill, B, D64, sq2) as those
+    two."""
     _require_all(rs, 'Krum')
     if not 2 <= rs.n <= L.FSAGG_PAIRGRAM_MAX_CLIENTS:
         raise ValueError('the Gram path takes 2..%d clients' %
@@ -1181,19 +1198,65 @@ def pairgram_rows_dist(rs, tol, workspace=None):
     ws = (workspace or _WS).get(rs.device, need)
     sq2 = torch.empty((2, rs.nseg, rs.n, rs.n), dtype=torch.float64,
                       device=rs.device)
-    buf = torch.empty((3, rs.n, rs.n), dtype=torch.int32, device=rs.device)
+    buf, D, ill, B, D64 = _gram_buf(rs.n, rs.device)
     L.check(lib.fsagg_pairgram_rows_f32(
         rs.ptr(), seg_lo.data_ptr(), seg_end.data_ptr(), extent, float(tol),
-        sq2[0].data_ptr(), sq2[1].data_ptr(), buf[0].data_ptr(),
-        buf[1].data_ptr(), buf[2].data_ptr(), ws.data_ptr(), ws.numel(),
+        sq2[0].data_ptr(), sq2[1].data_ptr(), D.data_ptr(), ill.data_ptr(),
+        B.data_ptr(), D64.data_ptr(), ws.data_ptr(), ws.numel(),
         _stream(rs.device)), 'fsagg_pairgram_rows_f32')
-    return buf, buf[0].view(torch.float32), buf[1], \
-        buf[2].view(torch.float32), sq2
+    return buf, D, ill, B, D64, sq2
 
 
 def pairdist_rows(rs, workspace=None):
     """Krum's distance matrix D[n][n] (fp32, device) over a row set."""
     return pairdist_finish(pairdist_rows_segsq(rs, workspace=workspace))
+
+
+def pairsel_rows_segsq(rs, sel, lo=0, hi=None, workspace=None):
+    """Per-key squared distances [nseg][len(sel)][n] (fp64, device) of the
+    clients ``sel`` (device int32) to every client over the keys'
+    coordinates in [lo, hi), in fp64 throughout (fsagg_pairsel_rows_segsq_f64;
+    summed across ranks by the caller, then :func:`pairsel_finish`)."""
+    _require_all(rs, 'Krum')
+    nsel = int(sel.numel())
+    if not 2 <= rs.n <= L.FSAGG_PAIRSEL_MAX_CLIENTS or \
+            not 1 <= nsel <= L.FSAGG_PAIRSEL_MAX_SEL:
+        raise ValueError('the selected-rows kernel takes 2..%d clients and '
+                         '1..%d selected' % (L.FSAGG_PAIRSEL_MAX_CLIENTS,
+                                             L.FSAGG_PAIRSEL_MAX_SEL))
+    if sel.dtype != torch.int32 or sel.device != rs.device or \
+            not sel.is_contiguous():
+        raise ValueError('sel must be a contiguous int32 tensor on the rows\' '
+                         'device')
+    lib = L.load()
+    chunks, nchunk = rs.layout.row_chunks(L.FSAGG_PAIRSEL_CHUNK, rs.device,
+                                          lo, hi)
+    need = lib.fsagg_pairsel_workspace_bytes(nsel, rs.n, max(nchunk, 1))
+    ws = (workspace or _WS).get(rs.device, need)
+    sq = torch.empty((rs.nseg, nsel, rs.n), dtype=torch.float64,
+                     device=rs.device)
+    L.check(lib.fsagg_pairsel_rows_segsq_f64(
+        rs.ptr(), sel.data_ptr(), nsel,
+        chunks.data_ptr() if chunks is not None else None, nchunk,
+        sq.data_ptr(), ws.data_ptr(), ws.numel(), _stream(rs.device)),
+        'fsagg_pairsel_rows_segsq_f64')
+    return sq
+
+
+def pairsel_finish(segsq, sel):
+    """D rows [len(sel)][n] (fp64, device): Σ_key sqrt of
+    :func:`pairsel_rows_segsq`'s output in key order, +inf at each selected
+    client's own column."""
+    if segsq.dim() != 3 or segsq.dtype != torch.float64 or \
+            not segsq.is_contiguous():
+        raise ValueError('segsq must be a contiguous fp64 [nseg][nsel][n] '
+                         'tensor')
+    nseg, nsel, n = (int(x) for x in segsq.shape)
+    D = torch.empty((nsel, n), dtype=torch.float64, device=segsq.device)
+    L.check(L.load().fsagg_pairsel_finish_f64(
+        segsq.data_ptr(), sel.data_ptr(), nsel, n, nseg, D.data_ptr(),
+        _stream(segsq.device)), 'fsagg_pairsel_finish_f64')
+    return D
 
 
 def rows_sqnorm(rs, lo=0, hi=None, workspace=None):

@@ -507,18 +507,49 @@ int fsagg_pairgram_rows_segsq_f32(const fsagg_rows *rows,
  * selection with; ill[a*n + b] = 1 where that bound exceeds tol · Σ_s d_s,
  * or d² came out negative beyond its bound, or D is not finite — the
  * caller recomputes those pairs with fsagg_pairdist_rows_segsq_f32 on the
- * clients involved (tol = +inf: only the non-finite ones). */
+ * clients involved (tol = +inf: only the non-finite ones).  dist64 (fp64,
+ * may be NULL): Σ_s sqrt(segsq[s][a][b]) in fp64, the sum bound[a][b]
+ * bounds without D's fp32 rounding (+inf on the diagonal) — what the
+ * caller certifies against. */
 int fsagg_pairgram_finish_f32(const double *segsq, const double *err, int n,
                               int nseg, double tol, float *D, uint32_t *ill,
-                              float *bound, fsagg_stream_t stream);
+                              float *bound, double *dist64,
+                              fsagg_stream_t stream);
 
 /* fsagg_pairgram_rows_segsq_f32 and fsagg_pairgram_finish_f32 in one call
  * (the unsharded path). */
 int fsagg_pairgram_rows_f32(const fsagg_rows *rows, const int64_t *seg_lo,
                             const int64_t *seg_end, int64_t numel, double tol,
                             double *segsq, double *err, float *D,
-                            uint32_t *ill, float *bound, void *workspace,
-                            size_t workspace_bytes, fsagg_stream_t stream);
+                            uint32_t *ill, float *bound, double *dist64,
+                            void *workspace, size_t workspace_bytes,
+                            fsagg_stream_t stream);
+
+/* Krum distances of a few selected clients to every client, in fp64 — the
+ * rows of D that decide a selection the Gram path's bounds leave ambiguous
+ * (the same torch.dist loop, krum_aggregator.py:41-73, for |sel| × n pairs;
+ * no reference counterpart of its own).  sel (device int32 [nsel], 1 <=
+ * nsel <= FSAGG_PAIRSEL_MAX_SEL, 2 <= n <= FSAGG_PAIRSEL_MAX_CLIENTS):
+ * segsq[s][a][b] (device fp64 [nseg][nsel][n]) = Σ_{p in key s} (x_sel[a][p]
+ * − x_b[p])² over the chunks (chunk unit FSAGG_PAIRSEL_CHUNK), fp64
+ * differences, squares and sums in a fixed order (deterministic; relative
+ * error below (coordinates + 64)·2^-53).  Sums over disjoint coordinate
+ * ranges (ranks) stay valid.  Workspace:
+ * fsagg_pairsel_workspace_bytes(nsel, n, nchunk). */
+#define FSAGG_PAIRSEL_MAX_SEL 32
+#define FSAGG_PAIRSEL_MAX_CLIENTS 256
+#define FSAGG_PAIRSEL_CHUNK 4096
+size_t fsagg_pairsel_workspace_bytes(int nsel, int n, int nchunk);
+int fsagg_pairsel_rows_segsq_f64(const fsagg_rows *rows, const int *sel,
+                                 int nsel, const fsagg_chunk *chunks,
+                                 int nchunk, double *segsq, void *workspace,
+                                 size_t workspace_bytes,
+                                 fsagg_stream_t stream);
+/* D[a][b] (device fp64 [nsel][n]) = Σ_s sqrt(segsq[s][a][b]) in key order,
+ * +inf where b == sel[a] (krum_aggregator.py:67-69). */
+int fsagg_pairsel_finish_f64(const double *segsq, const int *sel, int nsel,
+                             int n, int nseg, double *D,
+                             fsagg_stream_t stream);
 
 /* Per-(client, key segment) squared L2 norms over a row set in fp64:
  * sq[i][s] = Σ_{p in s} x_i[p]^2 (0 for a NULL entry), summed in a fixed

@@ -93,7 +93,7 @@ def _gram(rs):
     from federatedscope_amd import ops
     from federatedscope_amd.core.aggregators._engine import _GRAM_TOL
     sq2 = ops.pairgram_rows_segsq(rs)
-    _, D, ill, B = ops.pairgram_finish(sq2, _GRAM_TOL)
+    _, D, ill, B, _ = ops.pairgram_finish(sq2, _GRAM_TOL)
     flags = ill.cpu().numpy()
     sq2 = sq2.cpu().numpy()
     B = B.cpu().numpy().astype(np.float64)

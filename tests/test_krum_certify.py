@@ -83,3 +83,79 @@ def test_certificate_infinite_bound_fails():
     B = np.zeros((n, n))
     B[order[0], order[1]] = B[order[1], order[0]] = np.inf
     assert not certified_selection(D, B, f, 2, order, True)
+
+
+def _exact_D(X):
+    D = np.sqrt(((X[:, None] - X[None]) ** 2).sum(-1))
+    np.fill_diagonal(D, np.inf)
+    return D
+
+
+@pytest.mark.parametrize('ordered', [True, False])
+def test_refine_selection_recovers_the_exact_selection(ordered):
+    """The ambiguous clients' rows replaced by exact ones
+    (_engine.refine_selection): when it certifies, the selection is the
+    exact distances' one; the rows it asks for are the ambiguous ones."""
+    from federatedscope_amd.core.aggregators._engine import (
+        ambiguous_clients, refine_selection)
+    hits = 0
+    for seed in range(30):
+        rng = np.random.default_rng(100 + seed)
+        n, f = 24, 4
+        m = 6 if ordered else n - 2 * f
+        X = rng.standard_normal((n, 16))
+        De = _exact_D(X)
+        eps = 3e-4
+        B = eps * np.where(np.isfinite(De), De, 0.0)
+        noise = rng.uniform(-1, 1, (n, n)) * B
+        noise = np.triu(noise, 1) + np.triu(noise, 1).T
+        D = (De + noise).astype(np.float32)
+        np.fill_diagonal(D, np.inf)
+        order = torch.sort(krum_scores(torch.from_numpy(D), f))[1].numpy()
+        amb = ambiguous_clients(D, B, f, m, order, ordered)
+        if not amb:
+            continue
+        asked = []
+
+        def rows(sel):
+            asked.append(list(sel))
+            return De[sel]
+        got = refine_selection(D, B, f, m, ordered, amb, rows, 1e-14, 32)
+        assert asked[0] == sorted(amb)
+        if got is None:
+            continue
+        hits += 1
+        sc, o, nrows = got
+        want = np.argsort(np.sort(De, 1)[:, :n - f - 2].sum(1),
+                          kind='stable')
+        if ordered:
+            assert o[:m].tolist() == want[:m].tolist(), seed
+        else:
+            assert sorted(o[:m].tolist()) == sorted(want[:m].tolist()), seed
+        assert nrows == sum(len(a) for a in asked)
+    assert hits >= 3
+
+
+def test_refine_selection_gives_up_on_ties_and_nonfinite():
+    from federatedscope_amd.core.aggregators._engine import (
+        ambiguous_clients, refine_selection)
+    rng = np.random.default_rng(5)
+    n, f = 12, 2
+    X = rng.standard_normal((n, 4))
+    X[7] = X[3]                       # equal exact scores
+    De = _exact_D(X)
+    B = 1e-3 * np.where(np.isfinite(De), De, 0.0)
+    D = De.astype(np.float32)
+    order = torch.sort(krum_scores(torch.from_numpy(D), f))[1].numpy()
+    m = n - 1
+    amb = ambiguous_clients(D, B, f, m, order, True)
+    assert 3 in amb and 7 in amb
+    assert refine_selection(D, B, f, m, True, amb, lambda s: De[s], 1e-14,
+                            32) is None
+    bad = De.copy()
+    bad[3, 0] = np.nan
+    assert refine_selection(D, B, f, m, True, amb, lambda s: bad[s], 1e-14,
+                            32) is None
+    # more rows than allowed
+    assert refine_selection(D, B, f, m, True, amb, lambda s: De[s], 1e-14,
+                            1) is None

@@ -121,7 +121,7 @@ def krum_c4(dev, n=50, f=10):
                                   dtype=np.int64), dev, keepalive=(slab, ))
 
     def gram_D():
-        buf, D_, ill_, B_, sq2_ = ops.pairgram_rows_dist(rs, _GRAM_TOL)
+        buf, D_, ill_, B_, _, sq2_ = ops.pairgram_rows_dist(rs, _GRAM_TOL)
         return sq2_, D_, ill_, B_
 
     sq2, Dg, ill, Bg = gram_D()
