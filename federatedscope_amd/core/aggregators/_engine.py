@@ -303,9 +303,12 @@ class DeviceEngine:
         # fp64 differences and squares, sums of at most `big` terms per key
         # (+ slices, chunks and ranks), a sqrt and nseg adds per pair
         rel = ((big + 64 + world) / 2 + nseg + 8) * 2.0 ** -53
+        # the rows kernel costs ~ n·rows, the full VALU matrix ~ n²/2: at
+        # 50 × 6.6M, 8 rows 0.45 ms against 0.47 ms (tools/probe_pairsel.py)
+        max_rows = min(_lib.FSAGG_PAIRSEL_MAX_SEL, max(4, st.n // 6))
         return refine_selection(D, B, f, m, ordered, amb,
                                 lambda sel: self._exact_rows(st, sel), rel,
-                                _lib.FSAGG_PAIRSEL_MAX_SEL)
+                                max_rows)
 
     def _exact_rows(self, st, sel):
         """fp64 host [len(sel)][n]: the selected clients' rows of D in fp64

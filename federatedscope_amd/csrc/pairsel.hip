@@ -18,11 +18,11 @@
 //     consecutive 16-B pieces of one row) into registers one stage ahead,
 //     then written to LDS transposed, [coordinate][client] at a pitch of
 //     slots + 1 words (conflict-free reads; at most 2-way on the writes);
-//   * the selected rows stay out of LDS (a broadcast read delivers 64
-//     copies: the LDS return path, not the VALU, bounded the first form):
-//     each wave loads its own 32 coordinates of them lane-distributed one
-//     stage ahead and hands one value at a time to the fp64 updates as a
-//     scalar operand (readlane);
+//     the selected rows' stage goes to LDS as fp64 [coordinate][a]
+//     (pitch NA + 2 doubles), read as wave-uniform broadcasts (a readlane
+//     per value instead — the selected rows lane-distributed in registers,
+//     each value a scalar operand — measured 10-20 % slower at NA <= 8,
+//     tools/probe_pairsel.py);
 //   * lane ↔ client b (ceil(n/64) waves cover the clients, the other waves
 //     take other coordinate slices of the stage); each lane keeps NA fp64
 //     accumulators, one per selected client;
@@ -53,22 +53,14 @@ __host__ __device__ inline int pairsel_stage(int n) {
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef double d2v __attribute__((ext_vector_type(2)));
 
-// v's value in lane l (wave-uniform l), as a scalar operand
-__device__ __forceinline__ double lane_value(double v, int l) {
-  const uint64_t u = __builtin_bit_cast(uint64_t, v);
-  const uint32_t lo = __builtin_amdgcn_readlane(uint32_t(u), l);
-  const uint32_t hi = __builtin_amdgcn_readlane(uint32_t(u >> 32), l);
-  return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
-}
-
 template <int NA>
 __global__ __launch_bounds__(kBlock) void pairsel_chunk_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n,
     const int *__restrict__ sel, int nsel,
     const fsagg_chunk *__restrict__ chunks, double *__restrict__ partial) {
-  static_assert(NA % 2 == 0, "selected rows come in lane halves");
-  constexpr int kPer = 32;  // coordinates per wave per stage (T / slices)
+  constexpr int PA = NA + 2;  // doubles per staged coordinate of the rows a
   __shared__ __attribute__((aligned(16))) float lb[kRowFloats];
+  __shared__ __attribute__((aligned(16))) double la[kMaxStage * PA];
   const int c = blockIdx.x;
   const int64_t lo = chunks[c].lo;
   const int len = chunks[c].len;
@@ -79,11 +71,10 @@ __global__ __launch_bounds__(kBlock) void pairsel_chunk_kernel(
   const int slots = pairsel_slots(n), T = pairsel_stage(n);
   const int pb = slots + 1;  // LDS pitch (words) of a staged coordinate
   const int bset = slots / kWave;
-  const int slices = kWaves / bset;  // T = kPer · slices
+  const int slices = kWaves / bset;
   const int slice = wave / bset;
   const int b = (wave - slice * bset) * kWave + lane;
   const bool busy = slice < slices;
-  const int p0 = slice * kPer;  // this wave's coordinates of a stage
   // row pointers at this chunk: the clients', then the selected rows'
   __shared__ const float *rp[FSAGG_PAIRSEL_MAX_CLIENTS + NA];
   for (int r = tid; r < n; r += kBlock) rp[r] = rows[r] + lo;
@@ -95,22 +86,31 @@ __global__ __launch_bounds__(kBlock) void pairsel_chunk_kernel(
       tid >= n || (reinterpret_cast<uintptr_t>(rows[tid] + lo) & 15u) == 0);
   const float *const *sp = rp + FSAGG_PAIRSEL_MAX_CLIENTS;
 
-  // The clients' stage, staged in registers one stage ahead as float4
+  // Register staging of one whole stage.  The clients' rows as float4
   // units: thread tid takes piece q = tid % (T/4) of rows r0, r0 + rstep, …
-  // (T/4 divides the block, so the piece is fixed); at most 8 units
-  // (T·slots/4 <= 2048).
+  // (T/4 divides the block, so the piece is fixed); the selected rows as
+  // floats: coordinate pa = tid % T of rows a0, a0 + astep, ….  At most 8
+  // units (T·slots/4 <= 2048) and NA/2 floats per thread.
   constexpr int KB = 8;
+  constexpr int KA = NA * kMaxStage / kBlock;
   const int q4 = T / 4;
   const int q = tid % q4, r0 = tid / q4, rstep = kBlock / q4;
+  const int pa = tid % T, a0 = tid / T, astep = kBlock / T;
   f4v rb[KB];
-  auto fetch_b = [&](int s0) {
+  float ra[KA];
+  auto fetch = [&](int s0) {
 #pragma unroll
     for (int k = 0; k < KB; ++k) {
       const int r = r0 + k * rstep;
       if (r < n) rb[k] = gld_nt(reinterpret_cast<const f4v *>(rp[r] + s0) + q);
     }
+#pragma unroll
+    for (int k = 0; k < KA; ++k) {
+      const int a = a0 + k * astep;
+      if (a < NA) ra[k] = gld(sp[a] + s0 + pa);
+    }
   };
-  auto put_b = [&]() {
+  auto put = [&]() {
 #pragma unroll
     for (int k = 0; k < KB; ++k) {
       const int r = r0 + k * rstep;
@@ -122,72 +122,51 @@ __global__ __launch_bounds__(kBlock) void pairsel_chunk_kernel(
         d[3 * pb] = rb[k].w;
       }
     }
+#pragma unroll
+    for (int k = 0; k < KA; ++k) {
+      const int a = a0 + k * astep;
+      if (a < NA) la[pa * PA + a] = double(ra[k]);
+    }
   };
   // unaligned rows or a short tail stage: 4-B loads straight to LDS
-  auto put_b_scalar = [&](int s0) {
+  auto put_scalar = [&](int s0) {
     const int sl = len - s0 < T ? len - s0 : T;
     for (int u = tid; u < n * T; u += kBlock) {
       const int r = u / T, p = u - r * T;
       if (p < sl) lb[p * pb + r] = gld(rp[r] + s0 + p);
     }
+    for (int i = tid; i < NA * T; i += kBlock) {
+      const int a = i / T, p = i - a * T;
+      if (p < sl) la[p * PA + a] = double(gld(sp[a] + s0 + p));
+    }
   };
   auto whole = [&](int s0) { return vec && len - s0 >= T; };
-  // The selected rows never touch LDS: each wave loads its own 32
-  // coordinates of them, lane-distributed (lanes 0-31: row 2h, lanes
-  // 32-63: row 2h + 1), and broadcasts one value at a time with readlane
-  // (a scalar operand: no LDS broadcast traffic).
-  const int pl = p0 + (lane & (kPer - 1));
-  const int half = lane >> 5;
-  float xa_next[NA / 2];
-  double xa[NA / 2];
-  auto fetch_a = [&](int s0) {
-    const int sl = len - s0 < T ? len - s0 : T;
-#pragma unroll
-    for (int h = 0; h < NA / 2; ++h)
-      xa_next[h] = pl < sl ? gld(sp[2 * h + half] + s0 + pl) : 0.0f;
-  };
 
   double acc[NA];
 #pragma unroll
   for (int a = 0; a < NA; ++a) acc[a] = 0.0;
 
-  if (busy) fetch_a(0);
-  if (whole(0)) fetch_b(0);
+  if (whole(0)) fetch(0);
   for (int s0 = 0; s0 < len; s0 += T) {
-    if (whole(s0)) put_b();
-    else put_b_scalar(s0);
-#pragma unroll
-    for (int h = 0; h < NA / 2; ++h) xa[h] = double(xa_next[h]);
+    if (whole(s0)) put();
+    else put_scalar(s0);
     __syncthreads();
-    // the next stage's loads land while this one computes
-    if (busy && s0 + T < len) fetch_a(s0 + T);
-    if (whole(s0 + T)) fetch_b(s0 + T);
+    if (whole(s0 + T)) fetch(s0 + T);  // lands while this stage computes
     if (busy) {
       const int sl = len - s0 < T ? len - s0 : T;
-      const int cnt = sl - p0 < kPer ? sl - p0 : kPer;  // wave-uniform
-      const float *col = lb + p0 * pb + b;
-      if (cnt == kPer) {
+      const int per = T / slices;
+      const int p0 = slice * per;
+      const int p1 = p0 + per < sl ? p0 + per : sl;
 #pragma unroll 2
-        for (int j = 0; j < kPer; ++j) {
-          const double x = double(col[j * pb]);
+      for (int p = p0; p < p1; ++p) {
+        const double x = double(lb[p * pb + b]);
+        const d2v *r = reinterpret_cast<const d2v *>(la + p * PA);
 #pragma unroll
-          for (int h = 0; h < NA / 2; ++h) {
-            const double d0 = lane_value(xa[h], j) - x;
-            const double d1 = lane_value(xa[h], j + kPer) - x;
-            acc[2 * h] = __builtin_fma(d0, d0, acc[2 * h]);
-            acc[2 * h + 1] = __builtin_fma(d1, d1, acc[2 * h + 1]);
-          }
-        }
-      } else {
-        for (int j = 0; j < cnt; ++j) {
-          const double x = double(col[j * pb]);
-#pragma unroll
-          for (int h = 0; h < NA / 2; ++h) {
-            const double d0 = lane_value(xa[h], j) - x;
-            const double d1 = lane_value(xa[h], j + kPer) - x;
-            acc[2 * h] = __builtin_fma(d0, d0, acc[2 * h]);
-            acc[2 * h + 1] = __builtin_fma(d1, d1, acc[2 * h + 1]);
-          }
+        for (int h = 0; h < NA / 2; ++h) {
+          const d2v v = r[h];
+          const double d0 = v.x - x, d1 = v.y - x;
+          acc[2 * h] = __builtin_fma(d0, d0, acc[2 * h]);
+          acc[2 * h + 1] = __builtin_fma(d1, d1, acc[2 * h + 1]);
         }
       }
     }
@@ -200,15 +179,15 @@ __global__ __launch_bounds__(kBlock) void pairsel_chunk_kernel(
   const int nb = slots;
   constexpr int G = NA < 16 ? NA : 16;
 #pragma unroll
-  for (int a0 = 0; a0 < NA; a0 += G) {
+  for (int a0g = 0; a0g < NA; a0g += G) {
     if (busy) {
 #pragma unroll
-      for (int g = 0; g < G; ++g) red[(slice * G + g) * nb + b] = acc[a0 + g];
+      for (int g = 0; g < G; ++g) red[(slice * G + g) * nb + b] = acc[a0g + g];
     }
     __syncthreads();
     for (int o = tid; o < G * nb; o += kBlock) {
       const int g = o / nb, bb = o - g * nb;
-      const int a = a0 + g;
+      const int a = a0g + g;
       if (bb >= n || a >= nsel) continue;
       double t = 0.0;
       for (int k = 0; k < slices; ++k) t += red[(k * G + g) * nb + bb];
