@@ -93,7 +93,8 @@ class StagedSet:
     def subset(self, sel):
         """The clients ``sel`` in the new reduction order (every piece)."""
         rs = None if self.rs is None else self.rs.subset(sel)
-        pieces = [(j, lo, hi, r.subset(sel)) for j, lo, hi, r in self.pieces]
+        pieces = [(j, lo, hi, rs if r is self.rs else r.subset(sel))
+                  for j, lo, hi, r in self.pieces]
         return StagedSet(self.layout, rs, pieces=pieces, plan=self.plan)
 
 
@@ -235,12 +236,12 @@ class DeviceEngine:
         VALU kernel.  Above 208 clients: the VALU kernel (direct differences,
         ``last_pair_bound`` None)."""
         from ... import _lib
-        self.last_pair_bound = None
-        self.last_pair_cert = None
+        self._pair_info = None
         if not 2 <= st.n <= _lib.FSAGG_PAIRGRAM_MAX_CLIENTS:
             return self._pairdist_valu(st)
         if st.plan is None:
-            buf = ops.pairgram_rows_dist(st.rows(), _GRAM_TOL)[0]
+            # one graph launch for the chain's eight kernels (ops._GRAPHS)
+            buf = ops.pairgram_rows_dist_graph(st.rows(), _GRAM_TOL)[0]
             return _PendingD(self, st, buf=buf)
         sq2 = self._sum_pieces(
             st, lambda rs, lo, hi: ops.pairgram_rows_segsq(rs, lo, hi))
@@ -249,35 +250,59 @@ class DeviceEngine:
     def _pairdist_valu(self, st):
         """D on the VALU kernel (fsagg_pairdist_*)."""
         self.last_pairdist_path = 'valu'
-        self.last_pair_bound = None
-        self.last_pair_cert = None
+        self._pair_info = None
         segsq = self._sum_pieces(
             st, lambda rs, lo, hi: ops.pairdist_rows_segsq(rs, lo, hi))
         return _PendingD(self, st, D=ops.pairdist_finish(segsq))
 
+    @property
+    def last_pair_bound(self):
+        """Host fp64 [n][n] bounds on the last Gram-path D's error (None
+        after the VALU path)."""
+        info = self.__dict__.get('_pair_info')
+        return None if info is None else info.bound()
+
+    @property
+    def last_pair_cert(self):
+        """(D64, B64) of the last Gram-path D: what selections are
+        certified with (None after the VALU path)."""
+        info = self.__dict__.get('_pair_info')
+        return None if info is None else info.cert()
+
     def _certified_order(self, st, D, f, m, ordered):
         """(D, scores, order) for a Krum selection of ``m`` clients: from the
         Gram path's fp64 sums when their bounds certify the selection
-        (:func:`certified_selection`; ``ordered``: the order of the first
-        ``m`` as well, which fixes a multi-Krum average's summation order);
-        else with the ambiguous clients' rows recomputed in fp64
-        (:meth:`_refine_selection`); else from D recomputed on the VALU
-        kernel."""
+        (:func:`certified_selection`, natively in
+        ``_fsagg_host.gram_select`` when no pair was recomputed;
+        ``ordered``: the order of the first ``m`` as well, which fixes a
+        multi-Krum average's summation order); else with the ambiguous
+        clients' rows recomputed in fp64 (:meth:`_refine_selection`); else
+        from D recomputed on the VALU kernel."""
         import numpy as np
+        from ... import _lib
         from .krum_aggregator import krum_scores
-        cert = self.last_pair_cert if self.last_pair_bound is not None \
-            else None
-        if cert is None:
+        info = self.__dict__.get('_pair_info')
+        if info is None:
             scores = krum_scores(D, f)
             return D, scores, torch.sort(scores)[1]
-        D64, B64 = cert
-        n = D64.shape[0]
-        k = n - f - 2
-        sc = np.sort(D64, 1)[:, :max(k, 0)].sum(1)
-        order = np.argsort(sc, kind='stable')
-        amb = ambiguous_clients(D64, B64, f, m, order, ordered)
-        if amb is not None and not amb:
-            return D, torch.from_numpy(sc), torch.from_numpy(order)
+        amb = None
+        if info.raw:
+            got = _lib.host().gram_select(info.host.numpy(), info.nseg, f, m,
+                                          bool(ordered))
+            if got is not None:
+                sc, order, amb = got
+                if not amb:
+                    return D, torch.frombuffer(sc, dtype=torch.float64), \
+                        torch.frombuffer(order, dtype=torch.int64)
+        D64, B64 = info.cert()
+        if amb is None:
+            n = D64.shape[0]
+            k = n - f - 2
+            sc = np.sort(D64, 1)[:, :max(k, 0)].sum(1)
+            order = np.argsort(sc, kind='stable')
+            amb = ambiguous_clients(D64, B64, f, m, order, ordered)
+            if amb is not None and not amb:
+                return D, torch.from_numpy(sc), torch.from_numpy(order)
         got = self._refine_selection(st, D64, B64, f, m, ordered, amb)
         if got is not None:
             sc, o, nrows = got
@@ -705,16 +730,50 @@ def refine_selection(D, B, f, m, ordered, amb, exact_rows, rel, max_rows):
     return None
 
 
+class _PairInfo:
+    """The Gram path's per-pair data behind the last distance matrix, on
+    the host, built on demand from the finish buffer's host copy
+    (ops._gram_buf): ``cert()`` = (D64, B64), the fp64 key sums and the
+    kernel's bounds on them — what the selection is certified with (D's
+    fp32 rounding, about half of the full bound on i.i.d. data, is no part
+    of the exact distances); ``bound()`` = the bounds on the fp32 D (B64
+    plus D's own fp32 formation).  ``raw``: no pair was recomputed, so the
+    native certificate (_fsagg_host.gram_select) reads the buffer as is."""
+
+    def __init__(self, host, nseg, cert=None, bound=None):
+        self.host, self.nseg = host, nseg
+        self._cert, self._bound = cert, bound
+        self.raw = cert is None
+
+    def cert(self):
+        if self._cert is None:
+            import numpy as np
+            _, _, Bf, D64 = ops.gram_views(self.host)
+            D64 = D64.numpy().copy()
+            Bf = Bf.numpy().astype(np.float64)
+            # D64's own fp64 sum over the keys (relative 2^-53 per add)
+            self._cert = (D64, np.maximum(Bf, Bf.T) + (self.nseg + 2) *
+                          2.0 ** -52 * np.where(np.isfinite(D64), D64, 0.0))
+        return self._cert
+
+    def bound(self):
+        if self._bound is None:
+            import numpy as np
+            D = ops.gram_views(self.host)[0].numpy().astype(np.float64)
+            # D is the fp32 formation of the fp64 per-key distances (a
+            # rounded sqrt and an fp32 add per key)
+            self._bound = self.cert()[1] + (2 * self.nseg + 2) * \
+                2.0 ** -24 * np.where(np.isfinite(D), D, 0.0)
+        return self._bound
+
+
 class _PendingD:
     """Krum's distance matrix while its kernels run (``_pairdist``):
     ``cpu()`` copies D (and the Gram path's flags, bounds and fp64 sums) to
     the host, recomputes the flagged (non-finite) pairs exactly and returns
-    the host fp32 [n][n] matrix.  ``last_pair_bound``: the bounds on D (the
-    kernel's bound on the fp64 per-key sum plus D's own fp32 formation; for
-    the recomputed pairs the formation alone); ``last_pair_cert``: (D64,
-    B64), the fp64 sums and the kernel's bounds on them alone — what the
-    selection is certified with (D's fp32 rounding, about half of the
-    first bound on i.i.d. data, is no part of the exact distances)."""
+    the host fp32 [n][n] matrix; the per-pair data go to the engine's
+    ``_pair_info`` (:class:`_PairInfo`: ``last_pair_bound``,
+    ``last_pair_cert``)."""
 
     def __init__(self, eng, st, buf=None, D=None):
         self._eng, self._st, self._buf, self._D = eng, st, buf, D
@@ -724,44 +783,38 @@ class _PendingD:
             return self._D.cpu()
         import numpy as np
         eng, st = self._eng, self._st
-        D, flags, B64, D64 = ops.gram_views(self._buf.cpu())
-        D = D.clone()
-        flags = flags.numpy()
-        flags = (flags + flags.T) > 0
-        B64 = B64.numpy().astype(np.float64)
-        B64 = np.maximum(B64, B64.T)
-        D64 = D64.numpy().copy()
-        # D64's own fp64 sum over the keys (relative 2^-53 per add)
+        host = self._buf.cpu()
         nseg = max(1, len(st.layout.keys))
-        fin64 = np.where(np.isfinite(D64), D64, 0.0)
-        B64 = B64 + (nseg + 2) * 2.0 ** -52 * fin64
-        # D is the fp32 formation of the fp64 per-key distances (a rounded
-        # sqrt and an fp32 add per key)
-        B = B64 + (2 * nseg + 2) * 2.0 ** -24 * np.where(
-            np.isfinite(D.numpy()), D.numpy(), 0.0).astype(np.float64)
+        D, flags, _, _ = ops.gram_views(host)
         eng.last_pairdist_path = 'mfma'
-        if flags.any():
-            # the flagged pairs exactly: the VALU kernel over the clients
-            # involved (every pair among them)
-            sel = sorted(set(np.nonzero(flags)[0].tolist()))
-            exact = eng._sum_pieces(
-                st.subset(sel), lambda rs, lo, hi: ops.pairdist_rows_segsq(
-                    rs, lo, hi))
-            sub = ops.pairdist_finish(exact).cpu()
-            idx = torch.tensor(sel)
-            D[idx[:, None], idx[None, :]] = sub
-            # exact per-key sums, but D is still their fp32 formation (a
-            # rounded sqrt and an fp32 add per key)
-            s = sub.numpy().astype(np.float64)
-            form = (2 * nseg + 2) * 2.0 ** -24 * np.where(np.isfinite(s), s,
-                                                           0.0)
-            B[np.ix_(sel, sel)] = form
-            D64[np.ix_(sel, sel)] = s
-            B64[np.ix_(sel, sel)] = form
-            eng.last_pairdist_path = 'mfma + exact %d of %d clients' % (
-                len(sel), st.n)
-        eng.last_pair_bound = B
-        eng.last_pair_cert = (D64, B64)
+        flags = flags.numpy()
+        if not flags.any():
+            eng._pair_info = _PairInfo(host, nseg)
+            return D
+        info = _PairInfo(host, nseg)
+        D64, B64 = (a.copy() for a in info.cert())
+        B = info.bound().copy()
+        D = D.clone()
+        flags = (flags + flags.T) > 0
+        # the flagged pairs exactly: the VALU kernel over the clients
+        # involved (every pair among them)
+        sel = sorted(set(np.nonzero(flags)[0].tolist()))
+        exact = eng._sum_pieces(
+            st.subset(sel), lambda rs, lo, hi: ops.pairdist_rows_segsq(
+                rs, lo, hi))
+        sub = ops.pairdist_finish(exact).cpu()
+        idx = torch.tensor(sel)
+        D[idx[:, None], idx[None, :]] = sub
+        # exact per-key sums, but D is still their fp32 formation (a
+        # rounded sqrt and an fp32 add per key)
+        s = sub.numpy().astype(np.float64)
+        form = (2 * nseg + 2) * 2.0 ** -24 * np.where(np.isfinite(s), s, 0.0)
+        B[np.ix_(sel, sel)] = form
+        D64[np.ix_(sel, sel)] = s
+        B64[np.ix_(sel, sel)] = form
+        eng.last_pairdist_path = 'mfma + exact %d of %d clients' % (
+            len(sel), st.n)
+        eng._pair_info = _PairInfo(host, nseg, cert=(D64, B64), bound=B)
         return D
 
 

@@ -39,6 +39,8 @@
 // host/b64frame.cpp: the framing walk of one gRPC tensor upload
 PyObject *b64_frame(PyObject *, PyObject *args);
 PyObject *b64_frame_many(PyObject *, PyObject *args);
+// host/krumcert.cpp: the Krum selection certificate
+PyObject *gram_select(PyObject *, PyObject *args);
 
 namespace {
 
@@ -397,6 +399,9 @@ PyMethodDef kMethods[] = {
      "text_copy(text, lo, hi, dst_addr[, threads]): copy chars [lo, hi)"},
     {"views", views, METH_VARARGS,
      "views(flat, spec_bytes) -> [Tensor]: as_strided views per record"},
+    {"gram_select", gram_select, METH_VARARGS,
+     "gram_select(buf, nseg, f, m, ordered) -> None or (scores, order, "
+     "ambiguous)"},
     {"key_table", key_table, METH_VARARGS,
      "key_table(dicts, keys, shapes, device_index[, offs4]) -> (bytes, "
      "missing, aligned16) or None"},

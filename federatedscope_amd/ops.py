@@ -891,8 +891,12 @@ class RowSet:
         idx = _np.asarray([int(i) for i in sel], dtype=_np.int64)
         if len(idx) == 0 or idx.min() < 0 or idx.max() >= self.n:
             raise IndexError('row selection outside the %d clients' % self.n)
+        # a subset of a table without absent entries has none; each client
+        # of a uniform set is uniform on its own
         return RowSet(self.layout, self.host[idx], self.device,
-                      keepalive=self._keep, aligned16=self.aligned16)
+                      keepalive=self._keep, aligned16=self.aligned16,
+                      missing=0 if self.missing == 0 else None,
+                      uniform=self.uniform)
 
     def ptr(self):
         return ctypes.byref(self.struct)
@@ -1182,6 +1186,16 @@ def pairgram_finish(sq2, tol):
     return buf, D, ill, B, D64
 
 
+def _pairgram_rows_launch(rs, tol, seg_lo, seg_end, ws, sq2, buf):
+    D, ill, B, D64 = gram_views(buf)
+    L.check(L.load().fsagg_pairgram_rows_f32(
+        rs.ptr(), seg_lo.data_ptr(), seg_end.data_ptr(),
+        max(rs.layout.numel, 1), float(tol), sq2[0].data_ptr(),
+        sq2[1].data_ptr(), D.data_ptr(), ill.data_ptr(), B.data_ptr(),
+        D64.data_ptr(), ws.data_ptr(), ws.numel(), _stream(rs.device)),
+        'fsagg_pairgram_rows_f32')
+
+
 def pairgram_rows_dist(rs, tol, workspace=None):
     """:func:`pairgram_rows_segsq` and :func:`pairgram_finish` in one call
     (fsagg_pairgram_rows_f32).  Returns (buf, D, ill, B, D64, sq2) as those
@@ -1192,19 +1206,85 @@ def pairgram_rows_dist(rs, tol, workspace=None):
                          L.FSAGG_PAIRGRAM_MAX_CLIENTS)
     lay = rs.layout
     seg_lo, seg_end = lay.seg_bounds(rs.device, 0, lay.numel, None)
-    lib = L.load()
-    extent = max(lay.numel, 1)
-    need = lib.fsagg_pairgram_workspace_bytes(rs.n, extent, rs.nseg)
+    need = L.load().fsagg_pairgram_workspace_bytes(rs.n, max(lay.numel, 1),
+                                                   rs.nseg)
     ws = (workspace or _WS).get(rs.device, need)
     sq2 = torch.empty((2, rs.nseg, rs.n, rs.n), dtype=torch.float64,
                       device=rs.device)
-    buf, D, ill, B, D64 = _gram_buf(rs.n, rs.device)
-    L.check(lib.fsagg_pairgram_rows_f32(
-        rs.ptr(), seg_lo.data_ptr(), seg_end.data_ptr(), extent, float(tol),
-        sq2[0].data_ptr(), sq2[1].data_ptr(), D.data_ptr(), ill.data_ptr(),
-        B.data_ptr(), D64.data_ptr(), ws.data_ptr(), ws.numel(),
-        _stream(rs.device)), 'fsagg_pairgram_rows_f32')
-    return buf, D, ill, B, D64, sq2
+    buf = _gram_buf(rs.n, rs.device)[0]
+    _pairgram_rows_launch(rs, tol, seg_lo, seg_end, ws, sq2, buf)
+    return (buf,) + gram_views(buf) + (sq2,)
+
+
+class _GraphCache:
+    """Captured launch chains (HIP graphs, through torch.cuda.CUDAGraph) of
+    the multi-kernel paths whose launches cost more host time than their
+    small kernels run: the Gram chain is eight launches (~50 µs of host
+    time at C4, against ~10 µs for one graph launch).  An entry is keyed by
+    everything its kernels' arguments hold — the device row table's
+    address (the upload cache hands the same table tensor back for the same
+    rows), the shape, the tolerance — and owns its workspace and outputs,
+    so nothing another call allocates can move under it; it keeps the row
+    table alive, so its address cannot be reused while the graph lives.
+    The outputs are overwritten by the next replay: a caller consumes them
+    (copies them to the host) before its next call."""
+    MAX_ENTRIES = 8
+
+    def __init__(self):
+        from collections import OrderedDict
+        self.entries = OrderedDict()
+        self.enabled = True
+        self.captures = 0
+
+    def get(self, key, build):
+        e = self.entries.get(key)
+        if e is None:
+            e = self.entries[key] = build()
+            self.captures += 1
+            while len(self.entries) > self.MAX_ENTRIES:
+                self.entries.popitem(last=False)
+        else:
+            self.entries.move_to_end(key)
+        return e
+
+
+_GRAPHS = _GraphCache()
+
+
+def pairgram_rows_dist_graph(rs, tol):
+    """:func:`pairgram_rows_dist` replayed from a captured graph (captured
+    on the first call for these rows and shape, replayed after): returns
+    (buf, D, ill, B, D64) views of the entry's own buffer, valid until the
+    next call for the same rows."""
+    if not _GRAPHS.enabled:
+        return pairgram_rows_dist(rs, tol)[:5]
+    _require_all(rs, 'Krum')
+    if not 2 <= rs.n <= L.FSAGG_PAIRGRAM_MAX_CLIENTS:
+        raise ValueError('the Gram path takes 2..%d clients' %
+                         L.FSAGG_PAIRGRAM_MAX_CLIENTS)
+    lay = rs.layout
+    key = ('pairgram', rs.device.index, rs.tab.data_ptr(), rs.ss, rs.n,
+           rs.nseg, lay.signature(), float(tol))
+
+    def build():
+        seg_lo, seg_end = lay.seg_bounds(rs.device, 0, lay.numel, None)
+        need = L.load().fsagg_pairgram_workspace_bytes(
+            rs.n, max(lay.numel, 1), rs.nseg)
+        ws = torch.empty(max(int(need), 1), dtype=torch.uint8,
+                         device=rs.device)
+        sq2 = torch.empty((2, rs.nseg, rs.n, rs.n), dtype=torch.float64,
+                          device=rs.device)
+        buf = _gram_buf(rs.n, rs.device)[0]
+        # one eager run first (loads the code objects outside the capture)
+        _pairgram_rows_launch(rs, tol, seg_lo, seg_end, ws, sq2, buf)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            _pairgram_rows_launch(rs, tol, seg_lo, seg_end, ws, sq2, buf)
+        return g, buf, (rs.tab, seg_lo, seg_end, ws, sq2)
+
+    g, buf, _ = _GRAPHS.get(key, build)
+    g.replay()
+    return (buf,) + gram_views(buf)
 
 
 def pairdist_rows(rs, workspace=None):

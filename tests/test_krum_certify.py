@@ -159,3 +159,66 @@ def test_refine_selection_gives_up_on_ties_and_nonfinite():
     # more rows than allowed
     assert refine_selection(D, B, f, m, True, amb, lambda s: De[s], 1e-14,
                             1) is None
+
+
+def _gram_buffer(D64, Bf, flags=None):
+    n = D64.shape[0]
+    buf = np.zeros((5, n, n), dtype=np.int32)
+    buf[0:2].reshape(-1).view(np.float64)[:] = D64.reshape(-1)
+    buf[2] = D64.astype(np.float32).view(np.int32)
+    if flags is not None:
+        buf[3] = flags
+    buf[4] = Bf.astype(np.float32).view(np.int32)
+    return buf
+
+
+@pytest.mark.parametrize('ordered', [True, False])
+def test_native_certificate_matches_python(ordered):
+    """_fsagg_host.gram_select (csrc/host/krumcert.cpp) against the Python
+    restatement: the same ambiguous set and, when certified, the same
+    selection."""
+    from federatedscope_amd import _lib
+    from federatedscope_amd.core.aggregators._engine import ambiguous_clients
+    host = _lib.host()
+    seen = set()
+    for seed in range(40):
+        rng = np.random.default_rng(seed)
+        n, f = int(rng.integers(6, 60)), int(rng.integers(0, 5))
+        m = int(rng.integers(1, n + 1)) if ordered else max(1, n - 2 * f)
+        nseg = int(rng.integers(1, 12))
+        X = rng.standard_normal((n, 8))
+        D64 = np.sqrt(((X[:, None] - X[None]) ** 2).sum(-1))
+        np.fill_diagonal(D64, np.inf)
+        scale = 10.0 ** rng.uniform(-7, -2)
+        Bf = (scale * np.where(np.isfinite(D64), D64, 0.0) *
+              rng.random((n, n))).astype(np.float32)
+        np.fill_diagonal(Bf, 0)
+        got = host.gram_select(_gram_buffer(D64, Bf), nseg, f, m, ordered)
+        B64 = np.maximum(Bf, Bf.T).astype(np.float64) + (nseg + 2) * \
+            2.0 ** -52 * np.where(np.isfinite(D64), D64, 0.0)
+        k = n - f - 2
+        if k <= 0:
+            assert got is None
+            continue
+        sc = np.sort(D64, 1)[:, :k].sum(1)
+        order = np.argsort(sc, kind='stable')
+        want = ambiguous_clients(D64, B64, f, m, order, ordered)
+        g_sc, g_order, g_amb = got
+        g_sc = np.frombuffer(g_sc, dtype=np.float64)
+        g_order = np.frombuffer(g_order, dtype=np.int64).tolist()
+        assert np.allclose(g_sc, sc, rtol=1e-14)
+        assert g_amb == want, (seed, g_amb, want)
+        if not want:
+            if ordered:
+                assert g_order[:m] == order[:m].tolist()
+            else:
+                assert sorted(g_order[:m]) == sorted(order[:m].tolist())
+        seen.add(bool(want))
+    assert seen == {True, False}
+    # a flagged pair: the caller's repair path
+    D64 = np.ones((4, 4))
+    np.fill_diagonal(D64, np.inf)
+    fl = np.zeros((4, 4), dtype=np.int32)
+    fl[1, 2] = 1
+    assert host.gram_select(_gram_buffer(D64, np.zeros((4, 4)), fl), 1, 0,
+                            1, True) is None
