@@ -111,6 +111,8 @@ SIGNATURES['fsagg_coord_median_rows_f32'] = (
     _c_i, [_rows_p, _c_p, _c_i, _c_i64, _c_p, _c_i64, _c_p, _c_p])
 SIGNATURES['fsagg_orderstat_set_pair_min'] = (_c_i, [_c_i])
 SIGNATURES['fsagg_orderstat_set_group_max'] = (_c_i, [_c_i])
+SIGNATURES['fsagg_orderstat_set_group_range'] = (_c_i, [_c_i, _c_i])
+SIGNATURES['fsagg_orderstat_set_group_waves'] = (_c_i, [_c_i])
 SIGNATURES['fsagg_trimmed_mean_rows_f32'] = (
     _c_i, [_rows_p, _c_p, _c_i, _c_i64, _c_i, _c_f, _c_p, _c_i64, _c_p,
            _c_p])

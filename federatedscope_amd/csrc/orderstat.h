@@ -3,6 +3,7 @@
 // instantiations).  Not part of the public ABI.
 #pragma once
 
+#include <atomic>
 #include <utility>
 
 #include "common.h"
@@ -243,6 +244,8 @@ void launch_pair(const RowSrc &rs, unsigned grid, int n, int kk, float divisor,
 template <int MODE>
 bool launch_group(const RowSrc &rs, unsigned grid, int n, int kk,
                   float divisor, float *out, hipStream_t s);
+// its waves per block (fsagg_orderstat_set_group_waves)
+extern std::atomic<int> g_group_waves;
 
 // Launch the streaming select kernel for 255 < n <= 65535
 // (orderstat_stream.hip).

@@ -200,7 +200,15 @@ int launch(const RowSrc &rs, int nchunk, int n, int kk, float divisor,
     launch_pair<NN / 2, MODE>(rs, pgrid, n, kk, divisor, out, s);          \
   else                                                                     \
     launch_select<NN, MODE>(rs, grid, n, kk, divisor, out, s)
-  else if (n <= 255 && rs.numel <= (int64_t(1) << 30)) {
+  else if (n <= 255 && rs.numel <= (int64_t(1) << 30) &&
+           n >= g_group[MODE == kMedian ? 0 : 1][0].load() &&
+           n <= g_group[MODE == kMedian ? 0 : 1][1].load() &&
+           launch_group<MODE>(rs, rs.chunks ? unsigned(nchunk) * 4u
+                                            : unsigned((rs.numel + kWave - 1) /
+                                                       kWave),
+                              n, kk, divisor, out, s)) {
+    // the K-wave kernel, where a tuning hook opened it below 256 clients
+  } else if (n <= 255 && rs.numel <= (int64_t(1) << 30)) {
     // the two-wave form from g_pair_min clients up (orderstat_pair.h)
     const bool pair = n >= g_pair_min.load(std::memory_order_relaxed);
     const unsigned pgrid = rs.chunks ? unsigned(nchunk) * 4u
@@ -342,6 +350,19 @@ extern "C" int fsagg_trimmed_mean_rows_f32(const fsagg_rows *rows,
 
 extern "C" int fsagg_orderstat_set_pair_min(int n) {
   return g_pair_min.exchange(n < 0 ? kPairMinDefault : n);
+}
+
+extern "C" int fsagg_orderstat_set_group_range(int lo, int hi) {
+  const int prev = g_group[0][0].load();
+  for (int m = 0; m < 2; ++m) {
+    g_group[m][0] = lo < 0 ? kGroupDefault[m][0] : lo;
+    g_group[m][1] = lo < 0 ? kGroupDefault[m][1] : hi;
+  }
+  return prev;
+}
+
+extern "C" int fsagg_orderstat_set_group_waves(int k) {
+  return g_group_waves.exchange(k < 2 || k > 8 ? 8 : k);
 }
 
 extern "C" int fsagg_orderstat_set_group_max(int n) {

@@ -12,14 +12,17 @@ void launch_group_h(const RowSrc &rs, unsigned grid, int n, int kk,
                      dim3(waves * kWave), 0, s, rs, n, kk, divisor, out);
 }
 
+std::atomic<int> g_group_waves{kGroupMaxWaves};
+
 template <int MODE>
 bool launch_group(const RowSrc &rs, unsigned grid, int n, int kk,
                   float divisor, float *out, hipStream_t s) {
   // eight waves per block whatever n: two blocks (the LDS they take) fill a
   // CU's 16 wave slots — five waves per block at n = 300 left 10 of 16 and
   // ran slower than the two-pass streaming kernel
-  const int K = kGroupMaxWaves;
-  if (n <= 255 || n > K * kGroupRows) return false;
+  // (fsagg_orderstat_set_group_waves moves it for A/B)
+  const int K = g_group_waves.load(std::memory_order_relaxed);
+  if (n <= 64 || n > K * kGroupRows) return false;
   const int per = (n + K - 1) / K;
   switch ((per + 7) / 8 * 8) {
     case 32: launch_group_h<32, MODE>(rs, grid, n, kk, divisor, out, K, s); break;

@@ -453,6 +453,13 @@ int fsagg_orderstat_set_pair_min(int n);
  * one-lane streaming kernel, two passes).  Returns the previous median
  * upper bound.  For tests and A/B measurements. */
 int fsagg_orderstat_set_group_max(int n);
+/* The K-wave kernel's client range [lo, hi] for both statistics, from 65
+ * clients up (below 256 it then replaces the two-wave kernel); lo < 0
+ * restores the defaults.  Returns the previous median lower bound.  And
+ * its waves per workgroup, 2..8 (anything else: the default 8); returns
+ * the previous count.  For tests and A/B measurements. */
+int fsagg_orderstat_set_group_range(int lo, int hi);
+int fsagg_orderstat_set_group_waves(int k);
 
 /* Krum per-key squared distances over a row set: segment s covers
  * [seg_lo[s], seg_end[s]) (device int64 arrays; keys may leave gaps between
