@@ -117,6 +117,7 @@ SIGNATURES['fsagg_trimmed_mean_rows_f32'] = (
     _c_i, [_rows_p, _c_p, _c_i, _c_i64, _c_i, _c_f, _c_p, _c_i64, _c_p,
            _c_p])
 SIGNATURES['fsagg_pairgram_workspace_bytes'] = (_c_sz, [_c_i, _c_i64, _c_i])
+SIGNATURES['fsagg_pairgram_set_block8'] = (_c_i, [_c_i])
 SIGNATURES['fsagg_pairgram_rows_segsq_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_sz, _c_p])
 SIGNATURES['fsagg_pairgram_rows_f32'] = (

@@ -42,6 +42,9 @@
 // 16 + 4(l>>4) .. +3 of the k-step — any permutation of k is a valid
 // contraction as long as both operands use it); every value is read from
 // HBM once.
+#include <atomic>
+#include <type_traits>
+
 #include "common.h"
 
 namespace fsagg {
@@ -857,10 +860,312 @@ __global__ __launch_bounds__(256) void gram_finish_kernel(
   if (q < n * n) finish_pair(q, segsq, err, n, nseg, tol, D, ill, B, D64);
 }
 
+// n > 64 (T > 4 tiles): 8-tile workgroups.  The plane-line form above
+// stages and splits every tile on 4 lines (13 workgroups per chunk at
+// T = 13) and each wave forms every pair of its line for a quarter of the
+// k-steps, so each split serves 10 pairs but every tile is split 4 times
+// over.  Here a workgroup of 8 waves holds 8 tiles: per stage (64
+// coordinates = 2 k-steps) wave w splits ITS tile's limbs once into LDS and
+// then forms its share of the workgroup's tile pairs from there — every pair
+// owned by one wave for all k-steps, so no cross-wave sum — reading its own
+// tile's fragments once per k-step and each partner's per pair.  T <= 8
+// (n <= 128): one workgroup per chunk holds every tile.  9 <= T <= 13: four
+// workgroups per chunk, tile sets {0-7}, {5-12}, {0-4, 8-10}, {0-4, 11, 12},
+// each forming only the pairs no earlier set holds (36 + 30 + 15 + 10 = 91
+// pairs, each exactly once; 32 tile splits per chunk against 52 on lines).
+// LDS: the raw stage (128 rows × 256 B, global_load_lds with the source
+// swizzle of kGramStaged) and the limbs of two k-steps (2 × 8 tiles × 3 ×
+// 1 KiB) = 80 KiB, two workgroups per CU; the centre's values come from
+// global memory one stage ahead (every workgroup of a chunk reads the same
+// row, from L2).
+constexpr int kB8Waves = 8;
+constexpr int kB8Blk = kB8Waves * kWave;
+constexpr int kB8Stage = 2 * kKStep;                // 64 coordinates
+constexpr int kB8RowBytes = kB8Stage * 4;           // 256 B
+constexpr int kB8Raw = 16 * kB8Waves * kB8RowBytes; // 32 KiB
+constexpr int kB8Limbs = 2 * kB8Waves * 3 * 1024;   // 48 KiB
+constexpr int kB8MaxPairs = 5;
+// global tile of local tile lt, per block type (0: the one block of T <= 8;
+// 1-4: the four blocks of 9 <= T <= 13); -1 = none
+__constant__ int8_t kB8Tiles[5][8] = {
+    {0, 1, 2, 3, 4, 5, 6, 7},   {0, 1, 2, 3, 4, 5, 6, 7},
+    {5, 6, 7, 8, 9, 10, 11, 12}, {0, 1, 2, 3, 4, 8, 9, 10},
+    {0, 1, 2, 3, 4, 11, 12, -1}};
+// wave w's local tile pairs lo·8 + hi (lo <= hi, each includes tile w), -1
+// none; type 0 and 1: every pair of 8 tiles, (w, w + d mod 8) for d <= 3 and
+// (w, w + 4) for w < 4; type 2: without the pairs inside tiles 0-2 (block 1
+// holds them); types 3, 4: tiles 0-4 against 5-7 / 5-6
+__constant__ int8_t kB8Pairs[5][8][kB8MaxPairs] = {
+    {{0, 1, 2, 3, 4}, {9, 10, 11, 12, 13}, {18, 19, 20, 21, 22},
+     {27, 28, 29, 30, 31}, {36, 37, 38, 39, -1}, {45, 46, 47, 5, -1},
+     {54, 55, 6, 14, -1}, {63, 7, 15, 23, -1}},
+    {{0, 1, 2, 3, 4}, {9, 10, 11, 12, 13}, {18, 19, 20, 21, 22},
+     {27, 28, 29, 30, 31}, {36, 37, 38, 39, -1}, {45, 46, 47, 5, -1},
+     {54, 55, 6, 14, -1}, {63, 7, 15, 23, -1}},
+    {{3, 4, -1, -1, -1}, {11, 12, 13, -1, -1}, {19, 20, 21, 22, -1},
+     {27, 28, 29, 30, 31}, {36, 37, 38, 39, -1}, {45, 46, 47, 5, -1},
+     {54, 55, 6, 14, -1}, {63, 7, 15, 23, -1}},
+    {{5, 6, 7, -1, -1}, {13, 14, 15, -1, -1}, {21, 22, 23, -1, -1},
+     {29, 30, 31, -1, -1}, {37, 38, 39, -1, -1}, {-1, -1, -1, -1, -1},
+     {-1, -1, -1, -1, -1}, {-1, -1, -1, -1, -1}},
+    {{5, 6, -1, -1, -1}, {13, 14, -1, -1, -1}, {21, 22, -1, -1, -1},
+     {29, 30, -1, -1, -1}, {37, 38, -1, -1, -1}, {-1, -1, -1, -1, -1},
+     {-1, -1, -1, -1, -1}, {-1, -1, -1, -1, -1}}};
+
+// the 8 values of lane (row rr, group g) for k-step ks of a raw stage
+__device__ __forceinline__ void b8_read8(const char *buf, int rr, int ks,
+                                         int g, float (&v)[8]) {
+  typedef __attribute__((address_space(3))) const f32x4 lds_f32x4;
+  const int c0 = 8 * ks + g, c1 = c0 + 4;
+  const char *r = buf + rr * kB8RowBytes;
+  const f32x4 x = *(lds_f32x4 *)(uintptr_t)(r + 16 * (c0 ^ (rr & 15)));
+  const f32x4 y = *(lds_f32x4 *)(uintptr_t)(r + 16 * (c1 ^ (rr & 15)));
+  v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+}
+
+// limb fragment (k-step ks, local tile t, limb 0/1/2 = h/m/l) of this lane
+__device__ __forceinline__ frag8 *b8_limb(char *limbs, int ks, int t, int lb,
+                                         int lane) {
+  return reinterpret_cast<frag8 *>(limbs + ((ks * kB8Waves + t) * 3 + lb) *
+                                               1024 + lane * 16);
+}
+
+struct Limbs3 {
+  frag8 h, m, l;
+};
+
+__device__ __forceinline__ Limbs3 b8_load(char *limbs, int ks, int t,
+                                          int lane) {
+  Limbs3 f;
+  f.h = *b8_limb(limbs, ks, t, 0, lane);
+  f.m = *b8_limb(limbs, ks, t, 1, lane);
+  f.l = *b8_limb(limbs, ks, t, 2, lane);
+  return f;
+}
+
+// the six limb products of (a, b) for one k-step, small first (as
+// kstep_mfma), into fp64
+__device__ __forceinline__ void b8_pair(const Limbs3 &a, const Limbs3 &b,
+                                        double (&acc)[4]) {
+  f32x4 x = {0.0f, 0.0f, 0.0f, 0.0f};
+  x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, b.m, x, 0, 0, 0);
+  x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.l, x, 0, 0, 0);
+  x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, b.h, x, 0, 0, 0);
+  x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.m, x, 0, 0, 0);
+  x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, b.h, x, 0, 0, 0);
+  x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.h, x, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) acc[r] += double(x[r]);
+}
+
+template <bool CENTRED>
+__global__ __launch_bounds__(kB8Blk)
+__attribute__((amdgpu_waves_per_eu(4))) void gram_block8_kernel(
+    const float *const *__restrict__ tab, int64_t ss, int n, int T, int NB,
+    const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
+    int nseg, GramCtl ctl, int64_t w, int64_t cap,
+    const int *__restrict__ centre, double *__restrict__ partial) {
+  __shared__ __attribute__((aligned(1024))) char raw[kB8Raw];
+  __shared__ __attribute__((aligned(1024))) char limbs[kB8Limbs];
+  const int *__restrict__ prefix = ctl.prefix;
+  // blocks b and b + 8 share an XCD: a chunk's NB workgroups run on one
+  // XCD together and read its rows from that L2 after the first
+  const int kq = int(blockIdx.x >> 3);
+  const int chunk = (kq / NB) * 8 + int(blockIdx.x & 7);
+  const int type = NB == 1 ? 0 : 1 + kq % NB;
+  if (chunk >= prefix[nseg]) return;  // whole workgroup
+  int s = 0;
+  while (prefix[s + 1] <= chunk) ++s;
+  const int q = chunk - prefix[s];
+  const int wv = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / kWave);
+  const int lane = int(threadIdx.x) % kWave, g = lane >> 4;
+  int64_t send = seg_end[s];
+  if (cap > 0 && send > seg_lo[s] + cap) send = seg_lo[s] + cap;
+  const int64_t c0 = seg_lo[s] + int64_t(q) * w;
+  const int64_t c1 = min(c0 + w, send);
+  const int64_t len = c1 > c0 ? c1 - c0 : 0;
+  const float *const *rows = tab + int64_t(s) * ss;
+  auto client = [&](int lt, int r) {  // row r of local tile lt, clamped
+    const int gt = kB8Tiles[type][lt];
+    const int j = 16 * gt + r;
+    return gt < 0 || j >= n ? n - 1 : j;
+  };
+  // this wave's own tile row (the split) and the centre row
+  const float *own = rows[client(wv, lane & 15)];
+  const float *crow = CENTRED ? rows[*centre] : nullptr;
+  // the raw stage: pieces k = wv + 8m (m < 4), lane l → row 4k + (l >> 4),
+  // 16-B chunk l & 15, stored at slot (l & 15) ^ (row & 15) of that row
+  const float *src[4];
+  uint32_t dst[4];
+  bool ok = true;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int rr = 4 * (wv + kB8Waves * m) + (lane >> 4);
+    const float *rp = rows[client(rr >> 4, rr & 15)];
+    ok = ok && al16(rp + c0);
+    src[m] = rp + c0 + 4 * (lane & 15);
+    dst[m] = uint32_t(rr * kB8RowBytes + 16 * ((lane & 15) ^ (rr & 15)));
+  }
+  // the workgroup's agreement through the (still unused) limb area: a
+  // __syncthreads_and would take LDS of its own past the 80 KiB that lets
+  // two workgroups share a CU
+  uint32_t *flag = reinterpret_cast<uint32_t *>(limbs);
+  if (lane == 0) flag[wv] = __all(ok) ? 1u : 0u;
+  __syncthreads();
+  bool vec = true;
+#pragma unroll
+  for (int v = 0; v < kB8Waves; ++v) vec = vec && flag[v] != 0u;
+  __syncthreads();  // read before any limb is written
+
+  // this wave's pairs (wave-uniform): local (lo, hi), each holding tile wv
+  int np = 0;
+  int part[kB8MaxPairs];  // the partner tile of pair p (wv itself: diagonal)
+#pragma unroll
+  for (int p = 0; p < kB8MaxPairs; ++p) {
+    const int e = kB8Pairs[type][wv][p];
+    const int lo = e >= 0 ? e >> 3 : wv, hi = e >= 0 ? e & 7 : wv;
+    part[p] = __builtin_amdgcn_readfirstlane(lo == wv ? hi : lo);
+    np += e >= 0 ? 1 : 0;
+  }
+  np = __builtin_amdgcn_readfirstlane(np);
+  double acc[kB8MaxPairs][4];
+#pragma unroll
+  for (int p = 0; p < kB8MaxPairs; ++p)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[p][r] = 0.0;
+
+  const Neg kn = neg_consts();
+  // the products of k-step ks from the limbs, each pair formed with this
+  // wave's tile as the first operand (a pair whose first tile is the
+  // partner is stored transposed at the end).  Measured and not kept: the
+  // pairs' chains interleaved in a branch-free body (two at a time or all):
+  // at the 128-VGPR budget of two workgroups per CU it spills, at one
+  // workgroup per CU n = 100 took 1.39 ms against 0.93
+  auto mfma_phase = [&](int ks) {
+    const Limbs3 mine = b8_load(limbs, ks, wv, lane);
+#pragma unroll
+    for (int p = 0; p < kB8MaxPairs; ++p) {
+      if (p < np) {
+        if (part[p] == wv) {
+          b8_pair(mine, mine, acc[p]);
+        } else {
+          const Limbs3 o = b8_load(limbs, ks, part[p], lane);
+          b8_pair(mine, o, acc[p]);
+        }
+      }
+    }
+  };
+  auto split_to = [&](int ks, const float (&x)[8]) {
+    frag8 h, m, l;
+    split3(x, kn, h, m, l);
+    *b8_limb(limbs, ks, wv, 0, lane) = h;
+    *b8_limb(limbs, ks, wv, 1, lane) = m;
+    *b8_limb(limbs, ks, wv, 2, lane) = l;
+  };
+
+  const int nstage = vec ? int(len / kB8Stage) : 0;
+  float cb[2][8];
+  auto centre_load = [&](int st) {
+    if (CENTRED) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        ld8(crow + c0 + int64_t(st) * kB8Stage + ks * kKStep + 4 * g, cb[ks]);
+    }
+  };
+  // a stage's rows in flight in registers (16-B loads, each row's 256 B
+  // by one 16-lane group), written to the raw stage once every wave has
+  // read the previous one: the loads of stage st + 2 fly while stage st's
+  // products are formed and stage st + 1 is split
+  f32x4 pre[4];
+  auto fetch = [&](int st) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      pre[m] = gld_nt(reinterpret_cast<const f32x4 *>(
+          src[m] + int64_t(st) * kB8Stage));
+  };
+  auto put = [&]() {
+    typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      *(lds_f32x4 *)(uintptr_t)(raw + dst[m]) = pre[m];
+  };
+  if (nstage > 0) {
+    fetch(0);
+    centre_load(0);
+    put();
+    if (nstage > 1) fetch(1);
+  }
+  for (int st = 0; st < nstage; ++st) {
+    // stage st is in the raw buffer (every wave's part), and every wave is
+    // done reading the limbs of stage st − 1
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      float x[8];
+      b8_read8(raw, 16 * wv + (lane & 15), ks, g, x);
+      if (CENTRED) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] -= cb[ks][j];
+      }
+      split_to(ks, x);
+    }
+    // the limbs are written and the raw stage read by every wave
+    __syncthreads();
+    if (st + 1 < nstage) {
+      put();
+      centre_load(st + 1);
+      if (st + 2 < nstage) fetch(st + 2);
+    }
+    mfma_phase(0);
+    mfma_phase(1);
+  }
+  // the rest (unaligned rows: everything; aligned: the last partial stage),
+  // one k-step at a time from global memory
+  const int nall = int((len + kKStep - 1) / kKStep);
+  for (int i = 2 * nstage; i < nall; ++i) {
+    const int64_t k0 = c0 + int64_t(i) * kKStep;
+    __syncthreads();  // every wave is done with the limbs
+    float x[8], cc[8];
+    ld8_tail(own, k0, c1, g, x);
+    if (CENTRED) {
+      ld8_tail(crow, k0, c1, g, cc);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] -= cc[j];
+    }
+    split_to(0, x);
+    __syncthreads();
+    mfma_phase(0);
+  }
+  const int ntpg = T * (T + 1) / 2;
+  double *out = partial + int64_t(chunk) * ntpg * 256;
+#pragma unroll
+  for (int p = 0; p < kB8MaxPairs; ++p) {
+    if (p >= np) continue;
+    const int a = kB8Tiles[type][wv], b = kB8Tiles[type][part[p]];
+    if (a < 0 || b < 0 || a >= T || b >= T) continue;  // absent tiles
+    double *o = out + int64_t(pair_index(min(a, b), max(a, b), T)) * 256;
+    // acc holds block (a, b) in MFMA C-layout: row 4(lane >> 4) + r of
+    // tile a, column lane & 15 of tile b; block (b, a) is its transpose
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * (lane >> 4) + r, j = lane & 15;
+      o[a <= b ? r * 64 + lane : (j & 3) * 64 + (j >> 2) * 16 + i] =
+          acc[p][r];
+    }
+  }
+}
+
+// n > 64: 1 = the 8-tile workgroups (gram_block8_kernel) up to 128
+// clients, the plane lines above (default); 2 = 8-tile workgroups for every
+// n > 64; 0 = plane lines throughout (fsagg_pairgram_set_block8, A/B)
+std::atomic<int> g_block8{1};
+
 struct GramPlan {
   int nt;              // tiles of 16 clients
-  bool lines;          // nt > kFullTiles: one workgroup per plane line
-  int nlines;          // 13 (PG(2,3)) or 7 (Fano)
+  bool lines;          // nt > kFullTiles: several workgroups per chunk
+  bool block8;         // ... 8-tile workgroups (else plane lines)
+  int nlines;          // workgroups per chunk: 13 / 7 lines, or 1 / 4 blocks
   int ntpg;            // tile pairs
   int64_t w;           // main chunk length (multiple of kUnit)
   int main_chunks;     // upper bounds
@@ -872,13 +1177,24 @@ GramPlan gram_plan(int n, int64_t numel, int nseg) {
   GramPlan pl;
   pl.nt = (n + 15) / 16;
   pl.lines = pl.nt > kFullTiles;
-  pl.nlines = pl.lines ? (pl.nt <= 7 ? 7 : 13) : 1;
+  // 8-tile workgroups where they measured faster than the plane lines:
+  // one workgroup per chunk (T <= 8, n <= 128: 0.93 against 1.08 ms at
+  // n = 100); the four-workgroup covering of T <= 13 measured slower (3.7
+  // against 3.16 ms at n = 200) and runs only under the A/B setting 2
+  const int b8 = g_block8.load(std::memory_order_relaxed);
+  pl.block8 = pl.lines && (b8 == 2 || (b8 == 1 && pl.nt <= kB8Waves));
+  pl.nlines = !pl.lines ? 1
+              : pl.block8 ? (pl.nt <= kB8Waves ? 1 : 4)
+                          : (pl.nt <= 7 ? 7 : 13);
   pl.ntpg = ntp_of(pl.nt);
   // ~kMainChunks workgroups; LINES: ~kLineBlocks over all the lines
-  // (fewer, longer chunks: less partial traffic)
+  // (fewer, longer chunks: less partial traffic); 8-tile blocks: ~2048
+  // workgroups of 512 threads (1024 chunks of one block, 512 of four)
   const int64_t target =
-      pl.lines ? (kLineBlocks / pl.nlines > 64 ? kLineBlocks / pl.nlines : 64)
-               : kMainChunks;
+      !pl.lines ? kMainChunks
+      : pl.block8 ? (pl.nlines == 1 ? 1024 : 512)
+                  : (kLineBlocks / pl.nlines > 64 ? kLineBlocks / pl.nlines
+                                                  : 64);
   int64_t w = (numel + target - 1) / target;
   w = (w + kUnit - 1) / kUnit * kUnit;
   if (w < kUnit) w = kUnit;
@@ -943,6 +1259,25 @@ size_t gram_ws_layout(int n, int64_t numel, int nseg, void *ws, GramWs *w) {
 // Seven launches (eight with the finish): both plans; the sample pass, the
 // tile pairs' distance sums and the centre; the centred main pass, its group
 // sums, and per key and tile pair the Gram block, d² and bounds.
+// the sample (CENTRED false) or main pass's chunk kernel
+template <int NT, bool LINES, bool CENTRED>
+void gram_pass(const float *const *tab, int64_t ss, int n,
+               const int64_t *seg_lo, const int64_t *seg_end, int nseg,
+               const GramPlan &pl, GramCtl ctl, int64_t w, int64_t cap,
+               const int *centre, double *partial, int chunks,
+               hipStream_t st) {
+  if (LINES && pl.block8)
+    hipLaunchKernelGGL((gram_block8_kernel<CENTRED>),
+                       dim3(chunk_grid(pl, chunks)), dim3(kB8Blk), 0, st, tab,
+                       ss, n, pl.nt, pl.nlines, seg_lo, seg_end, nseg, ctl, w,
+                       cap, centre, partial);
+  else
+    hipLaunchKernelGGL((gram_chunk_kernel<NT, CENTRED, LINES>),
+                       dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab,
+                       ss, n, pl.nt, seg_lo, seg_end, nseg, ctl, w, cap,
+                       centre, partial);
+}
+
 template <int NT, bool LINES>
 void gram_launch(const float *const *tab, int64_t ss, int n,
                  const int64_t *seg_lo, const int64_t *seg_end, int nseg,
@@ -954,21 +1289,17 @@ void gram_launch(const float *const *tab, int64_t ss, int n,
                      seg_lo, seg_end, nseg, kSampleChunk, kSampleCoords, pl.w,
                      w.cs, w.cm);
   // 1. the centre: Gram of the first kSampleCoords of every key, raw
-  hipLaunchKernelGGL((gram_chunk_kernel<NT, false, LINES>),
-                     dim3(chunk_grid(pl, pl.sample_chunks)), dim3(kBlk), 0,
-                     st, tab, ss, n, T, seg_lo, seg_end, nseg, w.cs,
-                     kSampleChunk, kSampleCoords,
-                     static_cast<const int *>(nullptr), w.partial);
+  gram_pass<NT, LINES, false>(tab, ss, n, seg_lo, seg_end, nseg, pl, w.cs,
+                              kSampleChunk, kSampleCoords, nullptr, w.partial,
+                              pl.sample_chunks, st);
   hipLaunchKernelGGL(gram_centre_pairs_kernel, dim3(unsigned(pl.ntpg)),
                      dim3(256), 0, st, w.partial, w.cs, nseg, n, T, w.rsum);
   hipLaunchKernelGGL(gram_centre_pick_kernel, dim3(1), dim3(256), 0, st,
                      w.rsum, n, T, w.centre);
   // 2. the centred Gram of every key, its d² and bounds
-  hipLaunchKernelGGL((gram_chunk_kernel<NT, true, LINES>),
-                     dim3(chunk_grid(pl, pl.main_chunks)), dim3(kBlk), 0, st,
-                     tab, ss, n, T, seg_lo, seg_end, nseg, w.cm, pl.w,
-                     int64_t(0), static_cast<const int *>(w.centre),
-                     w.partial);
+  gram_pass<NT, LINES, true>(tab, ss, n, seg_lo, seg_end, nseg, pl, w.cm,
+                             pl.w, int64_t(0), w.centre, w.partial,
+                             pl.main_chunks, st);
   hipLaunchKernelGGL(gram_reduce1_kernel,
                      dim3(unsigned(pl.main_groups), unsigned(pl.ntpg)),
                      dim3(256), 0, st, w.partial, w.cm, nseg, pl.ntpg, w.red);
@@ -986,6 +1317,10 @@ void gram_launch(const float *const *tab, int64_t ss, int n,
 }  // namespace fsagg
 
 using namespace fsagg;
+
+extern "C" int fsagg_pairgram_set_block8(int on) {
+  return g_block8.exchange(on < 0 ? 1 : (on > 2 ? 2 : on));
+}
 
 extern "C" size_t fsagg_pairgram_workspace_bytes(int n, int64_t numel,
                                                  int nseg) {
