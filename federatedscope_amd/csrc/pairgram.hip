@@ -879,23 +879,31 @@ __global__ __launch_bounds__(256) void gram_finish_kernel(
 // global memory one stage ahead (every workgroup of a chunk reads the same
 // row, from L2).
 constexpr int kB8Waves = 8;
-constexpr int kB8Blk = kB8Waves * kWave;
 constexpr int kB8Stage = 2 * kKStep;                // 64 coordinates
 constexpr int kB8RowBytes = kB8Stage * 4;           // 256 B
-constexpr int kB8Raw = 16 * kB8Waves * kB8RowBytes; // 32 KiB
-constexpr int kB8Limbs = 2 * kB8Waves * 3 * 1024;   // 48 KiB
-constexpr int kB8MaxPairs = 5;
+// Two configurations: 8 tiles on 8 waves (types 0-4 below: T <= 8, or the
+// four-workgroup covering of T <= 13 under the A/B setting), and all 13
+// tiles on 16 waves (type 5: 9 <= T <= 13, one workgroup per chunk).
+template <int NT, int W>
+struct B8Cfg {
+  static constexpr int kBlk = W * kWave;
+  static constexpr int kRaw = 16 * NT * kB8RowBytes;   // 32 / 52 KiB
+  static constexpr int kLimbs = 2 * NT * 3 * 1024;     // 48 / 78 KiB
+  static constexpr int kPieces = 4 * NT;               // 4-row pieces
+  static constexpr int kMy = (kPieces + W - 1) / W;    // per wave
+  static constexpr int kMaxPairs = NT == 8 ? 5 : 6;
+};
 // global tile of local tile lt, per block type (0: the one block of T <= 8;
 // 1-4: the four blocks of 9 <= T <= 13); -1 = none
 __constant__ int8_t kB8Tiles[5][8] = {
     {0, 1, 2, 3, 4, 5, 6, 7},   {0, 1, 2, 3, 4, 5, 6, 7},
     {5, 6, 7, 8, 9, 10, 11, 12}, {0, 1, 2, 3, 4, 8, 9, 10},
     {0, 1, 2, 3, 4, 11, 12, -1}};
-// wave w's local tile pairs lo·8 + hi (lo <= hi, each includes tile w), -1
-// none; type 0 and 1: every pair of 8 tiles, (w, w + d mod 8) for d <= 3 and
-// (w, w + 4) for w < 4; type 2: without the pairs inside tiles 0-2 (block 1
-// holds them); types 3, 4: tiles 0-4 against 5-7 / 5-6
-__constant__ int8_t kB8Pairs[5][8][kB8MaxPairs] = {
+// wave w's local tile pairs lo·8 + hi (lo <= hi), -1 none; types 0 and 1:
+// every pair of 8 tiles, (w, w + d mod 8) for d <= 3 and (w, w + 4) for
+// w < 4; type 2: without the pairs inside tiles 0-2 (block 1 holds them);
+// types 3, 4: tiles 0-4 against 5-7 / 5-6
+__constant__ int8_t kB8Pairs[5][8][5] = {
     {{0, 1, 2, 3, 4}, {9, 10, 11, 12, 13}, {18, 19, 20, 21, 22},
      {27, 28, 29, 30, 31}, {36, 37, 38, 39, -1}, {45, 46, 47, 5, -1},
      {54, 55, 6, 14, -1}, {63, 7, 15, 23, -1}},
@@ -911,6 +919,18 @@ __constant__ int8_t kB8Pairs[5][8][kB8MaxPairs] = {
     {{5, 6, -1, -1, -1}, {13, 14, -1, -1, -1}, {21, 22, -1, -1, -1},
      {29, 30, -1, -1, -1}, {37, 38, -1, -1, -1}, {-1, -1, -1, -1, -1},
      {-1, -1, -1, -1, -1}, {-1, -1, -1, -1, -1}}};
+// 13 tiles on 16 waves: wave w's pairs t·16 + u (t <= u), -1 none — wave
+// w < 13 its own tile against (w + d mod 13), d = 0 … 5; the seventh of
+// each (d = 6) and the rest spread over waves 13-15 (91 pairs, <= 6 each)
+__constant__ uint8_t kWidePairs[16][6] = {
+    {0, 1, 2, 3, 4, 5},          {17, 18, 19, 20, 21, 22},
+    {34, 35, 36, 37, 38, 39},    {51, 52, 53, 54, 55, 56},
+    {68, 69, 70, 71, 72, 73},    {85, 86, 87, 88, 89, 90},
+    {102, 103, 104, 105, 106, 107}, {119, 120, 121, 122, 123, 124},
+    {136, 137, 138, 139, 140, 8}, {153, 154, 155, 156, 9, 25},
+    {170, 171, 172, 10, 26, 42}, {187, 188, 11, 27, 43, 59},
+    {204, 12, 28, 44, 60, 76},   {6, 23, 40, 57, 74, 91},
+    {7, 24, 41, 58, 75, 108},    {92, 255, 255, 255, 255, 255}};
 
 // the 8 values of lane (row rr, group g) for k-step ks of a raw stage
 __device__ __forceinline__ void b8_read8(const char *buf, int rr, int ks,
@@ -924,23 +944,25 @@ __device__ __forceinline__ void b8_read8(const char *buf, int rr, int ks,
   v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
 }
 
-// limb fragment (k-step ks, local tile t, limb 0/1/2 = h/m/l) of this lane
-__device__ __forceinline__ frag8 *b8_limb(char *limbs, int ks, int t, int lb,
-                                         int lane) {
-  return reinterpret_cast<frag8 *>(limbs + ((ks * kB8Waves + t) * 3 + lb) *
-                                               1024 + lane * 16);
-}
-
 struct Limbs3 {
   frag8 h, m, l;
 };
 
+// limb fragments (k-step ks, local tile t) of this lane: [ks][t][h|m|l]
+template <int NT>
+__device__ __forceinline__ frag8 *b8_limb(char *limbs, int ks, int t, int lb,
+                                         int lane) {
+  return reinterpret_cast<frag8 *>(limbs + ((ks * NT + t) * 3 + lb) * 1024 +
+                                   lane * 16);
+}
+
+template <int NT>
 __device__ __forceinline__ Limbs3 b8_load(char *limbs, int ks, int t,
                                           int lane) {
   Limbs3 f;
-  f.h = *b8_limb(limbs, ks, t, 0, lane);
-  f.m = *b8_limb(limbs, ks, t, 1, lane);
-  f.l = *b8_limb(limbs, ks, t, 2, lane);
+  f.h = *b8_limb<NT>(limbs, ks, t, 0, lane);
+  f.m = *b8_limb<NT>(limbs, ks, t, 1, lane);
+  f.l = *b8_limb<NT>(limbs, ks, t, 2, lane);
   return f;
 }
 
@@ -959,15 +981,22 @@ __device__ __forceinline__ void b8_pair(const Limbs3 &a, const Limbs3 &b,
   for (int r = 0; r < 4; ++r) acc[r] += double(x[r]);
 }
 
-template <bool CENTRED>
-__global__ __launch_bounds__(kB8Blk)
+// NT tiles on W waves (B8Cfg): per stage (64 coordinates = 2 k-steps) wave
+// w < NT splits local tile w's limbs into LDS once, then every wave forms
+// its pairs (t, u) from there — each pair owned by one wave for all
+// k-steps, so no cross-wave sum; the first operand's fragments are kept
+// while consecutive pairs share it.  NT = 8: block type 0-4 (kB8Tiles /
+// kB8Pairs); NT = 13: one workgroup with every tile (kWidePairs).
+template <int NT, int W, bool CENTRED>
+__global__ __launch_bounds__(W * kWave)
 __attribute__((amdgpu_waves_per_eu(4))) void gram_block8_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n, int T, int NB,
     const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
     int nseg, GramCtl ctl, int64_t w, int64_t cap,
     const int *__restrict__ centre, double *__restrict__ partial) {
-  __shared__ __attribute__((aligned(1024))) char raw[kB8Raw];
-  __shared__ __attribute__((aligned(1024))) char limbs[kB8Limbs];
+  typedef B8Cfg<NT, W> C;
+  __shared__ __attribute__((aligned(1024))) char raw[C::kRaw];
+  __shared__ __attribute__((aligned(1024))) char limbs[C::kLimbs];
   const int *__restrict__ prefix = ctl.prefix;
   // blocks b and b + 8 share an XCD: a chunk's NB workgroups run on one
   // XCD together and read its rows from that L2 after the first
@@ -986,72 +1015,90 @@ __attribute__((amdgpu_waves_per_eu(4))) void gram_block8_kernel(
   const int64_t c1 = min(c0 + w, send);
   const int64_t len = c1 > c0 ? c1 - c0 : 0;
   const float *const *rows = tab + int64_t(s) * ss;
+  auto gtile = [&](int lt) {
+    return NT == 8 ? int(kB8Tiles[type][lt]) : lt;
+  };
   auto client = [&](int lt, int r) {  // row r of local tile lt, clamped
-    const int gt = kB8Tiles[type][lt];
+    const int gt = gtile(lt);
     const int j = 16 * gt + r;
     return gt < 0 || j >= n ? n - 1 : j;
   };
   // this wave's own tile row (the split) and the centre row
-  const float *own = rows[client(wv, lane & 15)];
+  const bool splits = wv < NT;
+  const float *own = rows[client(splits ? wv : 0, lane & 15)];
   const float *crow = CENTRED ? rows[*centre] : nullptr;
-  // the raw stage: pieces k = wv + 8m (m < 4), lane l → row 4k + (l >> 4),
-  // 16-B chunk l & 15, stored at slot (l & 15) ^ (row & 15) of that row
-  const float *src[4];
-  uint32_t dst[4];
+  // the raw stage: pieces k = wv + W·m, lane l → row 4k + (l >> 4), 16-B
+  // chunk l & 15, stored at slot (l & 15) ^ (row & 15) of that row
+  const float *src[C::kMy];
+  uint32_t dst[C::kMy];
   bool ok = true;
 #pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int rr = 4 * (wv + kB8Waves * m) + (lane >> 4);
+  for (int m = 0; m < C::kMy; ++m) {
+    const int k = wv + W * m;
+    const int rr = 4 * (k < C::kPieces ? k : 0) + (lane >> 4);
     const float *rp = rows[client(rr >> 4, rr & 15)];
     ok = ok && al16(rp + c0);
     src[m] = rp + c0 + 4 * (lane & 15);
     dst[m] = uint32_t(rr * kB8RowBytes + 16 * ((lane & 15) ^ (rr & 15)));
   }
+  if (CENTRED) ok = ok && al16(crow + c0);
   // the workgroup's agreement through the (still unused) limb area: a
   // __syncthreads_and would take LDS of its own past the 80 KiB that lets
-  // two workgroups share a CU
+  // two 8-wave workgroups share a CU
   uint32_t *flag = reinterpret_cast<uint32_t *>(limbs);
   if (lane == 0) flag[wv] = __all(ok) ? 1u : 0u;
   __syncthreads();
   bool vec = true;
 #pragma unroll
-  for (int v = 0; v < kB8Waves; ++v) vec = vec && flag[v] != 0u;
+  for (int v = 0; v < W; ++v) vec = vec && flag[v] != 0u;
   __syncthreads();  // read before any limb is written
 
-  // this wave's pairs (wave-uniform): local (lo, hi), each holding tile wv
+  // this wave's pairs (wave-uniform): local (t, u), t <= u
   int np = 0;
-  int part[kB8MaxPairs];  // the partner tile of pair p (wv itself: diagonal)
+  int pt[C::kMaxPairs], pu[C::kMaxPairs];
 #pragma unroll
-  for (int p = 0; p < kB8MaxPairs; ++p) {
-    const int e = kB8Pairs[type][wv][p];
-    const int lo = e >= 0 ? e >> 3 : wv, hi = e >= 0 ? e & 7 : wv;
-    part[p] = __builtin_amdgcn_readfirstlane(lo == wv ? hi : lo);
+  for (int p = 0; p < C::kMaxPairs; ++p) {
+    int e, t, u;
+    if constexpr (NT == 8) {
+      e = kB8Pairs[type][wv][p];
+      t = e >= 0 ? e >> 3 : 0;
+      u = e >= 0 ? e & 7 : 0;
+    } else {
+      e = kWidePairs[wv][p] == 255 ? -1 : int(kWidePairs[wv][p]);
+      t = e >= 0 ? e >> 4 : 0;
+      u = e >= 0 ? e & 15 : 0;
+    }
+    pt[p] = __builtin_amdgcn_readfirstlane(t);
+    pu[p] = __builtin_amdgcn_readfirstlane(u);
     np += e >= 0 ? 1 : 0;
   }
   np = __builtin_amdgcn_readfirstlane(np);
-  double acc[kB8MaxPairs][4];
+  double acc[C::kMaxPairs][4];
 #pragma unroll
-  for (int p = 0; p < kB8MaxPairs; ++p)
+  for (int p = 0; p < C::kMaxPairs; ++p)
 #pragma unroll
     for (int r = 0; r < 4; ++r) acc[p][r] = 0.0;
 
   const Neg kn = neg_consts();
-  // the products of k-step ks from the limbs, each pair formed with this
-  // wave's tile as the first operand (a pair whose first tile is the
-  // partner is stored transposed at the end).  Measured and not kept: the
-  // pairs' chains interleaved in a branch-free body (two at a time or all):
-  // at the 128-VGPR budget of two workgroups per CU it spills, at one
-  // workgroup per CU n = 100 took 1.39 ms against 0.93
+  // the products of k-step ks from the limbs (measured and not kept: the
+  // pairs' chains interleaved in a branch-free body — at the 128-VGPR
+  // budget it spills, at one 8-wave workgroup per CU n = 100 took 1.39 ms
+  // against 0.93)
   auto mfma_phase = [&](int ks) {
-    const Limbs3 mine = b8_load(limbs, ks, wv, lane);
+    Limbs3 a;
+    int at = -1;
 #pragma unroll
-    for (int p = 0; p < kB8MaxPairs; ++p) {
+    for (int p = 0; p < C::kMaxPairs; ++p) {
       if (p < np) {
-        if (part[p] == wv) {
-          b8_pair(mine, mine, acc[p]);
+        if (pt[p] != at) {
+          a = b8_load<NT>(limbs, ks, pt[p], lane);
+          at = pt[p];
+        }
+        if (pu[p] == pt[p]) {
+          b8_pair(a, a, acc[p]);
         } else {
-          const Limbs3 o = b8_load(limbs, ks, part[p], lane);
-          b8_pair(mine, o, acc[p]);
+          const Limbs3 b = b8_load<NT>(limbs, ks, pu[p], lane);
+          b8_pair(a, b, acc[p]);
         }
       }
     }
@@ -1059,9 +1106,9 @@ __attribute__((amdgpu_waves_per_eu(4))) void gram_block8_kernel(
   auto split_to = [&](int ks, const float (&x)[8]) {
     frag8 h, m, l;
     split3(x, kn, h, m, l);
-    *b8_limb(limbs, ks, wv, 0, lane) = h;
-    *b8_limb(limbs, ks, wv, 1, lane) = m;
-    *b8_limb(limbs, ks, wv, 2, lane) = l;
+    *b8_limb<NT>(limbs, ks, wv, 0, lane) = h;
+    *b8_limb<NT>(limbs, ks, wv, 1, lane) = m;
+    *b8_limb<NT>(limbs, ks, wv, 2, lane) = l;
   };
 
   const int nstage = vec ? int(len / kB8Stage) : 0;
@@ -1077,18 +1124,20 @@ __attribute__((amdgpu_waves_per_eu(4))) void gram_block8_kernel(
   // by one 16-lane group), written to the raw stage once every wave has
   // read the previous one: the loads of stage st + 2 fly while stage st's
   // products are formed and stage st + 1 is split
-  f32x4 pre[4];
+  f32x4 pre[C::kMy];
   auto fetch = [&](int st) {
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
-      pre[m] = gld_nt(reinterpret_cast<const f32x4 *>(
-          src[m] + int64_t(st) * kB8Stage));
+    for (int m = 0; m < C::kMy; ++m)
+      if (wv + W * m < C::kPieces)
+        pre[m] = gld_nt(reinterpret_cast<const f32x4 *>(
+            src[m] + int64_t(st) * kB8Stage));
   };
   auto put = [&]() {
     typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
-      *(lds_f32x4 *)(uintptr_t)(raw + dst[m]) = pre[m];
+    for (int m = 0; m < C::kMy; ++m)
+      if (wv + W * m < C::kPieces)
+        *(lds_f32x4 *)(uintptr_t)(raw + dst[m]) = pre[m];
   };
   if (nstage > 0) {
     fetch(0);
@@ -1100,15 +1149,17 @@ __attribute__((amdgpu_waves_per_eu(4))) void gram_block8_kernel(
     // stage st is in the raw buffer (every wave's part), and every wave is
     // done reading the limbs of stage st − 1
     __syncthreads();
+    if (splits) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      float x[8];
-      b8_read8(raw, 16 * wv + (lane & 15), ks, g, x);
-      if (CENTRED) {
+      for (int ks = 0; ks < 2; ++ks) {
+        float x[8];
+        b8_read8(raw, 16 * wv + (lane & 15), ks, g, x);
+        if (CENTRED) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] -= cb[ks][j];
+          for (int j = 0; j < 8; ++j) x[j] -= cb[ks][j];
+        }
+        split_to(ks, x);
       }
-      split_to(ks, x);
     }
     // the limbs are written and the raw stage read by every wave
     __syncthreads();
@@ -1126,45 +1177,43 @@ __attribute__((amdgpu_waves_per_eu(4))) void gram_block8_kernel(
   for (int i = 2 * nstage; i < nall; ++i) {
     const int64_t k0 = c0 + int64_t(i) * kKStep;
     __syncthreads();  // every wave is done with the limbs
-    float x[8], cc[8];
-    ld8_tail(own, k0, c1, g, x);
-    if (CENTRED) {
-      ld8_tail(crow, k0, c1, g, cc);
+    if (splits) {
+      float x[8], cc[8];
+      ld8_tail(own, k0, c1, g, x);
+      if (CENTRED) {
+        ld8_tail(crow, k0, c1, g, cc);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] -= cc[j];
+        for (int j = 0; j < 8; ++j) x[j] -= cc[j];
+      }
+      split_to(0, x);
     }
-    split_to(0, x);
     __syncthreads();
     mfma_phase(0);
   }
   const int ntpg = T * (T + 1) / 2;
   double *out = partial + int64_t(chunk) * ntpg * 256;
 #pragma unroll
-  for (int p = 0; p < kB8MaxPairs; ++p) {
+  for (int p = 0; p < C::kMaxPairs; ++p) {
     if (p >= np) continue;
-    const int a = kB8Tiles[type][wv], b = kB8Tiles[type][part[p]];
-    if (a < 0 || b < 0 || a >= T || b >= T) continue;  // absent tiles
-    double *o = out + int64_t(pair_index(min(a, b), max(a, b), T)) * 256;
-    // acc holds block (a, b) in MFMA C-layout: row 4(lane >> 4) + r of
-    // tile a, column lane & 15 of tile b; block (b, a) is its transpose
+    const int a = gtile(pt[p]), b = gtile(pu[p]);
+    if (a < 0 || b < 0 || b >= T) continue;  // absent tiles
+    double *o = out + int64_t(pair_index(a, b, T)) * 256;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = 4 * (lane >> 4) + r, j = lane & 15;
-      o[a <= b ? r * 64 + lane : (j & 3) * 64 + (j >> 2) * 16 + i] =
-          acc[p][r];
-    }
+    for (int r = 0; r < 4; ++r) o[r * 64 + lane] = acc[p][r];
   }
 }
 
-// n > 64: 1 = the 8-tile workgroups (gram_block8_kernel) up to 128
-// clients, the plane lines above (default); 2 = 8-tile workgroups for every
-// n > 64; 0 = plane lines throughout (fsagg_pairgram_set_block8, A/B)
+// n > 64: 1 = tile-split workgroups (gram_block8_kernel: 8 tiles up to 128
+// clients, all 13 on 16 waves above; default); 2 = 8-tile workgroups for
+// every n > 64 (four per chunk above 128); 0 = plane lines throughout
+// (fsagg_pairgram_set_block8, A/B)
 std::atomic<int> g_block8{1};
 
 struct GramPlan {
   int nt;              // tiles of 16 clients
   bool lines;          // nt > kFullTiles: several workgroups per chunk
   bool block8;         // ... 8-tile workgroups (else plane lines)
+  bool wide;           // ... one 13-tile workgroup of 16 waves
   int nlines;          // workgroups per chunk: 13 / 7 lines, or 1 / 4 blocks
   int ntpg;            // tile pairs
   int64_t w;           // main chunk length (multiple of kUnit)
@@ -1177,14 +1226,19 @@ GramPlan gram_plan(int n, int64_t numel, int nseg) {
   GramPlan pl;
   pl.nt = (n + 15) / 16;
   pl.lines = pl.nt > kFullTiles;
-  // 8-tile workgroups where they measured faster than the plane lines:
-  // one workgroup per chunk (T <= 8, n <= 128: 0.93 against 1.08 ms at
-  // n = 100); the four-workgroup covering of T <= 13 measured slower (3.7
-  // against 3.16 ms at n = 200) and runs only under the A/B setting 2
+  // tile-split workgroups where they measured faster than the plane lines
+  // (profiles/r05/gram_block8_ab.jsonl): one 8-tile workgroup per chunk
+  // for T <= 8 (n = 100: 0.91 against 1.09 ms, n = 128: 0.99 against
+  // 2.91), one 13-tile workgroup of 16 waves for 9 <= T <= 13 (n = 200:
+  // 2.57 against 3.21 ms); the four 8-tile workgroups of the A/B setting 2
+  // measured slower (3.8 ms at n = 200)
   const int b8 = g_block8.load(std::memory_order_relaxed);
-  pl.block8 = pl.lines && (b8 == 2 || (b8 == 1 && pl.nt <= kB8Waves));
+  pl.block8 = pl.lines && b8 != 0;
+  // 9 <= T <= 13: one 16-wave workgroup with all 13 tiles (setting 1), or
+  // the four 8-tile workgroups (setting 2)
+  pl.wide = pl.block8 && pl.nt > kB8Waves && b8 == 1;
   pl.nlines = !pl.lines ? 1
-              : pl.block8 ? (pl.nt <= kB8Waves ? 1 : 4)
+              : pl.block8 ? (pl.nt <= kB8Waves || pl.wide ? 1 : 4)
                           : (pl.nt <= 7 ? 7 : 13);
   pl.ntpg = ntp_of(pl.nt);
   // ~kMainChunks workgroups; LINES: ~kLineBlocks over all the lines
@@ -1266,11 +1320,16 @@ void gram_pass(const float *const *tab, int64_t ss, int n,
                const GramPlan &pl, GramCtl ctl, int64_t w, int64_t cap,
                const int *centre, double *partial, int chunks,
                hipStream_t st) {
-  if (LINES && pl.block8)
-    hipLaunchKernelGGL((gram_block8_kernel<CENTRED>),
-                       dim3(chunk_grid(pl, chunks)), dim3(kB8Blk), 0, st, tab,
-                       ss, n, pl.nt, pl.nlines, seg_lo, seg_end, nseg, ctl, w,
-                       cap, centre, partial);
+  if (LINES && pl.wide)
+    hipLaunchKernelGGL((gram_block8_kernel<13, 16, CENTRED>),
+                       dim3(chunk_grid(pl, chunks)), dim3(16 * kWave), 0, st,
+                       tab, ss, n, pl.nt, pl.nlines, seg_lo, seg_end, nseg,
+                       ctl, w, cap, centre, partial);
+  else if (LINES && pl.block8)
+    hipLaunchKernelGGL((gram_block8_kernel<8, kB8Waves, CENTRED>),
+                       dim3(chunk_grid(pl, chunks)), dim3(kB8Waves * kWave),
+                       0, st, tab, ss, n, pl.nt, pl.nlines, seg_lo, seg_end,
+                       nseg, ctl, w, cap, centre, partial);
   else
     hipLaunchKernelGGL((gram_chunk_kernel<NT, CENTRED, LINES>),
                        dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab,

@@ -38,7 +38,7 @@ def main():
                          for c in clients], dtype=np.int64)
         rs = ops.RowSet.from_pointers(lay, ptrs, dev, keepalive=clients)
         Ds = {}
-        b8 = 2
+        b8 = int(os.environ.get('B8', '1'))
         for on in (b8, 0):
             lib.fsagg_pairgram_set_block8(on)
             Ds[on] = ops.pairgram_rows_dist(rs, _GRAM_TOL)[4].cpu().numpy()
