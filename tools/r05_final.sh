@@ -8,7 +8,7 @@ set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out/r05
 export TMPDIR=/tmp
-bash tools/gpu_job.sh smoke \
+bash tools/gpu_job.sh pytestall smoke \
   "timeout -k 10 400 python bench.py > gpurun_out/r05/bench.json" \
   "timeout -k 10 500 python bench.py --e2e --no-pmc --no-cpu-baseline > gpurun_out/r05/bench_e2e.json" \
   "timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r05/prof_bench -o run --output-format csv -- python bench.py --no-pmc --no-cpu-baseline > gpurun_out/r05/bench_traced.json" \
