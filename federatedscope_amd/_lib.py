@@ -135,7 +135,7 @@ SIGNATURES['fsagg_pairsel_finish_f64'] = (
     _c_i, [_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_p])
 FSAGG_PAIRSEL_MAX_SEL = 32
 FSAGG_PAIRSEL_MAX_CLIENTS = 256
-FSAGG_PAIRSEL_CHUNK = 4096
+FSAGG_PAIRSEL_CHUNK = 2048
 
 SIGNATURES['fsagg_online_inc_typed'] = (
     _c_i, [_c_p, _c_i, _c_p, _c_i, _c_p, _c_i, _c_i64, _c_i64, _c_i64, _c_p])

@@ -13,7 +13,13 @@
 //   * the row set's chunk table (fsagg_chunk, FSAGG_PAIRSEL_CHUNK
 //     coordinates, never straddling a key); one 256-thread workgroup per
 //     chunk, walking it in stages of T coordinates (T = 8192 / the client
-//     slots: 128 at n <= 64, 32 at n > 128);
+//     slots: 128 at n <= 64, 32 at n > 128).  2048-coordinate chunks: at
+//     4096 the C4 grid (1612 workgroups, 4 per CU) ends in a 0.6-full
+//     round — 2 rows of 50 clients × 6.6M took 0.279 against 0.251 ms
+//     (1024: 0.267, 512: 0.324; tools/probe_pairsel.py);
+//   * NA accumulator slots per lane, 2 / 4 / 8 / 16 / 32 (the one or two
+//     rows of a typical near-tie take the 2-slot kernel: 0.279 against
+//     0.348 ms on 4 slots);
 //   * every client's stage is loaded coalesced (consecutive lanes read
 //     consecutive 16-B pieces of one row) into registers one stage ahead,
 //     then written to LDS transposed, [coordinate][client] at a pitch of
@@ -289,7 +295,8 @@ extern "C" int fsagg_pairsel_rows_segsq_f64(const fsagg_rows *rows,
   hipLaunchKernelGGL(pairsel_chunk_kernel<NA>, dim3(unsigned(nchunk)),       \
                      dim3(kBlock), 0, s, rows->tab, rows->ss, rows->n, sel,  \
                      nsel, chunks, partial)
-    if (nsel <= 4) FSAGG_PAIRSEL(4);
+    if (nsel <= 2) FSAGG_PAIRSEL(2);
+    else if (nsel <= 4) FSAGG_PAIRSEL(4);
     else if (nsel <= 8) FSAGG_PAIRSEL(8);
     else if (nsel <= 16) FSAGG_PAIRSEL(16);
     else FSAGG_PAIRSEL(32);

@@ -554,7 +554,7 @@ int fsagg_pairgram_rows_f32(const fsagg_rows *rows, const int64_t *seg_lo,
  * fsagg_pairsel_workspace_bytes(nsel, n, nchunk). */
 #define FSAGG_PAIRSEL_MAX_SEL 32
 #define FSAGG_PAIRSEL_MAX_CLIENTS 256
-#define FSAGG_PAIRSEL_CHUNK 4096
+#define FSAGG_PAIRSEL_CHUNK 2048
 size_t fsagg_pairsel_workspace_bytes(int nsel, int n, int nchunk);
 int fsagg_pairsel_rows_segsq_f64(const fsagg_rows *rows, const int *sel,
                                  int nsel, const fsagg_chunk *chunks,

@@ -28,6 +28,26 @@ def main():
     ptrs = np.array([[c[k].data_ptr() for k in lay.keys] for c in clients],
                     dtype=np.int64)
     rs = ops.RowSet.from_pointers(lay, ptrs, dev, keepalive=clients)
+    from federatedscope_amd import _lib as L
+    for unit in (4096, 2048, 1024, 512):
+        L.FSAGG_PAIRSEL_CHUNK = unit
+        for nsel in (1, 2, 4, 8):
+            sel = torch.arange(0, 50, 50 // nsel, dtype=torch.int32,
+                               device=dev)[:nsel].contiguous()
+            for _ in range(3):
+                ops.pairsel_rows_segsq(rs, sel)
+            torch.cuda.synchronize()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ts = []
+            for _ in range(20):
+                ev[0].record()
+                ops.pairsel_rows_segsq(rs, sel)
+                ev[1].record()
+                ev[1].synchronize()
+                ts.append(ev[0].elapsed_time(ev[1]))
+            print('chunk %4d nsel %2d: %.3f ms (events, segsq launch pair)' % (
+                unit, nsel, statistics.median(ts)), flush=True)
+    L.FSAGG_PAIRSEL_CHUNK = 2048
     for nsel in (1, 2, 4, 8, 16, 32):
         sel = torch.arange(0, 50, 50 // nsel if nsel <= 50 else 1,
                            dtype=torch.int32, device=dev)[:nsel].contiguous()
