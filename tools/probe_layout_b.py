@@ -12,7 +12,7 @@ Times, interleaved (median of rounds of back-to-back calls):
   flat        ops.weighted_sum over the slab rows (the flat kernel)
 Run under rocprofv3 --kernel-trace --stats for the kernels' own durations.
 
-    python tools/probe_layout_b.py [--rounds 5] [--calls 10]
+    python tools/probe_layout_b.py [--rounds 5] [--calls 10] [--only rows_sep]
 """
 import argparse
 import json
@@ -35,6 +35,13 @@ def main():
     ap.add_argument('--clients', type=int, default=100)
     ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--calls', type=int, default=10)
+    ap.add_argument('--only', default=None,
+                    help='comma-separated legs to run (for per-leg counter '
+                         'passes), e.g. rows_sep')
+    ap.add_argument('--no-fill', action='store_true',
+                    help='allocate the separate tensors without copying the '
+                         'values in (16100 copy kernels are slow under a '
+                         'counter pass; the timings do not depend on values)')
     args = ap.parse_args()
     from federatedscope_amd import ops
     from federatedscope_amd.core.aggregators import ClientsAvgAggregator
@@ -52,7 +59,8 @@ def main():
     views = [(sizes[i], OrderedDict(
         (k, slab[i, lay.offsets[k]:lay.offsets[k] + lay.numels[k]].view(
             lay.shapes[k])) for k in lay.keys)) for i in range(n)]
-    sep = [(s, OrderedDict((k, v.clone()) for k, v in d.items()))
+    sep = [(s, OrderedDict((k, torch.empty_like(v) if args.no_fill
+                            else v.clone()) for k, v in d.items()))
            for s, d in views]
     cfg = SimpleNamespace(federate=SimpleNamespace(ignore_weight=False,
                                                    use_ss=False))
@@ -77,6 +85,9 @@ def main():
         'rows_sep': lambda: ops.weighted_sum_rows(rs_s, w, out),
         'flat': lambda: ops.weighted_sum(rows, w, flat),
     }
+    if args.only:
+        keep = args.only.split(',') + ['flat']
+        legs = {k: v for k, v in legs.items() if k in keep}
     for fn in legs.values():
         for _ in range(3):
             fn()
