@@ -155,10 +155,10 @@ def _separated(s, m, ordered, n):
 @pytest.mark.parametrize('n', [2, 5, 16, 17, 33, 50, 64, 65, 80, 100, 112,
                                120, 129, 200, 208])
 def test_pairgram_vs_fp64_and_valu(n):
-    """n <= 64: one workgroup forms every tile pair; n > 64: the lines of a
-    projective plane — Fano for 5..7 tiles (65, 80, 100, 112: every point
-    present), PG(2, 3) for 8..13 tiles (120: 5 points absent; 129; 200;
-    208: all 13) — with a last tile of 1 client at 65 and 129."""
+    """n <= 64: one workgroup forms every tile pair; n > 64 (the default
+    setting): one 8-tile workgroup per chunk up to 128 clients (65, 80,
+    100, 112, 120: 5..8 tiles), all 13 tiles on 16 waves above (129, 200,
+    208) — with a last tile of 1 client at 65 and 129."""
     from federatedscope_amd import ops
     clients = _clients(n, seed=n)
     lay, _, keyed, stacked = _sets(clients)
@@ -176,6 +176,28 @@ def test_pairgram_vs_fp64_and_valu(n):
     # 2.2e-7 at n = 80, 4.2e-7 at 129, 9.5e-7 at 208
     tol = 2e-7 if n <= 64 else 1.5e-6
     assert (np.abs(d_got[pos] - d_want[pos]) / d_want[pos]).max() <= tol
+
+
+@pytest.mark.parametrize('setting', [0, 2, 3])
+@pytest.mark.parametrize('n', [65, 90, 100, 128, 150])
+def test_pairgram_workgroup_settings(setting, n):
+    """Every n > 64 workgroup form of the A/B hook
+    (fsagg_pairgram_set_block8): 0 the projective-plane lines, 2 four
+    8-tile workgroups per chunk above 128 clients, 3 the producer/consumer
+    workgroup up to 128 (partner blocks stored transposed) — each within
+    the worst-case bounds of the fp64 distances."""
+    from federatedscope_amd import _lib as L
+    clients = _clients(n, seed=n + 1)
+    lay, _, keyed, _ = _sets(clients)
+    want = _fp64_segsq_dev(clients, lay)
+    lib = L.load()
+    prev = lib.fsagg_pairgram_set_block8(setting)
+    try:
+        got, err, D, flags, B = _gram(keyed)
+    finally:
+        lib.fsagg_pairgram_set_block8(prev)
+    assert not flags.any()
+    _check(got, err, D, flags, B, want)
 
 
 def test_pairgram_unaligned_rows():
