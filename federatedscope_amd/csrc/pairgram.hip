@@ -64,6 +64,7 @@ constexpr int kBlk = kWaves * kWave;
 constexpr int64_t kUnit = kKStep * kWaves;  // chunk lengths: multiples
 constexpr int kRed = 32;                  // chunks per first-level sum
 constexpr int kMainChunks = 1024;         // ~2 rounds at 2 blocks per CU
+constexpr int kOneMaxTiles = 7;           // one workgroup up to 112 clients
 constexpr int64_t kMaxW = 16384;          // chunk length cap (LDS centre)
 constexpr int64_t kSampleCoords = 2048;   // per key, for the centre choice
 constexpr int64_t kSampleChunk = 512;
@@ -470,7 +471,7 @@ __device__ __forceinline__ void stage_read8(const char *buf, int rr, int ks,
 // run on one XCD together and read its rows from that XCD's L2 after the
 // first.
 template <int NT, bool CENTRED, bool LINES>
-__global__ __launch_bounds__(kBlk, 2) void gram_chunk_kernel(
+__global__ __launch_bounds__(kBlk, (NT > kFullTiles ? 1 : 2)) void gram_chunk_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n, int T,
     const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
     int nseg, GramCtl ctl, int64_t w, int64_t cap,
@@ -1203,212 +1204,12 @@ __attribute__((amdgpu_waves_per_eu(4))) void gram_block8_kernel(
   }
 }
 
-// T <= 8 with the two roles in one workgroup of 16 waves: waves 0-7 are
-// producers — wave p loads ITS tile's 16 rows straight into registers (lane
-// (r, g) the 16-B pieces g, g + 4, 8 + g, 12 + g of row r's 256 B: exactly
-// its fragment slots, no raw LDS image), two stages ahead, and splits them
-// into the limb buffer of the next stage; waves 8-15 are consumers that form
-// the tile pairs of the current stage from the other limb buffer.  Consumer
-// c < T owns tile c and forms (c, c + d mod T) for d < NP (NP = 5, 4, 4, 3
-// at T = 8, 7, 6, 5: every pair once, plus at even T the d = T/2 pairs of
-// c >= T/2 again, formed and not stored), its own fragments kept and each
-// partner's read one pair ahead in straight-line code; a pair with
-// c > partner is the partner's block transposed and is stored so.  One
-// barrier per stage
-// separates the two buffers' roles, so a stage's split and loads run while
-// the previous stage's products are formed.  LDS: two limb buffers of 8
-// tiles × 2 k-steps × 3 limbs = 96 KiB, one workgroup per CU.
-constexpr int kPcWaves = 16;
-constexpr int kPcMaxTiles = 6;  // the default's range (gram_plan)
-constexpr int kPcLimbs = 2 * 8 * 3 * 1024;  // one stage's limbs
-
-template <int NP, bool CENTRED>
-__global__ __launch_bounds__(kPcWaves * kWave)
-__attribute__((amdgpu_waves_per_eu(4))) void gram_pc_kernel(
-    const float *const *__restrict__ tab, int64_t ss, int n, int T,
-    const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
-    int nseg, GramCtl ctl, int64_t w, int64_t cap,
-    const int *__restrict__ centre, double *__restrict__ partial) {
-  constexpr int NT = 8;
-  __shared__ __attribute__((aligned(1024))) char limbs[2 * kPcLimbs];
-  const int *__restrict__ prefix = ctl.prefix;
-  const int chunk = int(blockIdx.x);
-  if (chunk >= prefix[nseg]) return;  // whole workgroup
-  int s = 0;
-  while (prefix[s + 1] <= chunk) ++s;
-  const int q = chunk - prefix[s];
-  const int wv = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / kWave);
-  const int lane = int(threadIdx.x) % kWave, g = lane >> 4;
-  int64_t send = seg_end[s];
-  if (cap > 0 && send > seg_lo[s] + cap) send = seg_lo[s] + cap;
-  const int64_t c0 = seg_lo[s] + int64_t(q) * w;
-  const int64_t c1 = min(c0 + w, send);
-  const int64_t len = c1 > c0 ? c1 - c0 : 0;
-  const float *const *rows = tab + int64_t(s) * ss;
-  const bool producer = wv < NT;
-  const int cw = producer ? 0 : wv - NT;  // consumer index
-  // a producer's tile: absent tiles (>= T) neither load nor split
-  const bool splits = producer && wv < T;
-  const int j = 16 * (producer ? wv : 0) + (lane & 15);
-  const float *own = rows[j < n ? j : n - 1];
-  const float *crow = CENTRED ? rows[*centre] : nullptr;
-  bool ok = !splits || al16(own + c0);
-  if (CENTRED) ok = ok && al16(crow + c0);
-  uint32_t *flag = reinterpret_cast<uint32_t *>(limbs);
-  if (lane == 0) flag[wv] = __all(ok) ? 1u : 0u;
-  __syncthreads();
-  bool vec = true;
-#pragma unroll
-  for (int v = 0; v < kPcWaves; ++v) vec = vec && flag[v] != 0u;
-  __syncthreads();  // read before any limb is written
-
-  // the consumer's tile and partners (wave-uniform)
-  const int mine = cw;
-  int part[NP];
-#pragma unroll
-  for (int d = 0; d < NP; ++d) part[d] = (mine + d) % T;
-  double acc[NP][4];
-#pragma unroll
-  for (int p = 0; p < NP; ++p)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) acc[p][r] = 0.0;
-
-  const Neg kn = neg_consts();
-  auto mfma_phase = [&](char *lb, int ks) {
-    const Limbs3 a = b8_load<NT>(lb, ks, mine, lane);
-    Limbs3 bn = b8_load<NT>(lb, ks, part[1], lane);
-    b8_pair(a, a, acc[0]);
-#pragma unroll
-    for (int p = 1; p < NP; ++p) {
-      const Limbs3 b = bn;
-      if (p + 1 < NP) bn = b8_load<NT>(lb, ks, part[p + 1], lane);
-      b8_pair(a, b, acc[p]);
-    }
-  };
-  auto split_to = [&](char *lb, int ks, const float (&x)[8]) {
-    frag8 h, m, l;
-    split3(x, kn, h, m, l);
-    *b8_limb<NT>(lb, ks, wv, 0, lane) = h;
-    *b8_limb<NT>(lb, ks, wv, 1, lane) = m;
-    *b8_limb<NT>(lb, ks, wv, 2, lane) = l;
-  };
-
-  const int nstage = vec ? int(len / kB8Stage) : 0;
-  // a producer's register sets: stage st in set st & 1 (its two k-steps'
-  // 8 values, and the centre's)
-  float xr[2][2][8], cr[2][2][8];
-  auto fetch = [&](int st, int set) {
-    if (splits) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int64_t o = c0 + int64_t(st) * kB8Stage + ks * kKStep + 4 * g;
-        ld8(own + o, xr[set][ks]);
-        if (CENTRED) ld8(crow + o, cr[set][ks]);
-      }
-    }
-  };
-  auto split_stage = [&](int set) {
-    if (splits) {
-      char *lb = limbs + set * kPcLimbs;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        float x[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          x[e] = CENTRED ? xr[set][ks][e] - cr[set][ks][e] : xr[set][ks][e];
-        split_to(lb, ks, x);
-      }
-    }
-  };
-  const int nall = int((len + kKStep - 1) / kKStep);
-  // The two roles in separate loops with the same barriers (one per stage,
-  // two per tail k-step), so a wave holds only its own role's registers.
-  if (producer) {
-    // stage st of parity h: split stage st + 1 (register set 1 − h) into
-    // limb buffer 1 − h, then load stage st + 3 into that set
-    auto stage = [&](int st, int h) {
-      __syncthreads();
-      if (st + 1 < nstage) {
-        split_stage(1 - h);
-        if (st + 3 < nstage) fetch(st + 3, 1 - h);
-      }
-    };
-    if (nstage > 0) {
-      fetch(0, 0);
-      if (nstage > 1) fetch(1, 1);
-      split_stage(0);
-      if (nstage > 2) fetch(2, 0);
-    }
-    for (int st = 0; st < nstage; st += 2) {
-      stage(st, 0);
-      if (st + 1 < nstage) stage(st + 1, 1);
-    }
-    // the rest (unaligned rows: everything; aligned: the last partial
-    // stage), one k-step at a time from global memory through buffer 0
-    for (int i = 2 * nstage; i < nall; ++i) {
-      const int64_t k0 = c0 + int64_t(i) * kKStep;
-      __syncthreads();  // every consumer is done with the limbs
-      if (splits) {
-        float x[8], cc[8];
-        ld8_tail(own, k0, c1, g, x);
-        if (CENTRED) {
-          ld8_tail(crow, k0, c1, g, cc);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) x[e] -= cc[e];
-        }
-        split_to(limbs, 0, x);
-      }
-      __syncthreads();
-    }
-    return;
-  }
-  // consumers: stage st's products from limb buffer st & 1 (consumers of
-  // absent tiles only keep the barriers)
-  const bool active = mine < T;
-  for (int st = 0; st < nstage; ++st) {
-    __syncthreads();
-    char *lb = limbs + (st & 1) * kPcLimbs;
-    if (active) {
-      mfma_phase(lb, 0);
-      mfma_phase(lb, 1);
-    }
-  }
-  for (int i = 2 * nstage; i < nall; ++i) {
-    __syncthreads();
-    __syncthreads();
-    if (active) mfma_phase(limbs, 0);
-  }
-  if (!active) return;
-  const int ntpg = T * (T + 1) / 2;
-  double *out = partial + int64_t(chunk) * ntpg * 256;
-  const int jc = lane & 15;
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int x = part[p];
-    // at even T the d = T/2 pair belongs to the lower consumer
-    if (2 * p == T && mine >= p) continue;
-    if (mine <= x) {
-      double *o = out + int64_t(pair_index(mine, x, T)) * 256;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r * 64 + lane] = acc[p][r];
-    } else {
-      // block (x, mine) is this one transposed: lane's (i, j) — row i =
-      // 4·(lane >> 4) + r of tile mine, column j = lane & 15 of tile x — is
-      // its (j, i), held at r' = j & 3 of lane i + 16·(j >> 2)
-      double *o = out + int64_t(pair_index(x, mine, T)) * 256;
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        o[(jc & 3) * 64 + 4 * (lane >> 4) + r + 16 * (jc >> 2)] = acc[p][r];
-    }
-  }
-}
-
-// n > 64: 1 = tile-split workgroups (default): the producer/consumer
-// workgroup up to 96 clients (gram_pc_kernel), gram_block8_kernel's 8 tiles
-// up to 128, all 13 on 16 waves above; 2 = 8-tile workgroups for
-// every n > 64 (four per chunk above 128); 3 = the producer/consumer
-// workgroup for T <= 8 (gram_pc_kernel), 13 tiles above as 1; 0 = plane
-// lines throughout (fsagg_pairgram_set_block8, A/B)
+// n > 64: 1 (default) = up to 7 tiles (n <= 112) the n <= 64 kernel's
+// form — one 4-wave workgroup per chunk holding every tile, one per CU —
+// then gram_block8_kernel's 8 tiles, all 13 on 16 waves above; 2 = 8-tile
+// workgroups for every n > 64 (four per chunk above 128); 3 = the one-
+// workgroup form for every T <= 8, 13 tiles above as 1; 0 = plane lines
+// throughout (fsagg_pairgram_set_block8, A/B)
 std::atomic<int> g_block8{1};
 
 struct GramPlan {
@@ -1416,7 +1217,6 @@ struct GramPlan {
   bool lines;          // nt > kFullTiles: several workgroups per chunk
   bool block8;         // ... 8-tile workgroups (else plane lines)
   bool wide;           // ... one 13-tile workgroup of 16 waves
-  bool pc;             // ... one producer/consumer workgroup (T <= 8)
   int nlines;          // workgroups per chunk: 13 / 7 lines, or 1 / 4 blocks
   int ntpg;            // tile pairs
   int64_t w;           // main chunk length (multiple of kUnit)
@@ -1440,12 +1240,15 @@ GramPlan gram_plan(int n, int64_t numel, int nseg) {
   // 9 <= T <= 13: one 16-wave workgroup with all 13 tiles (setting 1), or
   // the four 8-tile workgroups (setting 2)
   pl.wide = pl.block8 && pl.nt > kB8Waves && (b8 == 1 || b8 == 3);
-  // the producer/consumer workgroup up to 6 tiles (n <= 96), where it
-  // measured faster than the 8-tile one (profiles/r05/gram_pc_ab.jsonl:
-  // n = 66 0.69 against 0.88 ms, n = 90 0.84 against 0.91; n = 100 equal,
-  // n = 128 1.32 against 1.05); every T <= 8 under setting 3
-  pl.pc = pl.block8 && (b8 == 3 ? pl.nt <= kB8Waves
-                                : b8 == 1 && pl.nt <= kPcMaxTiles);
+  // up to kOneMaxTiles (setting 3: 8) tiles the n <= 64 kernel's form: one
+  // 4-wave workgroup per chunk, each wave splitting every tile of its own
+  // k-steps and forming every pair from registers (up to 256 VGPRs + AGPRs,
+  // one workgroup per CU) — profiles/r05/gram_full_ab.jsonl: n = 66 0.49
+  // against 0.70 ms, n = 90 0.66 / 0.84, n = 100 0.90 / 0.97, but n = 113
+  // 1.12 / 1.01 and n = 128 1.13 / 1.03 against the 8-tile workgroup
+  if (pl.lines && (b8 == 1 || b8 == 3) &&
+      pl.nt <= (b8 == 3 ? kB8Waves : kOneMaxTiles))
+    pl.lines = pl.block8 = pl.wide = false;
   pl.nlines = !pl.lines ? 1
               : pl.block8 ? (pl.nt <= kB8Waves || pl.wide ? 1 : 4)
                           : (pl.nt <= 7 ? 7 : 13);
@@ -1529,18 +1332,7 @@ void gram_pass(const float *const *tab, int64_t ss, int n,
                const GramPlan &pl, GramCtl ctl, int64_t w, int64_t cap,
                const int *centre, double *partial, int chunks,
                hipStream_t st) {
-  if (LINES && pl.pc) {
-#define FSAGG_PC(NP)                                                         \
-  hipLaunchKernelGGL((gram_pc_kernel<NP, CENTRED>),                          \
-                     dim3(chunk_grid(pl, chunks)), dim3(kPcWaves * kWave), 0, \
-                     st, tab, ss, n, pl.nt, seg_lo, seg_end, nseg, ctl, w,    \
-                     cap, centre, partial)
-    if (pl.nt >= 8) FSAGG_PC(5);
-    else if (pl.nt >= 6) FSAGG_PC(4);
-    else FSAGG_PC(3);
-#undef FSAGG_PC
-  }
-  else if (LINES && pl.wide)
+  if (LINES && pl.wide)
     hipLaunchKernelGGL((gram_block8_kernel<13, 16, CENTRED>),
                        dim3(chunk_grid(pl, chunks)), dim3(16 * kWave), 0, st,
                        tab, ss, n, pl.nt, pl.nlines, seg_lo, seg_end, nseg,
@@ -1645,6 +1437,18 @@ int pairgram_rows(const char *what, const fsagg_rows *rows,
     case 4: gram_launch<4, false>(rows->tab, rows->ss, n, seg_lo, seg_end,
                                   nseg, pl, w, segsq, err, tol, D, ill, B,
                                   D64, st); break;
+#define FSAGG_FULL(NT)                                                       \
+  if (!pl.lines) {                                                           \
+    gram_launch<NT, false>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg, pl, \
+                           w, segsq, err, tol, D, ill, B, D64, st);          \
+    break;                                                                   \
+  }                                                                          \
+  [[fallthrough]]
+    case 5: FSAGG_FULL(5);
+    case 6: FSAGG_FULL(6);
+    case 7: FSAGG_FULL(7);
+    case 8: FSAGG_FULL(8);
+#undef FSAGG_FULL
     default:
       if (pl.nlines == 7)
         gram_launch<3, true>(rows->tab, rows->ss, n, seg_lo, seg_end, nseg,

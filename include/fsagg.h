@@ -498,15 +498,14 @@ int fsagg_pairdist_rows_segsq_f32(const fsagg_rows *rows,
  * 2..208). */
 size_t fsagg_pairgram_workspace_bytes(int n, int64_t numel, int nseg);
 /* Tuning hook (no reference counterpart): which workgroups form the Gram
- * passes for n > 64.  1 (default): tile-split workgroups (every tile split
- * once per workgroup, each wave forming its share of the tile pairs) — up
- * to 96 clients one 16-wave workgroup whose loading/splitting waves run a
- * stage ahead of its product waves, 8 tiles on 8 waves up to 128 clients,
- * all 13 tiles on 16 waves above; 2:
- * 8-tile workgroups for every n > 64 (four per chunk above 128); 3: up to
- * 128 clients one 16-wave workgroup per chunk whose loading/splitting waves
- * run a stage ahead of its product waves (13 tiles above as 1); 0:
- * projective-plane lines throughout; on < 0
+ * passes for n > 64.  1 (default): up to 112 clients one 4-wave workgroup
+ * per chunk holding every tile (the n <= 64 form, one workgroup per CU),
+ * then tile-split workgroups (every tile split once per workgroup, each
+ * wave forming its share of the tile pairs) — 8 tiles on 8 waves up to 128
+ * clients, all 13 tiles on 16 waves above; 2: 8-tile workgroups for every
+ * n > 64 (four per chunk above 128); 3: the one-workgroup form up to 128
+ * clients (13 tiles above as 1); 0: projective-plane lines throughout;
+ * on < 0
  * restores the default.  segsq / err agree within the stated bounds.
  * Returns the previous setting.  For A/B measurements. */
 int fsagg_pairgram_set_block8(int on);

@@ -155,10 +155,10 @@ def _separated(s, m, ordered, n):
 @pytest.mark.parametrize('n', [2, 5, 16, 17, 33, 50, 64, 65, 80, 100, 112,
                                120, 129, 200, 208])
 def test_pairgram_vs_fp64_and_valu(n):
-    """n <= 64: one workgroup forms every tile pair; n > 64 (the default
-    setting): one 8-tile workgroup per chunk up to 128 clients (65, 80,
-    100, 112, 120: 5..8 tiles), all 13 tiles on 16 waves above (129, 200,
-    208) — with a last tile of 1 client at 65 and 129."""
+    """n <= 112: one workgroup forms every tile pair (65, 80, 100, 112:
+    5..7 tiles, one workgroup per CU above 64); one 8-tile workgroup per
+    chunk up to 128 clients (120); all 13 tiles on 16 waves above (129,
+    200, 208) — with a last tile of 1 client at 65 and 129."""
     from federatedscope_amd import ops
     clients = _clients(n, seed=n)
     lay, _, keyed, stacked = _sets(clients)
@@ -183,9 +183,9 @@ def test_pairgram_vs_fp64_and_valu(n):
 def test_pairgram_workgroup_settings(setting, n):
     """Every n > 64 workgroup form of the A/B hook
     (fsagg_pairgram_set_block8): 0 the projective-plane lines, 2 four
-    8-tile workgroups per chunk above 128 clients, 3 the producer/consumer
-    workgroup up to 128 (partner blocks stored transposed) — each within
-    the worst-case bounds of the fp64 distances."""
+    8-tile workgroups per chunk above 128 clients, 3 one workgroup holding
+    every tile up to 128 (the default stops at 112) — each within the
+    worst-case bounds of the fp64 distances."""
     from federatedscope_amd import _lib as L
     clients = _clients(n, seed=n + 1)
     lay, _, keyed, _ = _sets(clients)
