@@ -35,7 +35,8 @@
 //   flagged and recomputed on the VALU kernel (its ±inf / NaN semantics).
 //
 // Work: a workgroup of 4 waves per chunk of one key; wave v takes the
-// chunk's k-steps v, v + 4, ...  The chunk's rows stream through LDS in
+// chunk's k-steps v, v + 4, ... (n <= 112; above, the tile-split
+// workgroups of gram_block8_kernel).  The chunk's rows stream through LDS in
 // stages (global_load_lds_dwordx4, 512-B runs per row: see kGramStaged) and
 // are read back in MFMA fragment order (lane l: client 16t + (l & 15);
 // fragment slots 0-3 = coordinates 4(l>>4) .. +3 and slots 4-7 =
@@ -458,8 +459,10 @@ __device__ __forceinline__ void stage_read8(const char *buf, int rr, int ks,
   v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
 }
 
-// One workgroup (4 waves) per chunk (n <= 64: its NT tiles are all the
-// tiles) or per chunk and plane line (LINES, n > 64).  partial[chunk][tp]
+// One workgroup (4 waves) per chunk (its NT tiles are all the tiles: n <=
+// 64 at two workgroups per CU, and up to kOneMaxTiles tiles at one per CU
+// with the accumulators spread over VGPRs and AGPRs) or per chunk and plane
+// line (LINES, the A/B setting 0 for n > 64).  partial[chunk][tp]
 // [reg][lane] (fp64, tp over the T(T+1)/2 tile pairs): the chunk's
 // (centred) Gram blocks in MFMA C-layout (row 4(lane>>4) + reg of tile t,
 // column lane & 15 of tile u).  !CENTRED: raw values (sample).  The rows
@@ -471,7 +474,8 @@ __device__ __forceinline__ void stage_read8(const char *buf, int rr, int ks,
 // run on one XCD together and read its rows from that XCD's L2 after the
 // first.
 template <int NT, bool CENTRED, bool LINES>
-__global__ __launch_bounds__(kBlk, (NT > kFullTiles ? 1 : 2)) void gram_chunk_kernel(
+__global__ __launch_bounds__(kBlk, (NT > kFullTiles ? 1 : 2))
+void gram_chunk_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n, int T,
     const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
     int nseg, GramCtl ctl, int64_t w, int64_t cap,
