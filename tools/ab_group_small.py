@@ -5,7 +5,7 @@ against the K-wave kernel opened below 256 clients
 and the trimmed mean (k = 40): interleaved rounds, median of 15 event-timed
 calls per round after a clock warm-up; results checked against the
 default kernel (median bit-exact, trimmed mean within 4e-6 relative).
-tools only.  usage: ab_group_small.py [n]"""
+tools only.  usage: [GROUP_KS=5,6,8] ab_group_small.py [n]"""
 import json
 import os
 import statistics
@@ -55,7 +55,11 @@ def main():
             ts.append(e0.elapsed_time(e1))
         return statistics.median(ts)
 
-    names = ['pair', 'group4', 'group8']
+    # GROUP_KS=5,6,8 picks the K-wave variants (default 4, 8); 'pair' is the
+    # library default at this n (the two-wave kernel below 256 clients, the
+    # streaming or K-wave kernel above)
+    ks = os.environ.get('GROUP_KS', '4,8').split(',')
+    names = ['pair'] + ['group%s' % x for x in ks]
     ref = {}
     for mode in ('median', 'trimmed'):
         variant('pair')
