@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
-"""A/B of the Gram chain for n > 64 (fsagg_pairgram_rows_f32): 8-tile
-workgroups (fsagg_pairgram_set_block8(1), the default) against the
-plane-line workgroups (0), interleaved (setting 2: 8-tile workgroups at
-every n), on C4's layout (ConvNet2-h2048,
+"""A/B of the Gram chain for n > 64 (fsagg_pairgram_rows_f32): the workgroup
+setting B8 (env, fsagg_pairgram_set_block8: 1 the default — one workgroup
+holding every tile up to 112 clients, 8-tile workgroups up to 128, 13 tiles
+on 16 waves above; 2 four 8-tile workgroups per chunk above 128; 3 the
+one-workgroup form up to 128) against the plane-line workgroups (0),
+interleaved, on C4's layout (ConvNet2-h2048,
 6.6M) for n = 100 and 200: median of 15 event-timed calls per round, 3
 rounds; the two D within 1e-6 relative of each other.  tools only."""
 import json
