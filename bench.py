@@ -174,6 +174,209 @@ def plugin_surface_leg(args, dev, slab, rows, sizes, w_dev, P, rounds=5,
     }
 
 
+def _interleaved(fns, rounds, calls):
+    """Median ms per call of each function, timed back to back in
+    interleaved rounds of ``calls`` calls."""
+    import statistics
+
+    import torch
+    ts = [[] for _ in fns]
+    for _ in range(rounds):
+        for fn, acc in zip(fns, ts):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(calls):
+                fn()
+            torch.cuda.synchronize()
+            acc.append((time.perf_counter() - t0) / calls * 1e3)
+    return [statistics.median(t) for t in ts]
+
+
+def plugin_fresh_leg(dev, slab, rows, sizes, w_dev, P, rounds=5, calls=10):
+    """The plugin surface as a server round meets it: every call gets NEW
+    client dicts (new tensor objects over the client rows) and the upload
+    cache is off, so each call walks the tensors, builds and uploads its
+    row table and weights like a round with freshly received uploads
+    (parallel_runner.py:290-293 hands aggregate() a deepcopy per upload);
+    against the bare kernel, interleaved, bit-exact."""
+    from types import SimpleNamespace
+
+    import torch
+    from federatedscope_amd import ops
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    n = len(sizes)
+    cfg = SimpleNamespace(federate=SimpleNamespace(ignore_weight=False,
+                                                   use_ss=False))
+    agg = ClientsAvgAggregator(device=dev, config=cfg)
+    flat = torch.empty(ops.round_up(P, 64), dtype=torch.float32, device=dev)
+    res = [None]
+    # distinct dict lists of distinct tensor objects, built before the
+    # timing (building 100 views costs ~0.3 ms of host time that is no part
+    # of aggregate()), cycled through
+    sets = [{'client_feedback': [(sizes[i], {'w': slab[i, :P]})
+                                 for i in range(n)], 'recover_fun': None}
+            for _ in range(8)]
+    nxt = [0]
+
+    def run_agg():
+        info = sets[nxt[0] % len(sets)]
+        nxt[0] += 1
+        res[0] = agg.aggregate(info)
+
+    def run_flat():
+        ops.weighted_sum(rows, w_dev, flat)
+
+    ring = ops._RING
+    prev = ring.cache_on
+    ring.cache_on = False
+    uploads = ring.uploads
+    try:
+        for _ in range(3):
+            run_agg()
+            run_flat()
+        torch.cuda.synchronize()
+        exact = torch.equal(res[0]['w'], flat[:P])
+        hits = ring.hits
+        a, f = _interleaved((run_agg, run_flat), rounds, calls)
+        # one isolated call (synchronised before and after), median of 9
+        lat = []
+        for _ in range(9):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            run_agg()
+            torch.cuda.synchronize()
+            lat.append((time.perf_counter() - t0) * 1e3)
+        lat.sort()
+        hits = ring.hits - hits
+    finally:
+        ring.cache_on = prev
+    log('plugin surface, fresh dicts + upload cache off: aggregate() %.4f '
+        'ms/call, bare kernel %.4f ms (ratio %.4f), isolated call %.4f ms, '
+        'bit-exact %s, cache hits %d' % (a, f, a / f, lat[4], exact, hits))
+    return {
+        'what': 'ClientsAvgAggregator.aggregate(agg_info) on %d NEW device '
+                'dicts x %d fp32 params per call (row table and weights '
+                'walked and uploaded every call: upload cache off); '
+                'back-to-back calls, median of %d interleaved rounds of %d; '
+                'isolated call = synchronised before and after, median of 9'
+                % (n, P, rounds, calls),
+        'ms_per_call': round(a, 4),
+        'GBps': round(4.0 * n * P / a / 1e6, 1),
+        'bare_kernel_ms': round(f, 4),
+        'ratio_vs_bare_kernel': round(a / f, 4),
+        'isolated_call_ms': round(lat[4], 4),
+        'upload_cache_hits': hits,
+        'table_uploads_per_call': round((ring.uploads - uploads) /
+                                        max(nxt[0], 1), 2),
+        'bit_exact_vs_kernel': exact,
+    }
+
+
+CONVNET2_H512 = [  # configs[1]: cv/model/cnn.py:14-50, trainable keys
+    ('conv1.weight', (32, 1, 5, 5)), ('conv1.bias', (32, )),
+    ('bn1.weight', (32, )), ('bn1.bias', (32, )),
+    ('conv2.weight', (64, 32, 5, 5)), ('conv2.bias', (64, )),
+    ('bn2.weight', (64, )), ('bn2.bias', (64, )),
+    ('fc1.weight', (512, 3136)), ('fc1.bias', (512, )),
+    ('fc2.weight', (62, 512)), ('fc2.bias', (62, ))]
+
+
+def c2_leg(dev, rounds=5, calls=20):
+    """configs[1] (BASELINE.json): FEMNIST ConvNet2 (hidden 512, 12
+    trainable keys, 1,690,238 fp32 params) x 100 clients, FedAvg on one
+    GPU.  The clients are 100 device-resident state_dicts whose keys are
+    separate allocations (a trained model's parameters); the bare row-set
+    kernel (fsagg_weighted_sum_rows_f32 over their key table) against
+    ClientsAvgAggregator.aggregate() on the same dicts, back to back, and
+    the isolated call; checked bit-exact against each other."""
+    from collections import OrderedDict
+    from types import SimpleNamespace
+
+    import torch
+    from federatedscope_amd import ops
+    from federatedscope_amd.core.aggregators import ClientsAvgAggregator
+    from federatedscope_amd.core.aggregators._engine import fedavg_weights
+    n = 100
+    sizes = sample_sizes(n, seed=1)
+    w = fedavg_weights(sizes)
+    g = torch.Generator(device=dev).manual_seed(SEED + 2)
+    clients = [(sizes[i], OrderedDict(
+        (k, torch.rand(s, device=dev, generator=g) * 2 - 1)
+        for k, s in CONVNET2_H512)) for i in range(n)]
+    P = sum(t.numel() for t in clients[0][1].values())
+    cfg = SimpleNamespace(federate=SimpleNamespace(ignore_weight=False,
+                                                   use_ss=False))
+    agg = ClientsAvgAggregator(device=dev, config=cfg)
+    info = {'client_feedback': clients, 'recover_fun': None}
+    st = agg._staged(clients)
+    rs = st.rows()
+    w_dev = torch.tensor(w, dtype=torch.float32, device=dev)
+    out = torch.empty(rs.layout.numel, dtype=torch.float32, device=dev)
+    res = [None]
+
+    def run_kernel():
+        ops.weighted_sum_rows(rs, w_dev, out)
+
+    def run_agg():
+        res[0] = agg.aggregate(info)
+
+    for _ in range(3):
+        run_kernel()
+        run_agg()
+    torch.cuda.synchronize()
+    lay = rs.layout
+    exact = all(torch.equal(res[0][k].reshape(-1),
+                            out[lay.offsets[k]:lay.offsets[k] +
+                                lay.numels[k]]) for k in lay.keys)
+    # per-launch kernel time on the launch stream (HIP events)
+    evs = []
+    st_ = torch.cuda.current_stream(dev)
+    for _ in range(50):
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(st_)
+        run_kernel()
+        b.record(st_)
+        evs.append((a, b))
+    torch.cuda.synchronize()
+    kern = sorted(a.elapsed_time(b) for a, b in evs)
+    k_ms = sum(kern) / len(kern)
+    t_k, t_a = _interleaved((run_kernel, run_agg), rounds, calls)
+    lat = []
+    for _ in range(9):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run_agg()
+        torch.cuda.synchronize()
+        lat.append((time.perf_counter() - t0) * 1e3)
+    lat.sort()
+    algo = 4.0 * n * P + 4.0 * P + 4.0 * n
+    log('C2 (ConvNet2 h512, %d x %d, %d keys): kernel %.4f ms/launch '
+        '(%.0f GB/s, %.3f of HBM), back to back %.4f ms; aggregate() %.4f '
+        'ms/call, isolated %.4f ms; bit-exact %s' %
+        (n, P, len(lay.keys), k_ms, algo / k_ms / 1e6,
+         algo / k_ms / 1e6 / HBM_PEAK_GBS, t_k, t_a, lat[4], exact))
+    del clients, info, st, rs
+    return {
+        'what': 'configs[1]: FedAvg over %d device-resident FEMNIST ConvNet2 '
+                '(h=512) state_dicts, %d keys as separate allocations, %d '
+                'fp32 params; kernel = fsagg_weighted_sum_rows_f32 over their '
+                'key table (HIP events per launch, mean of 50); back to back '
+                '= median of %d interleaved rounds of %d calls'
+                % (n, len(CONVNET2_H512), P, rounds, calls),
+        'clients': n,
+        'params': P,
+        'kernel_ms': round(k_ms, 4),
+        'kernel_GBps': round(algo / k_ms / 1e6, 1),
+        'kernel_frac_of_hbm': round(algo / k_ms / 1e6 / HBM_PEAK_GBS, 4),
+        'kernel_back_to_back_ms': round(t_k, 4),
+        'aggregate_ms_per_call': round(t_a, 4),
+        'aggregate_GBps': round(4.0 * n * P / t_a / 1e6, 1),
+        'aggregate_isolated_ms': round(lat[4], 4),
+        'bit_exact_vs_kernel': exact,
+    }
+
+
 def plugin_layout_b_leg(dev, sizes, w_dev, rounds=5, calls=10,
                         separate=False):
     """configs[2] layout B: the same call on the ResNet-50 layout (161 keys,
@@ -605,6 +808,8 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-plugin', action='store_true',
                     help='skip the ClientsAvgAggregator.aggregate() leg')
+    ap.add_argument('--no-c2', action='store_true',
+                    help='skip the configs[1] (FEMNIST ConvNet2) leg')
     ap.add_argument('--no-weak', action='store_true',
                     help='skip the secondary weak-scaling phase (N > 1)')
     ap.add_argument('--e2e', action='store_true',
@@ -776,12 +981,16 @@ def main():
         (t_step * 1e3, kern_ms, t_sharded * 1e3, mean_launch_ms, achieved,
          ok))
 
-    plugin = plugin_b = plugin_bs = None
+    plugin = plugin_b = plugin_bs = plugin_fresh = c2 = None
     if world == 1 and not args.no_plugin:
         plugin = plugin_surface_leg(args, dev, pieces[0][0], pieces[0][1],
                                     sizes, w_dev, P)
+        plugin_fresh = plugin_fresh_leg(dev, pieces[0][0], pieces[0][1],
+                                        sizes, w_dev, P)
         plugin_b = plugin_layout_b_leg(dev, sizes, w_dev)
         plugin_bs = plugin_layout_b_leg(dev, sizes, w_dev, separate=True)
+    if world == 1 and not args.no_c2:
+        c2 = c2_leg(dev)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -877,6 +1086,8 @@ def main():
                 'value': round(4.0 * n * P / t_sharded / 1e9, 2)},
             'weak_scaling': weak,
             'plugin_surface': plugin,
+            'plugin_surface_fresh': plugin_fresh,
+            'configs_1_c2': c2,
             'plugin_surface_layout_b': plugin_b,
             'plugin_surface_layout_b_separate': plugin_bs,
             'assembled_bit_exact': ok,

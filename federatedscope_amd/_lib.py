@@ -34,6 +34,7 @@ SIGNATURES = {
     'fsagg_trimmed_mean_f32': (_c_i, [_c_p, _c_i, _c_i64, _c_i, _c_f, _c_p,
                                       _c_p, _c_p]),
     'fsagg_pairdist_workspace_bytes': (_c_sz, [_c_i, _c_i64, _c_i]),
+    'fsagg_pairdist_chunk_elems': (_c_i64, [_c_i, _c_i64, _c_i]),
     'fsagg_pairdist_f32': (_c_i, [_c_p, _c_i, _c_i64, _c_p, _c_i, _c_p, _c_p,
                                   _c_sz, _c_p]),
     'fsagg_pairdist_segsq_f32': (_c_i, [_c_p, _c_i, _c_i64, _c_p, _c_i, _c_p,
@@ -118,6 +119,8 @@ SIGNATURES['fsagg_trimmed_mean_rows_f32'] = (
            _c_p])
 SIGNATURES['fsagg_pairgram_workspace_bytes'] = (_c_sz, [_c_i, _c_i64, _c_i])
 SIGNATURES['fsagg_pairgram_set_block8'] = (_c_i, [_c_i])
+SIGNATURES['fsagg_pairgram_block8'] = (_c_i, [])
+SIGNATURES['fsagg_pairgram_set_stages'] = (_c_i, [_c_i])
 SIGNATURES['fsagg_pairgram_rows_segsq_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_sz, _c_p])
 SIGNATURES['fsagg_pairgram_rows_f32'] = (

@@ -805,10 +805,22 @@ class _PendingD:
         sub = ops.pairdist_finish(exact).cpu()
         idx = torch.tensor(sel)
         D[idx[:, None], idx[None, :]] = sub
-        # exact per-key sums, but D is still their fp32 formation (a
-        # rounded sqrt and an fp32 add per key)
+        # the VALU kernel's sums: every fp32 per-chunk partial adds at most
+        # m = chunk + 256 non-negative terms (a k-slice's squares, then the
+        # slices), relative error <= (1 + u)^m − 1; the fp64 chunk sums add
+        # (chunks + 64)·2^-53 more (counted as 64·u); sqrt maps a relative
+        # δ to <= δ / (2(1 − δ)); then D's own fp32 formation (a rounded
+        # sqrt and an fp32 add per key)
+        import math
+        u = 2.0 ** -24
+        ext = max([hi - lo for _, lo, hi, _ in st.pieces] + [1])
+        chl = int(ops.L.load().fsagg_pairdist_chunk_elems(len(sel), ext,
+                                                           nseg))
+        acc = math.expm1((chl + 256) * math.log1p(u)) + 64 * u
+        rel = acc / (2.0 * (1.0 - acc)) if acc < 1.0 else math.inf
         s = sub.numpy().astype(np.float64)
-        form = (2 * nseg + 2) * 2.0 ** -24 * np.where(np.isfinite(s), s, 0.0)
+        fin = np.where(np.isfinite(s), s, 0.0)
+        form = (rel + (2 * nseg + 2) * u) * fin
         B[np.ix_(sel, sel)] = form
         D64[np.ix_(sel, sel)] = s
         B64[np.ix_(sel, sel)] = form

@@ -557,6 +557,11 @@ class PeerAssembly:
         if prev is not None:
             self._wait_done(prev)
             self._raise_status()
+        else:
+            # no earlier round to wait for: still read the status word (a
+            # non-blocking load of pinned memory) so that a failure already
+            # reported is raised here, not one round later
+            self._raise_status()
         return own[:self.numel]
 
     def _barrier(self):

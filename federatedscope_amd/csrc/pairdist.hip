@@ -1129,6 +1129,15 @@ static size_t partial_bytes(int n, int64_t numel, int nseg) {
                   size_t(pl.ntp) * size_t(pl.ts * pl.ts));
 }
 
+// The chunk length the distance kernels plan for (n, numel, nseg): every
+// fp32 partial of a pair sums at most this many squared differences (a
+// k-slice's coordinates, then the slices), which bounds its rounding.
+extern "C" int64_t fsagg_pairdist_chunk_elems(int n, int64_t numel,
+                                              int nseg) {
+  if (n < 1 || nseg < 1 || numel < 0) return 0;
+  return make_plan(n, numel, nseg).chl;
+}
+
 extern "C" size_t fsagg_pairdist_workspace_bytes(int n, int64_t numel,
                                                  int nseg) {
   if (n < 1 || nseg < 1) return 0;

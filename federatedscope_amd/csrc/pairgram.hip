@@ -459,6 +459,38 @@ __device__ __forceinline__ void stage_read8(const char *buf, int rr, int ks,
   v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
 }
 
+// Compact stages (!LINES, the default forms): the chunk's n client rows
+// only — row j of the stage is client j, the centre is read from its own
+// row (it is one of the clients), rows past n are never staged (their
+// fragment lanes read row n − 1, an LDS broadcast) — and NBUF buffers, so
+// NBUF − 1 stages are in flight while one is computed.  A stage of
+// ⌈n/2⌉ 1-KiB instructions; MAXI bounds it (the static LDS): at two
+// workgroups per CU (NT <= 4) three buffers fit 80 KiB up to 52 clients,
+// at one per CU (5 <= NT <= 7) 160 KiB up to 104.  Every wave issues the
+// same 2·NT loads per stage (instructions past the last one repeat it: the
+// same bytes into the same LDS slot, from L2), so `s_waitcnt vmcnt` can
+// name the loads of the stages still allowed in flight.
+template <int NT>
+constexpr int compact_maxi3() {
+  return NT <= kFullTiles ? (8 * NT < 26 ? 8 * NT : 26)
+                          : (8 * NT < 52 ? 8 * NT : 52);
+}
+
+// s_waitcnt vmcnt(k · loads) for the k stages still allowed in flight
+template <int LOADS>
+__device__ __forceinline__ void wait_stage(int ahead) {
+  if (ahead <= 0) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  } else if (ahead == 1) {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(LOADS)
+                 : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(
+                     2 * LOADS)
+                 : "memory");
+  }
+}
+
 // One workgroup (4 waves) per chunk (its NT tiles are all the tiles: n <=
 // 64 at two workgroups per CU, and up to kOneMaxTiles tiles at one per CU
 // with the accumulators spread over VGPRs and AGPRs) or per chunk and plane
@@ -473,7 +505,13 @@ __device__ __forceinline__ void stage_read8(const char *buf, int rr, int ks,
 // (k = b / 8): blocks b and b + 8 share an XCD, so one chunk's workgroups
 // run on one XCD together and read its rows from that XCD's L2 after the
 // first.
-template <int NT, bool CENTRED, bool LINES>
+template <int NT, bool CENTRED>
+constexpr int compact_smem(int maxi, int nbuf) {
+  constexpr int red = 2 * ntp_of(NT) * 4 * kWave * 8;
+  return red > nbuf * maxi * 1024 ? red : nbuf * maxi * 1024;
+}
+
+template <int NT, bool CENTRED, bool LINES, int MAXI = 0, int NBUF = 2>
 __global__ __launch_bounds__(kBlk, (NT > kFullTiles ? 1 : 2))
 void gram_chunk_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n, int T,
@@ -481,10 +519,15 @@ void gram_chunk_kernel(
     int nseg, GramCtl ctl, int64_t w, int64_t cap,
     const int *__restrict__ centre, double *__restrict__ partial) {
   static_assert(!LINES || NT == 3 || NT == 4, "plane lines hold 3 or 4");
+  static_assert(MAXI == 0 || (!LINES && (NBUF == 2 || NBUF == 3)),
+                "compact stages: MAXI instructions, 2 or 3 buffers");
   constexpr int NTP = ntp_of(NT);
   constexpr int kLines = NT == 4 ? 13 : 7;
   const int *__restrict__ prefix = ctl.prefix;
-  __shared__ __attribute__((aligned(1024))) char smem[chunk_smem<NT, CENTRED>()];
+  constexpr int kSmem = MAXI == 0 || !kGramStaged
+                            ? chunk_smem<NT, CENTRED>()
+                            : compact_smem<NT, CENTRED>(MAXI, NBUF);
+  __shared__ __attribute__((aligned(1024))) char smem[kSmem];
   double(*red)[NTP * 4][kWave] =
       reinterpret_cast<double(*)[NTP * 4][kWave]>(smem);
   float *cs = reinterpret_cast<float *>(smem);
@@ -539,7 +582,68 @@ void gram_chunk_kernel(
   if (CENTRED) ok = ok && al16(crow + c0);
   const bool vec = __all(ok);
   int i = wv;   // this wave's next k-step: wv, wv + 4, ...
-  if constexpr (kGramStaged) {
+  if constexpr (kGramStaged && MAXI > 0) {
+    const int nstage = vec ? int(len / kStage) : 0;
+    if (nstage > 0) {
+      // this wave's load instructions k = wv, wv + 4, ... (clamped to the
+      // last, NI − 1): client rows 2k (lanes 0-31) and 2k + 1 (lanes
+      // 32-63), each lane one 16-B chunk, its source swizzled (chunk
+      // (lane & 31) ^ (row & 15))
+      constexpr int MY = 2 * NT;
+      const int NI = (n + 1) >> 1;
+      const int sb = NI * 2 * kStageRowBytes;
+      const float *src[MY];
+      int dst[MY];
+#pragma unroll
+      for (int m = 0; m < MY; ++m) {
+        const int k = min(wv + kWaves * m, NI - 1);
+        const int rr = 2 * k + (lane >> 5);
+        src[m] = rows[rr < n ? rr : n - 1] + c0 + 4 * ((lane & 31) ^ (rr & 15));
+        dst[m] = k * 2 * kStageRowBytes;
+      }
+      auto issue = [&](int st) {
+        char *buf = smem + (st % NBUF) * sb;
+#pragma unroll
+        for (int m = 0; m < MY; ++m)
+          __builtin_amdgcn_global_load_lds(
+              (__attribute__((address_space(1))) void *)(src[m] + st * kStage),
+              (__attribute__((address_space(3))) void *)(uintptr_t)(buf +
+                                                                   dst[m]),
+              16, 0, 0);
+      };
+      // the rows this lane's fragments read: client 16t + (lane & 15), past
+      // n the last client (never stored); the centre's own row
+      int rrow[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int j = 16 * t + (lane & 15);
+        rrow[t] = j < n ? j : n - 1;
+      }
+      const int crr = CENTRED ? *centre : 0;
+#pragma unroll
+      for (int p = 0; p < NBUF - 1; ++p)
+        if (p < nstage) issue(p);
+      for (int st = 0; st < nstage; ++st) {
+        // stage st's loads have landed (this wave's: vmcnt; every wave's:
+        // the barrier), every wave is done reading stage st − 1, whose
+        // buffer the next issue overwrites
+        const int ahead = min(nstage - 1 - st, NBUF - 2);
+        wait_stage<MY>(ahead);
+        if (st + NBUF - 1 < nstage) issue(st + NBUF - 1);
+        const char *buf = smem + (st % NBUF) * sb;
+        float xb[NT][8], cb[8];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) stage_read8(buf, rrow[t], wv, g, xb[t]);
+        if (CENTRED) stage_read8(buf, crr, wv, g, cb);
+        Frags<NT> f;
+        kstep_split_c<NT, CENTRED>(xb, cb, kn, f);
+        kstep_mfma<NT>(f, acc);
+      }
+      i = nstage * kWaves + wv;
+      // the stage buffers are free again (the tail reads global memory)
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  } else if constexpr (kGramStaged) {
     const int nstage = vec ? int(len / kStage) : 0;
     if (nstage > 0) {
       // this wave's load instructions k = wv, wv + 4, ... of every stage:
@@ -1215,6 +1319,11 @@ __attribute__((amdgpu_waves_per_eu(4))) void gram_block8_kernel(
 // workgroup form for every T <= 8, 13 tiles above as 1; 0 = plane lines
 // throughout (fsagg_pairgram_set_block8, A/B)
 std::atomic<int> g_block8{1};
+// 1 (default): compact stage buffers (the n client rows), three of them
+// where they fit (two stages in flight); 0: the round-5 full-tile stages
+// (16·NT rows + the centre's, one in flight) — fsagg_pairgram_set_stages,
+// A/B
+std::atomic<int> g_compact{1};
 
 struct GramPlan {
   int nt;              // tiles of 16 clients
@@ -1336,21 +1445,40 @@ void gram_pass(const float *const *tab, int64_t ss, int n,
                const GramPlan &pl, GramCtl ctl, int64_t w, int64_t cap,
                const int *centre, double *partial, int chunks,
                hipStream_t st) {
-  if (LINES && pl.wide)
-    hipLaunchKernelGGL((gram_block8_kernel<13, 16, CENTRED>),
-                       dim3(chunk_grid(pl, chunks)), dim3(16 * kWave), 0, st,
-                       tab, ss, n, pl.nt, pl.nlines, seg_lo, seg_end, nseg,
-                       ctl, w, cap, centre, partial);
-  else if (LINES && pl.block8)
-    hipLaunchKernelGGL((gram_block8_kernel<8, kB8Waves, CENTRED>),
-                       dim3(chunk_grid(pl, chunks)), dim3(kB8Waves * kWave),
-                       0, st, tab, ss, n, pl.nt, pl.nlines, seg_lo, seg_end,
-                       nseg, ctl, w, cap, centre, partial);
-  else
-    hipLaunchKernelGGL((gram_chunk_kernel<NT, CENTRED, LINES>),
+  if constexpr (LINES) {
+    if (pl.wide)
+      hipLaunchKernelGGL((gram_block8_kernel<13, 16, CENTRED>),
+                         dim3(chunk_grid(pl, chunks)), dim3(16 * kWave), 0,
+                         st, tab, ss, n, pl.nt, pl.nlines, seg_lo, seg_end,
+                         nseg, ctl, w, cap, centre, partial);
+    else if (pl.block8)
+      hipLaunchKernelGGL((gram_block8_kernel<8, kB8Waves, CENTRED>),
+                         dim3(chunk_grid(pl, chunks)), dim3(kB8Waves * kWave),
+                         0, st, tab, ss, n, pl.nt, pl.nlines, seg_lo, seg_end,
+                         nseg, ctl, w, cap, centre, partial);
+    else
+      hipLaunchKernelGGL((gram_chunk_kernel<NT, CENTRED, true>),
+                         dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab,
+                         ss, n, pl.nt, seg_lo, seg_end, nseg, ctl, w, cap,
+                         centre, partial);
+  } else if (g_compact.load(std::memory_order_relaxed) == 0) {
+    // A/B: the full-tile stages (16·NT rows + the centre), one in flight
+    hipLaunchKernelGGL((gram_chunk_kernel<NT, CENTRED, false>),
                        dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab,
                        ss, n, pl.nt, seg_lo, seg_end, nseg, ctl, w, cap,
                        centre, partial);
+  } else if ((n + 1) / 2 <= compact_maxi3<NT>()) {
+    // three compact stage buffers: two stages in flight
+    hipLaunchKernelGGL(
+        (gram_chunk_kernel<NT, CENTRED, false, compact_maxi3<NT>(), 3>),
+        dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab, ss, n, pl.nt,
+        seg_lo, seg_end, nseg, ctl, w, cap, centre, partial);
+  } else {
+    hipLaunchKernelGGL((gram_chunk_kernel<NT, CENTRED, false, 8 * NT, 2>),
+                       dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab,
+                       ss, n, pl.nt, seg_lo, seg_end, nseg, ctl, w, cap,
+                       centre, partial);
+  }
 }
 
 template <int NT, bool LINES>
@@ -1395,6 +1523,14 @@ using namespace fsagg;
 
 extern "C" int fsagg_pairgram_set_block8(int on) {
   return g_block8.exchange(on < 0 ? 1 : (on > 3 ? 3 : on));
+}
+
+extern "C" int fsagg_pairgram_set_stages(int mode) {
+  return g_compact.exchange(mode < 0 ? 1 : (mode > 1 ? 1 : mode));
+}
+
+extern "C" int fsagg_pairgram_block8(void) {
+  return g_block8.load(std::memory_order_relaxed);
 }
 
 extern "C" size_t fsagg_pairgram_workspace_bytes(int n, int64_t numel,

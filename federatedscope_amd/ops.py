@@ -37,9 +37,16 @@ class _PinnedRing:
     # chunk lists and selections repeat likewise.  Entries are immutable
     # device tensors; each is marked used (record_stream) by every stream
     # it is handed to, so the caching allocator recycles an evicted entry's
-    # block only after the work that read it.
+    # block only after the work that read it.  A stream an entry was not
+    # uploaded for first waits for the entry's copy (its slot's event: the
+    # copies all run in order on one side stream, so that event — even
+    # re-recorded by a later upload into the slot — completes only after
+    # this entry's copy).  The cache is bounded by bytes (host keys plus
+    # device tables), not only by entries: tables that change every call
+    # (fresh client tensors) then cycle through a fixed footprint.
     CACHE_MAX_BYTES = 1 << 20      # = SLOT: the ResNet-50 key table fits
     CACHE_ENTRIES = 512
+    CACHE_TOTAL_BYTES = 32 << 20
 
     def __init__(self):
         from collections import OrderedDict
@@ -48,22 +55,39 @@ class _PinnedRing:
         self.i = 0
         self.streams = {}
         self.cache = OrderedDict()
+        self.cache_bytes = 0
         self.cache_on = True
         self.hits = 0
         self.misses = 0
+        self.uploads = 0
 
     def _cached(self, key, device):
         hit = self.cache.get(key)
         if hit is None:
             return None
         self.cache.move_to_end(key)
-        t, seen = hit
+        t, seen, ev = hit
         s = torch._C._cuda_getCurrentRawStream(device.index)
         if s not in seen:
-            t.record_stream(torch.cuda.current_stream(device))
+            cur = torch.cuda.current_stream(device)
+            cur.wait_event(ev)
+            t.record_stream(cur)
             seen.add(s)
         self.hits += 1
         return t
+
+    def _insert(self, key, t, ev, device):
+        self.cache[key] = (t, {torch._C._cuda_getCurrentRawStream(
+            device.index)}, ev)
+        self.cache_bytes += 2 * len(key[3])
+        while len(self.cache) > self.CACHE_ENTRIES or \
+                self.cache_bytes > self.CACHE_TOTAL_BYTES:
+            old, _ = self.cache.popitem(last=False)
+            self.cache_bytes -= 2 * len(old[3])
+
+    def clear(self):
+        self.cache.clear()
+        self.cache_bytes = 0
 
     def _copy_stream(self, device):
         s = self.streams.get(device.index)
@@ -95,20 +119,20 @@ class _PinnedRing:
             if t is not None:
                 return t
             self.misses += 1
-        t = self._upload(arr, raw, nb, device)
-        if key is not None:
-            self.cache[key] = (t, {torch._C._cuda_getCurrentRawStream(
-                device.index)})
-            if len(self.cache) > self.CACHE_ENTRIES:
-                self.cache.popitem(last=False)
+        t, ev = self._upload(arr, raw, nb, device)
+        self.uploads += 1
+        if key is not None and ev is not None:
+            self._insert(key, t, ev, device)
         return t
 
     def _upload(self, arr, raw, nb, device):
+        """(device tensor, the event its copy completes by — None for the
+        unpooled path, whose tables are never cached)."""
         import numpy as np
         if nb == 0 or nb > self.SLOT:
             host = torch.from_numpy(raw.copy())
             return host.pin_memory().to(device, non_blocking=True).view(
-                _TORCH_OF[arr.dtype.str]).reshape(arr.shape)
+                _TORCH_OF[arr.dtype.str]).reshape(arr.shape), None
         if self.buf is None:
             self.buf = torch.empty(self.SLOT * self.NSLOT, dtype=torch.uint8,
                                    pin_memory=True)
@@ -130,7 +154,7 @@ class _PinnedRing:
             ev.record(side)
         dev.record_stream(cur)
         cur.wait_event(ev)
-        return dev.view(_TORCH_OF[arr.dtype.str]).reshape(arr.shape)
+        return dev.view(_TORCH_OF[arr.dtype.str]).reshape(arr.shape), ev
 
 
 _TORCH_OF = {'<i8': torch.int64, '<i4': torch.int32, '<i2': torch.int16,
@@ -1223,29 +1247,58 @@ class _GraphCache:
     time at C4, against ~10 µs for one graph launch).  An entry is keyed by
     everything its kernels' arguments hold — the device row table's
     address (the upload cache hands the same table tensor back for the same
-    rows), the shape, the tolerance — and owns its workspace and outputs,
-    so nothing another call allocates can move under it; it keeps the row
-    table alive, so its address cannot be reused while the graph lives.
-    The outputs are overwritten by the next replay: a caller consumes them
-    (copies them to the host) before its next call."""
+    rows), the shape, the tolerance, the library's workgroup-form setting
+    (fsagg_pairgram_block8) — and keeps the row table alive, so its address
+    cannot be reused while the graph lives.  Each entry owns only its
+    output buffer (5n² words); the workspace and the per-key sums it
+    replays into are shared by every entry of the same shape and stream
+    (replays on one stream run in order), so the cache holds one
+    workspace per shape however many row tables it has seen.  A chain is
+    captured on the SECOND call with the same key: rows that change every
+    call (fresh upload tensors) run eagerly on the shared workspace and
+    never pay a capture.  The outputs are overwritten by the next replay: a
+    caller consumes them (copies them to the host) before its next call."""
     MAX_ENTRIES = 8
+    MAX_SEEN = 64
 
     def __init__(self):
         from collections import OrderedDict
         self.entries = OrderedDict()
+        self.seen = OrderedDict()
+        self.scratch = {}
         self.enabled = True
         self.captures = 0
 
-    def get(self, key, build):
+    def lookup(self, key):
+        """The entry of ``key``, or None; records the sighting."""
         e = self.entries.get(key)
-        if e is None:
-            e = self.entries[key] = build()
-            self.captures += 1
-            while len(self.entries) > self.MAX_ENTRIES:
-                self.entries.popitem(last=False)
-        else:
+        if e is not None:
             self.entries.move_to_end(key)
+            return e
+        return None
+
+    def second_sighting(self, key):
+        if key in self.seen:
+            del self.seen[key]
+            return True
+        self.seen[key] = True
+        while len(self.seen) > self.MAX_SEEN:
+            self.seen.popitem(last=False)
+        return False
+
+    def put(self, key, e):
+        self.entries[key] = e
+        self.captures += 1
+        while len(self.entries) > self.MAX_ENTRIES:
+            self.entries.popitem(last=False)
         return e
+
+    def shared(self, key, make):
+        """Scratch shared by the entries of one shape and stream."""
+        s = self.scratch.get(key)
+        if s is None:
+            s = self.scratch[key] = make()
+        return s
 
 
 _GRAPHS = _GraphCache()
@@ -1253,9 +1306,9 @@ _GRAPHS = _GraphCache()
 
 def pairgram_rows_dist_graph(rs, tol):
     """:func:`pairgram_rows_dist` replayed from a captured graph (captured
-    on the first call for these rows and shape, replayed after): returns
-    (buf, D, ill, B, D64) views of the entry's own buffer, valid until the
-    next call for the same rows."""
+    on the second call for these rows and shape, replayed after; the first
+    runs eagerly): returns (buf, D, ill, B, D64) views of a buffer valid
+    until the next call for the same rows."""
     if not _GRAPHS.enabled:
         return pairgram_rows_dist(rs, tol)[:5]
     _require_all(rs, 'Krum')
@@ -1263,26 +1316,35 @@ def pairgram_rows_dist_graph(rs, tol):
         raise ValueError('the Gram path takes 2..%d clients' %
                          L.FSAGG_PAIRGRAM_MAX_CLIENTS)
     lay = rs.layout
+    lib = L.load()
+    stages = lib.fsagg_pairgram_set_stages(-1)
+    lib.fsagg_pairgram_set_stages(stages)
     key = ('pairgram', rs.device.index, rs.tab.data_ptr(), rs.ss, rs.n,
-           rs.nseg, lay.signature(), float(tol))
+           rs.nseg, lay.signature(), float(tol), lib.fsagg_pairgram_block8(),
+           stages)
+    e = _GRAPHS.lookup(key)
+    if e is None:
+        if not _GRAPHS.second_sighting(key):
+            return pairgram_rows_dist(rs, tol)[:5]
+        stream = torch._C._cuda_getCurrentRawStream(rs.device.index)
+        need = max(int(lib.fsagg_pairgram_workspace_bytes(
+            rs.n, max(lay.numel, 1), rs.nseg)), 1)
 
-    def build():
+        def make():
+            return (torch.empty(need, dtype=torch.uint8, device=rs.device),
+                    torch.empty((2, rs.nseg, rs.n, rs.n),
+                                dtype=torch.float64, device=rs.device))
+        ws, sq2 = _GRAPHS.shared((rs.device.index, stream, need, rs.nseg,
+                                  rs.n), make)
         seg_lo, seg_end = lay.seg_bounds(rs.device, 0, lay.numel, None)
-        need = L.load().fsagg_pairgram_workspace_bytes(
-            rs.n, max(lay.numel, 1), rs.nseg)
-        ws = torch.empty(max(int(need), 1), dtype=torch.uint8,
-                         device=rs.device)
-        sq2 = torch.empty((2, rs.nseg, rs.n, rs.n), dtype=torch.float64,
-                          device=rs.device)
         buf = _gram_buf(rs.n, rs.device)[0]
-        # one eager run first (loads the code objects outside the capture)
-        _pairgram_rows_launch(rs, tol, seg_lo, seg_end, ws, sq2, buf)
+        # the first sighting ran this chain eagerly: its code objects are
+        # loaded, so the capture records launches only
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             _pairgram_rows_launch(rs, tol, seg_lo, seg_end, ws, sq2, buf)
-        return g, buf, (rs.tab, seg_lo, seg_end, ws, sq2)
-
-    g, buf, _ = _GRAPHS.get(key, build)
+        e = _GRAPHS.put(key, (g, buf, (rs.tab, seg_lo, seg_end)))
+    g, buf, _ = e
     g.replay()
     return (buf,) + gram_views(buf)
 

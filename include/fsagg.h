@@ -150,6 +150,11 @@ int fsagg_trimmed_mean_f32(const float *const *rows, int n, int64_t numel,
  * Workspace: fsagg_pairdist_workspace_bytes(n, numel, nseg) bytes (device).
  */
 size_t fsagg_pairdist_workspace_bytes(int n, int64_t numel, int nseg);
+/* Coordinates per chunk of the distance kernels for (n, numel, nseg): each
+ * fp32 per-chunk partial of a pair sums at most this many squared
+ * differences plus its k-slice sums (<= 256), so its relative rounding
+ * error is below (chunk + 256)·2^-24 (all terms are non-negative). */
+int64_t fsagg_pairdist_chunk_elems(int n, int64_t numel, int nseg);
 int fsagg_pairdist_f32(const float *const *rows, int n, int64_t numel,
                        const int64_t *seg_off, int nseg, float *D,
                        void *workspace, size_t workspace_bytes,
@@ -509,6 +514,15 @@ size_t fsagg_pairgram_workspace_bytes(int n, int64_t numel, int nseg);
  * restores the default.  segsq / err agree within the stated bounds.
  * Returns the previous setting.  For A/B measurements. */
 int fsagg_pairgram_set_block8(int on);
+/* The current setting of fsagg_pairgram_set_block8 (keys of captured
+ * launch chains, whose kernels it selects). */
+int fsagg_pairgram_block8(void);
+/* The chunk kernel's LDS stages (n <= 112 forms): 1 (default) compact —
+ * the n client rows, three buffers where they fit (two stages in flight);
+ * 0 the full-tile stages of round 5 (16·NT rows + the centre's, one in
+ * flight); < 0 restores the default.  Returns the previous setting.  For
+ * A/B measurements; the results are identical. */
+int fsagg_pairgram_set_stages(int mode);
 int fsagg_pairgram_rows_segsq_f32(const fsagg_rows *rows,
                                   const int64_t *seg_lo,
                                   const int64_t *seg_end, int64_t numel,

@@ -11,7 +11,12 @@ the same dicts.
 
 argv[1] = 'lost': rank 1 never runs its round; rank 0's flag barrier must
 give up within the timeout, ``run_bucket`` must raise, and both ranks must
-release the peer buffers and exit cleanly."""
+release the peer buffers and exit cleanly.
+
+argv[1] = 'lost_views': the same with result views
+(``run_bucket(copy=False)``, ``aggregator.shard_result_views``): the call
+returns before its barrier has run, so it cannot raise; the failure
+surfaces at ``check()`` (or the next run_bucket), naming rank 1."""
 import json
 import os
 import sys
@@ -108,11 +113,12 @@ def aggregate_mode(rank, world):
     return {'ok': done}
 
 
-def lost_mode(rank, world):
+def lost_mode(rank, world, views=False):
     from federatedscope_amd.core.sharding import Comm, PeerAssembly
     pa = PeerAssembly(4096, comm=Comm(), device=torch.device('cuda', 0),
-                      timeout_s=1.0)
+                      timeout_s=1.0, buffers=3 if views else 2)
     raised = None
+    at_call = None
     t0 = time.time()
     def compute(lo, hi, own, peers):
         own[lo:hi].fill_(1.0)
@@ -120,7 +126,10 @@ def lost_mode(rank, world):
 
     if rank == 0:
         try:
-            pa.run_bucket(compute)
+            pa.run_bucket(compute, copy=not views)
+            if views:
+                at_call = 'returned'
+                pa.check()
         except RuntimeError as e:
             raised = str(e)
     waited = time.time() - t0
@@ -146,7 +155,7 @@ def lost_mode(rank, world):
     dist.barrier()
     pa.close()
     return {'raised': raised, 'waited_s': round(waited, 3),
-            'second_round_ok': second}
+            'second_round_ok': second, 'views_call': at_call}
 
 
 def main():
@@ -155,7 +164,7 @@ def main():
     torch.cuda.set_device(0)
     mode = sys.argv[1]
     res = aggregate_mode(rank, world) if mode == 'aggregate' else \
-        lost_mode(rank, world)
+        lost_mode(rank, world, views=mode == 'lost_views')
     res.update(rank=rank, world=world, mode=mode)
     sys.stdout.write(json.dumps(res) + '\n')
     sys.stdout.flush()

@@ -29,6 +29,7 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
     import oracle as O
+    import trimmed_bounds as TB
     from golden_io import load_case
     from test_gpu_golden import (DictModel, assert_bit_exact, cfg, feedback,
                                  to_np)
@@ -68,12 +69,13 @@ def main():
             cfg(f=1, ratio=0.2))).aggregate(
                 {'client_feedback': feedback(clients)})
         want = O.add_init(init, O.trimmed_mean_update(clients, k))
-        grp = O.trimmed_group_bound(clients, k)
-        eps = np.finfo(np.float32).eps
         for key in got:
             g, o = to_np(got[key]).astype(np.float64), np.asarray(want[key])
-            assert (np.abs(g - o) <= grp[key] + 4 * eps * (np.abs(o) + np.abs(
-                np.asarray(init[key])))).all(), (name, key)
+            T = np.stack([np.asarray(d[key], np.float64).reshape(-1)
+                          for _, d in clients])
+            TB.check_vs_oracle('world2|%s|%s' % (name, key), g.reshape(-1),
+                               o.reshape(-1), T, len(clients) - 2 * k,
+                               init=np.asarray(init[key]).reshape(-1))
         done.append(name)
     for name in ('krum_n50_f10_a5', 'krum_n12_f2_a3', 'krum_n10_f10_a1'):
         meta, clients, out, init, extra = load_case(name)

@@ -14,6 +14,7 @@ import pytest
 import torch
 
 import oracle as O
+import trimmed_bounds as TB
 from golden_io import case_names, load_case
 
 pytestmark = pytest.mark.gpu
@@ -174,9 +175,8 @@ def test_median_and_trimmed(name):
         got = TrimmedmeanAggregator(model=DictModel(init), config=cfg(
             f=1, ratio=ratio)).aggregate({'client_feedback': fb})
         k = int(len(clients) * ratio)
-        tol = O.trimmed_tolerance(clients, k)
-        grp = O.trimmed_group_bound(clients, k)
         ours = O.add_init(init, O.trimmed_mean_update(clients, k))
+        div = len(clients) - 2 * k
         for key in got:
             g = to_np(got[key]).astype(np.float64)
             ref = extra['tm|%s|%s' % (ratio, key)]
@@ -184,15 +184,15 @@ def test_median_and_trimmed(name):
             fin = np.isfinite(ref)
             assert np.array_equal(np.isnan(g), np.isnan(ref)), (name, ratio)
             assert np.array_equal(g[np.isinf(ref)], ref[np.isinf(ref)])
+            T = np.stack([np.asarray(d[key], dtype=np.float64).reshape(-1)
+                          for _, d in clients])[:, fin.reshape(-1)]
             g, ref, o = g[fin], ref[fin], np.asarray(ours[key])[fin]
-            t, ini = np.asarray(tol[key])[fin], np.asarray(init[key])[fin]
-            gb = np.asarray(grp[key])[fin]
-            # vs the reference (ATen cascade sum): its own rounding bound
-            assert (np.abs(g - ref) <= t + 4 * eps * np.abs(ref)).all()
-            # vs the oracle's fp64 middle sum: the kernel's fp32 group sums
-            # plus a few ulps
-            assert (np.abs(g - o) <= gb + 4 * eps * (np.abs(o) +
-                                                     np.abs(ini))).all()
+            ini = np.asarray(init[key])[fin]
+            tag = '%s|tm%s|%s' % (name, ratio, key)
+            # vs the reference (ATen cascade sum): §8(c)'s contract
+            TB.check_vs_ref(tag, g, ref, T, div)
+            # vs the oracle's fp64 middle sum: the regression bound
+            TB.check_vs_oracle(tag, g, o, T, div, init=ini)
 
 
 @pytest.mark.parametrize('name', case_names('bulyan_'))
@@ -212,18 +212,18 @@ def test_bulyan(name):
     # middle sum
     k = int(meta['rate'] * meta['f'])
     chosen = [clients[i] for i in sel]
-    tol = O.trimmed_tolerance(chosen, k, divisor=keep - 2 * k)
-    grp = O.trimmed_group_bound(chosen, k, divisor=keep - 2 * k)
     ours, osel = O.bulyan_aggregate(clients, meta['f'], meta['rate'], init)
     assert osel == sel
-    eps = np.finfo(np.float32).eps
     for key in out:
-        g = to_np(got[key]).astype(np.float64)
-        ref, o = out[key].astype(np.float64), np.asarray(ours[key])
-        ini = np.asarray(init[key], dtype=np.float64)
-        assert (np.abs(g - ref) <= tol[key] + 4 * eps * np.abs(ref)).all()
-        assert (np.abs(g - o) <= grp[key] + 4 * eps * (np.abs(o) +
-                                                       np.abs(ini))).all()
+        g = to_np(got[key]).astype(np.float64).reshape(-1)
+        ref = out[key].astype(np.float64).reshape(-1)
+        o = np.asarray(ours[key]).reshape(-1)
+        ini = np.asarray(init[key], dtype=np.float64).reshape(-1)
+        T = np.stack([np.asarray(d[key], dtype=np.float64).reshape(-1)
+                      for _, d in chosen])
+        tag = '%s|%s' % (name, key)
+        TB.check_vs_ref(tag, g, ref, T, keep - 2 * k)
+        TB.check_vs_oracle(tag, g, o, T, keep - 2 * k, init=ini)
 
 
 @pytest.mark.parametrize('name', case_names('normbound_'))

@@ -7,6 +7,7 @@ import pytest
 import torch
 
 import oracle as O
+import trimmed_bounds as TB
 
 pytestmark = pytest.mark.gpu
 
@@ -137,10 +138,9 @@ def test_median_trimmed_all_kernels(n):
         ops.trimmed_mean(rows, k, out)
         want = O.trimmed_mean_update(models, k)['w']
         eps = np.finfo(np.float32).eps
-        grp = O.trimmed_group_bound(models, k)['w']
-        err = np.abs(out.cpu().numpy().astype(np.float64) - want)
-        # the kernel's fp32 group sums of the clamped middle
-        assert (err <= grp + 2 * eps * np.abs(want)).all(), (n, k, err.max())
+        g = out.cpu().numpy()
+        T = np.stack([m[1]['w'] for m in models])
+        TB.check_vs_oracle('kernels|n%d|k%d' % (n, k), g, want, T, n - 2 * k)
 
 
 def test_orderstat_nonfinite_columns():
@@ -306,9 +306,9 @@ def test_orderstat_refinement_stress(n):
     for k in (1, n // 5, n // 2 - 1):
         ops.trimmed_mean(rows, k, out)
         want = O.trimmed_mean_update(models, k)['w']
-        grp = O.trimmed_group_bound(models, k)['w']
-        err = np.abs(out.cpu().numpy().astype(np.float64) - want)
-        assert (err <= grp + 2 * eps * np.abs(want)).all(), (k, err.max())
+        g = out.cpu().numpy()
+        T = np.stack([m[1]['w'] for m in models])
+        TB.check_vs_oracle('stream|n%d|k%d' % (n, k), g, want, T, n - 2 * k)
 
 
 @pytest.mark.parametrize('n', [12, 50, 130, 255, 256, 300])

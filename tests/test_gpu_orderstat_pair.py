@@ -12,6 +12,7 @@ import pytest
 import torch
 
 import oracle as O
+import trimmed_bounds as TB
 
 pytestmark = pytest.mark.gpu
 
@@ -29,11 +30,15 @@ def pair_min(n):
         lib.fsagg_orderstat_set_pair_min(prev)
 
 
-def trimmed_tol(X, k, want):
-    """|ours − oracle|: the kernel's fp32 group sums of the clamped middle
-    (O.trimmed_group_bound) plus the final roundings (ε|want|)."""
-    models = [(1, {'w': X[i]}) for i in range(X.shape[0])]
-    return O.trimmed_group_bound(models, k)['w'] + 2 * EPS * np.abs(want)
+def trimmed_tol(X, k, want, got=None, tag='kernel'):
+    """|ours − oracle| <= the regression bound of tests/trimmed_bounds.py
+    (ORACLE_UNITS·ε·Σ|x|/(n − 2k) + 4ε|want|); with ``got`` the measured
+    error is logged ($FSAGG_ERR_LOG)."""
+    u = TB.units(X, X.shape[0] - 2 * k)
+    slack = 4 * EPS * np.abs(want)
+    if got is not None:
+        TB.log(tag, np.abs(np.asarray(got, np.float64) - want), u, slack)
+    return TB.ORACLE_UNITS * u + slack
 
 
 def columns(n, P, seed):
@@ -85,7 +90,8 @@ def test_pair_kernel_vs_oracle_and_one_wave(n):
         k = int(n * ratio)
         want = O.trimmed_mean_update(models, k)['w']
         err = np.abs(got[k].astype(np.float64) - want)
-        assert (err <= trimmed_tol(X, k, want)).all(), (n, k, err.max())
+        tol = trimmed_tol(X, k, want, got[k], 'pair|n%d|k%d' % (n, k))
+        assert (err <= tol).all(), (n, k, err.max())
 
 
 @pytest.mark.parametrize('n', [130, 200, 255])
@@ -139,7 +145,7 @@ def test_pair_kernel_refinement_and_nonfinite(n):
                                   want[~fin & ~np.isnan(want)])
             err = np.abs(g[fin].astype(np.float64) - want[fin])
             tol = trimmed_tol(np.where(np.isfinite(X), X, 0)[:, fin], k,
-                              want[fin])
+                              want[fin], g[fin], 'pair_refine|n%d|k%d' % (n, k))
             assert (err <= tol).all(), (k, err.max())
 
 

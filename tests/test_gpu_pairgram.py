@@ -200,6 +200,34 @@ def test_pairgram_workgroup_settings(setting, n):
     _check(got, err, D, flags, B, want)
 
 
+@pytest.mark.parametrize('n', [2, 17, 31, 33, 49, 50, 52, 53, 64, 65, 100,
+                               104, 105, 112])
+def test_pairgram_compact_stages(n):
+    """The compact stage buffers (the n client rows, three buffers where
+    they fit: two stages in flight; fsagg_pairgram_set_stages 1, the
+    default) against the round-5 full-tile stages (0) on the same rows:
+    every Gram sum is formed in the same order, so the per-key d², bounds
+    and distances are identical bit for bit — both for keyed (separately
+    allocated) and stacked rows — and within the fp64 distances' bounds."""
+    from federatedscope_amd import _lib as L
+    clients = _clients(n, sizes=[70_001, 4097, 33, 1_000_000], seed=n + 7)
+    lay, _, keyed, stacked = _sets(clients)
+    lib = L.load()
+    res = {}
+    for mode in (0, 1):
+        prev = lib.fsagg_pairgram_set_stages(mode)
+        try:
+            res[mode] = [_gram(keyed), _gram(stacked)]
+        finally:
+            lib.fsagg_pairgram_set_stages(prev)
+    for a, b in zip(res[0], res[1]):
+        for x, y in zip(a, b):
+            assert np.asarray(x).tobytes() == np.asarray(y).tobytes(), n
+    got, err, D, flags, B = res[1][0]
+    assert not flags.any()
+    _check(got, err, D, flags, B, _fp64_segsq_dev(clients, lay))
+
+
 def test_pairgram_unaligned_rows():
     """Key tensors at 4-B offsets: the per-element load path."""
     from federatedscope_amd import ops
@@ -313,12 +341,27 @@ def test_pairgram_flags_and_exact_repair(case):
         ix = np.ix_(sel, sel)
         assert np.allclose(De.numpy()[ix], Dv[ix], rtol=2e-7, atol=0,
                            equal_nan=True)
-        # the recomputed pairs carry only D's own fp32 formation bound
+        # the recomputed pairs carry the VALU kernel's own bound: its fp32
+        # per-chunk sums of at most chunk + 256 non-negative terms, halved
+        # by the sqrt, plus D's own fp32 formation
+        import math
         Dr = De.numpy()[ix].astype(np.float64)
         nseg = len(lay.keys)
-        want_b = (2 * nseg + 2) * 2.0 ** -24 * np.where(np.isfinite(Dr), Dr,
+        u = 2.0 ** -24
+        chl = ops.L.load().fsagg_pairdist_chunk_elems(len(sel), lay.numel,
+                                                      nseg)
+        assert chl >= 2048
+        acc = math.expm1((chl + 256) * math.log1p(u)) + 64 * u
+        rel = acc / (2.0 * (1.0 - acc))
+        want_b = (rel + (2 * nseg + 2) * u) * np.where(np.isfinite(Dr), Dr,
                                                         0.0)
-        assert np.array_equal(agg.last_pair_bound[ix], want_b)
+        assert np.allclose(agg.last_pair_bound[ix], want_b, rtol=1e-12,
+                           atol=0)
+        # and it holds: |D − Σ_key sqrt(exact d²)| on the finite pairs
+        with np.errstate(invalid='ignore'):
+            exact = np.sqrt(want).sum(0)[ix]
+        fin = np.isfinite(Dr) & np.isfinite(exact) & (Dr > 0)
+        assert (np.abs(Dr - exact)[fin] <= agg.last_pair_bound[ix][fin]).all()
         return
     assert not flags.any()
     assert agg.last_pairdist_path == 'mfma'

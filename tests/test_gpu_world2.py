@@ -143,15 +143,19 @@ def test_peer_assembly_aggregate(world):
                            'trimmed_mean', 'krum'], r
 
 
-def test_peer_assembly_lost_rank():
+@pytest.mark.parametrize('mode', ['lost', 'lost_views'])
+def test_peer_assembly_lost_rank(mode):
     """Rank 1 never runs its round: rank 0's barrier gives up after the 1 s
-    timeout, run_bucket raises naming rank 1, and both ranks release the
-    peer buffers and exit 0."""
-    recs = _run2([os.path.join('tests', '_peer_worker.py'), 'lost'])
+    timeout, run_bucket raises naming rank 1 (with result views the call
+    itself returns — its barrier has not run yet — and check() raises), and
+    both ranks release the peer buffers and exit 0."""
+    recs = _run2([os.path.join('tests', '_peer_worker.py'), mode])
     by = {r['rank']: r for r in recs}
     assert set(by) == {0, 1}
     assert by[1]['raised'] is None
     assert 'rank 1' in (by[0]['raised'] or ''), by[0]
+    if mode == 'lost_views':
+        assert by[0]['views_call'] == 'returned', by[0]
     assert 0.9 <= by[0]['waited_s'] <= 30.0, by[0]
     # once the late rank has caught up, the next round succeeds everywhere
     assert by[0]['second_round_ok'] is True, by[0]

@@ -262,13 +262,16 @@ def orderstat_c5(dev, n=200, ratio=0.2, P=None, tag='C5'):
     return res
 
 
-def dropin_rules(dev):
+def dropin_rules(dev, fresh=False):
     """The drop-in aggregators' whole aggregate() call (Python, staging of the
     client dicts into the device stack, kernels, init + update) on
     device-resident ConvNet2-h2048 dicts (12 keys, 6.6M params): Krum
     (multi-Krum 5) and Bulyan at n = 50, f = 10; FedAvg, median, trimmed
     mean and norm bounding at n = 200.  Wall clock with the GPU synchronised on both
-    sides; the result stays on the device."""
+    sides; the result stays on the device.  ``fresh``: every call gets new
+    dict objects and the upload cache is off, so every call walks, builds
+    and uploads its tables (a server round with freshly received uploads;
+    the Gram chain then runs eagerly, never from a captured graph)."""
     from collections import OrderedDict
     from types import SimpleNamespace
     from federatedscope_amd.core.aggregators import (
@@ -324,19 +327,31 @@ def dropin_rules(dev):
                                                      device=dev,
                                                      config=cfg(bound=5.0))),
     ]
+    prev_cache = ops._RING.cache_on
+    if fresh:
+        ops._RING.cache_on = False
     for name, n, agg in rules:
         fb = c50 if n == 50 else c200
-        info = {'client_feedback': fb, 'recover_fun': None}
+        # fresh: 8 distinct dict lists (new dict objects over the same
+        # tensors), cycled; the tables are rebuilt and uploaded every call
+        infos = [{'client_feedback': [(s, OrderedDict(d)) for s, d in fb]
+                  if fresh else fb, 'recover_fun': None}
+                 for _ in range(8 if fresh else 1)]
+        it = [0]
+
+        def call():
+            agg.aggregate(infos[it[0] % len(infos)])
+            it[0] += 1
         torch.cuda.synchronize()
         w0 = time.perf_counter()
         while time.perf_counter() - w0 < 0.05:   # clocks up (see timed)
-            agg.aggregate(info)
+            call()
             torch.cuda.synchronize()
         ts = []
         for _ in range(20):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            agg.aggregate(info)
+            call()
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         t = statistics.median(ts)
@@ -345,9 +360,13 @@ def dropin_rules(dev):
                                              None),
                     'ms_aggregate': round(t * 1e3, 3),
                     'GBps_algorithmic': round(4.0 * n * P / t / 1e9, 1),
+                    'fresh_uploads': bool(fresh),
                     'what': 'aggregate() on device-resident dicts read in '
-                            'place (row sets), kernels + init+update'})
-        log('%s: %.2f ms' % (name, t * 1e3))
+                            'place (row sets), kernels + init+update' + (
+                                '; new dict objects every call, upload '
+                                'cache off' if fresh else '')})
+        log('%s%s: %.2f ms' % (name, ' (fresh)' if fresh else '', t * 1e3))
+    ops._RING.cache_on = prev_cache
     return out
 
 
@@ -380,6 +399,9 @@ def main():
             torch.cuda.empty_cache()
     if 'dropin' in which:
         for r in dropin_rules(dev):
+            print(json.dumps(r), flush=True)
+    if 'dropin_fresh' in which:
+        for r in dropin_rules(dev, fresh=True):
             print(json.dumps(r), flush=True)
 
 

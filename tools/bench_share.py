@@ -286,7 +286,7 @@ def aggregate_share(args):
     for world, views in [(1, False)] + [(W, v) for v in (False, True)]:
         for cache in ((True, ) if world == 1 else (True, False)):
             ops._RING.cache_on = cache
-            ops._RING.cache.clear()
+            ops._RING.clear()
             agg = ClientsAvgAggregator(device=dev, config=cfg)
             emu = None
             if world > 1:
