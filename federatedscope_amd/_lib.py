@@ -121,6 +121,7 @@ SIGNATURES['fsagg_pairgram_workspace_bytes'] = (_c_sz, [_c_i, _c_i64, _c_i])
 SIGNATURES['fsagg_pairgram_set_block8'] = (_c_i, [_c_i])
 SIGNATURES['fsagg_pairgram_block8'] = (_c_i, [])
 SIGNATURES['fsagg_pairgram_set_stages'] = (_c_i, [_c_i])
+SIGNATURES['fsagg_pairgram_set_chunks'] = (_c_i, [_c_i])
 SIGNATURES['fsagg_pairgram_rows_segsq_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_sz, _c_p])
 SIGNATURES['fsagg_pairgram_rows_f32'] = (
@@ -163,6 +164,10 @@ SIGNATURES['fsagg_peer_close'] = (_c_i, [_c_i, _c_p])
 SIGNATURES['fsagg_peer_pci_bus_id'] = (_c_i, [_c_i, ctypes.c_char_p, _c_i])
 SIGNATURES['fsagg_peer_can_access'] = (_c_i, [_c_i, ctypes.c_char_p])
 SIGNATURES['fsagg_weighted_sum_bcast_f32'] = (
+    _c_i, [_c_p, _c_p, _c_p, _c_i, _c_i64, _c_p, ctypes.POINTER(_c_p), _c_i,
+           _c_p])
+FSAGG_HOSTTAB_MAX_CLIENTS = 128
+SIGNATURES['fsagg_weighted_sum_hosttab_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i, _c_i64, _c_p, ctypes.POINTER(_c_p), _c_i,
            _c_p])
 SIGNATURES['fsagg_peer_push_f32'] = (

@@ -1324,6 +1324,9 @@ std::atomic<int> g_block8{1};
 // (16·NT rows + the centre's, one in flight) — fsagg_pairgram_set_stages,
 // A/B
 std::atomic<int> g_compact{1};
+// main-pass chunks (n <= 112 forms): about kMainChunks workgroups — two
+// rounds at two per CU; fsagg_pairgram_set_chunks, A/B
+std::atomic<int> g_main_chunks{kMainChunks};
 
 struct GramPlan {
   int nt;              // tiles of 16 clients
@@ -1370,7 +1373,7 @@ GramPlan gram_plan(int n, int64_t numel, int nseg) {
   // (fewer, longer chunks: less partial traffic); 8-tile blocks: ~2048
   // workgroups of 512 threads (1024 chunks of one block, 512 of four)
   const int64_t target =
-      !pl.lines ? kMainChunks
+      !pl.lines ? int64_t(g_main_chunks.load(std::memory_order_relaxed))
       : pl.block8 ? (pl.nlines == 1 ? 1024 : 512)
                   : (kLineBlocks / pl.nlines > 64 ? kLineBlocks / pl.nlines
                                                   : 64);
@@ -1461,8 +1464,17 @@ void gram_pass(const float *const *tab, int64_t ss, int n,
                          dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab,
                          ss, n, pl.nt, seg_lo, seg_end, nseg, ctl, w, cap,
                          centre, partial);
+  } else if constexpr (NT > kFullTiles) {
+    // NT > 4 (one workgroup per CU, up to 256 VGPRs + AGPRs): the full-tile
+    // stages — the compact form spilled there (n = 100: 0.99 against
+    // 0.89 ms, profiles/r06/gram_stages_ab.jsonl)
+    hipLaunchKernelGGL((gram_chunk_kernel<NT, CENTRED, false>),
+                       dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab,
+                       ss, n, pl.nt, seg_lo, seg_end, nseg, ctl, w, cap,
+                       centre, partial);
   } else if (g_compact.load(std::memory_order_relaxed) == 0) {
-    // A/B: the full-tile stages (16·NT rows + the centre), one in flight
+    // A/B: the round-5 full-tile stages (16·NT rows + the centre), one in
+    // flight
     hipLaunchKernelGGL((gram_chunk_kernel<NT, CENTRED, false>),
                        dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab,
                        ss, n, pl.nt, seg_lo, seg_end, nseg, ctl, w, cap,
@@ -1527,6 +1539,11 @@ extern "C" int fsagg_pairgram_set_block8(int on) {
 
 extern "C" int fsagg_pairgram_set_stages(int mode) {
   return g_compact.exchange(mode < 0 ? 1 : (mode > 1 ? 1 : mode));
+}
+
+extern "C" int fsagg_pairgram_set_chunks(int chunks) {
+  return g_main_chunks.exchange(chunks <= 0 ? kMainChunks
+                                            : (chunks < 64 ? 64 : chunks));
 }
 
 extern "C" int fsagg_pairgram_block8(void) {

@@ -326,6 +326,97 @@ void launch_wsum_any(const float *const *rows, const float *weights,
 }
 
 // ---------------------------------------------------------------------------
+// Host tables in the kernel arguments (fsagg_weighted_sum_hosttab_f32): up
+// to FSAGG_HOSTTAB_MAX_CLIENTS row pointers, weights and prescales travel in
+// the launch's kernel-argument block (2 KiB), which the kernels read with
+// scalar loads exactly as they read a device table — no upload, no copy on
+// any stream before the launch.  The aggregate() path for a flat or uniform
+// row set of fresh uploads (new tensors every round) spends most of its
+// host time on those small uploads otherwise.
+// ---------------------------------------------------------------------------
+struct ArgTab {
+  const float *rows[FSAGG_HOSTTAB_MAX_CLIENTS];
+  float w[FSAGG_HOSTTAB_MAX_CLIENTS];
+  float pre[FSAGG_HOSTTAB_MAX_CLIENTS];
+};
+
+template <int U, int V, bool PRE, bool BASE, bool NT, class O>
+__global__ __launch_bounds__(kBlock) void wsum_f32_arg_kernel(
+    const ArgTab tab, int n, int64_t nvec, const float *__restrict__ base,
+    O out) {
+  constexpr int64_t tile = int64_t(kBlock) * V;
+  const int64_t full = nvec / tile * tile;
+  for (int64_t t0 = int64_t(blockIdx.x) * tile; t0 < nvec;
+       t0 += int64_t(gridDim.x) * tile) {
+    if (t0 < full)
+      wsum_tile<U, V, PRE, BASE, NT, false>(tab.rows, tab.w, tab.pre, n, nvec,
+                                            t0, base, out);
+    else
+      wsum_tile<U, V, PRE, BASE, NT, true>(tab.rows, tab.w, tab.pre, n, nvec,
+                                           t0, base, out);
+  }
+}
+
+template <class O>
+__global__ __launch_bounds__(kTailBlock) void wsum_f32_arg_tail_kernel(
+    const ArgTab tab, int pre_on, int n, int64_t start, int64_t numel,
+    const float *__restrict__ base, O out) {
+  const int e = threadIdx.x;
+  const int m = int(numel - start);  // 1..3
+  if (e >= m) return;
+  // n <= FSAGG_HOSTTAB_MAX_CLIENTS: one thread per tail element walks the
+  // clients (their loads are independent of the running sum)
+  float acc = 0.0f;
+  for (int c = 0; c < n; ++c) {
+    float x = gld(tab.rows[c] + start + e);
+    if (pre_on) x = mul_rn(x, tab.pre[c]);
+    const float t = mul_rn(x, tab.w[c]);
+    acc = c == 0 ? t : add_rn(acc, t);
+  }
+  if (base) acc = add_rn(base[start + e], acc);
+  put1(out, start + e, acc);
+}
+
+template <bool PRE, bool BASE, int V, class O>
+void launch_wsum_arg_v(const ArgTab &tab, int n, int64_t nvec,
+                       const float *base, O out, hipStream_t s) {
+  const int64_t tiles = (nvec + int64_t(kBlock) * V - 1) / (int64_t(kBlock) * V);
+  const unsigned grid = stream_grid(tiles, 1, 256 * 16);
+  hipLaunchKernelGGL((wsum_f32_arg_kernel<kU, V, PRE, BASE, true, O>),
+                     dim3(grid), dim3(kBlock), 0, s, tab, n, nvec, base, out);
+}
+
+template <bool PRE, bool BASE, class O>
+void launch_wsum_arg(const ArgTab &tab, int n, int64_t nvec,
+                     const float *base, O out, hipStream_t s) {
+  switch (wsum_width(nvec, n)) {
+    case 24: launch_wsum_arg_v<PRE, BASE, 24>(tab, n, nvec, base, out, s); break;
+    case 16: launch_wsum_arg_v<PRE, BASE, 16>(tab, n, nvec, base, out, s); break;
+    case 8: launch_wsum_arg_v<PRE, BASE, 8>(tab, n, nvec, base, out, s); break;
+    case 4: launch_wsum_arg_v<PRE, BASE, 4>(tab, n, nvec, base, out, s); break;
+    default: launch_wsum_arg_v<PRE, BASE, 1>(tab, n, nvec, base, out, s);
+  }
+}
+
+template <class O>
+void launch_wsum_arg_any(const ArgTab &tab, bool pre, int n, int64_t numel,
+                         const float *base, O out, hipStream_t s) {
+  const int64_t nvec = numel / 4;
+  if (nvec > 0) {
+    if (pre) {
+      if (base) launch_wsum_arg<true, true>(tab, n, nvec, base, out, s);
+      else launch_wsum_arg<true, false>(tab, n, nvec, base, out, s);
+    } else {
+      if (base) launch_wsum_arg<false, true>(tab, n, nvec, base, out, s);
+      else launch_wsum_arg<false, false>(tab, n, nvec, base, out, s);
+    }
+  }
+  if (numel > nvec * 4)
+    hipLaunchKernelGGL((wsum_f32_arg_tail_kernel<O>), dim3(1), dim3(kWave), 0,
+                       s, tab, pre ? 1 : 0, n, nvec * 4, numel, base, out);
+}
+
+// ---------------------------------------------------------------------------
 // row sets: clients' key tensors read in place (include/fsagg.h fsagg_rows)
 // ---------------------------------------------------------------------------
 // One chunk of <= kBlock·V float4 coordinates of one key segment.  The
@@ -753,6 +844,57 @@ extern "C" int fsagg_weighted_sum_bcast_f32(const float *const *rows,
   launch_wsum_any(rows, weights, prescale, n, numel, base, o,
                   as_stream(stream));
   return check_launch("fsagg_weighted_sum_bcast_f32");
+}
+
+extern "C" int fsagg_weighted_sum_hosttab_f32(
+    const uint64_t *rows, const float *weights, const float *prescale, int n,
+    int64_t numel, const float *base, float *const *outs, int nout,
+    fsagg_stream_t stream) {
+  if (!rows || !weights || !outs || n < 1 ||
+      n > FSAGG_HOSTTAB_MAX_CLIENTS || numel < 0 || nout < 1 ||
+      nout > FSAGG_MAX_PEERS) {
+    set_error("fsagg_weighted_sum_hosttab_f32: invalid argument (n=%d, at "
+              "most %d; numel=%lld nout=%d)", n, FSAGG_HOSTTAB_MAX_CLIENTS,
+              (long long)numel, nout);
+    return FSAGG_EINVAL;
+  }
+  ArgTab tab;
+  for (int i = 0; i < n; ++i) {
+    tab.rows[i] = reinterpret_cast<const float *>(rows[i]);
+    if (!tab.rows[i] || !aligned16(tab.rows[i])) {
+      set_error("fsagg_weighted_sum_hosttab_f32: row %d is NULL or not "
+                "16-byte aligned", i);
+      return FSAGG_EINVAL;
+    }
+    tab.w[i] = weights[i];
+    tab.pre[i] = prescale ? prescale[i] : 1.0f;
+  }
+  for (int i = n; i < FSAGG_HOSTTAB_MAX_CLIENTS; ++i) {
+    tab.rows[i] = nullptr;
+    tab.w[i] = tab.pre[i] = 0.0f;
+  }
+  for (int k = 0; k < nout; ++k)
+    if (!outs[k] || !aligned16(outs[k])) {
+      set_error("fsagg_weighted_sum_hosttab_f32: out %d is NULL or not "
+                "16-byte aligned", k);
+      return FSAGG_EINVAL;
+    }
+  if (base && !aligned16(base)) {
+    set_error("fsagg_weighted_sum_hosttab_f32: base must be 16-byte "
+              "aligned");
+    return FSAGG_EINVAL;
+  }
+  if (numel == 0) return FSAGG_OK;
+  hipStream_t s = as_stream(stream);
+  if (nout == 1) {
+    launch_wsum_arg_any(tab, prescale != nullptr, n, numel, base, outs[0], s);
+  } else {
+    Bcast o{};
+    o.n = nout;
+    for (int k = 0; k < nout; ++k) o.p[k] = outs[k];
+    launch_wsum_arg_any(tab, prescale != nullptr, n, numel, base, o, s);
+  }
+  return check_launch("fsagg_weighted_sum_hosttab_f32");
 }
 
 extern "C" int64_t fsagg_wsum_chunk_elems(int64_t numel) {

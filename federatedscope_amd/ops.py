@@ -857,10 +857,12 @@ class RowSet:
         self.aligned16 = bool(aligned16)
         self.missing = int(absent(layout, table).sum()) if missing is None \
             else int(missing)
-        self.tab = _h2d_np(table.T if segmajor is None else segmajor,
-                           self.device)
-        self.struct = L.Rows(self.tab.data_ptr(), self.ss, self.n,
-                             self.nseg)
+        # the device table is uploaded on first use: the flat weighted sum
+        # of up to FSAGG_HOSTTAB_MAX_CLIENTS rows passes the host copy in
+        # its kernel arguments and never needs it
+        self._segmajor = segmajor
+        self._tab = None
+        self._struct = None
         self._keep = tuple(keepalive)
         # uniform: every client's keys lie in ONE storage at their bucket
         # offsets (csrc/host/keytable.cpp), so client i's bucket is the
@@ -909,6 +911,21 @@ class RowSet:
         return cls(layout, None, device, keepalive=keepalive,
                    aligned16=aligned16, missing=missing, segmajor=segmajor,
                    uniform=uniform)
+
+    @property
+    def tab(self):
+        """The device table ([nseg][n], or [1][n] for ss = 0)."""
+        if self._tab is None:
+            self._tab = _h2d_np(self.host.T if self._segmajor is None
+                                else self._segmajor, self.device)
+        return self._tab
+
+    @property
+    def struct(self):
+        if self._struct is None:
+            self._struct = L.Rows(self.tab.data_ptr(), self.ss, self.n,
+                                  self.nseg)
+        return self._struct
 
     def subset(self, sel):
         """The clients ``sel`` (indices, in the new reduction order)."""
@@ -1046,6 +1063,12 @@ def _weighted_sum_rows_flat(rs, weights, out, prescale, base, lo, hi, lib,
         return out
     if a % 4:
         raise ValueError('row range start %d is not 16-byte aligned' % a)
+    if rs.n <= L.FSAGG_HOSTTAB_MAX_CLIENTS and \
+            not isinstance(weights, torch.Tensor) and \
+            not isinstance(prescale, torch.Tensor):
+        # host tables in the kernel arguments: nothing to upload
+        return _weighted_sum_hosttab(rs, weights, out, prescale, base, a, b,
+                                     lib, peers)
     # entry i = the client's virtual base: coordinate p at entry + 4·p
     if a == 0:
         table = rs.tab
@@ -1077,6 +1100,37 @@ def _weighted_sum_rows_flat(rs, weights, out, prescale, base, lo, hi, lib,
         table.data_ptr(), w.data_ptr(),
         pre.data_ptr() if pre is not None else None, rs.n, b - a, bptr,
         out.data_ptr() + 4 * a, _stream(rs.device)), 'fsagg_weighted_sum_f32')
+    return out
+
+
+def _weighted_sum_hosttab(rs, weights, out, prescale, base, a, b, lib,
+                          peers):
+    """The flat weighted sum of ``rs``'s coordinates [a, b) with its row
+    table, weights and prescales in the kernel arguments
+    (fsagg_weighted_sum_hosttab_f32)."""
+    n = rs.n
+    if len(weights) != n:
+        raise ValueError('%d weights for %d rows' % (len(weights), n))
+    rows = _np.ascontiguousarray(rs.host[:, 0] + 4 * a, dtype=_np.uint64)
+    w = _np.asarray(weights, dtype=_np.float32)
+    pre = None
+    if prescale is not None:
+        if len(prescale) != n:
+            raise ValueError('prescale length mismatch')
+        pre = _np.asarray(prescale, dtype=_np.float32)
+    bptr = None
+    if base is not None:
+        bptr = int(base.host[0]) + 4 * a
+        if bptr % ALIGN_BYTES:
+            raise ValueError('base is not 16-byte aligned at %d' % a)
+    outs = [out.data_ptr() + 4 * a]
+    if peers is not None:
+        outs += [int(p) + 4 * a for p in peers]
+    arr = (ctypes.c_void_p * len(outs))(*outs)
+    L.check(lib.fsagg_weighted_sum_hosttab_f32(
+        rows.ctypes.data, w.ctypes.data,
+        pre.ctypes.data if pre is not None else None, n, b - a, bptr, arr,
+        len(outs), _stream(rs.device)), 'fsagg_weighted_sum_hosttab_f32')
     return out
 
 
@@ -1319,9 +1373,11 @@ def pairgram_rows_dist_graph(rs, tol):
     lib = L.load()
     stages = lib.fsagg_pairgram_set_stages(-1)
     lib.fsagg_pairgram_set_stages(stages)
+    chunks = lib.fsagg_pairgram_set_chunks(0)
+    lib.fsagg_pairgram_set_chunks(chunks)
     key = ('pairgram', rs.device.index, rs.tab.data_ptr(), rs.ss, rs.n,
            rs.nseg, lay.signature(), float(tol), lib.fsagg_pairgram_block8(),
-           stages)
+           stages, chunks)
     e = _GRAPHS.lookup(key)
     if e is None:
         if not _GRAPHS.second_sighting(key):

@@ -523,6 +523,11 @@ int fsagg_pairgram_block8(void);
  * flight); < 0 restores the default.  Returns the previous setting.  For
  * A/B measurements; the results are identical. */
 int fsagg_pairgram_set_stages(int mode);
+/* The main pass's target chunk count for the n <= 112 forms (default 1024,
+ * two rounds of two workgroups per CU; <= 0 restores it).  Returns the
+ * previous setting.  For A/B measurements: only the fp64 summation order of
+ * the chunk partials changes. */
+int fsagg_pairgram_set_chunks(int chunks);
 int fsagg_pairgram_rows_segsq_f32(const fsagg_rows *rows,
                                   const int64_t *seg_lo,
                                   const int64_t *seg_end, int64_t numel,
@@ -657,6 +662,24 @@ int fsagg_normbound_prescale_f32(const double *sq, int n, int nseg,
  *                    with fsagg_peer_status_free.
  */
 #define FSAGG_MAX_PEERS 8
+
+/* fsagg_weighted_sum_f32 / _bcast_f32 with the tables on the HOST: `rows`
+ * (n device addresses, 16-byte aligned), `weights` and `prescale` (NULL:
+ * none) are host arrays of n <= FSAGG_HOSTTAB_MAX_CLIENTS entries, copied
+ * into the launch's kernel arguments — nothing is uploaded before the
+ * launch.  `outs`: host array of `nout` (1..FSAGG_MAX_PEERS) output
+ * addresses (this GPU's first, then peers' imported copies), each receiving
+ * the same numel results.  Same arithmetic, bit for bit.  Replaces the
+ * per-call table uploads of ClientsAvgAggregator.aggregate() on a flat row
+ * set (clients_avg_aggregator.py:60-100 over fresh uploads,
+ * core/parallel/parallel_runner.py:290-293). */
+#define FSAGG_HOSTTAB_MAX_CLIENTS 128
+int fsagg_weighted_sum_hosttab_f32(const uint64_t *rows,
+                                   const float *weights,
+                                   const float *prescale, int n,
+                                   int64_t numel, const float *base,
+                                   float *const *outs, int nout,
+                                   fsagg_stream_t stream);
 size_t fsagg_peer_handle_bytes(void);
 int fsagg_peer_alloc(int device, size_t bytes, void **ptr);
 int fsagg_peer_free(int device, void *ptr);

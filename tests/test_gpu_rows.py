@@ -348,3 +348,65 @@ def test_uniform_row_sets_take_the_flat_kernel():
     for d in mixed:
         d['d'] = d['d'].clone()
     assert not agg._staged_rows([(1, d) for d in mixed]).rs.uniform
+
+
+@pytest.mark.parametrize('n', [1, 7, 100, 128, 129])
+def test_hosttab_weighted_sum(n):
+    """The flat weighted sum with its row table, weights and prescales in
+    the kernel arguments (fsagg_weighted_sum_hosttab_f32: up to 128 rows,
+    host lists; 129 rows take the device-table kernel) equals the
+    device-table kernel bit for bit — plain, with prescale and base, with
+    several outputs (the peer-assembly epilogue) and over a sub-range
+    (a rank's piece) with a ragged tail — and the oracle."""
+    from federatedscope_amd import _lib as L
+    from federatedscope_amd import ops
+    P = 1_000_003
+    slab = torch.empty((n, P + 61), dtype=torch.float32, device='cuda')
+    ops.fill_uniform(slab, P + 61, seed=n)
+    rows_dev = ops.RowTable.from_slab(slab, numel=P)
+    from federatedscope_amd.layout import BucketLayout
+    lay = BucketLayout(OrderedDict([('w', torch.empty(P, device='meta'))]))
+    ptrs = np.array([[slab[i].data_ptr()] for i in range(n)], dtype=np.int64)
+    rs = ops.RowSet.from_pointers(lay, ptrs, 'cuda', keepalive=(slab, ))
+    rng = np.random.default_rng(n)
+    w = [float(x) for x in rng.random(n) / n]
+    pre = [float(x) for x in rng.random(n) + 0.5]
+    base = torch.randn(ops.round_up(P, 64), device='cuda')
+    for kw in ({}, {'prescale': pre}, {'prescale': pre, 'base': True}):
+        b = ops.BaseRows.from_bucket(base) if kw.get('base') else None
+        got = torch.full((ops.round_up(P, 64), ), 7.0, device='cuda')
+        ops.weighted_sum_rows(rs, w, got, prescale=kw.get('prescale'),
+                              base=b)
+        want = torch.empty_like(got)
+        ops.weighted_sum(rows_dev, w, want, prescale=kw.get('prescale'),
+                         base=base if b is not None else None)
+        assert torch.equal(got[:P], want[:P]), (n, kw)
+        # a sub-range (a rank's piece), with peers' copies
+        lo, hi = 64 * 1001, P
+        o1 = torch.full_like(got, 3.0)
+        o2 = torch.full_like(got, 5.0)
+        assert ops.weighted_sum_rows_bcast(
+            rs, w, o1, [o2.data_ptr()], prescale=kw.get('prescale'), base=b,
+            lo=lo, hi=hi)
+        assert torch.equal(o1[lo:hi], want[lo:hi])
+        assert torch.equal(o2[lo:hi], want[lo:hi])
+        assert bool((o1[:lo] == 3.0).all()) and bool((o2[:lo] == 5.0).all())
+    # the oracle on the first columns
+    x = slab[:, :4096].cpu().numpy()
+    ref = O.para_weighted_avg([(1, {'w': x[i]}) for i in range(n)],
+                              weights=w)['w']
+    got = torch.empty(ops.round_up(P, 64), device='cuda')
+    ops.weighted_sum_rows(rs, w, got)
+    assert got[:4096].cpu().numpy().tobytes() == ref.tobytes()
+    if n > L.FSAGG_HOSTTAB_MAX_CLIENTS:
+        arr = (ctypes_p() * 1)(got.data_ptr())
+        tab = np.array([slab[i].data_ptr() for i in range(n)], np.uint64)
+        wf = np.asarray(w, np.float32)
+        assert L.load().fsagg_weighted_sum_hosttab_f32(
+            tab.ctypes.data, wf.ctypes.data, None, n, P, None, arr, 1,
+            None) != 0
+
+
+def ctypes_p():
+    import ctypes
+    return ctypes.c_void_p
