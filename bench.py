@@ -309,7 +309,7 @@ def c2_leg(dev, rounds=5, calls=20):
     agg = ClientsAvgAggregator(device=dev, config=cfg)
     info = {'client_feedback': clients, 'recover_fun': None}
     st = agg._staged(clients)
-    rs = st.rows()
+    rs = st.rows().persist()      # kept across the calls below
     w_dev = torch.tensor(w, dtype=torch.float32, device=dev)
     out = torch.empty(rs.layout.numel, dtype=torch.float32, device=dev)
     res = [None]

@@ -150,7 +150,7 @@ SIGNATURES['fsagg_normbound_prescale_f32'] = (
     _c_i, [_c_p, _c_i, _c_i, ctypes.c_float, _c_p, _c_p])
 
 FSAGG_MAX_PEERS = 8
-FSAGG_PAIRGRAM_MAX_CLIENTS = 208
+FSAGG_PAIRGRAM_MAX_CLIENTS = 256
 _c_u32 = ctypes.c_uint32
 SIGNATURES['fsagg_peer_handle_bytes'] = (_c_sz, [])
 SIGNATURES['fsagg_peer_alloc'] = (_c_i, [_c_i, _c_sz, ctypes.POINTER(_c_p)])
@@ -167,6 +167,9 @@ SIGNATURES['fsagg_weighted_sum_bcast_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i, _c_i64, _c_p, ctypes.POINTER(_c_p), _c_i,
            _c_p])
 FSAGG_HOSTTAB_MAX_CLIENTS = 128
+SIGNATURES['fsagg_upload_h2d'] = (
+    _c_i, [_c_p, _c_p, _c_sz, _c_p, _c_i, _c_i, _c_p, _c_p])
+SIGNATURES['fsagg_upload_wait'] = (_c_i, [_c_i, _c_p])
 SIGNATURES['fsagg_weighted_sum_hosttab_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i, _c_i64, _c_p, ctypes.POINTER(_c_p), _c_i,
            _c_p])

@@ -227,13 +227,13 @@ class DeviceEngine:
 
     def _pairdist(self, st):
         """Krum's distance matrix D (fp32 [n][n]) of a client set, as a
-        pending result whose ``.cpu()`` waits for it.  Up to 208 clients: on
+        pending result whose ``.cpu()`` waits for it.  Up to 256 clients: on
         the matrix cores (fsagg_pairgram_*: the Gram of the rows centred on a
         central client, fp32 split exactly into bf16 limbs), every pair with
         a worst-case bound on its error (``last_pair_bound``, host fp64
         [n][n]) that the callers certify their selection with
         (:meth:`_certified_order`); non-finite pairs are recomputed on the
-        VALU kernel.  Above 208 clients: the VALU kernel (direct differences,
+        VALU kernel.  Above 256 clients: the VALU kernel (direct differences,
         ``last_pair_bound`` None)."""
         from ... import _lib
         self._pair_info = None
@@ -440,7 +440,8 @@ class DeviceEngine:
                     not ops.absent(layout, kt[0]).any():
                 return ops.BaseRows.from_pointers(layout, kt[0][0],
                                                   self.compute_device,
-                                                  keepalive=(model, ))
+                                                  keepalive=(model, ),
+                                                  ephemeral=True)
         return ops.BaseRows.from_bucket(self._bucket(layout, model,
                                                      as_float=as_float))
 
@@ -530,8 +531,8 @@ class DeviceEngine:
         rst.load_many(dicts)
         present = st.slots          # the presence matrix (see below)
         pieces = [(j, lo, hi, ops.RowSet.from_stack(
-            rst, range(len(dicts)), present=present, offset=rst.offset(j)))
-            for j, (lo, hi) in enumerate(spans)]
+            rst, range(len(dicts)), present=present, offset=rst.offset(j),
+            ephemeral=True)) for j, (lo, hi) in enumerate(spans)]
         return StagedSet(st.layout, pieces=pieces, plan=plan)
 
     def _staged_rows(self, models, as_float=False, require_all=False,
@@ -564,7 +565,7 @@ class DeviceEngine:
                             raise KeyError('client %d lacks keys' % i)
                 slots = [d.slot for d in dicts]
                 return StagedSet(ing.layout, ops.RowSet.from_stack(
-                    ing.stack, slots), ing.stack, slots)
+                    ing.stack, slots, ephemeral=True), ing.stack, slots)
         # device-resident fp32 dicts: read in place through a key table
         d0 = dicts[0]
         fk = (tuple(d0.keys()), bool(as_float))
@@ -586,7 +587,7 @@ class DeviceEngine:
                     gone = int(absent.sum())
                 return StagedSet(layout, ops.RowSet.from_virtual(
                     layout, virt, self.compute_device, keepalive=(dicts, ),
-                    missing=gone, uniform=uniform))
+                    missing=gone, uniform=uniform, ephemeral=True))
         # staged through a device stack
         layout = self._layout(d0, as_float=as_float)
         present = [[k in d for k in layout.keys] for d in dicts]
@@ -601,7 +602,8 @@ class DeviceEngine:
         stack = self._stack(layout, dicts, as_float=as_float)
         slots = list(range(len(dicts)))
         return StagedSet(layout, ops.RowSet.from_stack(stack, slots,
-                                                       present=present),
+                                                       present=present,
+                                                       ephemeral=True),
                          stack, slots)
 
     def _stage_all(self, models, as_float=True):

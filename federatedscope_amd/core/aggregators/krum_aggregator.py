@@ -4,13 +4,13 @@ Device path: the client updates are read where they lie (a row set: the
 clients' own device tensors, or their staged stack rows).  The n×n distance
 matrix (the per-key L2 distances summed over keys, +inf diagonal, :58-73):
 
-* up to 208 clients on the matrix cores (fsagg_pairgram_rows_f32: the Gram of
+* up to 256 clients on the matrix cores (fsagg_pairgram_rows_f32: the Gram of
   the rows centred on a central client, fp32 split exactly into three bf16
   limbs, fp64 accumulation), with a worst-case error bound per pair — the
   selection below is certified against those bounds, and recomputed from
   the VALU kernel's matrix when the score gaps do not clear them
   (_engine._certified_order, DESIGN §3.3);
-* above 208 clients on the VALU kernel (fsagg_pairdist_rows_segsq_f32 +
+* above 256 clients on the VALU kernel (fsagg_pairdist_rows_segsq_f32 +
   fsagg_pairdist_finish_f64: direct differences).
 
 The matrix (≤ 200² floats) comes back to the host where the score/sort/select

@@ -57,7 +57,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int kGramMaxTiles = 13;         // n <= 208
+constexpr int kGramMaxTiles = 16;         // n <= 256
+constexpr int kPlaneTiles = 13;           // PG(2, 3): the lines' limit
 constexpr int kFullTiles = 4;             // one workgroup forms every pair
 constexpr int kKStep = 32;                // coordinates per MFMA k-step
 constexpr int kWaves = 4;                 // waves per workgroup (chunk)
@@ -1003,16 +1004,24 @@ struct B8Cfg {
   static constexpr int kMaxPairs = NT == 8 ? 5 : 6;
 };
 // global tile of local tile lt, per block type (0: the one block of T <= 8;
-// 1-4: the four blocks of 9 <= T <= 13); -1 = none
-__constant__ int8_t kB8Tiles[5][8] = {
+// 1-4: the four blocks of 9 <= T <= 13; 5-10: the six blocks of
+// 14 <= T <= 16 — the tile groups A = 0-3, B = 4-7, C = 8-11, D = 12-15 as
+// A∪B and C∪D, every pair inside each, then A∪C, A∪D, B∪C, B∪D, the
+// cross pairs only: 36 + 36 + 4 · 16 = 136 pairs, each once); -1 = none
+__constant__ int8_t kB8Tiles[11][8] = {
     {0, 1, 2, 3, 4, 5, 6, 7},   {0, 1, 2, 3, 4, 5, 6, 7},
     {5, 6, 7, 8, 9, 10, 11, 12}, {0, 1, 2, 3, 4, 8, 9, 10},
-    {0, 1, 2, 3, 4, 11, 12, -1}};
-// wave w's local tile pairs lo·8 + hi (lo <= hi), -1 none; types 0 and 1:
-// every pair of 8 tiles, (w, w + d mod 8) for d <= 3 and (w, w + 4) for
-// w < 4; type 2: without the pairs inside tiles 0-2 (block 1 holds them);
-// types 3, 4: tiles 0-4 against 5-7 / 5-6
-__constant__ int8_t kB8Pairs[5][8][5] = {
+    {0, 1, 2, 3, 4, 11, 12, -1},
+    {0, 1, 2, 3, 4, 5, 6, 7},     {8, 9, 10, 11, 12, 13, 14, 15},
+    {0, 1, 2, 3, 8, 9, 10, 11},   {0, 1, 2, 3, 12, 13, 14, 15},
+    {4, 5, 6, 7, 8, 9, 10, 11},   {4, 5, 6, 7, 12, 13, 14, 15}};
+// wave w's local tile pairs lo·8 + hi (lo <= hi), -1 none; types 0, 1, 5
+// and 6: every pair of 8 tiles, (w, w + d mod 8) for d <= 3 and (w, w + 4)
+// for w < 4; type 2: without the pairs inside tiles 0-2 (block 1 holds
+// them); types 3, 4: tiles 0-4 against 5-7 / 5-6; types 7-10: local tiles
+// 0-3 against 4-7, wave w the pairs of tile w & 3 with 4 + 2(w >> 2) and
+// the next (one first operand per wave)
+__constant__ int8_t kB8Pairs[11][8][5] = {
     {{0, 1, 2, 3, 4}, {9, 10, 11, 12, 13}, {18, 19, 20, 21, 22},
      {27, 28, 29, 30, 31}, {36, 37, 38, 39, -1}, {45, 46, 47, 5, -1},
      {54, 55, 6, 14, -1}, {63, 7, 15, 23, -1}},
@@ -1027,7 +1036,19 @@ __constant__ int8_t kB8Pairs[5][8][5] = {
      {-1, -1, -1, -1, -1}, {-1, -1, -1, -1, -1}},
     {{5, 6, -1, -1, -1}, {13, 14, -1, -1, -1}, {21, 22, -1, -1, -1},
      {29, 30, -1, -1, -1}, {37, 38, -1, -1, -1}, {-1, -1, -1, -1, -1},
-     {-1, -1, -1, -1, -1}, {-1, -1, -1, -1, -1}}};
+     {-1, -1, -1, -1, -1}, {-1, -1, -1, -1, -1}},
+#define FSAGG_B8_ALL                                                       \
+  {{0, 1, 2, 3, 4}, {9, 10, 11, 12, 13}, {18, 19, 20, 21, 22},              \
+   {27, 28, 29, 30, 31}, {36, 37, 38, 39, -1}, {45, 46, 47, 5, -1},         \
+   {54, 55, 6, 14, -1}, {63, 7, 15, 23, -1}}
+#define FSAGG_B8_CROSS                                                     \
+  {{4, 5, -1, -1, -1}, {12, 13, -1, -1, -1}, {20, 21, -1, -1, -1},          \
+   {28, 29, -1, -1, -1}, {6, 7, -1, -1, -1}, {14, 15, -1, -1, -1},          \
+   {22, 23, -1, -1, -1}, {30, 31, -1, -1, -1}}
+    FSAGG_B8_ALL, FSAGG_B8_ALL, FSAGG_B8_CROSS, FSAGG_B8_CROSS,
+    FSAGG_B8_CROSS, FSAGG_B8_CROSS};
+#undef FSAGG_B8_ALL
+#undef FSAGG_B8_CROSS
 // 13 tiles on 16 waves: wave w's pairs t·16 + u (t <= u), -1 none — wave
 // w < 13 its own tile against (w + d mod 13), d = 0 … 5; the seventh of
 // each (d = 6) and the rest spread over waves 13-15 (91 pairs, <= 6 each)
@@ -1111,7 +1132,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void gram_block8_kernel(
   // XCD together and read its rows from that L2 after the first
   const int kq = int(blockIdx.x >> 3);
   const int chunk = (kq / NB) * 8 + int(blockIdx.x & 7);
-  const int type = NB == 1 ? 0 : 1 + kq % NB;
+  const int type = NB == 1 ? 0 : (NB == 6 ? 5 : 1) + kq % NB;
   if (chunk >= prefix[nseg]) return;  // whole workgroup
   int s = 0;
   while (prefix[s + 1] <= chunk) ++s;
@@ -1352,10 +1373,13 @@ GramPlan gram_plan(int n, int64_t numel, int nseg) {
   // 2.57 against 3.21 ms); the four 8-tile workgroups of the A/B setting 2
   // measured slower (3.8 ms at n = 200)
   const int b8 = g_block8.load(std::memory_order_relaxed);
-  pl.block8 = pl.lines && b8 != 0;
+  // T > 13: the six 8-tile workgroups whatever the setting (the plane lines
+  // and the 13-tile workgroup stop at 13)
+  pl.block8 = pl.lines && (b8 != 0 || pl.nt > kPlaneTiles);
   // 9 <= T <= 13: one 16-wave workgroup with all 13 tiles (setting 1), or
   // the four 8-tile workgroups (setting 2)
-  pl.wide = pl.block8 && pl.nt > kB8Waves && (b8 == 1 || b8 == 3);
+  pl.wide = pl.block8 && pl.nt > kB8Waves && pl.nt <= kPlaneTiles &&
+            (b8 == 1 || b8 == 3);
   // up to kOneMaxTiles (setting 3: 8) tiles the n <= 64 kernel's form: one
   // 4-wave workgroup per chunk, each wave splitting every tile of its own
   // k-steps and forming every pair from registers (up to 256 VGPRs + AGPRs,
@@ -1366,7 +1390,9 @@ GramPlan gram_plan(int n, int64_t numel, int nseg) {
       pl.nt <= (b8 == 3 ? kB8Waves : kOneMaxTiles))
     pl.lines = pl.block8 = pl.wide = false;
   pl.nlines = !pl.lines ? 1
-              : pl.block8 ? (pl.nt <= kB8Waves || pl.wide ? 1 : 4)
+              : pl.block8 ? (pl.nt <= kB8Waves || pl.wide
+                                 ? 1
+                                 : (pl.nt <= kPlaneTiles ? 4 : 6))
                           : (pl.nt <= 7 ? 7 : 13);
   pl.ntpg = ntp_of(pl.nt);
   // ~kMainChunks workgroups; LINES: ~kLineBlocks over all the lines

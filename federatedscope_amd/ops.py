@@ -18,43 +18,49 @@ ALIGN_BYTES = 16
 class _PinnedRing:
     """Reusable pinned staging for the small host tables every call uploads
     (row pointers, weights, chunk lists): NSLOT slots of SLOT bytes, used
-    round robin; a slot is refilled only after the copy that last read it
-    has run (its event).  torch's pin_memory() per table cost ~10-20 µs of
-    host time per upload in the drop-in path, and a fresh pinned allocation
-    waits for the device: with 64-KiB slots the 129-KB key table of 100
-    clients x 161 keys (the ResNet-50 layout) took that path, and every
-    aggregate() then waited for the previous call's kernel before launching
-    its own (a 33 µs gap between back-to-back calls, profiles/r04).  Slots
-    of 1 MiB hold the key table of up to ~800 clients of that layout."""
+    round robin, each backed by a slot of a device ring.  An upload is ONE
+    native call (fsagg_upload_h2d): the bytes go into the pinned slot, a
+    side stream copies them into the device slot and the caller's stream
+    waits for that copy — the copy never sits behind the previous call's
+    kernel on the caller's stream, and the host spends a few microseconds
+    where the torch-level sequence (stream switch, allocation, copy, event)
+    cost ~33 (profiles/r06/upload_cost.json).  A device slot is rewritten
+    only after the consumer work enqueued within NSLOT/2 uploads of its
+    previous use (the library's per-slot events).  Slots of 1 MiB hold the
+    key table of up to ~800 clients of the ResNet-50 layout."""
     SLOT = 1 << 20
-    NSLOT = 32
+    NSLOT = 64
     # Content-addressed cache of the uploaded tables (the kernels only read
     # them): a table whose bytes were uploaded before is handed out again
     # without a copy.  Row tables hold the clients' tensor addresses, which
     # stay the same from call to call whenever the clients' tensors do (the
     # standalone simulator's persistent client models, a server's stack
     # slots, and every repeated aggregate() over the same dicts); weights,
-    # chunk lists and selections repeat likewise.  Entries are immutable
-    # device tensors; each is marked used (record_stream) by every stream
-    # it is handed to, so the caching allocator recycles an evicted entry's
-    # block only after the work that read it.  A stream an entry was not
-    # uploaded for first waits for the entry's copy (its slot's event: the
-    # copies all run in order on one side stream, so that event — even
-    # re-recorded by a later upload into the slot — completes only after
-    # this entry's copy).  The cache is bounded by bytes (host keys plus
-    # device tables), not only by entries: tables that change every call
-    # (fresh client tensors) then cycle through a fixed footprint.
+    # chunk lists and selections repeat likewise.  A table enters the cache
+    # on its SECOND sighting (a persistent device tensor of its own); the
+    # first goes through the ring, so tables that never repeat (fresh
+    # upload tensors every round) cost one native copy and nothing else.
+    # Entries are immutable device tensors; each is marked used
+    # (record_stream) by every stream it is handed to, so the caching
+    # allocator recycles an evicted entry's block only after the work that
+    # read it, and a stream an entry was not uploaded for first waits for
+    # the entry's copy (fsagg_upload_wait on its slot: every copy runs in
+    # order on one side stream, so the slot's latest copy completes after
+    # the entry's).  The cache is bounded by bytes (host keys plus device
+    # tables), not only by entries.
     CACHE_MAX_BYTES = 1 << 20      # = SLOT: the ResNet-50 key table fits
     CACHE_ENTRIES = 512
     CACHE_TOTAL_BYTES = 32 << 20
+    SEEN_ENTRIES = 1024
 
     def __init__(self):
         from collections import OrderedDict
         self.buf = None
-        self.events = [None] * self.NSLOT
         self.i = 0
         self.streams = {}
+        self.rings = {}
         self.cache = OrderedDict()
+        self.seen = OrderedDict()
         self.cache_bytes = 0
         self.cache_on = True
         self.hits = 0
@@ -66,19 +72,19 @@ class _PinnedRing:
         if hit is None:
             return None
         self.cache.move_to_end(key)
-        t, seen, ev = hit
+        t, seen, slot = hit
         s = torch._C._cuda_getCurrentRawStream(device.index)
         if s not in seen:
-            cur = torch.cuda.current_stream(device)
-            cur.wait_event(ev)
-            t.record_stream(cur)
+            L.check(L.load().fsagg_upload_wait(slot, ctypes_ptr(s)),
+                    'fsagg_upload_wait')
+            t.record_stream(torch.cuda.current_stream(device))
             seen.add(s)
         self.hits += 1
         return t
 
-    def _insert(self, key, t, ev, device):
+    def _insert(self, key, t, slot, device):
         self.cache[key] = (t, {torch._C._cuda_getCurrentRawStream(
-            device.index)}, ev)
+            device.index)}, slot)
         self.cache_bytes += 2 * len(key[3])
         while len(self.cache) > self.CACHE_ENTRIES or \
                 self.cache_bytes > self.CACHE_TOTAL_BYTES:
@@ -87,6 +93,7 @@ class _PinnedRing:
 
     def clear(self):
         self.cache.clear()
+        self.seen.clear()
         self.cache_bytes = 0
 
     def _copy_stream(self, device):
@@ -95,17 +102,13 @@ class _PinnedRing:
             s = self.streams[device.index] = torch.cuda.Stream(device=device)
         return s
 
-    def upload(self, arr, device):
-        """numpy array -> device tensor of its dtype and shape (async).
-
-        The copy runs on a side stream of the device and the caller's
-        stream waits for it: enqueued on the caller's stream, a table's
-        copy sat behind the previous call's kernel and held back the next
-        launch by its own latency (~34 µs between back-to-back aggregate()
-        calls at the ResNet-50 layout).  The device tensor is allocated on
-        the side stream and marked used by the caller's stream, so the
-        allocator never hands its block to a copy while a kernel may still
-        read it."""
+    def upload(self, arr, device, ephemeral=False):
+        """numpy array -> device tensor of its dtype and shape (async, see
+        the class docstring).  ``ephemeral``: the caller launches the
+        kernels that read it before NSLOT/2 further uploads and keeps no
+        reference beyond that (per-call tables) — it may then come from the
+        device ring (a view that later uploads overwrite) unless it is
+        cached; otherwise it is a device tensor of its own."""
         import numpy as np
         if device.index is None:
             device = torch.device('cuda', torch.cuda.current_device())
@@ -119,42 +122,49 @@ class _PinnedRing:
             if t is not None:
                 return t
             self.misses += 1
-        t, ev = self._upload(arr, raw, nb, device)
+            if ephemeral:
+                if key in self.seen:
+                    del self.seen[key]
+                else:
+                    self.seen[key] = None
+                    while len(self.seen) > self.SEEN_ENTRIES:
+                        self.seen.popitem(last=False)
+                    key = None       # first sighting: the ring
         self.uploads += 1
-        if key is not None and ev is not None:
-            self._insert(key, t, ev, device)
-        return t
-
-    def _upload(self, arr, raw, nb, device):
-        """(device tensor, the event its copy completes by — None for the
-        unpooled path, whose tables are never cached)."""
-        import numpy as np
-        if nb == 0 or nb > self.SLOT:
+        if nb == 0 or nb > self.SLOT or \
+                device.index != torch.cuda.current_device():
             host = torch.from_numpy(raw.copy())
             return host.pin_memory().to(device, non_blocking=True).view(
-                _TORCH_OF[arr.dtype.str]).reshape(arr.shape), None
+                _TORCH_OF[arr.dtype.str]).reshape(arr.shape)
         if self.buf is None:
             self.buf = torch.empty(self.SLOT * self.NSLOT, dtype=torch.uint8,
                                    pin_memory=True)
-            self.np = self.buf.numpy()
+            self.buf_ptr = self.buf.data_ptr()
         k = self.i
         self.i = (k + 1) % self.NSLOT
-        ev = self.events[k]
-        if ev is not None:
-            ev.synchronize()            # the copy that last read slot k
         lo = k * self.SLOT
-        self.np[lo:lo + nb] = raw
-        if ev is None:
-            ev = self.events[k] = torch.cuda.Event()
-        cur = torch.cuda.current_stream(device)
         side = self._copy_stream(device)
-        with torch.cuda.stream(side):
-            dev = torch.empty(nb, dtype=torch.uint8, device=device)
-            dev.copy_(self.buf[lo:lo + nb], non_blocking=True)
-            ev.record(side)
-        dev.record_stream(cur)
-        cur.wait_event(ev)
-        return dev.view(_TORCH_OF[arr.dtype.str]).reshape(arr.shape), ev
+        if key is None and ephemeral:
+            ring = self.rings.get(device.index)
+            if ring is None:
+                ring = self.rings[device.index] = torch.empty(
+                    self.SLOT * self.NSLOT, dtype=torch.uint8, device=device)
+            dst = ring[lo:lo + nb]
+        else:
+            # a persistent entry: allocated from the copy stream's pool and
+            # marked used by the caller's stream
+            with torch.cuda.stream(side):
+                dst = torch.empty(nb, dtype=torch.uint8, device=device)
+            dst.record_stream(torch.cuda.current_stream(device))
+        L.check(L.load().fsagg_upload_h2d(
+            dst.data_ptr(), raw.ctypes.data, nb, self.buf_ptr + lo, k,
+            self.NSLOT, ctypes_ptr(side.cuda_stream),
+            ctypes_ptr(torch._C._cuda_getCurrentRawStream(device.index))),
+            'fsagg_upload_h2d')
+        t = dst.view(_TORCH_OF[arr.dtype.str]).reshape(arr.shape)
+        if key is not None:
+            self._insert(key, t, k, device)
+        return t
 
 
 _TORCH_OF = {'<i8': torch.int64, '<i4': torch.int32, '<i2': torch.int16,
@@ -164,10 +174,10 @@ _NP_OF = {}
 _RING = _PinnedRing()
 
 
-def _h2d(values, dtype, device):
+def _h2d(values, dtype, device, ephemeral=False):
     """A small host table (row pointers, weights, offsets) on ``device``:
-    staged through pinned memory and copied asynchronously on the current
-    stream, so a call never blocks the host on the GPU's queue."""
+    staged through pinned memory and copied asynchronously, so a call never
+    blocks the host on the GPU's queue (``ephemeral``: _PinnedRing.upload)."""
     import numpy as np
     device = torch.device(device)
     if device.type != 'cuda':
@@ -175,7 +185,8 @@ def _h2d(values, dtype, device):
     npt = _NP_OF.get(dtype)
     if npt is None:
         npt = _NP_OF[dtype] = torch.empty(0, dtype=dtype).numpy().dtype
-    return _RING.upload(np.asarray(values, dtype=npt), device)
+    return _RING.upload(np.asarray(values, dtype=npt), device,
+                        ephemeral=ephemeral)
 
 
 def _h2d_bytes(arr, device):
@@ -185,11 +196,11 @@ def _h2d_bytes(arr, device):
                         torch.device(device))
 
 
-def _h2d_np(arr, device):
+def _h2d_np(arr, device, ephemeral=False):
     """A numpy array as a flat device tensor of its dtype (pinned, async)."""
     import numpy as np
     return _RING.upload(np.ascontiguousarray(arr).reshape(-1),
-                        torch.device(device))
+                        torch.device(device), ephemeral=ephemeral)
 
 
 def _stream(device):
@@ -285,7 +296,9 @@ class RowTable:
 
 
 def _fp32_dev(values, device):
-    return _h2d([float(v) for v in values], torch.float32, device)
+    """Per-call weights / prescales (read by the launch that follows)."""
+    return _h2d([float(v) for v in values], torch.float32, device,
+                ephemeral=True)
 
 
 def _check_out(out, numel, device, what='out', align=ALIGN_BYTES):
@@ -829,7 +842,7 @@ class RowSet:
     copy ([n][1] for a stack without absent keys, else [n][nseg])."""
 
     def __init__(self, layout, table, device, keepalive=(), aligned16=True,
-                 missing=None, segmajor=None, uniform=False):
+                 missing=None, segmajor=None, uniform=False, ephemeral=False):
         if segmajor is not None:
             # the device layout built by the caller ([nseg][n]); the host
             # copy is its transposed view
@@ -863,6 +876,10 @@ class RowSet:
         self._segmajor = segmajor
         self._tab = None
         self._struct = None
+        # a per-call row set (the engine's): its device table may come from
+        # the upload ring (see _PinnedRing.upload); persist() before keeping
+        # it beyond the call
+        self.ephemeral = bool(ephemeral)
         self._keep = tuple(keepalive)
         # uniform: every client's keys lie in ONE storage at their bucket
         # offsets (csrc/host/keytable.cpp), so client i's bucket is the
@@ -871,7 +888,8 @@ class RowSet:
             self.host.shape[1] == self.nseg
 
     @classmethod
-    def from_stack(cls, stack, slots, present=None, offset=0):
+    def from_stack(cls, stack, slots, present=None, offset=0,
+                   ephemeral=False):
         """Rows ``slots`` of a ClientStack; ``present`` (bool [n][nseg])
         marks absent keys (NULL entries).  Bucket coordinate p is at row
         element p + ``offset`` (a range stack holds a piece of the bucket)."""
@@ -884,7 +902,7 @@ class RowSet:
             tab = _np.where(_np.asarray(present, bool), tab, 0)
         return cls(stack.layout, tab, stack.device, keepalive=(stack.slab, ),
                    aligned16=ld % ALIGN_BYTES == 0 and
-                   base % ALIGN_BYTES == 0)
+                   base % ALIGN_BYTES == 0, ephemeral=ephemeral)
 
     @classmethod
     def from_pointers(cls, layout, ptrs, device, keepalive=(),
@@ -903,22 +921,32 @@ class RowSet:
 
     @classmethod
     def from_virtual(cls, layout, segmajor, device, keepalive=(),
-                     aligned16=True, missing=None, uniform=False):
+                     aligned16=True, missing=None, uniform=False,
+                     ephemeral=False):
         """[nseg][n] virtual bases (0: absent), i.e. the device table as
         csrc/host/keytable.cpp builds it with offsets (``uniform``: its
         report that each client's keys are views of one storage at their
         bucket offsets)."""
         return cls(layout, None, device, keepalive=keepalive,
                    aligned16=aligned16, missing=missing, segmajor=segmajor,
-                   uniform=uniform)
+                   uniform=uniform, ephemeral=ephemeral)
 
     @property
     def tab(self):
         """The device table ([nseg][n], or [1][n] for ss = 0)."""
         if self._tab is None:
             self._tab = _h2d_np(self.host.T if self._segmajor is None
-                                else self._segmajor, self.device)
+                                else self._segmajor, self.device,
+                                ephemeral=self.ephemeral)
         return self._tab
+
+    def persist(self):
+        """Give the row set a device table of its own (for holders beyond
+        the call, e.g. a captured launch chain)."""
+        if self.ephemeral:
+            self.ephemeral = False
+            self._tab = self._struct = None
+        return self
 
     @property
     def struct(self):
@@ -937,7 +965,7 @@ class RowSet:
         return RowSet(self.layout, self.host[idx], self.device,
                       keepalive=self._keep, aligned16=self.aligned16,
                       missing=0 if self.missing == 0 else None,
-                      uniform=self.uniform)
+                      uniform=self.uniform, ephemeral=self.ephemeral)
 
     def ptr(self):
         return ctypes.byref(self.struct)
@@ -961,13 +989,14 @@ class BaseRows:
                    keepalive=(flat, ), host=[flat.data_ptr()])
 
     @classmethod
-    def from_pointers(cls, layout, ptrs, device, keepalive=()):
+    def from_pointers(cls, layout, ptrs, device, keepalive=(),
+                      ephemeral=False):
         ptrs = _np.asarray(ptrs, dtype=_np.int64).reshape(-1)
         offs = _np.array([layout.offsets[k] for k in layout.keys],
                          dtype=_np.int64)
         virt = ptrs - 4 * offs
-        return cls(_h2d_np(virt, _cuda_index(device)), 1,
-                   keepalive=keepalive, host=[int(v) for v in virt])
+        return cls(_h2d_np(virt, _cuda_index(device), ephemeral=ephemeral),
+                   1, keepalive=keepalive, host=[int(v) for v in virt])
 
     def ptr(self):
         return self.tab.data_ptr()
@@ -1073,7 +1102,7 @@ def _weighted_sum_rows_flat(rs, weights, out, prescale, base, lo, hi, lib,
     if a == 0:
         table = rs.tab
     else:
-        table = _h2d_np(rs.host[:, 0] + 4 * a, rs.device)
+        table = _h2d_np(rs.host[:, 0] + 4 * a, rs.device, ephemeral=True)
     w = weights if isinstance(weights, torch.Tensor) else _fp32_dev(
         weights, rs.device)
     pre = None
@@ -1202,7 +1231,7 @@ def pairdist_rows_segsq(rs, lo=0, hi=None, workspace=None, keep=None,
 
 
 def pairgram_rows_segsq(rs, lo=0, hi=None, workspace=None, keep=None):
-    """As :func:`pairdist_rows_segsq`, on the matrix cores (n <= 208,
+    """As :func:`pairdist_rows_segsq`, on the matrix cores (n <= 256,
     fsagg_pairgram_rows_segsq_f32): returns ``[2][nseg][n][n]`` fp64 —
     [0] the per-key squared distances, [1] their predicted absolute error
     bounds (both may be summed over ranks); :func:`pairgram_finish` turns
@@ -1297,48 +1326,33 @@ def pairgram_rows_dist(rs, tol, workspace=None):
 class _GraphCache:
     """Captured launch chains (HIP graphs, through torch.cuda.CUDAGraph) of
     the multi-kernel paths whose launches cost more host time than their
-    small kernels run: the Gram chain is eight launches (~50 µs of host
-    time at C4, against ~10 µs for one graph launch).  An entry is keyed by
-    everything its kernels' arguments hold — the device row table's
-    address (the upload cache hands the same table tensor back for the same
-    rows), the shape, the tolerance, the library's workgroup-form setting
-    (fsagg_pairgram_block8) — and keeps the row table alive, so its address
-    cannot be reused while the graph lives.  Each entry owns only its
-    output buffer (5n² words); the workspace and the per-key sums it
-    replays into are shared by every entry of the same shape and stream
-    (replays on one stream run in order), so the cache holds one
-    workspace per shape however many row tables it has seen.  A chain is
-    captured on the SECOND call with the same key: rows that change every
-    call (fresh upload tensors) run eagerly on the shared workspace and
-    never pay a capture.  The outputs are overwritten by the next replay: a
-    caller consumes them (copies them to the host) before its next call."""
+    small kernels run: the Gram chain is eight launches (~100 µs of host
+    time at C4, against ~10 µs for one graph launch).  One entry per SHAPE
+    — client count, table stride, the layout, the tolerance, the library's
+    workgroup-form settings, the stream — owning everything the captured
+    kernels' arguments name: a device row table, the workspace, the per-key
+    sums and the output buffer.  A call copies ITS row table (the clients'
+    addresses, fresh or not) into the entry's table on its own stream and
+    replays: so rounds of freshly received uploads replay a graph as well as
+    repeated calls over the same dicts do.  The copy is ordered after the
+    previous replay on that stream, which has read the old table; the
+    outputs are overwritten by the next call of the same shape — a caller
+    consumes them (copies them to the host) before its next call.  The
+    first call of a shape runs the chain eagerly (its result) and captures
+    it (the capture only records launches)."""
     MAX_ENTRIES = 8
-    MAX_SEEN = 64
 
     def __init__(self):
         from collections import OrderedDict
         self.entries = OrderedDict()
-        self.seen = OrderedDict()
-        self.scratch = {}
         self.enabled = True
         self.captures = 0
 
     def lookup(self, key):
-        """The entry of ``key``, or None; records the sighting."""
         e = self.entries.get(key)
         if e is not None:
             self.entries.move_to_end(key)
-            return e
-        return None
-
-    def second_sighting(self, key):
-        if key in self.seen:
-            del self.seen[key]
-            return True
-        self.seen[key] = True
-        while len(self.seen) > self.MAX_SEEN:
-            self.seen.popitem(last=False)
-        return False
+        return e
 
     def put(self, key, e):
         self.entries[key] = e
@@ -1347,22 +1361,36 @@ class _GraphCache:
             self.entries.popitem(last=False)
         return e
 
-    def shared(self, key, make):
-        """Scratch shared by the entries of one shape and stream."""
-        s = self.scratch.get(key)
-        if s is None:
-            s = self.scratch[key] = make()
-        return s
-
 
 _GRAPHS = _GraphCache()
 
 
+def _copy_table(host, dst, device):
+    """The row table ``host`` into the device buffer ``dst`` on the current
+    stream (ordered after the work already queued there)."""
+    import numpy as np
+    raw = np.ascontiguousarray(host).reshape(-1).view(np.uint8)
+    if raw.size > _RING.SLOT or raw.size != dst.numel() * dst.element_size():
+        raise ValueError('row table of %d bytes for a %d-byte slot' %
+                         (raw.size, dst.numel() * dst.element_size()))
+    ring = _RING
+    if ring.buf is None:
+        ring.buf = torch.empty(ring.SLOT * ring.NSLOT, dtype=torch.uint8,
+                               pin_memory=True)
+        ring.buf_ptr = ring.buf.data_ptr()
+    k = ring.i
+    ring.i = (k + 1) % ring.NSLOT
+    cur = ctypes_ptr(torch._C._cuda_getCurrentRawStream(device.index))
+    L.check(L.load().fsagg_upload_h2d(
+        dst.data_ptr(), raw.ctypes.data, raw.size,
+        ring.buf_ptr + k * ring.SLOT, k, ring.NSLOT, cur, cur),
+        'fsagg_upload_h2d')
+
+
 def pairgram_rows_dist_graph(rs, tol):
-    """:func:`pairgram_rows_dist` replayed from a captured graph (captured
-    on the second call for these rows and shape, replayed after; the first
-    runs eagerly): returns (buf, D, ill, B, D64) views of a buffer valid
-    until the next call for the same rows."""
+    """:func:`pairgram_rows_dist` replayed from the captured chain of its
+    shape (see _GraphCache): returns (buf, D, ill, B, D64) views of a buffer
+    valid until the next call of the same shape."""
     if not _GRAPHS.enabled:
         return pairgram_rows_dist(rs, tol)[:5]
     _require_all(rs, 'Krum')
@@ -1375,32 +1403,39 @@ def pairgram_rows_dist_graph(rs, tol):
     lib.fsagg_pairgram_set_stages(stages)
     chunks = lib.fsagg_pairgram_set_chunks(0)
     lib.fsagg_pairgram_set_chunks(chunks)
-    key = ('pairgram', rs.device.index, rs.tab.data_ptr(), rs.ss, rs.n,
+    stream = torch._C._cuda_getCurrentRawStream(rs.device.index)
+    host = rs.host.T if rs._segmajor is None else rs._segmajor
+    key = ('pairgram', rs.device.index, stream, host.shape, rs.ss, rs.n,
            rs.nseg, lay.signature(), float(tol), lib.fsagg_pairgram_block8(),
            stages, chunks)
     e = _GRAPHS.lookup(key)
     if e is None:
-        if not _GRAPHS.second_sighting(key):
-            return pairgram_rows_dist(rs, tol)[:5]
-        stream = torch._C._cuda_getCurrentRawStream(rs.device.index)
         need = max(int(lib.fsagg_pairgram_workspace_bytes(
             rs.n, max(lay.numel, 1), rs.nseg)), 1)
-
-        def make():
-            return (torch.empty(need, dtype=torch.uint8, device=rs.device),
-                    torch.empty((2, rs.nseg, rs.n, rs.n),
-                                dtype=torch.float64, device=rs.device))
-        ws, sq2 = _GRAPHS.shared((rs.device.index, stream, need, rs.nseg,
-                                  rs.n), make)
+        ws = torch.empty(need, dtype=torch.uint8, device=rs.device)
+        sq2 = torch.empty((2, rs.nseg, rs.n, rs.n), dtype=torch.float64,
+                          device=rs.device)
         seg_lo, seg_end = lay.seg_bounds(rs.device, 0, lay.numel, None)
         buf = _gram_buf(rs.n, rs.device)[0]
-        # the first sighting ran this chain eagerly: its code objects are
-        # loaded, so the capture records launches only
+        tab = torch.empty(host.size, dtype=torch.int64, device=rs.device)
+        rows = L.Rows(tab.data_ptr(), rs.ss, rs.n, rs.nseg)
+        _copy_table(host, tab, rs.device)
+
+        def launch():
+            L.check(lib.fsagg_pairgram_rows_f32(
+                ctypes.byref(rows), seg_lo.data_ptr(), seg_end.data_ptr(),
+                max(lay.numel, 1), float(tol), sq2[0].data_ptr(),
+                sq2[1].data_ptr(), *[v.data_ptr() for v in gram_views(buf)],
+                ws.data_ptr(), ws.numel(), _stream(rs.device)),
+                'fsagg_pairgram_rows_f32')
+        launch()              # this call's result (and the code objects)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            _pairgram_rows_launch(rs, tol, seg_lo, seg_end, ws, sq2, buf)
-        e = _GRAPHS.put(key, (g, buf, (rs.tab, seg_lo, seg_end)))
-    g, buf, _ = e
+            launch()
+        _GRAPHS.put(key, (g, buf, tab, (rows, ws, sq2, seg_lo, seg_end)))
+        return (buf,) + gram_views(buf)
+    g, buf, tab, _ = e
+    _copy_table(host, tab, rs.device)
     g.replay()
     return (buf,) + gram_views(buf)
 

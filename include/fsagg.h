@@ -478,7 +478,7 @@ int fsagg_pairdist_rows_segsq_f32(const fsagg_rows *rows,
                                   size_t workspace_bytes,
                                   fsagg_stream_t stream);
 
-/* Krum per-key squared distances on the matrix cores (n <= 208; segsq as
+/* Krum per-key squared distances on the matrix cores (n <= 256; segsq as
  * fsagg_pairdist_rows_segsq_f32).  d²(a, b) = G_aa + G_bb − 2·G_ab from a
  * Gram matrix of the rows centred on a central client (the argmin of the
  * summed distances over the first 2048 coordinates of every key), every
@@ -494,13 +494,14 @@ int fsagg_pairdist_rows_segsq_f32(const fsagg_rows *rows,
  * valid.  Replaces the same torch.dist loop (krum_aggregator.py:41-73) as
  * fsagg_pairdist_f32, with fsagg_pairgram_finish_f32 in place of
  * fsagg_pairdist_finish_f64.  The rows stream through LDS in 512-B runs
- * per row (global_load_lds), whatever their placement.  Up to 64 clients
- * one workgroup per chunk forms every 16x16 tile pair; above, the tiles
- * form super tiles of two and one workgroup per chunk and super-tile pair
- * forms the pairs across (XCD-grouped, so a chunk's rows are read from
- * HBM once and from L2 after).  Workspace:
+ * per row (global_load_lds), whatever their placement.  Up to 112 clients
+ * one workgroup per chunk forms every 16x16 tile pair; up to 128 one
+ * 8-tile workgroup, up to 208 one 13-tile workgroup of 16 waves, up to 256
+ * six 8-tile workgroups per chunk (tile groups of 4 paired up, each pair
+ * of tiles formed once; XCD-grouped, so a chunk's rows are read from HBM
+ * once and from L2 after).  Workspace:
  * fsagg_pairgram_workspace_bytes(n, numel, nseg) (0 when n is outside
- * 2..208). */
+ * 2..256). */
 size_t fsagg_pairgram_workspace_bytes(int n, int64_t numel, int nseg);
 /* Tuning hook (no reference counterpart): which workgroups form the Gram
  * passes for n > 64.  1 (default): up to 112 clients one 4-wave workgroup
@@ -674,6 +675,20 @@ int fsagg_normbound_prescale_f32(const double *sq, int n, int nseg,
  * set (clients_avg_aggregator.py:60-100 over fresh uploads,
  * core/parallel/parallel_runner.py:290-293). */
 #define FSAGG_HOSTTAB_MAX_CLIENTS 128
+/* Host plumbing for the small per-call tables (row tables, weights, chunk
+ * lists; no reference counterpart): copy `nbytes` from host `src` into the
+ * caller's pinned staging slot `stage` and from there, on `copy_stream`,
+ * into device `dst` (slot `slot` of an `nslot`-slot device ring, nslot <=
+ * 256); `consumer` waits for the copy.  The pinned slot is refilled only
+ * after its previous copy ran; the device slot is overwritten only after
+ * the consumer work enqueued within nslot/2 uploads of its previous use
+ * (so a consumer must launch within nslot/2 uploads of its table's).  One
+ * call, a few microseconds of host time (a torch-level upload costs ~33).
+ * fsagg_upload_wait: `stream` waits for slot `slot`'s copy. */
+int fsagg_upload_h2d(void *dst, const void *src, size_t nbytes, void *stage,
+                     int slot, int nslot, fsagg_stream_t copy_stream,
+                     fsagg_stream_t consumer);
+int fsagg_upload_wait(int slot, fsagg_stream_t stream);
 int fsagg_weighted_sum_hosttab_f32(const uint64_t *rows,
                                    const float *weights,
                                    const float *prescale, int n,

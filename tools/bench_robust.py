@@ -268,10 +268,13 @@ def dropin_rules(dev, fresh=False):
     device-resident ConvNet2-h2048 dicts (12 keys, 6.6M params): Krum
     (multi-Krum 5) and Bulyan at n = 50, f = 10; FedAvg, median, trimmed
     mean and norm bounding at n = 200.  Wall clock with the GPU synchronised on both
-    sides; the result stays on the device.  ``fresh``: every call gets new
-    dict objects and the upload cache is off, so every call walks, builds
-    and uploads its tables (a server round with freshly received uploads;
-    the Gram chain then runs eagerly, never from a captured graph)."""
+    sides; the result stays on the device.  ``fresh``: every call gets
+    client tensors at addresses no earlier call used — each client key is a
+    view at a new offset into a per-key pool, the way a server round's
+    freshly received uploads are new tensors — so the clients' row tables
+    are new every call (no upload-cache hit, no captured Gram chain to
+    replay), while the server model and the layout's tables stay what they
+    are in a real server (the same every round)."""
     from collections import OrderedDict
     from types import SimpleNamespace
     from federatedscope_amd.core.aggregators import (
@@ -309,8 +312,29 @@ def dropin_rules(dev, fresh=False):
             (k, 1e-2 * torch.randn(s, device=dev, generator=g))
             for k, s in keys)) for i in range(n)]
 
+    # fresh: per client and key a pool of numel + NOFF·64 values; call c of
+    # rule r sees the key at offset 64·(30r + c) (16-B aligned, an address
+    # no earlier call of any rule used)
+    NWARM, NCALLS = 10, 20
+    NOFF = 6 * (NWARM + NCALLS)
+
+    def pools(n):
+        return [[1e-2 * torch.randn(int(np.prod(s)) + 64 * NOFF,
+                                    device=dev, generator=g)
+                 for k, s in keys] for _ in range(n)]
+
+    def fresh_sets(pool, r):
+        first = r * (NWARM + NCALLS)
+        return [[(int(1 + i), OrderedDict(
+            (k, pool[i][j][64 * c:64 * c + int(np.prod(s))].view(s))
+            for j, (k, s) in enumerate(keys))) for i in range(len(pool))]
+            for c in range(first, first + NWARM + NCALLS)]
+
     out = []
-    c50, c200 = clients(50), clients(200)
+    if fresh:
+        c50, c200 = pools(50), pools(200)
+    else:
+        c50, c200 = clients(50), clients(200)
     rules = [
         ('fedavg', 200, ClientsAvgAggregator(model=M(init), device=dev,
                                              config=cfg())),
@@ -327,35 +351,50 @@ def dropin_rules(dev, fresh=False):
                                                      device=dev,
                                                      config=cfg(bound=5.0))),
     ]
-    prev_cache = ops._RING.cache_on
-    if fresh:
-        ops._RING.cache_on = False
-    for name, n, agg in rules:
+    for r, (name, n, agg) in enumerate(rules):
         fb = c50 if n == 50 else c200
-        # fresh: 8 distinct dict lists (new dict objects over the same
-        # tensors), cycled; the tables are rebuilt and uploaded every call
-        infos = [{'client_feedback': [(s, OrderedDict(d)) for s, d in fb]
-                  if fresh else fb, 'recover_fun': None}
-                 for _ in range(8 if fresh else 1)]
+        infos = [{'client_feedback': f, 'recover_fun': None}
+                 for f in (fresh_sets(fb, r) if fresh else [fb])]
         it = [0]
 
         def call():
             agg.aggregate(infos[it[0] % len(infos)])
             it[0] += 1
         torch.cuda.synchronize()
-        w0 = time.perf_counter()
-        while time.perf_counter() - w0 < 0.05:   # clocks up (see timed)
-            call()
-            torch.cuda.synchronize()
+        if fresh:
+            for _ in range(NWARM):       # clocks up, one offset each
+                call()
+                torch.cuda.synchronize()
+        else:
+            w0 = time.perf_counter()
+            while time.perf_counter() - w0 < 0.05:   # clocks up (timed)
+                call()
+                torch.cuda.synchronize()
         ts = []
-        for _ in range(20):
+        for _ in range(NCALLS):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             call()
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         t = statistics.median(ts)
+        same = None
+        if fresh:
+            # the same call repeated on one of those client sets (its tables
+            # cached after the second sighting, the Gram chain replayed): the
+            # kernels' time on exactly this placement, host caches warm
+            for _ in range(3):
+                agg.aggregate(infos[0])
+            tw = []
+            for _ in range(NCALLS):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                agg.aggregate(infos[0])
+                torch.cuda.synchronize()
+                tw.append(time.perf_counter() - t0)
+            same = round(statistics.median(tw) * 1e3, 3)
         out.append({'rule': name, 'clients': n, 'params': P,
+                    'ms_same_rows_repeated': same,
                     'pairdist_path': getattr(agg, 'last_pairdist_path',
                                              None),
                     'ms_aggregate': round(t * 1e3, 3),
@@ -363,10 +402,9 @@ def dropin_rules(dev, fresh=False):
                     'fresh_uploads': bool(fresh),
                     'what': 'aggregate() on device-resident dicts read in '
                             'place (row sets), kernels + init+update' + (
-                                '; new dict objects every call, upload '
-                                'cache off' if fresh else '')})
+                                '; client tensors at new addresses every '
+                                'call (fresh uploads)' if fresh else '')})
         log('%s%s: %.2f ms' % (name, ' (fresh)' if fresh else '', t * 1e3))
-    ops._RING.cache_on = prev_cache
     return out
 
 
@@ -381,7 +419,7 @@ def main():
     if 'krum_large' in which:
         # n > 64: the Gram path on projective-plane lines, C4's layout and byte
         # count per client
-        for n in (100, 200):
+        for n in (100, 200, 256):
             t0 = time.time()
             print(json.dumps(krum_c4(dev, n=n, f=n // 5)), flush=True)
             log('krum n=%d done in %.1fs' % (n, time.time() - t0))

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 6, second full pass: the GPU suite at the final trimmed bounds, the
+# bench line, the drop-in rules warm and with fresh uploads, the Krum host
+# phases, the upload cost, the 8-rank share.
+set -u
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out/r06
+export TMPDIR=/tmp
+export FSAGG_ERR_LOG=$PWD/gpurun_out/r06/trimmed_err_final.jsonl
+bash tools/gpu_job.sh pytestall smoke \
+  "timeout -k 10 400 python bench.py > gpurun_out/r06/bench2.json" \
+  "timeout -k 10 500 python -u tools/bench_robust.py dropin dropin_fresh > gpurun_out/r06/dropin2.jsonl" \
+  "timeout -k 10 300 python tools/time_krum_phases.py > gpurun_out/r06/krum_phases2.txt 2>&1" \
+  "FRESH=1 timeout -k 10 300 python tools/time_krum_phases.py > gpurun_out/r06/krum_phases2_fresh.txt 2>&1" \
+  "timeout -k 10 300 python tools/probe_upload_cost.py > gpurun_out/r06/upload_cost2.json" \
+  "timeout -k 10 300 python tools/bench_share.py --aggregate --world 8 > gpurun_out/r06/share2.jsonl"

@@ -25,14 +25,35 @@ def main():
     g = torch.Generator(device=dev).manual_seed(7)
     init = OrderedDict((k, torch.randn(s, device=dev, generator=g))
                        for k, s in CONVNET2_H2048)
+    fresh = bool(os.environ.get('FRESH'))
+    if fresh:
+        # fresh uploads: every call's clients at new addresses (views at a
+        # new offset into per-key pools), as a server round's new tensors
+        import numpy as np
+        NOFF = 440
+        pools = [[1e-2 * torch.randn(int(np.prod(s)) + 64 * NOFF, device=dev,
+                                     generator=g) for k, s in CONVNET2_H2048]
+                 for _ in range(50)]
+        sets = [[(1 + i, OrderedDict(
+            (k, pools[i][j][64 * c:64 * c + int(np.prod(s))].view(s))
+            for j, (k, s) in enumerate(CONVNET2_H2048))) for i in range(50)]
+            for c in range(NOFF)]
     models = [(1 + i, OrderedDict(
         (k, 1e-2 * torch.randn(s, device=dev, generator=g))
         for k, s in CONVNET2_H2048)) for i in range(50)]
+    nxt = [0]
+
+    def next_models():
+        if not fresh:
+            return models
+        nxt[0] += 1
+        return sets[nxt[0] - 1]
     agg = KrumAggregator(model=M(init), device=dev,
                          config=cfg(f=10, agg_num=5))
     marks = defaultdict(list)
 
     def one():
+        models = next_models()
         t0 = time.perf_counter()
         m = lambda k: marks[k].append((time.perf_counter() - t0) * 1e6)
         st = agg._stage_all(models)
@@ -70,7 +91,8 @@ def main():
     for _ in range(200):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        agg.aggregate({'client_feedback': models, 'recover_fun': None})
+        agg.aggregate({'client_feedback': next_models(),
+                       'recover_fun': None})
         torch.cuda.synchronize()
         ts.append((time.perf_counter() - t0) * 1e6)
     for k in sorted(marks):
