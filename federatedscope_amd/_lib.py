@@ -122,6 +122,7 @@ SIGNATURES['fsagg_pairgram_set_block8'] = (_c_i, [_c_i])
 SIGNATURES['fsagg_pairgram_block8'] = (_c_i, [])
 SIGNATURES['fsagg_pairgram_set_stages'] = (_c_i, [_c_i])
 SIGNATURES['fsagg_pairgram_set_chunks'] = (_c_i, [_c_i])
+SIGNATURES['fsagg_pairgram_set_desync'] = (_c_i, [_c_i])
 SIGNATURES['fsagg_pairgram_rows_segsq_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_sz, _c_p])
 SIGNATURES['fsagg_pairgram_rows_f32'] = (

@@ -115,6 +115,7 @@ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 struct GramCtl {
   int *prefix;      // [nseg + 1]
   int *gprefix;     // [nseg + 1]
+  int desync;       // A/B: main-pass start offset (fsagg_pairgram_set_desync)
 };
 
 // One wave: lane l takes keys l, l + 64, ...; the chunk and group counts
@@ -544,6 +545,12 @@ void gram_chunk_kernel(
                  : lt;
   };
   if (chunk >= prefix[nseg]) return;   // whole workgroup
+  if (CENTRED && ctl.desync > 3) {
+    const int sel = ctl.desync & 3;
+    const unsigned bit = sel == 1 ? blockIdx.x : blockIdx.x >> (sel + 6);
+    if (bit & 1u)
+      for (int i = 0; i < (ctl.desync >> 2); ++i) __builtin_amdgcn_s_sleep(8);
+  }
   int s = 0;
   while (prefix[s + 1] <= chunk) ++s;
   const int q = chunk - prefix[s];
@@ -1348,6 +1355,10 @@ std::atomic<int> g_compact{1};
 // main-pass chunks (n <= 112 forms): about kMainChunks workgroups — two
 // rounds at two per CU; fsagg_pairgram_set_chunks, A/B
 std::atomic<int> g_main_chunks{kMainChunks};
+// A/B: bits 0-1 pick the main-pass workgroups that start late (1: odd
+// blocks, 2: bit 8, 3: bit 9), bits 2+ the delay in 512-cycle sleeps;
+// fsagg_pairgram_set_desync
+std::atomic<int> g_desync{0};
 
 struct GramPlan {
   int nt;              // tiles of 16 clients
@@ -1446,6 +1457,7 @@ size_t gram_ws_layout(int n, int64_t numel, int nseg, void *ws, GramWs *w) {
     GramCtl c;
     c.prefix = p;
     c.gprefix = p + (nseg + 1);
+    c.desync = g_desync.load(std::memory_order_relaxed);
     return c;
   };
   const GramCtl cs = ctl(), cm = ctl();
@@ -1565,6 +1577,10 @@ extern "C" int fsagg_pairgram_set_block8(int on) {
 
 extern "C" int fsagg_pairgram_set_stages(int mode) {
   return g_compact.exchange(mode < 0 ? 1 : (mode > 1 ? 1 : mode));
+}
+
+extern "C" int fsagg_pairgram_set_desync(int mode) {
+  return g_desync.exchange(mode < 0 ? 0 : mode);
 }
 
 extern "C" int fsagg_pairgram_set_chunks(int chunks) {

@@ -1403,11 +1403,13 @@ def pairgram_rows_dist_graph(rs, tol):
     lib.fsagg_pairgram_set_stages(stages)
     chunks = lib.fsagg_pairgram_set_chunks(0)
     lib.fsagg_pairgram_set_chunks(chunks)
+    desync = lib.fsagg_pairgram_set_desync(0)
+    lib.fsagg_pairgram_set_desync(desync)
     stream = torch._C._cuda_getCurrentRawStream(rs.device.index)
     host = rs.host.T if rs._segmajor is None else rs._segmajor
     key = ('pairgram', rs.device.index, stream, host.shape, rs.ss, rs.n,
            rs.nseg, lay.signature(), float(tol), lib.fsagg_pairgram_block8(),
-           stages, chunks)
+           stages, chunks, desync)
     e = _GRAPHS.lookup(key)
     if e is None:
         need = max(int(lib.fsagg_pairgram_workspace_bytes(

@@ -529,6 +529,12 @@ int fsagg_pairgram_set_stages(int mode);
  * previous setting.  For A/B measurements: only the fp64 summation order of
  * the chunk partials changes. */
 int fsagg_pairgram_set_chunks(int chunks);
+
+/* A/B knob: delay the start of about half of the Gram main pass's
+ * workgroups (bits 0-1: which — 1 odd blocks, 2 block bit 8, 3 block bit 9;
+ * bits 2+: the delay in 512-cycle sleeps; 0 = off, the default).  Returns
+ * the previous setting. */
+int fsagg_pairgram_set_desync(int mode);
 int fsagg_pairgram_rows_segsq_f32(const fsagg_rows *rows,
                                   const int64_t *seg_lo,
                                   const int64_t *seg_end, int64_t numel,

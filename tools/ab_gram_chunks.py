@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""A/B of the Gram chain's main-pass chunk count (fsagg_pairgram_set_chunks:
-the settings in $CHUNKS, default 1024,512,768), interleaved, on C4's layout
+"""A/B of a Gram chain knob — the main-pass chunk count
+(fsagg_pairgram_set_chunks: $CHUNKS, default 1024,512,768) or, with
+KNOB=desync, the main pass's start offset (fsagg_pairgram_set_desync:
+$CHUNKS as its settings) — interleaved, on C4's layout
 (ConvNet2-h2048, 6.6M, separately allocated keys) for the given n (default
 50): median of 15 event-timed calls of the whole chain
 (fsagg_pairgram_rows_f32) per round, 4 rounds; D64 within 1e-12 relative
@@ -25,6 +27,9 @@ def main():
     from federatedscope_amd.core.aggregators._engine import _GRAM_TOL
     from federatedscope_amd.layout import BucketLayout
     lib = L.load()
+    setk = (lib.fsagg_pairgram_set_desync
+            if os.environ.get('KNOB') == 'desync'
+            else lib.fsagg_pairgram_set_chunks)
     dev = torch.device('cuda', 0)
     ns = [int(a) for a in sys.argv[1:]] or [50]
     for n in ns:
@@ -41,7 +46,7 @@ def main():
                                                 '1024,512,768').split(',')]
         d64 = {}
         for mode in modes:
-            lib.fsagg_pairgram_set_chunks(mode)
+            setk(mode)
             d64[mode] = ops.pairgram_rows_dist(rs, _GRAM_TOL)[4].cpu().numpy()
         off = ~np.eye(n, dtype=bool)
         rel = max(float(np.max(np.abs(d64[m][off] - d64[modes[0]][off]) /
@@ -49,7 +54,7 @@ def main():
         res = {m: [] for m in modes}
         for rnd in range(4):
             for mode in (modes if rnd % 2 == 0 else modes[::-1]):
-                lib.fsagg_pairgram_set_chunks(mode)
+                setk(mode)
                 for _ in range(5):
                     ops.pairgram_rows_dist(rs, _GRAM_TOL)
                 torch.cuda.synchronize()
@@ -62,8 +67,9 @@ def main():
                     e1.synchronize()
                     ts.append(e0.elapsed_time(e1))
                 res[mode].append(statistics.median(ts))
-        lib.fsagg_pairgram_set_chunks(0)
-        print(json.dumps({'n': n, 'chunks_ms': {
+        setk(0)
+        print(json.dumps({'n': n, 'knob': os.environ.get('KNOB', 'chunks'),
+                          'chunks_ms': {
             str(m): [round(x, 4) for x in res[m]] for m in modes},
             'median_ms': {str(m): round(statistics.median(res[m]), 4)
                           for m in modes},

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of weighted-sum variants (rows in flight U ×
-float4 columns per lane V × nt loads × grid) on 100 × 25M, plus the
+float4 columns per lane V × nt loads × grid) on N × P (default 100 × 25M;
+rows at a 256-B aligned leading dimension), plus the
 read-only stream ceiling.  Prints one line per variant: median/min ms and
 GB/s.  GPU only; run through tools/gpu_job.sh."""
 import ctypes
@@ -35,9 +36,11 @@ def main():
                                       ctypes.c_void_p, ctypes.c_int64,
                                       ctypes.c_void_p, ctypes.c_void_p]
     dev = torch.device('cuda', 0)
-    slab = torch.empty((n, P), dtype=torch.float32, device=dev)
-    ops.fill_uniform(slab, P, seed=1)
-    rows = ops.RowTable.from_slab(slab)
+    # rows 256-B aligned as every staged or bench slab lays them out
+    ld = ops.round_up(P, 64)
+    slab = torch.empty((n, ld), dtype=torch.float32, device=dev)
+    ops.fill_uniform(slab, ld, seed=1)
+    rows = ops.RowTable.from_slab(slab, numel=P)
     w = torch.full((n, ), 1.0 / n, dtype=torch.float32, device=dev)
     out = torch.empty(P, dtype=torch.float32, device=dev)
     ref = torch.empty_like(out)
@@ -50,11 +53,13 @@ def main():
             str(k) for k in VARIANTS)).split(',')]:
         for g in grids:
             cases.append(('wsum', v, g))
-    for v in PART:
+    for v in ([int(x) for x in os.environ['PVARS'].split(',')]
+              if os.environ.get('PVARS') is not None and os.environ['PVARS']
+              else ([] if 'PVARS' in os.environ else PART)):
         for g in [int(x) for x in os.environ.get(
                 'PGRIDS', '256,512,768,1024,2048').split(',')]:
             cases.append(('part', v, g))
-    for nt in (0, 1):
+    for nt in ((0, 1) if not os.environ.get('NOREAD') else ()):
         for g in (4096, 8192, 16384):
             cases.append(('read', nt, g))
     times = {c: [] for c in cases}
@@ -74,7 +79,7 @@ def main():
                                                out.data_ptr(), st), 'tune')
             else:
                 _lib.check(lib.fsagg_tune_readbw(c[1], c[2], slab.data_ptr(),
-                                                 n * P, red.data_ptr(), st),
+                                                 n * ld, red.data_ptr(), st),
                            'readbw')
             e1.record()
             e1.synchronize()
