@@ -106,6 +106,7 @@ _rows_p = ctypes.POINTER(Rows)
 FSAGG_ROWS_OS_CHUNK = 256
 SIGNATURES['fsagg_wsum_chunk_elems'] = (_c_i64, [_c_i64])
 SIGNATURES['fsagg_wsum_chunk_elems_n'] = (_c_i64, [_c_i64, _c_i])
+SIGNATURES['fsagg_wsum_set_rows_width'] = (_c_i, [_c_i])
 SIGNATURES['fsagg_weighted_sum_rows_f32'] = (
     _c_i, [_rows_p, _c_p, _c_i, _c_i64, _c_p, _c_p, _c_p, _c_i64, _c_p, _c_p])
 SIGNATURES['fsagg_coord_median_rows_f32'] = (

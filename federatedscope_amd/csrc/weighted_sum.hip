@@ -16,6 +16,7 @@
 //   * the adds happen strictly in client order, which keeps the result
 //     bit-identical to the reference;
 //   * row pointers and weights are wave-uniform → scalar (SGPR) loads.
+#include <atomic>
 #include <hip/hip_fp16.h>
 
 #include "common.h"
@@ -277,17 +278,45 @@ void launch_wsum_v(const float *const *rows, const float *w, const float *pre,
                      base, out);
 }
 
-// V of the streaming kernels for nvec float4 columns of n clients: the
-// largest V that leaves >= min_tiles one-tile workgroups.  1000 (two rounds
-// of the 2 × 256 resident workgroups) below 150 clients; with n >= 150 a
-// tile runs long enough that ~400 workgroups keep HBM busy and the wider V
-// wins: 200 × 6.6M, V = 16 (403 tiles) 0.79 ms against V = 4 (1612) 0.83 ms
-// and V = 24 (269) 1.06 ms (profiles/r02_tune_wsum_200x6p6M.txt).
-inline int wsum_width(int64_t nvec, int n) {
+// V of the row-set kernel's chunks (wsum_rows_kernel) for nvec float4
+// columns of n clients: the largest V that leaves >= min_tiles one-tile
+// workgroups.  1000 (two rounds of the 2 × 256 resident workgroups) below
+// 150 clients; with n >= 150 a tile runs long enough that ~400 workgroups
+// keep HBM busy and the wider V wins: 200 × 6.6M, V = 16 (403 tiles)
+// 0.79 ms against V = 4 (1612) 0.83 ms and V = 24 (269) 1.06 ms
+// (profiles/r02_tune_wsum_200x6p6M.txt).
+inline int wsum_width_rows(int64_t nvec, int n) {
   const int64_t min_tiles = n >= 150 ? 400 : 1000;
   auto tiles = [&](int v) { return (nvec + 256 * v - 1) / (256 * v); };
   for (int v : {24, 16, 8, 4})
     if (tiles(v) >= min_tiles) return v;
+  return 1;
+}
+
+// V of the flat streaming kernels (wsum_f32_vec_kernel, the host-table
+// kernel).  Fitted to an interleaved sweep of V = 1/4/8/12/16/24 over
+// 1.69M–50M coordinates at n = 30/50/100/200 (tools/tune_wsum.py,
+// profiles/r06/tune_wsum_sizes_*.txt; 256-B aligned rows).  V = 24 (244
+// VGPRs, two workgroups per CU: 512 resident) wins whenever its last round
+// of workgroups is at least half full — r = tiles/512 >= 0.9 with
+// frac(r) >= 0.5 (12M: 0.680 against 0.733 ms for V = 16; 23.5M: 1.357
+// against 1.442; 25M; 32M; 50M) — and loses up to 20 % when that round is
+// mostly empty (15M, r = 1.19: 1.141 against 0.950; 28M, r = 2.22: 1.866
+// against 1.746).  Otherwise V = 16 (164 VGPRs, three per CU) from 400
+// tiles up or while its tiles fit one per CU from 160 (3M: 0.170 ms against
+// 0.193 for V = 1; at 305 tiles, 5M, the CUs holding two take twice as
+// long: 0.366 against 0.317 for V = 4); then V = 4 from 1000 tiles, V = 8
+// from 200 (1.69M: 0.097 against 0.103 for V = 1), else V = 1.  The choice
+// never changes a result bit: each element sums its clients in order.
+inline int wsum_width(int64_t nvec, int n) {
+  (void)n;
+  auto tiles = [&](int v) { return (nvec + 256 * v - 1) / (256 * v); };
+  const double r = double(tiles(24)) / 512.0;
+  if (r >= 0.9 && r - double(int64_t(r)) >= 0.5) return 24;
+  const int64_t t16 = tiles(16);
+  if (t16 >= 400 || (t16 >= 160 && t16 <= 256)) return 16;
+  if (tiles(4) >= 1000) return 4;
+  if (tiles(8) >= 200) return 8;
   return 1;
 }
 
@@ -334,6 +363,8 @@ void launch_wsum_any(const float *const *rows, const float *weights,
 // row set of fresh uploads (new tensors every round) spends most of its
 // host time on those small uploads otherwise.
 // ---------------------------------------------------------------------------
+static_assert(FSAGG_HOSTTAB_MAX_CLIENTS <= 256,
+              "the host-table tail kernel loads one client per thread");
 struct ArgTab {
   const float *rows[FSAGG_HOSTTAB_MAX_CLIENTS];
   float w[FSAGG_HOSTTAB_MAX_CLIENTS];
@@ -361,17 +392,30 @@ template <class O>
 __global__ __launch_bounds__(kTailBlock) void wsum_f32_arg_tail_kernel(
     const ArgTab tab, int pre_on, int n, int64_t start, int64_t numel,
     const float *__restrict__ base, O out) {
-  const int e = threadIdx.x;
+  // n <= FSAGG_HOSTTAB_MAX_CLIENTS < kTailBlock: thread c loads client c's
+  // (<= 3) tail values into LDS — one memory latency for all clients (a
+  // thread walking the clients waited out their loads one by one: 46 us at
+  // n = 100, profiles/r06/layout_b_trace) — then thread e sums element e in
+  // client order
+  __shared__ float xs[3][kTailBlock];
   const int m = int(numel - start);  // 1..3
+  const int c = threadIdx.x;
+  if (c < n) {
+    const float *r = tab.rows[c];
+    const float sc = pre_on ? tab.pre[c] : 1.0f;
+    for (int k = 0; k < m; ++k) {
+      float x = gld(r + start + k);
+      if (pre_on) x = mul_rn(x, sc);
+      xs[k][c] = x;
+    }
+  }
+  __syncthreads();
+  const int e = threadIdx.x;
   if (e >= m) return;
-  // n <= FSAGG_HOSTTAB_MAX_CLIENTS: one thread per tail element walks the
-  // clients (their loads are independent of the running sum)
   float acc = 0.0f;
-  for (int c = 0; c < n; ++c) {
-    float x = gld(tab.rows[c] + start + e);
-    if (pre_on) x = mul_rn(x, tab.pre[c]);
-    const float t = mul_rn(x, tab.w[c]);
-    acc = c == 0 ? t : add_rn(acc, t);
+  for (int j = 0; j < n; ++j) {
+    const float t = mul_rn(xs[e][j], tab.w[j]);
+    acc = j == 0 ? t : add_rn(acc, t);
   }
   if (base) acc = add_rn(base[start + e], acc);
   put1(out, start + e, acc);
@@ -412,7 +456,7 @@ void launch_wsum_arg_any(const ArgTab &tab, bool pre, int n, int64_t numel,
     }
   }
   if (numel > nvec * 4)
-    hipLaunchKernelGGL((wsum_f32_arg_tail_kernel<O>), dim3(1), dim3(kWave), 0,
+    hipLaunchKernelGGL((wsum_f32_arg_tail_kernel<O>), dim3(1), dim3(kTailBlock), 0,
                        s, tab, pre ? 1 : 0, n, nvec * 4, numel, base, out);
 }
 
@@ -552,9 +596,15 @@ __global__ __launch_bounds__(kBlock) void wsum_rows_kernel(
   }
 }
 
-// V of the flat launcher (launch_wsum) for a bucket of `numel` coordinates
-// of n clients
-int wsum_vec_width(int64_t numel, int n) { return wsum_width(numel / 4, n); }
+// V of the row-set kernel's chunks for a bucket of `numel` coordinates of n
+// clients (fsagg_wsum_chunk_elems)
+// A/B: a fixed row-set chunk width (fsagg_wsum_set_rows_width; 0 = the rule)
+std::atomic<int> g_rows_width{0};
+
+int wsum_vec_width(int64_t numel, int n) {
+  const int v = g_rows_width.load(std::memory_order_relaxed);
+  return v > 0 ? v : wsum_width_rows(numel / 4, n);
+}
 
 template <int V, bool PRE, bool BASE>
 void launch_wsum_rows(const fsagg_rows &rs, const fsagg_chunk *chunks,
@@ -895,6 +945,11 @@ extern "C" int fsagg_weighted_sum_hosttab_f32(
     launch_wsum_arg_any(tab, prescale != nullptr, n, numel, base, o, s);
   }
   return check_launch("fsagg_weighted_sum_hosttab_f32");
+}
+
+extern "C" int fsagg_wsum_set_rows_width(int v) {
+  const int w = v == 24 || v == 16 || v == 8 || v == 4 || v == 1 ? v : 0;
+  return fsagg::g_rows_width.exchange(w);
 }
 
 extern "C" int64_t fsagg_wsum_chunk_elems(int64_t numel) {

@@ -413,6 +413,12 @@ int64_t fsagg_wsum_chunk_elems(int64_t numel);
  * (fewer, longer workgroups; measured faster at 200 x 6.6M). */
 int64_t fsagg_wsum_chunk_elems_n(int64_t numel, int n);
 
+/* A/B knob: the row-set kernel's chunk width V (chunk_elems = 1024·V) that
+ * fsagg_wsum_chunk_elems[_n] return — 24, 16, 8, 4 or 1; 0 (or anything
+ * else) = the built-in rule.  Results do not depend on it.  Returns the
+ * previous setting. */
+int fsagg_wsum_set_rows_width(int v);
+
 /*
  * fsagg_weighted_sum_f32 over a row set: out[p] for every chunk coordinate,
  * clients in table order, NULL entries skipped (the first present client

@@ -11,6 +11,8 @@ Times, interleaved (median of rounds of back-to-back calls):
   rows_sep    the same on the separate tensors' row set
   flat        ops.weighted_sum over the slab rows (the flat kernel)
 Run under rocprofv3 --kernel-trace --stats for the kernels' own durations.
+--rows-widths 0,24,8 adds rows_sep_V / agg_sep_V legs at a fixed row-set
+chunk width (fsagg_wsum_set_rows_width).
 
     python tools/probe_layout_b.py [--rounds 5] [--calls 10] [--only rows_sep]
 """
@@ -38,6 +40,10 @@ def main():
     ap.add_argument('--only', default=None,
                     help='comma-separated legs to run (for per-leg counter '
                          'passes), e.g. rows_sep')
+    ap.add_argument('--rows-widths', default=None,
+                    help='comma-separated row-set chunk widths V to time as '
+                         'extra legs rows_sep_V / agg_sep_V '
+                         '(fsagg_wsum_set_rows_width; 0 = the rule)')
     ap.add_argument('--no-fill', action='store_true',
                     help='allocate the separate tensors without copying the '
                          'values in (16100 copy kernels are slow under a '
@@ -85,6 +91,21 @@ def main():
         'rows_sep': lambda: ops.weighted_sum_rows(rs_s, w, out),
         'flat': lambda: ops.weighted_sum(rows, w, flat),
     }
+    if args.rows_widths:
+        from federatedscope_amd import _lib as L
+        lib = L.load()
+
+        def at(v, fn):
+            def run():
+                prev = lib.fsagg_wsum_set_rows_width(v)
+                try:
+                    return fn()
+                finally:
+                    lib.fsagg_wsum_set_rows_width(prev)
+            return run
+        for v in [int(x) for x in args.rows_widths.split(',')]:
+            legs['rows_sep_%d' % v] = at(v, legs['rows_sep'])
+            legs['agg_sep_%d' % v] = at(v, legs['agg_sep'])
     if args.only:
         keep = args.only.split(',') + ['flat']
         legs = {k: v for k, v in legs.items() if k in keep}
