@@ -169,6 +169,17 @@ SIGNATURES['fsagg_weighted_sum_bcast_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i, _c_i64, _c_p, ctypes.POINTER(_c_p), _c_i,
            _c_p])
 FSAGG_HOSTTAB_MAX_CLIENTS = 128
+FSAGG_HOSTTAB_ROWS_MAX_CLIENTS = 64
+FSAGG_KRUMSEL_MAX_CLIENTS = 256
+FSAGG_KRUMSEL_MAX_SEGS = 64
+SIGNATURES['fsagg_krum_select_f32'] = (
+    _c_i, [_c_p, _c_i, _c_i, _c_i, _c_i, _c_i, _c_p, _c_i, _c_p, _c_p, _c_i64,
+           _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p])
+FSAGG_HOSTTAB_ROWS_MAX_PTRS = 256
+FSAGG_HOSTTAB_ROWS_MAX_SEGS = 64
+SIGNATURES['fsagg_weighted_sum_rows_hosttab_f32'] = (
+    _c_i, [_c_p, _c_i, _c_i, _c_p, _c_i, _c_i64, _c_p, _c_p, _c_p, _c_p,
+           _c_p])
 SIGNATURES['fsagg_upload_h2d'] = (
     _c_i, [_c_p, _c_p, _c_sz, _c_p, _c_i, _c_i, _c_p, _c_p])
 SIGNATURES['fsagg_upload_wait'] = (_c_i, [_c_i, _c_p])

@@ -241,8 +241,10 @@ class DeviceEngine:
             return self._pairdist_valu(st)
         if st.plan is None:
             # one graph launch for the chain's eight kernels (ops._GRAPHS)
-            buf = ops.pairgram_rows_dist_graph(st.rows(), _GRAM_TOL)[0]
-            return _PendingD(self, st, buf=buf)
+            rs = st.rows()
+            buf = ops.pairgram_rows_dist_graph(rs, _GRAM_TOL)[0]
+            return _PendingD(self, st, buf=buf,
+                             tab=rs.__dict__.get('_gram_tab'))
         sq2 = self._sum_pieces(
             st, lambda rs, lo, hi: ops.pairgram_rows_segsq(rs, lo, hi))
         return _PendingD(self, st, buf=ops.pairgram_finish(sq2, _GRAM_TOL)[0])
@@ -777,8 +779,10 @@ class _PendingD:
     ``_pair_info`` (:class:`_PairInfo`: ``last_pair_bound``,
     ``last_pair_cert``)."""
 
-    def __init__(self, eng, st, buf=None, D=None):
+    def __init__(self, eng, st, buf=None, D=None, tab=None):
         self._eng, self._st, self._buf, self._D = eng, st, buf, D
+        # the Gram chain's device copy of the row table (ops.krum_select)
+        self._tab = tab
 
     def cpu(self):
         if self._D is not None:

@@ -13,10 +13,14 @@ matrix (the per-key L2 distances summed over keys, +inf diagonal, :58-73):
 * above 256 clients on the VALU kernel (fsagg_pairdist_rows_segsq_f32 +
   fsagg_pairdist_finish_f64: direct differences).
 
-The matrix (≤ 200² floats) comes back to the host where the score/sort/select
-logic runs with the same torch CPU ops as the reference (:75-87); the
-selected clients are then averaged in ascending-score order with init + avg
-fused into the kernel (fsagg_weighted_sum_rows_f32).
+On the Gram path the scores, their stable order and the selection's
+certificate are computed on the device from the fp64 key sums and their
+bounds (fsagg_krum_select_f32), which also writes the selected clients' row
+table and weights; their average (init + avg fused, ascending-score order,
+fsagg_weighted_sum_rows_f32) is launched right behind it and the host reads
+back one flag and the order.  An uncertified selection, and the VALU path,
+take the host route: the matrix comes back, the certificate runs natively
+(or the ambiguous rows are recomputed, :75-87), then the average.
 """
 import torch
 
@@ -63,6 +67,9 @@ class KrumAggregator(ClientsAvgAggregator):
         # host work that does not need the selection runs while the
         # distance kernels do (the .cpu() below waits for them)
         base = self._base(layout, self.model.state_dict(), as_float=True)
+        out = self._select_on_device(st, D, models, agg_num, base)
+        if out is not None:
+            return layout, out, list(models[0][1].keys())
         _, _, index_order = self._certified_order(
             st, D.cpu(), self.byzantine_node_num, agg_num, ordered=True)
         sel = [int(i) for i in index_order[:agg_num]]
@@ -75,3 +82,78 @@ class KrumAggregator(ClientsAvgAggregator):
             bcast=lambda rs, o, peers, lo, hi: ops.weighted_sum_rows_bcast(
                 rs, weights, o, peers, base=base, lo=lo, hi=hi))
         return layout, out, list(models[0][1].keys())
+
+    def _select_on_device(self, st, D, models, agg_num, base):
+        """The multi-Krum average with its selection certified on the
+        device (ops.krum_select: the scores, order and certificate of
+        _certified_order's native path, from the Gram finish buffer) and the
+        selected clients' average launched right behind it — the host reads
+        back one flag and the order instead of the n x n buffer, and
+        certifies, gathers and uploads nothing in between.  None (nothing
+        launched that the caller needs) when the path does not apply or the
+        selection is not certified: the host path then runs as before."""
+        import numbers
+
+        import numpy as np
+        from ... import _lib
+        from ._engine import _PairInfo
+        tab = getattr(D, '_tab', None)
+        buf = getattr(D, '_buf', None)
+        n = st.n
+        if tab is None or buf is None or st.plan is not None or \
+                n > _lib.FSAGG_KRUMSEL_MAX_CLIENTS or agg_num < 1:
+            return None
+        sizes = []
+        for s, _ in models:
+            if isinstance(s, bool) or not isinstance(s, numbers.Real):
+                return None
+            v = float(s)
+            # fedavg_weights' Python arithmetic, exactly, in fp64
+            if not np.isfinite(v) or v != s or v <= 0.0 or abs(v) >= 2**53:
+                return None
+            sizes.append(v)
+        layout = st.layout
+        nseg = max(1, len(layout.keys))
+        rs = st.rows()
+        bh = None
+        if base is not None:
+            if base.host is None or nseg > _lib.FSAGG_KRUMSEL_MAX_SEGS:
+                return None
+            bh = list(base.host) if base.bss else [base.host[0]] * nseg
+        msel = min(int(agg_num), n)
+        sel, sub_tab, sub_w, sub_base = ops.krum_select(
+            buf, nseg, self.byzantine_node_num, agg_num, True, sizes,
+            self.cfg.federate.ignore_weight, tab, rs.ss,
+            nseg if rs.ss else 1, bh)
+        # the flag, order and finish buffer go to the host on a side stream
+        # while the average runs on this one
+        dev = self.compute_device
+        cur = torch.cuda.current_stream(dev)
+        side = self.__dict__.get('_ksel_stream')
+        if side is None or side.device != dev:
+            side = self._ksel_stream = torch.cuda.Stream(device=dev)
+        pins = self.__dict__.setdefault('_ksel_pinned', {})
+        hb = pins.get(n)
+        if hb is None:
+            hb = pins[n] = (torch.empty(2 + n, dtype=torch.int32,
+                                        pin_memory=True),
+                            torch.empty(tuple(buf.shape), dtype=torch.int32,
+                                        pin_memory=True))
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            hb[0].copy_(sel, non_blocking=True)
+            hb[1].copy_(buf, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        sel.record_stream(side)
+        out = torch.empty(layout.numel, dtype=torch.float32, device=dev)
+        ops.weighted_sum_rows_devtab(layout, sub_tab, msel if rs.ss else 0,
+                                     msel, sub_w, out, base=sub_base)
+        ev.synchronize()
+        got = hb[0].numpy()
+        if not got[0]:
+            return None
+        self.last_selection = [int(i) for i in got[2:2 + msel]]
+        self.last_pairdist_path = 'mfma'
+        self._pair_info = _PairInfo(hb[1].clone(), nseg)
+        return out

@@ -557,7 +557,7 @@ __device__ __forceinline__ void wsum_rows_chunk(
 }
 
 template <int V, bool PRE, bool BASE>
-__global__ __launch_bounds__(kBlock) void wsum_rows_kernel(
+__device__ __forceinline__ void wsum_rows_body(
     const float *const *__restrict__ tab, int64_t ss, int n,
     const fsagg_chunk *__restrict__ chunks, int nchunk,
     const float *__restrict__ w, const float *__restrict__ pre,
@@ -594,6 +594,57 @@ __global__ __launch_bounds__(kBlock) void wsum_rows_kernel(
       out[p] = acc;
     }
   }
+}
+
+template <int V, bool PRE, bool BASE>
+__global__ __launch_bounds__(kBlock) void wsum_rows_kernel(
+    const float *const *__restrict__ tab, int64_t ss, int n,
+    const fsagg_chunk *__restrict__ chunks, int nchunk,
+    const float *__restrict__ w, const float *__restrict__ pre,
+    const float *const *__restrict__ btab, int64_t bss,
+    float *__restrict__ out) {
+  wsum_rows_body<V, PRE, BASE>(tab, ss, n, chunks, nchunk, w, pre, btab, bss,
+                               out);
+}
+
+// The row set's pointer table [nseg][n], weights, prescales and base table
+// in the kernel arguments (fsagg_weighted_sum_rows_hosttab_f32): small row
+// sets — a multi-Krum selection's average, a handful of clients of a
+// multi-key model — whose per-call uploads cost more host time than the
+// kernel (each H2D copy ~19 us, profiles/r06/upload_cost.json).
+static_assert(FSAGG_HOSTTAB_ROWS_MAX_CLIENTS <= FSAGG_HOSTTAB_ROWS_MAX_PTRS,
+              "row-set host table limits");
+struct ArgRows {
+  const float *tab[FSAGG_HOSTTAB_ROWS_MAX_PTRS];
+  const float *base[FSAGG_HOSTTAB_ROWS_MAX_SEGS];
+  float w[FSAGG_HOSTTAB_ROWS_MAX_CLIENTS];
+  float pre[FSAGG_HOSTTAB_ROWS_MAX_CLIENTS];
+};
+
+template <int V, bool PRE, bool BASE>
+__global__ __launch_bounds__(kBlock) void wsum_rows_arg_kernel(
+    const ArgRows a, int n, const fsagg_chunk *__restrict__ chunks,
+    int nchunk, float *__restrict__ out) {
+  wsum_rows_body<V, PRE, BASE>(a.tab, n, n, chunks, nchunk, a.w, a.pre,
+                               a.base, 1, out);
+}
+
+template <int V>
+void launch_wsum_rows_arg(const ArgRows &a, bool pre, bool base, int n,
+                          const fsagg_chunk *chunks, int nchunk, float *out,
+                          hipStream_t s) {
+  const unsigned grid = stream_grid(nchunk, 1, 256 * 16);
+#define FSAGG_RA(P, B)                                                      \
+  hipLaunchKernelGGL((wsum_rows_arg_kernel<V, P, B>), dim3(grid),          \
+                     dim3(kBlock), 0, s, a, n, chunks, nchunk, out)
+  if (pre) {
+    if (base) FSAGG_RA(true, true);
+    else FSAGG_RA(true, false);
+  } else {
+    if (base) FSAGG_RA(false, true);
+    else FSAGG_RA(false, false);
+  }
+#undef FSAGG_RA
 }
 
 // V of the row-set kernel's chunks for a bucket of `numel` coordinates of n
@@ -991,6 +1042,57 @@ extern "C" int fsagg_weighted_sum_rows_f32(const fsagg_rows *rows,
       return FSAGG_EINVAL;
   }
   return check_launch("fsagg_weighted_sum_rows_f32");
+}
+
+extern "C" int fsagg_weighted_sum_rows_hosttab_f32(
+    const uint64_t *tab, int n, int nseg, const fsagg_chunk *chunks,
+    int nchunk, int64_t chunk_elems, const float *weights,
+    const float *prescale, const uint64_t *base, float *out,
+    fsagg_stream_t stream) {
+  if (!tab || n < 1 || n > FSAGG_HOSTTAB_ROWS_MAX_CLIENTS || nseg < 1 ||
+      int64_t(n) * nseg > FSAGG_HOSTTAB_ROWS_MAX_PTRS ||
+      (base && nseg > FSAGG_HOSTTAB_ROWS_MAX_SEGS) || !weights || !out ||
+      nchunk < 0 || (nchunk > 0 && !chunks)) {
+    set_error("fsagg_weighted_sum_rows_hosttab_f32: invalid argument (n=%d "
+              "nseg=%d; at most %d clients, %d pointers, %d base keys)", n,
+              nseg, FSAGG_HOSTTAB_ROWS_MAX_CLIENTS,
+              FSAGG_HOSTTAB_ROWS_MAX_PTRS, FSAGG_HOSTTAB_ROWS_MAX_SEGS);
+    return FSAGG_EINVAL;
+  }
+  if (!aligned16(out)) {
+    set_error("fsagg_weighted_sum_rows_hosttab_f32: out must be 16-byte "
+              "aligned");
+    return FSAGG_EINVAL;
+  }
+  if (nchunk == 0) return FSAGG_OK;
+  ArgRows a;
+  for (int i = 0; i < n * nseg; ++i)
+    a.tab[i] = reinterpret_cast<const float *>(uintptr_t(tab[i]));
+  for (int i = n * nseg; i < FSAGG_HOSTTAB_ROWS_MAX_PTRS; ++i)
+    a.tab[i] = nullptr;
+  for (int k = 0; k < FSAGG_HOSTTAB_ROWS_MAX_SEGS; ++k)
+    a.base[k] = base && k < nseg
+                    ? reinterpret_cast<const float *>(uintptr_t(base[k]))
+                    : nullptr;
+  for (int i = 0; i < FSAGG_HOSTTAB_ROWS_MAX_CLIENTS; ++i) {
+    a.w[i] = i < n ? weights[i] : 0.0f;
+    a.pre[i] = i < n && prescale ? prescale[i] : 1.0f;
+  }
+  hipStream_t s = as_stream(stream);
+  const bool pre = prescale != nullptr, b = base != nullptr;
+  switch (chunk_elems) {
+    case 1024 * 24: launch_wsum_rows_arg<24>(a, pre, b, n, chunks, nchunk, out, s); break;
+    case 1024 * 16: launch_wsum_rows_arg<16>(a, pre, b, n, chunks, nchunk, out, s); break;
+    case 1024 * 8: launch_wsum_rows_arg<8>(a, pre, b, n, chunks, nchunk, out, s); break;
+    case 1024 * 4: launch_wsum_rows_arg<4>(a, pre, b, n, chunks, nchunk, out, s); break;
+    case 1024: launch_wsum_rows_arg<1>(a, pre, b, n, chunks, nchunk, out, s); break;
+    default:
+      set_error("fsagg_weighted_sum_rows_hosttab_f32: chunk_elems %lld is "
+                "not a fsagg_wsum_chunk_elems() unit",
+                (long long)chunk_elems);
+      return FSAGG_EINVAL;
+  }
+  return check_launch("fsagg_weighted_sum_rows_hosttab_f32");
 }
 
 extern "C" int fsagg_weighted_sum_typed(const void *const *rows, int in_dtype,

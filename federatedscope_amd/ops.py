@@ -976,17 +976,18 @@ class BaseRows:
     of the robust rules' init + update): per-key virtual bases of device
     tensors, or one flat bucket."""
 
-    def __init__(self, tab, bss, keepalive=(), host=None):
-        self.tab = tab
+    def __init__(self, host, bss, device, keepalive=(), ephemeral=False):
         self.bss = bss
         self.host = host      # the per-key virtual bases (host copy)
+        self.device = device
+        self.ephemeral = bool(ephemeral)
+        self._tab = None
         self._keep = tuple(keepalive)
 
     @classmethod
     def from_bucket(cls, flat):
         _check_f32_cuda(flat, 'base bucket')
-        return cls(_h2d([flat.data_ptr()], torch.int64, flat.device), 0,
-                   keepalive=(flat, ), host=[flat.data_ptr()])
+        return cls([flat.data_ptr()], 0, flat.device, keepalive=(flat, ))
 
     @classmethod
     def from_pointers(cls, layout, ptrs, device, keepalive=(),
@@ -995,8 +996,17 @@ class BaseRows:
         offs = _np.array([layout.offsets[k] for k in layout.keys],
                          dtype=_np.int64)
         virt = ptrs - 4 * offs
-        return cls(_h2d_np(virt, _cuda_index(device), ephemeral=ephemeral),
-                   1, keepalive=keepalive, host=[int(v) for v in virt])
+        return cls([int(v) for v in virt], 1, _cuda_index(device),
+                   keepalive=keepalive, ephemeral=ephemeral)
+
+    @property
+    def tab(self):
+        """The device table, uploaded on first use (the kernel-argument
+        paths read the host copy and never need it)."""
+        if self._tab is None:
+            self._tab = _h2d_np(_np.asarray(self.host, dtype=_np.int64),
+                                self.device, ephemeral=self.ephemeral)
+        return self._tab
 
     def ptr(self):
         return self.tab.data_ptr()
@@ -1031,6 +1041,28 @@ def weighted_sum_rows(rs, weights, out, prescale=None, base=None, lo=0,
     chunks, nchunk = rs.layout.row_chunks(unit, rs.device, lo, hi)
     if nchunk == 0:
         return out
+    if _rows_hosttab(rs, weights, prescale, base):
+        # a small row set: its tables in the kernel arguments, no upload
+        tab = rs._segmajor if rs._segmajor is not None else rs.host.T
+        if tab.shape[0] != rs.nseg:          # a stack row: every key
+            tab = _np.broadcast_to(tab, (rs.nseg, rs.n))
+        tab = _np.ascontiguousarray(tab, dtype=_np.int64)
+        w = _np.asarray(weights, dtype=_np.float32)
+        pre = None if prescale is None else _np.asarray(prescale,
+                                                        dtype=_np.float32)
+        if pre is not None and len(pre) != rs.n:
+            raise ValueError('prescale length mismatch')
+        bt = None
+        if base is not None:
+            bt = _np.asarray(base.host, dtype=_np.int64)
+            if base.bss == 0:
+                bt = _np.full(rs.nseg, bt[0], dtype=_np.int64)
+        L.check(lib.fsagg_weighted_sum_rows_hosttab_f32(
+            tab.ctypes.data, rs.n, rs.nseg, chunks.data_ptr(), nchunk, unit,
+            w.ctypes.data, pre.ctypes.data if pre is not None else None,
+            bt.ctypes.data if bt is not None else None, out.data_ptr(),
+            _stream(rs.device)), 'fsagg_weighted_sum_rows_hosttab_f32')
+        return out
     w = weights if isinstance(weights, torch.Tensor) else _fp32_dev(
         weights, rs.device)
     pre = None
@@ -1046,6 +1078,19 @@ def weighted_sum_rows(rs, weights, out, prescale=None, base=None, lo=0,
         base.bss if base is not None else 0, out.data_ptr(),
         _stream(rs.device)), 'fsagg_weighted_sum_rows_f32')
     return out
+
+
+def _rows_hosttab(rs, weights, prescale, base):
+    """Whether a multi-key row set's weighted sum takes its tables in the
+    kernel arguments (fsagg_weighted_sum_rows_hosttab_f32): few rows, host
+    weights and prescales, a base with a host table."""
+    return rs.n <= L.FSAGG_HOSTTAB_ROWS_MAX_CLIENTS and \
+        rs.n * rs.nseg <= L.FSAGG_HOSTTAB_ROWS_MAX_PTRS and \
+        not isinstance(weights, torch.Tensor) and \
+        not isinstance(prescale, torch.Tensor) and (
+            base is None or (base.host is not None and
+                             rs.nseg <= L.FSAGG_HOSTTAB_ROWS_MAX_SEGS and
+                             len(base.host) in (1, rs.nseg)))
 
 
 def _flat_rows(rs, base):
@@ -1435,11 +1480,74 @@ def pairgram_rows_dist_graph(rs, tol):
         with torch.cuda.graph(g):
             launch()
         _GRAPHS.put(key, (g, buf, tab, (rows, ws, sq2, seg_lo, seg_end)))
+        rs._gram_tab = tab
         return (buf,) + gram_views(buf)
     g, buf, tab, _ = e
     _copy_table(host, tab, rs.device)
     g.replay()
+    # the chain's own device copy of this call's row table (valid until the
+    # next call of the shape): krum_select gathers the selection from it
+    rs._gram_tab = tab
     return (buf,) + gram_views(buf)
+
+
+def krum_select(buf, nseg, f, m, ordered, sizes, ignore_weight, tab, ss,
+                nsegt, base=None):
+    """Krum's certified selection on the device from a Gram finish buffer
+    (fsagg_krum_select_f32), with the first min(m, n) clients' row table,
+    fp32 weights and base table for :func:`weighted_sum_rows_devtab`.
+    ``tab``: the clients' device table [nsegt][n] (ss = n) or [1][n]
+    (ss = 0); ``base``: nseg virtual bases (host ints) or None.  Returns
+    (sel, sub_tab, sub_w, sub_base) device views of one allocation: sel
+    int32 [2 + n] = certified, valid, order."""
+    n = int(buf.shape[1])
+    msel = min(int(m), n)
+    nsb = len(base) if base is not None else 0
+    w_sel = (2 + n + 1) // 2
+    w_tab = nsegt * msel
+    w_w = (msel + 1) // 2
+    blob = torch.empty(4 * n + w_sel + w_tab + w_w + nsb, dtype=torch.int64,
+                       device=buf.device)
+    work = blob[:4 * n]
+    o = 4 * n
+    sel = blob[o:o + w_sel].view(torch.int32)[:2 + n]
+    o += w_sel
+    sub_tab = blob[o:o + w_tab].view(nsegt, msel)
+    o += w_tab
+    sub_w = blob[o:o + w_w].view(torch.float32)[:msel]
+    o += w_w
+    sub_base = blob[o:o + nsb] if nsb else None
+    sz = _np.ascontiguousarray(sizes, dtype=_np.float64)
+    bt = _np.ascontiguousarray(base, dtype=_np.int64) if nsb else None
+    L.check(L.load().fsagg_krum_select_f32(
+        buf.data_ptr(), n, int(nseg), int(f), int(m), int(bool(ordered)),
+        sz.ctypes.data, int(bool(ignore_weight)),
+        bt.ctypes.data if bt is not None else None, tab.data_ptr(), int(ss),
+        int(nsegt), work.data_ptr(), sel.data_ptr(), sub_tab.data_ptr(),
+        sub_w.data_ptr(), sub_base.data_ptr() if nsb else None,
+        _stream(buf.device)), 'fsagg_krum_select_f32')
+    return sel, sub_tab, sub_w, sub_base
+
+
+def weighted_sum_rows_devtab(layout, tab, ss, n, weights, out, base=None):
+    """fsagg_weighted_sum_rows_f32 over a row table that already lives on
+    the device ([nseg][n] virtual bases with ss = n, or [1][n] with ss = 0;
+    device fp32 ``weights``; ``base`` a device [nseg] table or None) into
+    the flat ``out`` bucket — the average behind :func:`krum_select`."""
+    lib = L.load()
+    dev = out.device
+    unit = lib.fsagg_wsum_chunk_elems_n(layout.numel, n)
+    chunks, nchunk = layout.row_chunks(unit, dev, 0, None)
+    if nchunk == 0:
+        return out
+    rows = L.Rows(tab.data_ptr(), int(ss), int(n), max(len(layout.keys), 1))
+    L.check(lib.fsagg_weighted_sum_rows_f32(
+        ctypes.byref(rows), chunks.data_ptr(), nchunk, unit,
+        weights.data_ptr(), None,
+        base.data_ptr() if base is not None else None,
+        1 if base is not None else 0, out.data_ptr(), _stream(dev)),
+        'fsagg_weighted_sum_rows_f32')
+    return out
 
 
 def pairdist_rows(rs, workspace=None):

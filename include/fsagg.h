@@ -707,6 +707,52 @@ int fsagg_weighted_sum_hosttab_f32(const uint64_t *rows,
                                    int64_t numel, const float *base,
                                    float *const *outs, int nout,
                                    fsagg_stream_t stream);
+/* fsagg_weighted_sum_rows_f32 with the row set's tables on the HOST, in
+ * the launch's kernel arguments: `tab` the segment-major [nseg][n] virtual
+ * bases (fsagg_rows' tab with ss = n; 0 = a client lacking the key),
+ * `weights` / `prescale` (NULL: none) n floats, `base` (NULL: none) nseg
+ * virtual bases of the init model; n <= FSAGG_HOSTTAB_ROWS_MAX_CLIENTS,
+ * n·nseg <= FSAGG_HOSTTAB_ROWS_MAX_PTRS, nseg <= FSAGG_HOSTTAB_ROWS_MAX_SEGS
+ * with a base.  `chunks` / `chunk_elems` as for fsagg_weighted_sum_rows_f32
+ * (a device chunk list, cached per layout).  Same arithmetic, bit for bit.
+ * For small multi-key row sets whose per-call table uploads cost more host
+ * time than the kernel: a multi-Krum selection's average over fresh
+ * uploads (krum_aggregator.py:81-90 through the weighted sum). */
+#define FSAGG_HOSTTAB_ROWS_MAX_CLIENTS 64
+#define FSAGG_HOSTTAB_ROWS_MAX_PTRS 256
+#define FSAGG_HOSTTAB_ROWS_MAX_SEGS 64
+int fsagg_weighted_sum_rows_hosttab_f32(const uint64_t *tab, int n, int nseg,
+                                        const fsagg_chunk *chunks, int nchunk,
+                                        int64_t chunk_elems,
+                                        const float *weights,
+                                        const float *prescale,
+                                        const uint64_t *base, float *out,
+                                        fsagg_stream_t stream);
+/* Krum's certified selection on the device (krum_aggregator.py:75-90):
+ * from the Gram chain's finish buffer `buf` (int32 [5][n][n]: D64, D, the
+ * flags, B — fsagg_pairgram_rows_f32's outputs laid out as the Python
+ * layer's ops._gram_buf), the scores over D64 (the sum of each row's
+ * n − f − 2 smallest), their stable order and the certificate of the
+ * first m (`ordered`: their order too) against the per-pair bounds —
+ * csrc/host/krumcert.cpp's, on the device.  Writes `sel` (int32 [2 + n]:
+ * certified, valid — no flagged pair and n − f − 2 > 0 —, then the order)
+ * and, for the first min(m, n) clients in that order, the row-set table
+ * `sub_tab` ([nsegt][msel] from `tab`, the clients' device table [nsegt][n]
+ * with ss = n, or [1][n] with ss = 0), fp32 weights `sub_w` (fedavg
+ * weights of their `sizes`, host fp64 [n]; 1/msel with ignore_weight) and,
+ * with a `base` (host array of nseg device virtual bases), `sub_base`
+ * (int64 [nseg]) — the operands of fsagg_weighted_sum_rows_f32, which the
+ * caller launches behind this call without waiting for the host.
+ * `work`: device fp64 [4n].  n <= FSAGG_KRUMSEL_MAX_CLIENTS, nseg <=
+ * FSAGG_KRUMSEL_MAX_SEGS with a base. */
+#define FSAGG_KRUMSEL_MAX_CLIENTS 256
+#define FSAGG_KRUMSEL_MAX_SEGS 64
+int fsagg_krum_select_f32(const int32_t *buf, int n, int nseg, int f, int m,
+                          int ordered, const double *sizes, int ignore_weight,
+                          const float *const *base, const int64_t *tab,
+                          int64_t ss, int nsegt, double *work, int32_t *sel,
+                          int64_t *sub_tab, float *sub_w, int64_t *sub_base,
+                          fsagg_stream_t stream);
 size_t fsagg_peer_handle_bytes(void);
 int fsagg_peer_alloc(int device, size_t bytes, void **ptr);
 int fsagg_peer_free(int device, void *ptr);

@@ -410,3 +410,49 @@ def test_hosttab_weighted_sum(n):
 def ctypes_p():
     import ctypes
     return ctypes.c_void_p
+
+
+@pytest.mark.parametrize('n', [1, 5, 25])
+def test_rows_hosttab_weighted_sum(n):
+    """A small multi-key row set's weighted sum with its pointer table,
+    weights, prescales and base table in the kernel arguments
+    (fsagg_weighted_sum_rows_hosttab_f32: n <= 64, n·nseg <= 256) equals the
+    device-table kernel bit for bit — keyed rows with absent keys, stack
+    rows, prescales, a per-key base (device tensors) and a bucket base — and
+    makes no table upload."""
+    from federatedscope_amd import _lib as L
+    from federatedscope_amd import ops
+    clients = _clients(n, seed=n + 3)
+    lay, st, keyed, stacked = _sets(clients)
+    assert n * keyed.nseg <= L.FSAGG_HOSTTAB_ROWS_MAX_PTRS
+    # absent keys: client 0 lacks k2, the last client k4
+    ptrs = np.array([[c[k].data_ptr() for k in lay.keys] for c in clients],
+                    dtype=np.int64)
+    ptrs[0, lay.keys.index('k2')] = 0
+    ptrs[-1, lay.keys.index('k4')] = 0
+    holey = ops.RowSet.from_pointers(lay, ptrs, 'cuda', keepalive=clients)
+    rng = np.random.default_rng(n)
+    w = [float(x) for x in rng.random(n)]
+    pre = [float(x) for x in rng.random(n) + 0.5]
+    server = OrderedDict((k, torch.randn(v.shape, device='cuda'))
+                         for k, v in clients[0].items())
+    bp = np.array([server[k].data_ptr() for k in lay.keys], dtype=np.int64)
+    bases = [None, ops.BaseRows.from_pointers(lay, bp, 'cuda',
+                                              keepalive=(server, )),
+             ops.BaseRows.from_bucket(torch.randn(lay.numel, device='cuda'))]
+    wd = torch.tensor(w, dtype=torch.float32, device='cuda')
+    pd = torch.tensor(pre, dtype=torch.float32, device='cuda')
+    # the layout's chunk list (cached per layout) exists before counting
+    ops.weighted_sum_rows(keyed, w, torch.empty(lay.numel, device='cuda'))
+    for rs in (keyed, holey, stacked):
+        for b in bases:
+            for use_pre in (False, True):
+                got = torch.full((lay.numel, ), 7.0, device='cuda')
+                before = ops._RING.uploads
+                ops.weighted_sum_rows(rs, w, got, base=b,
+                                      prescale=pre if use_pre else None)
+                assert ops._RING.uploads == before
+                want = torch.full((lay.numel, ), 7.0, device='cuda')
+                ops.weighted_sum_rows(rs, wd, want, base=b,
+                                      prescale=pd if use_pre else None)
+                assert _key_ranges(lay, got, want), (n, use_pre, b)
