@@ -124,6 +124,7 @@ SIGNATURES['fsagg_pairgram_block8'] = (_c_i, [])
 SIGNATURES['fsagg_pairgram_set_stages'] = (_c_i, [_c_i])
 SIGNATURES['fsagg_pairgram_set_chunks'] = (_c_i, [_c_i])
 SIGNATURES['fsagg_pairgram_set_desync'] = (_c_i, [_c_i])
+SIGNATURES['fsagg_pairgram_set_fused'] = (_c_i, [_c_i])
 SIGNATURES['fsagg_pairgram_rows_segsq_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_sz, _c_p])
 SIGNATURES['fsagg_pairgram_rows_f32'] = (
@@ -183,6 +184,7 @@ SIGNATURES['fsagg_weighted_sum_rows_hosttab_f32'] = (
 SIGNATURES['fsagg_upload_h2d'] = (
     _c_i, [_c_p, _c_p, _c_sz, _c_p, _c_i, _c_i, _c_p, _c_p])
 SIGNATURES['fsagg_upload_wait'] = (_c_i, [_c_i, _c_p])
+SIGNATURES['fsagg_fetch_mapped_u64'] = (_c_i, [_c_p, _c_p, _c_i64, _c_p])
 SIGNATURES['fsagg_weighted_sum_hosttab_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i, _c_i64, _c_p, ctypes.POINTER(_c_p), _c_i,
            _c_p])

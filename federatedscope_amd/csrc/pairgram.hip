@@ -162,7 +162,11 @@ __device__ void plan_pass(const int64_t *__restrict__ seg_lo,
 __global__ __launch_bounds__(2 * kWave) void gram_prefix_kernel(
     const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
     int nseg, int64_t w_sample, int64_t cap_sample, int64_t w_main,
-    GramCtl cs, GramCtl cm) {
+    GramCtl cs, GramCtl cm, unsigned *__restrict__ tickets, int ntickets) {
+  // the fused tail's arrival tickets (vector stores: per-lane addresses)
+  for (int i = int(threadIdx.x); i < ntickets; i += 2 * kWave)
+    __hip_atomic_store(tickets + i, 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   if (threadIdx.x < kWave)
     plan_pass(seg_lo, seg_end, nseg, w_sample, cap_sample, cs);
   else
@@ -411,6 +415,64 @@ __device__ __forceinline__ void finish_pair(int q, const double *segsq,
   ill[q] = (!inf && close && dist < __builtin_inff()) ? 0u : 1u;
   // the bound on |D − the exact per-key distances' sum|, rounded up to fp32
   if (B) B[q] = inf ? __builtin_inff() : __double2float_ru(bound);
+}
+
+// finish_pair of pair q, stored at q and at its mirror q2 (the key sums
+// are symmetric, so both entries are the same values): the keys' d² and
+// bounds are loaded eight keys at a time (a loop of dependent loads costs
+// the fused tail's last workgroups one memory round trip per key — they
+// read other workgroups' fresh stores, which no cache holds); the
+// arithmetic is finish_pair's, in the same order.
+__device__ __forceinline__ void finish_pair_sym(int q, int q2,
+                                                const double *segsq,
+                                                const double *err, int n,
+                                                int nseg, double tol,
+                                                float *D, uint32_t *ill,
+                                                float *B, double *D64) {
+  if (q / n == q % n) {
+    finish_pair(q, segsq, err, n, nseg, tol, D, ill, B, D64);
+    return;
+  }
+  const int64_t nn = int64_t(n) * n;
+  float dist = 0.0f;
+  double sum_d = 0.0, bound = 0.0;
+  bool inf = false;
+  for (int s0 = 0; s0 < nseg; s0 += 8) {
+    double d2v[8], ev[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t at = int64_t(min(s0 + j, nseg - 1)) * nn + q;
+      d2v[j] = segsq[at];
+      ev[j] = err[at];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (s0 + j >= nseg) break;
+      const double d2 = d2v[j], e = ev[j];
+      const double d = sqrt(d2);
+      dist = add_rn(dist, float(d));
+      sum_d += d;
+      inf = inf || !(e < __builtin_inf());
+      if (e > 0.0) {
+        const double up = sqrt(d2 + e) - d;
+        const double dn = d - sqrt(fmax(d2 - e, 0.0));
+        bound += fmax(up, dn);
+      }
+    }
+  }
+  const bool close = !(tol < __builtin_inf()) || bound <= tol * sum_d;
+  const uint32_t flag = (!inf && close && dist < __builtin_inff()) ? 0u : 1u;
+  const float bq = inf ? __builtin_inff() : __double2float_ru(bound);
+  D[q] = dist;
+  ill[q] = flag;
+  if (B) B[q] = bq;
+  if (D64) D64[q] = sum_d;
+  if (q2 != q) {
+    D[q2] = dist;
+    ill[q2] = flag;
+    if (B) B[q2] = bq;
+    if (D64) D64[q2] = sum_d;
+  }
 }
 
 // Staged loads (kGramStaged): the chunk streams through LDS in stages of
@@ -967,6 +1029,157 @@ __global__ __launch_bounds__(256) void gram_key_kernel(
   err[o + int64_t(b) * n + a] = er;
 }
 
+// ---- Fused tail (round 6): the centre pick behind the sample pass's pair
+// sums, and key + finish in one launch behind the main pass's level-1 sums.  Both
+// hand results between workgroups of one launch by an arrival ticket (the
+// in-launch split-K recipe of the CDNA guide, write-through form: the
+// handed-off values are stored sc1, every storing wave drains its stores,
+// the workgroup's barrier, one lane's relaxed agent-scope ticket add; the
+// workgroup whose add comes last takes an agent-scope acquire fence and
+// reads the others' stores with plain loads).
+// The tickets are zeroed by gram_prefix_kernel at the head of every chain.
+
+// A handed-off store: write-through (global_store … sc1, agent scope), so
+// the hand-off needs no release fence — a release (buffer_wbl2) in each of
+// the tail's 120 workgroups at C4 cost the first build ~80 µs, the
+// write-backs of one XCD's L2 running one after another.
+__device__ __forceinline__ void store_wt(double *p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The drain + ticket of one workgroup whose handed-off bytes were all
+// stored write-through (store_wt); true in every thread of the workgroup
+// that drew the last ticket (after its acquire).
+__device__ __forceinline__ bool last_arrival(unsigned *ticket,
+                                             unsigned arrivals,
+                                             int *flag_lds) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(
+        ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == arrivals - 1u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag_lds = last;
+  }
+  __syncthreads();
+  return *flag_lds != 0;
+}
+
+// gram_centre_pairs_kernel, and the last of its ntpg workgroups picks the
+// centre from every pair's row sums (gram_centre_pick_kernel's loop).
+__global__ __launch_bounds__(320) void gram_centre_fused_kernel(
+    const double *__restrict__ partial, GramCtl ctl, int nseg, int n, int T,
+    double *__restrict__ rsum, unsigned *__restrict__ ticket,
+    int *__restrict__ centre) {
+  __shared__ double dg[32];
+  __shared__ double dd[16][17];
+  __shared__ double tot[256];
+  __shared__ int flag;
+  const int p = blockIdx.x, e = threadIdx.x;
+  const int ntpg = T * (T + 1) / 2, nch = ctl.prefix[nseg];
+  int t, u;
+  tp_tiles(p, T, t, u);
+  // waves 0-3 the block's entries, wave 4 the two tiles' diagonals, at the
+  // same time (pair_block's sums)
+  double gab = 0.0;
+  if (e < 256) {
+    gab = sum_items(partial, 0, nch, ntpg, p, e);
+  } else if (e < 256 + 32) {
+    const int q = e - 256, tt = q < 16 ? t : u;
+    dg[q] = sum_items(partial, 0, nch, ntpg, pair_index(tt, tt, T),
+                      diag_entry(q & 15));
+  }
+  __syncthreads();
+  const int l = e & 63, r = (e >> 6) & 3, ia = 4 * (l >> 4) + r, ib = l & 15;
+  if (e < 256) {
+    double d = 0.0;
+    if (16 * t + ia < n && 16 * u + ib < n) {
+      const double d2 = dg[ia] + dg[16 + ib] - 2.0 * gab;
+      d = d2 > 0.0 ? sqrt(d2) : 0.0;
+    }
+    dd[ia][ib] = d;
+  }
+  __syncthreads();
+  if (e < 32) {
+    double sum = 0.0;
+    for (int j = 0; j < 16; ++j) sum += e < 16 ? dd[e][j] : dd[j][e - 16];
+    store_wt(rsum + p * 32 + e, sum);
+  }
+  if (!last_arrival(ticket, unsigned(gridDim.x), &flag)) return;
+  const int a = e;
+  double sum = 0.0;
+  if (a < n && a < 256) {
+    const int ta = a >> 4, i = a & 15;
+    for (int v = 0; v < T; ++v)
+      sum += ta <= v ? rsum[pair_index(ta, v, T) * 32 + i]
+                     : rsum[pair_index(v, ta, T) * 32 + 16 + i];
+  }
+  if (a < 256) tot[a] = sum;
+  __syncthreads();
+  if (a == 0) {
+    int best = 0;
+    for (int b = 1; b < n; ++b)
+      if (tot[b] < tot[best]) best = b;
+    *centre = best;
+  }
+}
+
+// gram_key_kernel (grid nseg x ntpg: the pair's Gram block summed over the
+// key's first-level groups, d² and bound at (a, b) and (b, a)) with the
+// finish fused: the last of tile pair p's nseg workgroups finishes the
+// block's pairs (finish_pair_sym, as gram_finish_kernel) from every key's
+// d² and bound.  The first-level sums stay a kernel of their own
+// (gram_reduce1_kernel, one workgroup per group and tile pair): summed here
+// per key they ran one memory round trip per group, and the largest key's
+// ~20 groups in a row took 90 µs at C4 (profiles/r06/gram_fused_ab*.jsonl).
+__global__ __launch_bounds__(320) void gram_keyfin_kernel(
+    const double *__restrict__ red, GramCtl ctl, int n, int T,
+    const int64_t *__restrict__ seg_lo, const int64_t *__restrict__ seg_end,
+    int nseg, double *__restrict__ segsq, double *__restrict__ err,
+    unsigned *__restrict__ ticket, double tol, float *__restrict__ D,
+    uint32_t *__restrict__ ill, float *__restrict__ B,
+    double *__restrict__ D64) {
+  __shared__ double dg[32];
+  __shared__ int flag;
+  const int s = blockIdx.x, p = blockIdx.y, e = threadIdx.x;
+  const int ntpg = T * (T + 1) / 2;
+  int t, u;
+  tp_tiles(p, T, t, u);
+  // waves 0-3 the block's 256 entries, wave 4 the two tiles' diagonals
+  // (at the same time: the first build summed them behind the entries)
+  double gab = 0.0;
+  if (e < 256) {
+    gab = sum_items(red, ctl.gprefix[s], ctl.gprefix[s + 1], ntpg, p, e);
+  } else if (e < 256 + 32) {
+    const int d = e - 256;
+    const int tt = d < 16 ? t : u;
+    dg[d] = sum_items(red, ctl.gprefix[s], ctl.gprefix[s + 1], ntpg,
+                      pair_index(tt, tt, T), diag_entry(d & 15));
+  }
+  __syncthreads();
+  const int l = e & 63, r = (e >> 6) & 3, ia = 4 * (l >> 4) + r, ib = l & 15;
+  const int a = e < 256 ? 16 * t + ia : n, b = 16 * u + ib;
+  if (a < n && b < n && !(t == u && ia > ib)) {
+    double d2, er;
+    segsq_pair(dg[ia], dg[16 + ib], gab, a == b, seg_end[s] - seg_lo[s], d2,
+               er);
+    const int64_t o = int64_t(s) * n * n;
+    store_wt(segsq + o + int64_t(a) * n + b, d2);
+    store_wt(err + o + int64_t(a) * n + b, er);
+    store_wt(segsq + o + int64_t(b) * n + a, d2);
+    store_wt(err + o + int64_t(b) * n + a, er);
+  }
+  if (!D) return;
+  if (!last_arrival(ticket + p, unsigned(nseg), &flag)) return;
+  if (a < n && b < n)
+    finish_pair_sym(a * n + b, b * n + a, segsq, err, n, nseg, tol, D, ill,
+                    B, D64);
+}
+
 // The finish of a sharded call, after the ranks' d² and bounds were summed
 // (fsagg_pairgram_finish_f32): finish_pair on every pair.
 __global__ __launch_bounds__(256) void gram_finish_kernel(
@@ -1359,6 +1572,11 @@ std::atomic<int> g_main_chunks{kMainChunks};
 // blocks, 2: bit 8, 3: bit 9), bits 2+ the delay in 512-cycle sleeps;
 // fsagg_pairgram_set_desync
 std::atomic<int> g_desync{0};
+// 1 (default): the fused tail — the centre picked by the last pair-sum
+// workgroup, key + finish in gram_keyfin_kernel (six launches per chain);
+// 0: the round-5 eight launches (fsagg_pairgram_set_fused, A/B; the results
+// are bit-identical)
+std::atomic<int> g_fused{1};
 
 struct GramPlan {
   int nt;              // tiles of 16 clients
@@ -1436,6 +1654,7 @@ unsigned chunk_grid(const GramPlan &pl, int chunks) {
 struct GramWs {
   GramCtl cs, cm;          // sample and main pass plans
   int *centre;
+  unsigned *tickets;       // [ntpg] keyfin, [ntpg] the centre pick
   double *partial, *red, *rsum;
 };
 
@@ -1462,6 +1681,7 @@ size_t gram_ws_layout(int n, int64_t numel, int nseg, void *ws, GramWs *w) {
   };
   const GramCtl cs = ctl(), cm = ctl();
   char *p_c = take(256),
+       *p_tk = take(sizeof(unsigned) * (ntp + 1)),
        *p_rs = take(sizeof(double) * ntp * 32),
        *p_red = take(sizeof(double) * groups * ntp * 256),
        *p_part = take(sizeof(double) * chunks * ntp * 256);
@@ -1469,6 +1689,7 @@ size_t gram_ws_layout(int n, int64_t numel, int nseg, void *ws, GramWs *w) {
     w->cs = cs;
     w->cm = cm;
     w->centre = reinterpret_cast<int *>(p_c);
+    w->tickets = reinterpret_cast<unsigned *>(p_tk);
     w->rsum = reinterpret_cast<double *>(p_rs);
     w->red = reinterpret_cast<double *>(p_red);
     w->partial = reinterpret_cast<double *>(p_part);
@@ -1538,17 +1759,24 @@ void gram_launch(const float *const *tab, int64_t ss, int n,
                  double *err, double tol, float *D, uint32_t *ill, float *B,
                  double *D64, hipStream_t st) {
   const int T = pl.nt;
+  const bool fused = g_fused.load(std::memory_order_relaxed) != 0;
   hipLaunchKernelGGL(gram_prefix_kernel, dim3(1), dim3(2 * kWave), 0, st,
                      seg_lo, seg_end, nseg, kSampleChunk, kSampleCoords, pl.w,
-                     w.cs, w.cm);
+                     w.cs, w.cm, w.tickets, pl.ntpg + 1);
   // 1. the centre: Gram of the first kSampleCoords of every key, raw
   gram_pass<NT, LINES, false>(tab, ss, n, seg_lo, seg_end, nseg, pl, w.cs,
                               kSampleChunk, kSampleCoords, nullptr, w.partial,
                               pl.sample_chunks, st);
-  hipLaunchKernelGGL(gram_centre_pairs_kernel, dim3(unsigned(pl.ntpg)),
-                     dim3(256), 0, st, w.partial, w.cs, nseg, n, T, w.rsum);
-  hipLaunchKernelGGL(gram_centre_pick_kernel, dim3(1), dim3(256), 0, st,
-                     w.rsum, n, T, w.centre);
+  if (fused) {
+    hipLaunchKernelGGL(gram_centre_fused_kernel, dim3(unsigned(pl.ntpg)),
+                       dim3(320), 0, st, w.partial, w.cs, nseg, n, T, w.rsum,
+                       w.tickets + pl.ntpg, w.centre);
+  } else {
+    hipLaunchKernelGGL(gram_centre_pairs_kernel, dim3(unsigned(pl.ntpg)),
+                       dim3(256), 0, st, w.partial, w.cs, nseg, n, T, w.rsum);
+    hipLaunchKernelGGL(gram_centre_pick_kernel, dim3(1), dim3(256), 0, st,
+                       w.rsum, n, T, w.centre);
+  }
   // 2. the centred Gram of every key, its d² and bounds
   gram_pass<NT, LINES, true>(tab, ss, n, seg_lo, seg_end, nseg, pl, w.cm,
                              pl.w, int64_t(0), w.centre, w.partial,
@@ -1556,6 +1784,13 @@ void gram_launch(const float *const *tab, int64_t ss, int n,
   hipLaunchKernelGGL(gram_reduce1_kernel,
                      dim3(unsigned(pl.main_groups), unsigned(pl.ntpg)),
                      dim3(256), 0, st, w.partial, w.cm, nseg, pl.ntpg, w.red);
+  if (fused) {
+    hipLaunchKernelGGL(gram_keyfin_kernel,
+                       dim3(unsigned(nseg), unsigned(pl.ntpg)), dim3(320), 0,
+                       st, w.red, w.cm, n, T, seg_lo, seg_end, nseg, segsq,
+                       err, w.tickets, tol, D, ill, B, D64);
+    return;
+  }
   hipLaunchKernelGGL(gram_key_kernel,
                      dim3(unsigned(nseg), unsigned(pl.ntpg)), dim3(256), 0,
                      st, w.red, w.cm, n, T, seg_lo, seg_end, segsq, err);
@@ -1573,6 +1808,10 @@ using namespace fsagg;
 
 extern "C" int fsagg_pairgram_set_block8(int on) {
   return g_block8.exchange(on < 0 ? 1 : (on > 3 ? 3 : on));
+}
+
+extern "C" int fsagg_pairgram_set_fused(int on) {
+  return g_fused.exchange(on < 0 ? 1 : (on > 0 ? 1 : 0));
 }
 
 extern "C" int fsagg_pairgram_set_stages(int mode) {

@@ -1450,11 +1450,13 @@ def pairgram_rows_dist_graph(rs, tol):
     lib.fsagg_pairgram_set_chunks(chunks)
     desync = lib.fsagg_pairgram_set_desync(0)
     lib.fsagg_pairgram_set_desync(desync)
+    fused = lib.fsagg_pairgram_set_fused(-1)
+    lib.fsagg_pairgram_set_fused(fused)
     stream = torch._C._cuda_getCurrentRawStream(rs.device.index)
     host = rs.host.T if rs._segmajor is None else rs._segmajor
     key = ('pairgram', rs.device.index, stream, host.shape, rs.ss, rs.n,
            rs.nseg, lay.signature(), float(tol), lib.fsagg_pairgram_block8(),
-           stages, chunks, desync)
+           stages, chunks, desync, fused)
     e = _GRAPHS.lookup(key)
     if e is None:
         need = max(int(lib.fsagg_pairgram_workspace_bytes(
@@ -1465,10 +1467,18 @@ def pairgram_rows_dist_graph(rs, tol):
         seg_lo, seg_end = lay.seg_bounds(rs.device, 0, lay.numel, None)
         buf = _gram_buf(rs.n, rs.device)[0]
         tab = torch.empty(host.size, dtype=torch.int64, device=rs.device)
+        # the row table's pinned source: the graph's first kernel reads it
+        # (fsagg_fetch_mapped_u64), the host refills it before each replay
+        pin = torch.empty(host.size, dtype=torch.int64, pin_memory=True)
+        pin_np = pin.numpy().reshape(host.shape)
+        done = torch.cuda.Event()
         rows = L.Rows(tab.data_ptr(), rs.ss, rs.n, rs.nseg)
-        _copy_table(host, tab, rs.device)
+        pin_np[...] = host
 
         def launch():
+            L.check(lib.fsagg_fetch_mapped_u64(
+                pin.data_ptr(), tab.data_ptr(), host.size,
+                _stream(rs.device)), 'fsagg_fetch_mapped_u64')
             L.check(lib.fsagg_pairgram_rows_f32(
                 ctypes.byref(rows), seg_lo.data_ptr(), seg_end.data_ptr(),
                 max(lay.numel, 1), float(tol), sq2[0].data_ptr(),
@@ -1479,12 +1489,18 @@ def pairgram_rows_dist_graph(rs, tol):
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             launch()
-        _GRAPHS.put(key, (g, buf, tab, (rows, ws, sq2, seg_lo, seg_end)))
+        done.record()
+        _GRAPHS.put(key, (g, buf, tab, (pin_np, done),
+                          (rows, ws, sq2, seg_lo, seg_end, pin)))
         rs._gram_tab = tab
         return (buf,) + gram_views(buf)
-    g, buf, tab, _ = e
-    _copy_table(host, tab, rs.device)
+    g, buf, tab, (pin_np, done), _ = e
+    # the previous replay's fetch has read the pinned table (a caller that
+    # consumed that replay's outputs has waited for it already: no wait)
+    done.synchronize()
+    pin_np[...] = host
     g.replay()
+    done.record()
     # the chain's own device copy of this call's row table (valid until the
     # next call of the shape): krum_select gathers the selection from it
     rs._gram_tab = tab

@@ -541,6 +541,12 @@ int fsagg_pairgram_set_chunks(int chunks);
  * bits 2+: the delay in 512-cycle sleeps; 0 = off, the default).  Returns
  * the previous setting. */
 int fsagg_pairgram_set_desync(int mode);
+/* A/B knob: 1 (default) the fused chain tail — the centre picked by the
+ * last of the sample pass's pair-sum workgroups, each key's d², bounds and
+ * the finish in one launch (six launches per chain); 0 the round-5 chain of
+ * eight launches; < 0 restores the default.  The results are
+ * bit-identical.  Returns the previous setting. */
+int fsagg_pairgram_set_fused(int on);
 int fsagg_pairgram_rows_segsq_f32(const fsagg_rows *rows,
                                   const int64_t *seg_lo,
                                   const int64_t *seg_end, int64_t numel,
@@ -701,6 +707,13 @@ int fsagg_upload_h2d(void *dst, const void *src, size_t nbytes, void *stage,
                      int slot, int nslot, fsagg_stream_t copy_stream,
                      fsagg_stream_t consumer);
 int fsagg_upload_wait(int slot, fsagg_stream_t stream);
+/* A kernel copies `n` 8-byte words from pinned, device-mapped host memory
+ * `host_src` (hipHostMalloc / torch pin_memory) into device `dst` on
+ * `stream` — capturable into a HIP graph, so a replayed launch chain reads
+ * its per-call row table from a fixed pinned buffer that the host refills
+ * before each replay (no copy-engine call per replay). */
+int fsagg_fetch_mapped_u64(const void *host_src, void *dst, int64_t n,
+                           fsagg_stream_t stream);
 int fsagg_weighted_sum_hosttab_f32(const uint64_t *rows,
                                    const float *weights,
                                    const float *prescale, int n,

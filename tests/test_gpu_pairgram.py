@@ -230,6 +230,45 @@ def test_pairgram_compact_stages(n):
     _check(got, err, D, flags, B, _fp64_segsq_dev(clients, lay))
 
 
+@pytest.mark.parametrize('n', [2, 17, 50, 64, 65, 100, 129, 200, 256])
+def test_pairgram_fused_tail(n):
+    """The fused chain tail (fsagg_pairgram_set_fused 1, the default: the
+    centre picked by the last pair-sum workgroup, each key's d² + bounds +
+    the finish in one launch whose last workgroup per tile pair finishes
+    it) against the round-5 eight-launch chain (0) on the same rows, keyed
+    and stacked: the same sums in the same order, so d², bounds, D, flags
+    and B are identical bit for bit."""
+    from federatedscope_amd import _lib as L
+    clients = _clients(n, sizes=[70_001, 4097, 33, 1_000_000] if n <= 100
+                       else [4097, 33, 200_003], seed=n + 11)
+    lay, _, keyed, stacked = _sets(clients)
+    from federatedscope_amd import ops
+    from federatedscope_amd.core.aggregators._engine import _GRAM_TOL
+    lib = L.load()
+
+    def chain(rs):
+        # the whole chain with its finish (fsagg_pairgram_rows_f32): buf =
+        # D64, D, ill, B; sq2 = every key's d² and bound
+        out = ops.pairgram_rows_dist(rs, _GRAM_TOL)
+        return [out[0].cpu().numpy(), out[5].cpu().numpy()]
+    res = {}
+    for mode in (0, 1):
+        prev = lib.fsagg_pairgram_set_fused(mode)
+        try:
+            res[mode] = [_gram(keyed), _gram(stacked), _gram(keyed),
+                         chain(keyed), chain(stacked)]
+        finally:
+            lib.fsagg_pairgram_set_fused(prev)
+    for a, b in zip(res[0], res[1]):
+        for x, y in zip(a, b):
+            assert np.asarray(x).tobytes() == np.asarray(y).tobytes(), n
+    for x, y in zip(res[1][0], res[1][2]):
+        assert np.asarray(x).tobytes() == np.asarray(y).tobytes(), n
+    got, err, D, flags, B = res[1][0]
+    assert not flags.any()
+    _check(got, err, D, flags, B, _fp64_segsq_dev(clients, lay))
+
+
 def test_pairgram_unaligned_rows():
     """Key tensors at 4-B offsets: the per-element load path."""
     from federatedscope_amd import ops
@@ -543,3 +582,26 @@ def test_pairgram_stress_families(family):
     if log:
         with open(log, 'a') as fh:
             fh.write(json.dumps(rec) + '\n')
+
+
+def test_pairgram_graph_fresh_tables():
+    """The captured chain (ops.pairgram_rows_dist_graph: one graph per
+    shape whose first kernel fetches the row table from a pinned buffer
+    the host refills per call) over three client sets of one shape at
+    different addresses, in alternation and back to back without a
+    synchronize between the calls: every call's buffer is bit-identical to
+    the eager chain on the same rows."""
+    from federatedscope_amd import ops
+    from federatedscope_amd.core.aggregators._engine import _GRAM_TOL
+    sets = []
+    for seed in (1, 2, 3):
+        clients = _clients(37, sizes=[4097, 33, 70_001], seed=seed)
+        sets.append(_sets(clients)[2])
+    want = [ops.pairgram_rows_dist(rs, _GRAM_TOL)[0].cpu().numpy()
+            for rs in sets]
+    got = []
+    for i in (0, 1, 2, 1, 0, 2, 2, 0):
+        buf = ops.pairgram_rows_dist_graph(sets[i], _GRAM_TOL)[0]
+        got.append((i, buf.to('cpu', non_blocking=False).numpy().copy()))
+    for i, g in got:
+        assert g.tobytes() == want[i].tobytes(), i

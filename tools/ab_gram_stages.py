@@ -5,7 +5,9 @@ stages in flight) against 0 the round-5 full-tile stages (16·NT rows + the
 centre's, one in flight), interleaved, on C4's layout (ConvNet2-h2048,
 6.6M, separately allocated keys) for the given n (default 50 100): median
 of 15 event-timed calls of the whole chain (fsagg_pairgram_rows_f32) per
-round, 4 rounds; D64 must be identical bit for bit.  tools only."""
+round, 4 rounds; D64 must be identical bit for bit.  KNOB=fused: the fused
+chain tail (fsagg_pairgram_set_fused 1) against the round-5 eight launches
+(0) instead.  tools only."""
 import json
 import os
 import statistics
@@ -26,6 +28,9 @@ def main():
     from federatedscope_amd.core.aggregators._engine import _GRAM_TOL
     from federatedscope_amd.layout import BucketLayout
     lib = L.load()
+    knob = os.environ.get('KNOB', 'stages')
+    setk = (lib.fsagg_pairgram_set_fused if knob == 'fused'
+            else lib.fsagg_pairgram_set_stages)
     dev = torch.device('cuda', 0)
     ns = [int(a) for a in sys.argv[1:]] or [50, 100]
     for n in ns:
@@ -40,13 +45,13 @@ def main():
         rs = ops.RowSet.from_pointers(lay, ptrs, dev, keepalive=clients)
         bufs = {}
         for mode in (1, 0):
-            lib.fsagg_pairgram_set_stages(mode)
+            setk(mode)
             bufs[mode] = ops.pairgram_rows_dist(rs, _GRAM_TOL)[0].cpu().numpy()
         same = bufs[1].tobytes() == bufs[0].tobytes()
         res = {1: [], 0: []}
         for rnd in range(4):
             for mode in ((1, 0) if rnd % 2 == 0 else (0, 1)):
-                lib.fsagg_pairgram_set_stages(mode)
+                setk(mode)
                 for _ in range(5):
                     ops.pairgram_rows_dist(rs, _GRAM_TOL)
                 torch.cuda.synchronize()
@@ -59,8 +64,8 @@ def main():
                     e1.synchronize()
                     ts.append(e0.elapsed_time(e1))
                 res[mode].append(statistics.median(ts))
-        lib.fsagg_pairgram_set_stages(-1)
-        print(json.dumps({'n': n, 'compact_ms': [round(x, 4) for x in res[1]],
+        setk(-1)
+        print(json.dumps({'n': n, 'knob': knob, 'compact_ms': [round(x, 4) for x in res[1]],
                           'fulltile_ms': [round(x, 4) for x in res[0]],
                           'compact_median': round(statistics.median(res[1]),
                                                   4),
