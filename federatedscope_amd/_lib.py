@@ -125,6 +125,7 @@ SIGNATURES['fsagg_pairgram_set_stages'] = (_c_i, [_c_i])
 SIGNATURES['fsagg_pairgram_set_chunks'] = (_c_i, [_c_i])
 SIGNATURES['fsagg_pairgram_set_desync'] = (_c_i, [_c_i])
 SIGNATURES['fsagg_pairgram_set_fused'] = (_c_i, [_c_i])
+SIGNATURES['fsagg_pairgram_knobs'] = (_c_i64, [])
 SIGNATURES['fsagg_pairgram_rows_segsq_f32'] = (
     _c_i, [_c_p, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_sz, _c_p])
 SIGNATURES['fsagg_pairgram_rows_f32'] = (

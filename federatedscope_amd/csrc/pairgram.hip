@@ -575,7 +575,8 @@ constexpr int compact_smem(int maxi, int nbuf) {
   return red > nbuf * maxi * 1024 ? red : nbuf * maxi * 1024;
 }
 
-template <int NT, bool CENTRED, bool LINES, int MAXI = 0, int NBUF = 2>
+template <int NT, bool CENTRED, bool LINES, int MAXI = 0, int NBUF = 2,
+          bool EARLY = false, bool PRIO = false>
 __global__ __launch_bounds__(kBlk, (NT > kFullTiles ? 1 : 2))
 void gram_chunk_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n, int T,
@@ -691,9 +692,32 @@ void gram_chunk_kernel(
       }
       const int crr = CENTRED ? *centre : 0;
 #pragma unroll
-      for (int p = 0; p < NBUF - 1; ++p)
+      for (int p = 0; p < NBUF - (EARLY ? 0 : 1); ++p)
         if (p < nstage) issue(p);
       for (int st = 0; st < nstage; ++st) {
+        if constexpr (EARLY) {
+          // early release: NBUF stages in flight while one is computed.
+          // Stage st has landed (this wave's loads: vmcnt, the stages
+          // issued after it may stay in flight; every wave's: the
+          // barrier); its fragments go to registers, and once every wave
+          // has read them (the second barrier) the buffer takes stage
+          // st + NBUF — the compute below runs from registers, so the
+          // buffer need not sit idle under it (Little's law: the bytes in
+          // flight per CU set the bandwidth at ~5 µs loaded latency)
+          const int ahead = min(nstage - 1 - st, NBUF - 1);
+          wait_stage<MY>(ahead);
+          const char *buf = smem + (st % NBUF) * sb;
+          float xb[NT][8], cb[8];
+#pragma unroll
+          for (int t = 0; t < NT; ++t) stage_read8(buf, rrow[t], wv, g, xb[t]);
+          if (CENTRED) stage_read8(buf, crr, wv, g, cb);
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          if (st + NBUF < nstage) issue(st + NBUF);
+          Frags<NT> f;
+          kstep_split_c<NT, CENTRED>(xb, cb, kn, f);
+          kstep_mfma<NT>(f, acc);
+          continue;
+        }
         // stage st's loads have landed (this wave's: vmcnt; every wave's:
         // the barrier), every wave is done reading stage st − 1, whose
         // buffer the next issue overwrites
@@ -707,7 +731,10 @@ void gram_chunk_kernel(
         if (CENTRED) stage_read8(buf, crr, wv, g, cb);
         Frags<NT> f;
         kstep_split_c<NT, CENTRED>(xb, cb, kn, f);
+        // A/B (PRIO): the MFMA cluster at priority 1 (CDNA guide T5)
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
         kstep_mfma<NT>(f, acc);
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
       }
       i = nstage * kWaves + wv;
       // the stage buffers are free again (the tail reads global memory)
@@ -1738,6 +1765,32 @@ void gram_pass(const float *const *tab, int64_t ss, int n,
                        dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab,
                        ss, n, pl.nt, seg_lo, seg_end, nseg, ctl, w, cap,
                        centre, partial);
+  } else if (g_compact.load(std::memory_order_relaxed) == 3) {
+    // A/B: the compact stages with the MFMA cluster at priority 1
+    if ((n + 1) / 2 <= compact_maxi3<NT>())
+      hipLaunchKernelGGL(
+          (gram_chunk_kernel<NT, CENTRED, false, compact_maxi3<NT>(), 3,
+                             false, true>),
+          dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab, ss, n, pl.nt,
+          seg_lo, seg_end, nseg, ctl, w, cap, centre, partial);
+    else
+      hipLaunchKernelGGL(
+          (gram_chunk_kernel<NT, CENTRED, false, 8 * NT, 2, false, true>),
+          dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab, ss, n, pl.nt,
+          seg_lo, seg_end, nseg, ctl, w, cap, centre, partial);
+  } else if (g_compact.load(std::memory_order_relaxed) == 2) {
+    // early release: every buffer's stage in flight under the compute
+    if ((n + 1) / 2 <= compact_maxi3<NT>())
+      hipLaunchKernelGGL(
+          (gram_chunk_kernel<NT, CENTRED, false, compact_maxi3<NT>(), 3,
+                             true>),
+          dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab, ss, n, pl.nt,
+          seg_lo, seg_end, nseg, ctl, w, cap, centre, partial);
+    else
+      hipLaunchKernelGGL(
+          (gram_chunk_kernel<NT, CENTRED, false, 8 * NT, 2, true>),
+          dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab, ss, n, pl.nt,
+          seg_lo, seg_end, nseg, ctl, w, cap, centre, partial);
   } else if ((n + 1) / 2 <= compact_maxi3<NT>()) {
     // three compact stage buffers: two stages in flight
     hipLaunchKernelGGL(
@@ -1815,7 +1868,7 @@ extern "C" int fsagg_pairgram_set_fused(int on) {
 }
 
 extern "C" int fsagg_pairgram_set_stages(int mode) {
-  return g_compact.exchange(mode < 0 ? 1 : (mode > 1 ? 1 : mode));
+  return g_compact.exchange(mode < 0 ? 1 : (mode > 3 ? 3 : mode));
 }
 
 extern "C" int fsagg_pairgram_set_desync(int mode) {
@@ -1825,6 +1878,14 @@ extern "C" int fsagg_pairgram_set_desync(int mode) {
 extern "C" int fsagg_pairgram_set_chunks(int chunks) {
   return g_main_chunks.exchange(chunks <= 0 ? kMainChunks
                                             : (chunks < 64 ? 64 : chunks));
+}
+
+extern "C" int64_t fsagg_pairgram_knobs(void) {
+  return int64_t(g_block8.load(std::memory_order_relaxed) & 3) |
+         (int64_t(g_compact.load(std::memory_order_relaxed) & 3) << 2) |
+         (int64_t(g_fused.load(std::memory_order_relaxed) & 1) << 4) |
+         (int64_t(g_desync.load(std::memory_order_relaxed) & 0xffff) << 5) |
+         (int64_t(g_main_chunks.load(std::memory_order_relaxed)) << 21);
 }
 
 extern "C" int fsagg_pairgram_block8(void) {

@@ -67,8 +67,13 @@ class BucketLayout:
         self.numel = max(off, KEY_ALIGN)
 
     def signature(self):
-        return (tuple(self.order), tuple(
-            (k, self.shapes[k]) for k in self.keys), tuple(self.other.items()))
+        sig = self.__dict__.get('_signature')
+        if sig is None:
+            sig = self.__dict__['_signature'] = (
+                tuple(self.order), tuple((k, self.shapes[k])
+                                         for k in self.keys),
+                tuple(self.other.items()))
+        return sig
 
     @property
     def key_numels(self):

@@ -1444,19 +1444,11 @@ def pairgram_rows_dist_graph(rs, tol):
                          L.FSAGG_PAIRGRAM_MAX_CLIENTS)
     lay = rs.layout
     lib = L.load()
-    stages = lib.fsagg_pairgram_set_stages(-1)
-    lib.fsagg_pairgram_set_stages(stages)
-    chunks = lib.fsagg_pairgram_set_chunks(0)
-    lib.fsagg_pairgram_set_chunks(chunks)
-    desync = lib.fsagg_pairgram_set_desync(0)
-    lib.fsagg_pairgram_set_desync(desync)
-    fused = lib.fsagg_pairgram_set_fused(-1)
-    lib.fsagg_pairgram_set_fused(fused)
     stream = torch._C._cuda_getCurrentRawStream(rs.device.index)
     host = rs.host.T if rs._segmajor is None else rs._segmajor
+    # the workgroup-form settings (A/B knobs) select the captured kernels
     key = ('pairgram', rs.device.index, stream, host.shape, rs.ss, rs.n,
-           rs.nseg, lay.signature(), float(tol), lib.fsagg_pairgram_block8(),
-           stages, chunks, desync, fused)
+           rs.nseg, lay.signature(), float(tol), lib.fsagg_pairgram_knobs())
     e = _GRAPHS.lookup(key)
     if e is None:
         need = max(int(lib.fsagg_pairgram_workspace_bytes(

@@ -206,8 +206,9 @@ def test_pairgram_workgroup_settings(setting, n):
                                104, 105, 112])
 def test_pairgram_compact_stages(n):
     """The compact stage buffers (the n client rows, three buffers where
-    they fit: two stages in flight; fsagg_pairgram_set_stages 1, the
-    default) against the round-5 full-tile stages (0) on the same rows:
+    they fit: two stages in flight; fsagg_pairgram_set_stages 1) and the
+    same with early release (2: every buffer's stage in flight under the
+    compute) against the round-5 full-tile stages (0) on the same rows:
     every Gram sum is formed in the same order, so the per-key d², bounds
     and distances are identical bit for bit — both for keyed (separately
     allocated) and stacked rows — and within the fp64 distances' bounds."""
@@ -216,15 +217,17 @@ def test_pairgram_compact_stages(n):
     lay, _, keyed, stacked = _sets(clients)
     lib = L.load()
     res = {}
-    for mode in (0, 1):
+    for mode in (0, 1, 2, 3):
         prev = lib.fsagg_pairgram_set_stages(mode)
         try:
             res[mode] = [_gram(keyed), _gram(stacked)]
         finally:
             lib.fsagg_pairgram_set_stages(prev)
-    for a, b in zip(res[0], res[1]):
-        for x, y in zip(a, b):
-            assert np.asarray(x).tobytes() == np.asarray(y).tobytes(), n
+    for m in (1, 2, 3):
+        for a, b in zip(res[0], res[m]):
+            for x, y in zip(a, b):
+                assert np.asarray(x).tobytes() == np.asarray(y).tobytes(), \
+                    (n, m)
     got, err, D, flags, B = res[1][0]
     assert not flags.any()
     _check(got, err, D, flags, B, _fp64_segsq_dev(clients, lay))

@@ -29,6 +29,9 @@ def main():
     from federatedscope_amd.layout import BucketLayout
     lib = L.load()
     knob = os.environ.get('KNOB', 'stages')
+    # MODES=a,b: the two settings compared (default 1,0; reported as
+    # compact_* = a and fulltile_* = b)
+    ma, mb = [int(x) for x in os.environ.get('MODES', '1,0').split(',')]
     setk = (lib.fsagg_pairgram_set_fused if knob == 'fused'
             else lib.fsagg_pairgram_set_stages)
     dev = torch.device('cuda', 0)
@@ -44,13 +47,13 @@ def main():
                          for c in clients], dtype=np.int64)
         rs = ops.RowSet.from_pointers(lay, ptrs, dev, keepalive=clients)
         bufs = {}
-        for mode in (1, 0):
+        for mode in (ma, mb):
             setk(mode)
             bufs[mode] = ops.pairgram_rows_dist(rs, _GRAM_TOL)[0].cpu().numpy()
-        same = bufs[1].tobytes() == bufs[0].tobytes()
-        res = {1: [], 0: []}
+        same = bufs[ma].tobytes() == bufs[mb].tobytes()
+        res = {ma: [], mb: []}
         for rnd in range(4):
-            for mode in ((1, 0) if rnd % 2 == 0 else (0, 1)):
+            for mode in ((ma, mb) if rnd % 2 == 0 else (mb, ma)):
                 setk(mode)
                 for _ in range(5):
                     ops.pairgram_rows_dist(rs, _GRAM_TOL)
@@ -65,11 +68,11 @@ def main():
                     ts.append(e0.elapsed_time(e1))
                 res[mode].append(statistics.median(ts))
         setk(-1)
-        print(json.dumps({'n': n, 'knob': knob, 'compact_ms': [round(x, 4) for x in res[1]],
-                          'fulltile_ms': [round(x, 4) for x in res[0]],
-                          'compact_median': round(statistics.median(res[1]),
+        print(json.dumps({'n': n, 'knob': knob, 'modes': [ma, mb], 'compact_ms': [round(x, 4) for x in res[ma]],
+                          'fulltile_ms': [round(x, 4) for x in res[mb]],
+                          'compact_median': round(statistics.median(res[ma]),
                                                   4),
-                          'fulltile_median': round(statistics.median(res[0]),
+                          'fulltile_median': round(statistics.median(res[mb]),
                                                    4),
                           'identical': same}), flush=True)
         del clients, rs

@@ -48,19 +48,22 @@ def main():
                          config=cfg(f=10, agg_num=5))
     marks = defaultdict(list)
     t0 = [0.0]
-    on = [False]
+    on = [False, 0]
 
     def wrap(obj, name, label):
         fn = getattr(obj, name)
 
         def w(*a, **k):
             r = fn(*a, **k)
-            if on[0]:
+            if on[0] and len(marks[label]) < on[1]:
                 marks[label].append((time.perf_counter() - t0[0]) * 1e6)
             return r
         setattr(obj, name, w)
     wrap(agg, '_stage_all', '1 staged')
-    wrap(ops, '_copy_table', '2a gram table copied')
+    wrap(ops, '_require_all', '2a0 require_all')
+    wrap(ops._GRAPHS, 'lookup', '2a1 graph lookup')
+    wrap(torch.cuda.CUDAGraph, 'replay', '2a3 replayed')
+    wrap(torch.cuda.Event, 'synchronize', '2a2 event sync (1st)')
     wrap(agg, '_pairdist', '2 gram launched')
     wrap(agg, '_base', '3 base table')
     wrap(ops, 'krum_select', '4 select launched')
@@ -70,6 +73,7 @@ def main():
         models = next_models()
         torch.cuda.synchronize()
         on[0] = it >= 60
+        on[1] = it - 59
         e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
         t0[0] = time.perf_counter()
         e0.record()
