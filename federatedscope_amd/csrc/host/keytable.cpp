@@ -30,8 +30,12 @@
 #include <Python.h>
 #include <torch/csrc/autograd/python_variable.h>
 
+#include <immintrin.h>
+
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -385,7 +389,219 @@ PyObject *text_copy_many(PyObject *, PyObject *args) {
   Py_RETURN_NONE;
 }
 
+// ---------------------------------------------------------------------------
+// host_pack(items, dst_addr[, threads]) -> None
+// The host half of the pinned H2D staging of host-resident client updates
+// (layout.HostStager): `items` is [(src, nbytes, dst_off)] — src a
+// bytes-like object (a CPU fp32 tensor's numpy view) or None for a run of
+// zeros (padding, absent keys) — packed into the pinned buffer at dst_addr.
+// The bytes of all items are split evenly over a persistent pool of
+// threads (no thread start per upload) and written with non-temporal
+// stores: the pinned buffer is only read again by the DMA engine, so the
+// stores skip the read-for-ownership of each destination line (a third of
+// a cached copy's memory traffic).  The GIL is released while the pool
+// copies.
+namespace {
+
+struct PackItem {
+  const char *src;   // nullptr: zeros
+  char *out;
+  size_t n;
+};
+
+__attribute__((target("avx2"))) void nt_copy_avx2(char *d, const char *s,
+                                                  size_t n) {
+  while (n && (reinterpret_cast<uintptr_t>(d) & 31)) {
+    *d++ = s ? *s++ : 0;
+    --n;
+  }
+  const size_t m = n & ~size_t(127);
+  if (s) {
+    for (size_t i = 0; i < m; i += 128) {
+      const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i));
+      const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i + 32));
+      const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i + 64));
+      const __m256i e = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i + 96));
+      _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i), a);
+      _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i + 32), b);
+      _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i + 64), c);
+      _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i + 96), e);
+    }
+  } else {
+    const __m256i z = _mm256_setzero_si256();
+    for (size_t i = 0; i < m; i += 32)
+      _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i), z);
+  }
+  _mm_sfence();
+  if (s)
+    std::memcpy(d + m, s + m, n - m);
+  else
+    std::memset(d + m, 0, n - m);
+}
+
+void plain_copy(char *d, const char *s, size_t n) {
+  if (s)
+    std::memcpy(d, s, n);
+  else
+    std::memset(d, 0, n);
+}
+
+using CopyFn = void (*)(char *, const char *, size_t);
+
+CopyFn pick_copy() {
+  __builtin_cpu_init();
+  return __builtin_cpu_supports("avx2") ? nt_copy_avx2 : plain_copy;
+}
+
+// A fixed pool of worker threads, started on first use and kept: each job
+// hands every worker one byte range of the concatenated items.
+class PackPool {
+ public:
+  void run(const std::vector<PackItem> &items, size_t total, int threads) {
+    std::lock_guard<std::mutex> job(job_mu_);
+    if (threads < 1) threads = 1;
+    if (threads > kMax) threads = kMax;
+    const size_t per_min = size_t(2) << 20;  // below 2 MiB a thread is overhead
+    if (size_t(threads) > total / per_min)
+      threads = int(total / per_min) < 1 ? 1 : int(total / per_min);
+    start(threads - 1);
+    const size_t step = ((total + threads - 1) / threads + 4095) & ~size_t(4095);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      items_ = &items;
+      total_ = total;
+      step_ = step;
+      active_ = threads - 1;
+      pending_ = threads - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work(0);                       // the caller takes range 0
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return pending_ == 0; });
+    items_ = nullptr;
+  }
+
+ private:
+  static constexpr int kMax = 64;
+  void start(int want) {
+    while (int(workers_.size()) < want) {
+      const int id = int(workers_.size()) + 1;
+      workers_.emplace_back([this, id] { loop(id); });
+      workers_.back().detach();
+    }
+  }
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return gen_ != seen; });
+      seen = gen_;
+      const bool mine = id <= active_;
+      lk.unlock();
+      if (!mine) continue;
+      work(id);
+      lk.lock();
+      if (--pending_ == 0) done_cv_.notify_one();
+    }
+  }
+  void work(int part) {
+    static const CopyFn copy = pick_copy();
+    const size_t a = size_t(part) * step_;
+    const size_t b = a + step_ < total_ ? a + step_ : total_;
+    if (a >= b) return;
+    size_t base = 0;
+    for (const auto &it : *items_) {
+      const size_t e = base + it.n;
+      if (e > a && base < b) {
+        const size_t x = a > base ? a - base : 0;
+        const size_t y = (b < e ? b : e) - base;
+        copy(it.out + x, it.src ? it.src + x : nullptr, y - x);
+      }
+      base = e;
+      if (base >= b) break;
+    }
+  }
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> workers_;
+  const std::vector<PackItem> *items_ = nullptr;
+  size_t total_ = 0, step_ = 0;
+  int active_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+};
+
+PackPool *pack_pool() {
+  static PackPool *p = new PackPool();   // never destroyed: detached workers
+  return p;
+}
+
+}  // namespace
+
+PyObject *host_pack(PyObject *, PyObject *args) {
+  PyObject *seq;
+  unsigned long long dst;
+  int threads = 8;
+  if (!PyArg_ParseTuple(args, "OK|i", &seq, &dst, &threads)) return nullptr;
+  if (dst == 0) {
+    PyErr_SetString(PyExc_ValueError, "host_pack: NULL destination");
+    return nullptr;
+  }
+  PyObject *fast = PySequence_Fast(seq, "host_pack takes a sequence");
+  if (!fast) return nullptr;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(fast);
+  std::vector<PackItem> items;
+  std::vector<Py_buffer> views;
+  items.reserve(size_t(n));
+  views.reserve(size_t(n));
+  bool fail = false;
+  for (Py_ssize_t i = 0; i < n && !fail; ++i) {
+    PyObject *obj;
+    long long nb, off;
+    if (!PyArg_ParseTuple(PySequence_Fast_GET_ITEM(fast, i), "OLL", &obj, &nb,
+                          &off)) {
+      fail = true;
+      break;
+    }
+    if (nb < 0 || off < 0) {
+      PyErr_SetString(PyExc_ValueError, "host_pack: negative size");
+      fail = true;
+      break;
+    }
+    const char *src = nullptr;
+    if (obj != Py_None) {
+      Py_buffer v{};
+      if (PyObject_GetBuffer(obj, &v, PyBUF_C_CONTIGUOUS) != 0) {
+        fail = true;
+        break;
+      }
+      views.push_back(v);
+      if (v.len < nb) {
+        PyErr_SetString(PyExc_ValueError, "host_pack: source too short");
+        fail = true;
+        break;
+      }
+      src = static_cast<const char *>(v.buf);
+    }
+    items.push_back({src, reinterpret_cast<char *>(dst) + off, size_t(nb)});
+  }
+  if (!fail) {
+    size_t total = 0;
+    for (const auto &it : items) total += it.n;
+    Py_BEGIN_ALLOW_THREADS
+    pack_pool()->run(items, total, threads);
+    Py_END_ALLOW_THREADS
+  }
+  for (auto &v : views) PyBuffer_Release(&v);
+  Py_DECREF(fast);
+  if (fail) return nullptr;
+  Py_RETURN_NONE;
+}
+
 PyMethodDef kMethods[] = {
+    {"host_pack", host_pack, METH_VARARGS,
+     "host_pack([(src or None, nbytes, dst_off)], dst_addr[, threads]): "
+     "pack host buffers (None: zeros) into pinned memory, non-temporal"},
     {"device_tensor", device_tensor, METH_VARARGS,
      "device_tensor(ptr, numel, kind, device_index) -> Tensor (no ownership)"},
     {"b64_frame", b64_frame, METH_VARARGS,

@@ -12,6 +12,7 @@ A :class:`ClientStack` is the device-resident ``[capacity][numel]`` slab the
 server fills as client updates arrive (host dicts are staged through pinned
 buffers and copied asynchronously) and the aggregators stream over.
 """
+import os
 from collections import OrderedDict
 
 import torch
@@ -264,6 +265,46 @@ def _pinned(numel, slot=0):
     return b[:numel]
 
 
+# A/B: FSAGG_NATIVE_PACK=0 packs through torch copies (BucketLayout.pack_host)
+_NATIVE_PACK_OFF = os.environ.get('FSAGG_NATIVE_PACK', '1') == '0'
+
+
+def _native_pack(layout, model, host):
+    """layout.pack_host through the host extension (_fsagg_host.host_pack:
+    a persistent thread pool, non-temporal stores into the pinned buffer)
+    when every present key is a contiguous CPU fp32 tensor of its layout
+    size; False (nothing written) otherwise.  Byte-identical to pack_host:
+    keys at their offsets, absent keys and padding zero."""
+    if not isinstance(layout, BucketLayout) or _NATIVE_PACK_OFF:
+        return False
+    from .core.aggregators._engine import _host_ext
+    h = _host_ext()
+    if h is None or not hasattr(h, 'host_pack'):
+        return False
+    f32 = torch.float32
+    items = []
+    keys = layout.keys
+    ends = [layout.offsets[k] for k in keys[1:]] + [layout.numel]
+    for k, end in zip(keys, ends):
+        o, m = layout.offsets[k], layout.numels[k]
+        v = model.get(k)
+        if v is None:
+            if k in model:
+                return False
+            items.append((None, 4 * (end - o), 4 * o))
+            continue
+        if not isinstance(v, torch.Tensor) or v.dtype is not f32 or \
+                v.device.type != 'cpu' or v.numel() != m or \
+                not v.is_contiguous():
+            return False
+        if m:
+            items.append((v.detach().numpy(), 4 * m, 4 * o))
+        if end > o + m:
+            items.append((None, 4 * (end - o - m), 4 * (o + m)))
+    h.host_pack(items, host.data_ptr(), torch.get_num_threads())
+    return True
+
+
 class HostStager:
     """Double-buffered host→device staging of client buckets.
 
@@ -291,7 +332,8 @@ class HostStager:
                 layout, model, dst_row, slot, tag):
             return
         host = _pinned(layout.numel, slot)
-        layout.pack_host(model, host)
+        if not _native_pack(layout, model, host):
+            layout.pack_host(model, host)
         with torch.cuda.stream(self.stream):
             dst_row.copy_(host, non_blocking=True)
             ev = torch.cuda.Event()

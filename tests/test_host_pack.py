@@ -1,0 +1,84 @@
+"""The native host pack (_fsagg_host.host_pack): host buffers and zero runs
+packed into one destination by a persistent thread pool with non-temporal
+stores — the host half of layout.HostStager's pinned staging.  CPU only:
+the destination here is ordinary memory."""
+import numpy as np
+import pytest
+
+
+def _ext():
+    from federatedscope_amd.core.aggregators._engine import _host_ext
+    h = _host_ext()
+    if h is None or not hasattr(h, 'host_pack'):
+        pytest.skip('_fsagg_host.so not built')
+    return h
+
+
+@pytest.mark.parametrize('threads', [1, 3, 16])
+def test_host_pack_items_and_zeros(threads):
+    h = _ext()
+    rng = np.random.default_rng(threads)
+    sizes = [1, 7, 4096, 3 << 20, 13, (5 << 20) + 3, 0, 64]
+    srcs = [rng.standard_normal(s).astype(np.float32) for s in sizes]
+    # layout: each item at a 4-B offset with gaps of zeros between some
+    items, off, want = [], 0, []
+    for i, a in enumerate(srcs):
+        items.append((a, a.nbytes, off))
+        want.append((off, a.view(np.uint8)))
+        off += a.nbytes
+        if i % 3 == 1:
+            items.append((None, 4 * 1001, off))
+            want.append((off, np.zeros(4 * 1001, np.uint8)))
+            off += 4 * 1001
+    dst = np.full(off + 64, 0xAB, dtype=np.uint8)
+    h.host_pack(items, dst.ctypes.data, threads)
+    for o, ref in want:
+        assert np.array_equal(dst[o:o + ref.size], ref)
+    assert (dst[off:] == 0xAB).all()          # nothing past the last item
+
+
+def test_host_pack_repeated_and_unaligned():
+    h = _ext()
+    rng = np.random.default_rng(5)
+    a = rng.standard_normal((9 << 20) // 4).astype(np.float32)
+    for shift in (0, 4, 12, 60):
+        dst = np.zeros(a.nbytes + 128, dtype=np.uint8)
+        h.host_pack([(a, a.nbytes, shift)], dst.ctypes.data, 8)
+        assert np.array_equal(dst[shift:shift + a.nbytes], a.view(np.uint8))
+        assert not dst[:shift].any() and not dst[shift + a.nbytes:].any()
+
+
+def test_host_pack_rejects_short_source():
+    h = _ext()
+    a = np.zeros(10, np.float32)
+    dst = np.zeros(100, np.uint8)
+    with pytest.raises(ValueError):
+        h.host_pack([(a, 41, 0)], dst.ctypes.data, 2)
+
+
+def test_native_pack_matches_pack_host():
+    """layout._native_pack against BucketLayout.pack_host on a layout with
+    padding, an absent key and a zero-size key (CPU tensors)."""
+    import torch
+    from collections import OrderedDict
+    from federatedscope_amd.layout import BucketLayout, _native_pack
+    _ext()
+    g = torch.Generator().manual_seed(3)
+    tmpl = OrderedDict([('a', torch.rand(1001, generator=g)),
+                        ('b', torch.rand(3, 5, generator=g)),
+                        ('e', torch.rand(0)),
+                        ('c', torch.rand(70_000, generator=g))])
+    lay = BucketLayout(tmpl)
+    model = OrderedDict((k, torch.rand(v.shape, generator=g))
+                        for k, v in tmpl.items() if k != 'b')
+    want = torch.full((lay.numel,), 7.0)
+    lay.pack_host(model, want)
+    got = torch.full((lay.numel,), -3.0)
+    assert _native_pack(lay, model, got)
+    assert torch.equal(got, want)
+    # a non-contiguous or non-fp32 key: not taken, nothing written
+    bad = OrderedDict(model)
+    bad['c'] = model['c'].double()
+    got2 = torch.full((lay.numel,), -3.0)
+    assert not _native_pack(lay, bad, got2)
+    assert (got2 == -3.0).all()
