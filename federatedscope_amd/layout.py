@@ -275,7 +275,7 @@ def _native_pack(layout, model, host):
     when every present key is a contiguous CPU fp32 tensor of its layout
     size; False (nothing written) otherwise.  Byte-identical to pack_host:
     keys at their offsets, absent keys and padding zero."""
-    if not isinstance(layout, BucketLayout) or _NATIVE_PACK_OFF:
+    if _NATIVE_PACK_OFF or not isinstance(layout, (BucketLayout, RangeStack)):
         return False
     from .core.aggregators._engine import _host_ext
     h = _host_ext()
@@ -283,6 +283,27 @@ def _native_pack(layout, model, host):
         return False
     f32 = torch.float32
     items = []
+    if isinstance(layout, RangeStack):
+        # this rank's pieces only, as RangeStack.pack_host (absent keys are
+        # left as they are: the presence matrix masks them)
+        lay = layout.layout
+        arrs = {}
+        for sp in layout.spans:
+            for k, src, dst, ln in sp:
+                if k not in model:
+                    continue
+                a = arrs.get(k)
+                if a is None:
+                    v = model[k]
+                    if not isinstance(v, torch.Tensor) or \
+                            v.dtype is not f32 or v.device.type != 'cpu' or \
+                            v.numel() != lay.numels[k] or \
+                            not v.is_contiguous():
+                        return False
+                    a = arrs[k] = v.detach().reshape(-1).numpy()
+                items.append((a[src:src + ln], 4 * ln, 4 * dst))
+        h.host_pack(items, host.data_ptr(), torch.get_num_threads())
+        return True
     keys = layout.keys
     ends = [layout.offsets[k] for k in keys[1:]] + [layout.numel]
     for k, end in zip(keys, ends):

@@ -82,3 +82,44 @@ def test_native_pack_matches_pack_host():
     got2 = torch.full((lay.numel,), -3.0)
     assert not _native_pack(lay, bad, got2)
     assert (got2 == -3.0).all()
+
+
+def test_native_pack_range_stack():
+    """The parameter-range shard's pack (RangeStack: this rank's pieces of
+    every key) through host_pack equals RangeStack.pack_host."""
+    import torch
+    from collections import OrderedDict
+    from federatedscope_amd.layout import (BucketLayout, RangeStack,
+                                           _native_pack)
+    _ext()
+    g = torch.Generator().manual_seed(4)
+    tmpl = OrderedDict([('a', torch.rand(1001, generator=g)),
+                        ('b', torch.rand(3, 5, generator=g)),
+                        ('c', torch.rand(70_000, generator=g))])
+    lay = BucketLayout(tmpl)
+    # the constructor's span bookkeeping, without its device slab
+    rs = RangeStack.__new__(RangeStack)
+    pieces = [(5, 900), (1010, 40_000), (60_000, lay.numel)]
+    rs.layout = lay
+    rs.pieces = pieces
+    rs.loc, off = [], 0
+    for a, b in pieces:
+        rs.loc.append(off)
+        off += -(-max(b - a, 0) // RangeStack.ALIGN) * RangeStack.ALIGN
+    rs.numel = off
+    rs.spans = []
+    for (a, b), loc in zip(pieces, rs.loc):
+        sp = []
+        for k in lay.keys:
+            o, m = lay.offsets[k], lay.numels[k]
+            x, y = max(a, o), min(b, o + m)
+            if y > x:
+                sp.append((k, x - o, loc + x - a, y - x))
+        rs.spans.append(sp)
+    model = OrderedDict((k, torch.rand(v.shape, generator=g))
+                        for k, v in tmpl.items())
+    want = torch.full((rs.numel,), 5.0)
+    rs.pack_host(model, want)
+    got = torch.full((rs.numel,), 5.0)
+    assert _native_pack(rs, model, got)
+    assert torch.equal(got, want)
