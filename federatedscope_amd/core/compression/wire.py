@@ -142,10 +142,52 @@ class QuantPlan:
         else:
             for j, v in enumerate(sv):
                 scales[j] = scale_to_f32(v)
-        for dt, a, b, wkeys in self.spans:
-            torch.cat([wire[wk].detach().reshape(-1).to('cpu')
-                       for wk in wkeys], out=buf[a:b].view(dt))
+        if not self._pack_native(wire, buf):
+            for dt, a, b, wkeys in self.spans:
+                torch.cat([wire[wk].detach().reshape(-1).to('cpu')
+                           for wk in wkeys], out=buf[a:b].view(dt))
         return buf
+
+    def _pack_native(self, wire, buf):
+        """The code and fp32 regions through _fsagg_host.host_pack (a
+        persistent thread pool, non-temporal stores) when every wire tensor
+        is a contiguous CPU tensor of its region's dtype; False (nothing
+        written) otherwise.  Byte-identical to the torch.cat path."""
+        from ...layout import _NATIVE_PACK_OFF
+        if _NATIVE_PACK_OFF:
+            return False
+        from ..aggregators._engine import _host_ext
+        h = _host_ext()
+        if h is None or not hasattr(h, 'host_pack'):
+            return False
+        if isinstance(wire, dict) and hasattr(h, 'host_pack_dict'):
+            # the dict walk in C++: every region's wire key, offset, bytes
+            from ...layout import _SCALAR_CODE
+            spec = self.__dict__.get('_pack_spec')
+            if spec is None:
+                spec = self._pack_spec = [
+                    (wk, off, self.layout.numels[k] *
+                     torch.empty((), dtype=dt).element_size(),
+                     _SCALAR_CODE[dt], 0)
+                    for k, wk, off, dt in self.regions]
+            return h.host_pack_dict(wire, spec, [], buf.data_ptr(),
+                                    torch.get_num_threads())
+        items = []
+        for dt, a, b, wkeys in self.spans:
+            off = a
+            for wk in wkeys:
+                t = wire[wk]
+                if not isinstance(t, torch.Tensor) or t.dtype != dt or \
+                        t.device.type != 'cpu' or not t.is_contiguous():
+                    return False
+                nb = t.numel() * t.element_size()
+                if nb:
+                    items.append((t.detach().reshape(-1).numpy(), nb, off))
+                off += nb
+            if off != b:
+                return False
+        h.host_pack(items, buf.data_ptr(), torch.get_num_threads())
+        return True
 
 
 class WireStager:

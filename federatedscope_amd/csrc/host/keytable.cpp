@@ -598,7 +598,95 @@ PyObject *host_pack(PyObject *, PyObject *args) {
   Py_RETURN_NONE;
 }
 
+// host_pack_dict(model, spec, zero_runs, dst_addr[, threads]) -> bool
+// host_pack with the dict walk in C++: `spec` is [(key, byte offset,
+// nbytes, scalar type code, absent_ok)] — each key's CPU tensor, which must
+// be contiguous, of that scalar type and exactly nbytes long, goes to
+// dst + offset; an absent key (absent_ok) becomes a run of zeros;
+// `zero_runs` is [(byte offset, nbytes)] of padding.  Returns False, with
+// nothing written, when any present value is not such a tensor or a key
+// without absent_ok is missing (the caller then packs in Python).
+PyObject *host_pack_dict(PyObject *, PyObject *args) {
+  PyObject *model, *spec, *zeros;
+  unsigned long long dst;
+  int threads = 8;
+  if (!PyArg_ParseTuple(args, "OOOK|i", &model, &spec, &zeros, &dst,
+                        &threads))
+    return nullptr;
+  if (!PyDict_Check(model) || dst == 0) Py_RETURN_FALSE;
+  PyObject *fs = PySequence_Fast(spec, "host_pack_dict: spec");
+  if (!fs) return nullptr;
+  PyObject *fz = PySequence_Fast(zeros, "host_pack_dict: zero runs");
+  if (!fz) {
+    Py_DECREF(fs);
+    return nullptr;
+  }
+  std::vector<PackItem> items;
+  const Py_ssize_t ns = PySequence_Fast_GET_SIZE(fs);
+  const Py_ssize_t nz = PySequence_Fast_GET_SIZE(fz);
+  items.reserve(size_t(ns + nz));
+  char *out = reinterpret_cast<char *>(dst);
+  bool ok = true, err = false;
+  for (Py_ssize_t i = 0; i < ns && ok; ++i) {
+    PyObject *key;
+    long long off, nb;
+    int code, absent_ok;
+    if (!PyArg_ParseTuple(PySequence_Fast_GET_ITEM(fs, i), "OLLii", &key,
+                          &off, &nb, &code, &absent_ok)) {
+      err = true;
+      break;
+    }
+    PyObject *v = PyDict_GetItemWithError(model, key);   // borrowed
+    if (!v) {
+      if (PyErr_Occurred()) {
+        err = true;
+        break;
+      }
+      if (!absent_ok) {
+        ok = false;
+        break;
+      }
+      if (nb) items.push_back({nullptr, out + off, size_t(nb)});
+      continue;
+    }
+    if (!THPVariable_Check(v)) {
+      ok = false;
+      break;
+    }
+    const at::Tensor &t = THPVariable_Unpack(v);
+    if (!t.device().is_cpu() || int(t.scalar_type()) != code ||
+        !t.is_contiguous() || (long long)t.nbytes() != nb) {
+      ok = false;
+      break;
+    }
+    if (nb)
+      items.push_back({static_cast<const char *>(t.data_ptr()), out + off,
+                       size_t(nb)});
+  }
+  for (Py_ssize_t i = 0; i < nz && ok && !err; ++i) {
+    long long off, nb;
+    if (!PyArg_ParseTuple(PySequence_Fast_GET_ITEM(fz, i), "LL", &off, &nb)) {
+      err = true;
+      break;
+    }
+    if (nb > 0) items.push_back({nullptr, out + off, size_t(nb)});
+  }
+  Py_DECREF(fs);
+  Py_DECREF(fz);
+  if (err) return nullptr;
+  if (!ok) Py_RETURN_FALSE;
+  size_t total = 0;
+  for (const auto &it : items) total += it.n;
+  Py_BEGIN_ALLOW_THREADS
+  pack_pool()->run(items, total, threads);
+  Py_END_ALLOW_THREADS
+  Py_RETURN_TRUE;
+}
+
 PyMethodDef kMethods[] = {
+    {"host_pack_dict", host_pack_dict, METH_VARARGS,
+     "host_pack_dict(model, [(key, off, nbytes, dtype_code, absent_ok)], "
+     "[(off, nbytes)], dst_addr[, threads]) -> bool"},
     {"host_pack", host_pack, METH_VARARGS,
      "host_pack([(src or None, nbytes, dst_off)], dst_addr[, threads]): "
      "pack host buffers (None: zeros) into pinned memory, non-temporal"},

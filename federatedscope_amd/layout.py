@@ -265,6 +265,9 @@ def _pinned(numel, slot=0):
     return b[:numel]
 
 
+# c10::ScalarType codes of the dtypes the host pack takes
+_SCALAR_CODE = {torch.int8: 1, torch.int16: 2, torch.float32: 6}
+
 # A/B: FSAGG_NATIVE_PACK=0 packs through torch copies (BucketLayout.pack_host)
 _NATIVE_PACK_OFF = os.environ.get('FSAGG_NATIVE_PACK', '1') == '0'
 
@@ -282,6 +285,22 @@ def _native_pack(layout, model, host):
     if h is None or not hasattr(h, 'host_pack'):
         return False
     f32 = torch.float32
+    if isinstance(layout, BucketLayout) and isinstance(model, dict) and \
+            hasattr(h, 'host_pack_dict'):
+        # the dict walk in C++ (one call per upload)
+        spec = layout.__dict__.get('_pack_spec')
+        if spec is None:
+            keys = layout.keys
+            ends = [layout.offsets[k] for k in keys[1:]] + [layout.numel]
+            spec = ([(k, 4 * layout.offsets[k], 4 * layout.numels[k],
+                      _SCALAR_CODE[f32], 1) for k in keys],
+                    [(4 * (layout.offsets[k] + layout.numels[k]),
+                      4 * (e - layout.offsets[k] - layout.numels[k]))
+                     for k, e in zip(keys, ends)
+                     if e > layout.offsets[k] + layout.numels[k]])
+            layout.__dict__['_pack_spec'] = spec
+        return h.host_pack_dict(model, spec[0], spec[1], host.data_ptr(),
+                                torch.get_num_threads())
     items = []
     if isinstance(layout, RangeStack):
         # this rank's pieces only, as RangeStack.pack_host (absent keys are

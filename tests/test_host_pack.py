@@ -123,3 +123,43 @@ def test_native_pack_range_stack():
     got = torch.full((rs.numel,), 5.0)
     assert _native_pack(rs, model, got)
     assert torch.equal(got, want)
+
+
+def test_quant_plan_native_pack_matches_cat():
+    """QuantPlan.pack_host through host_pack (int8 / int16 codes and fp32
+    keys at their regions) is byte-identical to the torch.cat path."""
+    import torch
+    from collections import OrderedDict
+    from federatedscope_amd.core.compression import wire as W
+    _ext()
+    g = torch.Generator().manual_seed(6)
+
+    def codes(shape, dt):
+        lim = 127 if dt == torch.int8 else 32767
+        return torch.randint(-lim, lim + 1, shape, generator=g).to(dt)
+    tmpl = OrderedDict([
+        ('conv.weight_quant', codes((64, 3, 3, 3), torch.int8)),
+        ('conv.weight_scale', torch.tensor(0.01)),
+        ('bn.bias', torch.rand(64, generator=g)),
+        ('fc.weight_quant', codes((10, 5001), torch.int16)),
+        ('fc.weight_scale', torch.tensor(0.002)),
+        ('fc.bias', torch.rand(10, generator=g)),
+        ('head.weight_quant', codes((777,), torch.int8)),
+        ('head.weight_scale', torch.tensor(0.5))])
+    plan = W.QuantPlan(tmpl)
+    up = OrderedDict((k, (codes(v.shape, v.dtype) if v.dtype in
+                          (torch.int8, torch.int16) else
+                          torch.rand(v.shape, generator=g)))
+                     for k, v in tmpl.items())
+    want = torch.full((plan.nbytes,), 0x5A, dtype=torch.uint8)
+    got = want.clone()
+    plan.pack_host(up, got)
+    assert plan._pack_native(up, got)
+    ref = want.clone()
+    # the torch.cat path on the same buffer bytes
+    scales = ref[:4 * max(plan.nscale, 1)].view(torch.float32)
+    for j, sk in enumerate(plan.scale_keys):
+        scales[j] = float(up[sk])
+    for dt, a, b, wkeys in plan.spans:
+        torch.cat([up[wk].reshape(-1) for wk in wkeys], out=ref[a:b].view(dt))
+    assert torch.equal(got, ref)
