@@ -131,6 +131,24 @@ class QuantPlan:
             if sk not in wire:
                 raise KeyError(sk)
 
+    def pack_host_checked(self, wire, buf):
+        """check + pack_host in one native pass when the upload is the
+        common form (a dict of contiguous CPU tensors, 1-element fp32
+        scales): host_pack_dict checks every region's tensor (dtype, byte
+        size) as it packs, which implies :meth:`check`.  False (the caller
+        then checks and packs the general way) otherwise."""
+        if not isinstance(wire, dict):
+            return False
+        sv = [wire.get(sk) for sk in self.scale_keys]
+        if not all(isinstance(v, torch.Tensor) and v.numel() == 1 and
+                   v.dtype == torch.float32 and v.device.type == 'cpu'
+                   for v in sv):
+            return False
+        if sv:
+            scales = buf[:4 * self.nscale].view(torch.float32)
+            torch.cat([v.reshape(1) for v in sv], out=scales)
+        return self._pack_native(wire, buf)
+
     def pack_host(self, wire, buf):
         """Pack one upload into the pinned uint8 buffer ``buf``."""
         scales = buf[:4 * max(self.nscale, 1)].view(torch.float32)
@@ -212,12 +230,13 @@ class WireStager:
         """Stage one upload (a wire dict of host or device tensors) into the
         fp32 row ``dst_row``."""
         plan = self.plan
-        plan.check(wire)
         b = self.i % self.nbuf
-        self.i += 1
         if self.events[b] is not None:
             self.events[b].synchronize()   # the DMA that last read host[b]
-        plan.pack_host(wire, self.host[b])
+        if not plan.pack_host_checked(wire, self.host[b]):
+            plan.check(wire)
+            plan.pack_host(wire, self.host[b])
+        self.i += 1
         with torch.cuda.stream(self.stream):
             self.dev[b].copy_(self.host[b], non_blocking=True)
             ev = torch.cuda.Event()

@@ -163,3 +163,36 @@ def test_quant_plan_native_pack_matches_cat():
     for dt, a, b, wkeys in plan.spans:
         torch.cat([up[wk].reshape(-1) for wk in wkeys], out=ref[a:b].view(dt))
     assert torch.equal(got, ref)
+
+
+def test_quant_plan_checked_pack_rejects_like_check():
+    """pack_host_checked packs exactly when QuantPlan.check would pass: a
+    wrong dtype, a wrong size or a missing scale makes it return False (the
+    caller then raises through check)."""
+    import torch
+    from collections import OrderedDict
+    from federatedscope_amd.core.compression import wire as W
+    _ext()
+    tmpl = OrderedDict([
+        ('conv.weight_quant', torch.zeros(8, 3, dtype=torch.int8)),
+        ('conv.weight_scale', torch.tensor(0.01)),
+        ('bias', torch.zeros(8))])
+    plan = W.QuantPlan(tmpl)
+    buf = torch.zeros(plan.nbytes, dtype=torch.uint8)
+    good = OrderedDict([
+        ('conv.weight_quant', torch.ones(8, 3, dtype=torch.int8)),
+        ('conv.weight_scale', torch.tensor(0.5)),
+        ('bias', torch.full((8,), 2.0))])
+    assert plan.pack_host_checked(good, buf)
+    ref = torch.zeros_like(buf)
+    plan.pack_host(good, ref)
+    assert torch.equal(buf, ref)
+    for bad in (
+            OrderedDict(good, **{'conv.weight_quant':
+                                 torch.ones(8, 3, dtype=torch.int16)}),
+            OrderedDict(good, bias=torch.zeros(9)),
+            OrderedDict((k, v) for k, v in good.items()
+                        if k != 'conv.weight_scale')):
+        assert not plan.pack_host_checked(bad, buf)
+        with pytest.raises((ValueError, KeyError)):
+            plan.check(bad)
