@@ -265,6 +265,9 @@ def _pinned(numel, slot=0):
     return b[:numel]
 
 
+# pinned staging buffers per HostStager (A/B: FSAGG_STAGE_BUFFERS)
+_STAGE_BUFFERS = max(1, int(os.environ.get('FSAGG_STAGE_BUFFERS', '2')))
+
 # c10::ScalarType codes of the dtypes the host pack takes
 _SCALAR_CODE = {torch.int8: 1, torch.int16: 2, torch.float32: 6}
 
@@ -352,7 +355,9 @@ class HostStager:
     overlaps the DMA of client i out of the other buffer; the copies run on
     a side stream and the consumer stream waits on it once at the end."""
 
-    def __init__(self, device, nbuf=2):
+    def __init__(self, device, nbuf=None):
+        if nbuf is None:
+            nbuf = _STAGE_BUFFERS
         self.device = torch.device(device)
         self.stream = torch.cuda.Stream(self.device)
         # the rows being overwritten may still be read by kernels queued on
