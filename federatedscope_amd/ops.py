@@ -1403,7 +1403,14 @@ class _GraphCache:
         self.entries[key] = e
         self.captures += 1
         while len(self.entries) > self.MAX_ENTRIES:
-            self.entries.popitem(last=False)
+            _, old = self.entries.popitem(last=False)
+            # the evicted chain's last replay must have read its pinned
+            # table before the pinned block can go back to torch's host
+            # allocator (which does not see the kernel's read)
+            fetch = old[3] if len(old) > 3 else None
+            if isinstance(fetch, tuple) and len(fetch) == 2 and \
+                    isinstance(fetch[1], torch.cuda.Event):
+                fetch[1].synchronize()
         return e
 
 

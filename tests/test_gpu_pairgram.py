@@ -608,3 +608,22 @@ def test_pairgram_graph_fresh_tables():
         got.append((i, buf.to('cpu', non_blocking=False).numpy().copy()))
     for i, g in got:
         assert g.tobytes() == want[i].tobytes(), i
+
+
+def test_pairgram_graph_cache_eviction():
+    """More captured shapes than the cache holds: every call's buffer still
+    matches the eager chain (evicted entries wait for their last replay's
+    pinned-table fetch before their buffers are released)."""
+    from federatedscope_amd import ops
+    from federatedscope_amd.core.aggregators._engine import _GRAM_TOL
+    cap = ops._GraphCache.MAX_ENTRIES
+    sets = []
+    for j in range(cap + 3):
+        clients = _clients(3 + j, sizes=[4097, 33], seed=100 + j)
+        sets.append(_sets(clients)[2])
+    want = [ops.pairgram_rows_dist(rs, _GRAM_TOL)[0].cpu().numpy()
+            for rs in sets]
+    for rnd in range(2):
+        for j, rs in enumerate(sets):
+            got = ops.pairgram_rows_dist_graph(rs, _GRAM_TOL)[0].cpu()
+            assert got.numpy().tobytes() == want[j].tobytes(), (rnd, j)
