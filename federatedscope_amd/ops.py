@@ -1371,20 +1371,23 @@ def pairgram_rows_dist(rs, tol, workspace=None):
 class _GraphCache:
     """Captured launch chains (HIP graphs, through torch.cuda.CUDAGraph) of
     the multi-kernel paths whose launches cost more host time than their
-    small kernels run: the Gram chain is eight launches (~100 µs of host
+    small kernels run: the Gram chain is six launches (~100 µs of host
     time at C4, against ~10 µs for one graph launch).  One entry per SHAPE
     — client count, table stride, the layout, the tolerance, the library's
     workgroup-form settings, the stream — owning everything the captured
-    kernels' arguments name: a device row table, the workspace, the per-key
-    sums and the output buffer.  A call copies ITS row table (the clients'
-    addresses, fresh or not) into the entry's table on its own stream and
-    replays: so rounds of freshly received uploads replay a graph as well as
-    repeated calls over the same dicts do.  The copy is ordered after the
-    previous replay on that stream, which has read the old table; the
-    outputs are overwritten by the next call of the same shape — a caller
-    consumes them (copies them to the host) before its next call.  The
-    first call of a shape runs the chain eagerly (its result) and captures
-    it (the capture only records launches)."""
+    kernels' arguments name: a pinned host table, a device row table, the
+    workspace, the per-key sums and the output buffer.  A call writes ITS
+    row table (the clients' addresses, fresh or not) into the entry's
+    pinned table, once the previous replay's fetch of it has completed (the
+    entry's event), and replays; the graph's first kernel fetches the
+    pinned table into the device table (fsagg_fetch_mapped_u64).  So rounds
+    of freshly received uploads replay a graph as well as repeated calls
+    over the same dicts do.  The outputs are overwritten by the next call
+    of the same shape — a caller consumes them (copies them to the host)
+    before its next call.  The first call of a shape runs the chain eagerly
+    (its result) and captures it (the capture only records launches).  An
+    evicted entry waits for its last fetch before its buffers go back to
+    torch's allocators."""
     MAX_ENTRIES = 8
 
     def __init__(self):
