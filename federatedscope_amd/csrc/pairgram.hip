@@ -569,6 +569,14 @@ __device__ __forceinline__ void wait_stage(int ahead) {
 // (k = b / 8): blocks b and b + 8 share an XCD, so one chunk's workgroups
 // run on one XCD together and read its rows from that XCD's L2 after the
 // first.
+// cache policy of the stage loads: NT (non-temporal, gfx950 CPol bit 1) —
+// the rows are read once.  Interleaved A/B of the whole chain against plain
+// loads (stages 4; profiles/r06/gram_nt_default_ab.jsonl, medians of 8
+// rounds): n = 40 0.2370 against 0.2458 ms, 50 0.3101 / 0.3112, 64
+// 0.3508 / 0.3519, 66 0.478 / 0.483, 100 0.880 / 0.887, 112 0.885 /
+// 0.897; D64 identical
+constexpr int kStageNT = 2;
+
 template <int NT, bool CENTRED>
 constexpr int compact_smem(int maxi, int nbuf) {
   constexpr int red = 2 * ntp_of(NT) * 4 * kWave * 8;
@@ -576,7 +584,7 @@ constexpr int compact_smem(int maxi, int nbuf) {
 }
 
 template <int NT, bool CENTRED, bool LINES, int MAXI = 0, int NBUF = 2,
-          bool EARLY = false, bool PRIO = false>
+          bool EARLY = false, bool PRIO = false, int AUX = kStageNT>
 __global__ __launch_bounds__(kBlk, (NT > kFullTiles ? 1 : 2))
 void gram_chunk_kernel(
     const float *const *__restrict__ tab, int64_t ss, int n, int T,
@@ -680,7 +688,7 @@ void gram_chunk_kernel(
               (__attribute__((address_space(1))) void *)(src[m] + st * kStage),
               (__attribute__((address_space(3))) void *)(uintptr_t)(buf +
                                                                    dst[m]),
-              16, 0, 0);
+              16, 0, AUX);
       };
       // the rows this lane's fragments read: client 16t + (lane & 15), past
       // n the last client (never stored); the centre's own row
@@ -770,7 +778,7 @@ void gram_chunk_kernel(
                                                            st * kStage),
                 (__attribute__((address_space(3))) void *)(uintptr_t)(
                     buf + k * 2 * kStageRowBytes),
-                16, 0, 0);
+                16, 0, AUX);
         }
       };
       issue(0);
@@ -1745,19 +1753,27 @@ void gram_pass(const float *const *tab, int64_t ss, int n,
                          dim3(chunk_grid(pl, chunks)), dim3(kB8Waves * kWave),
                          0, st, tab, ss, n, pl.nt, pl.nlines, seg_lo, seg_end,
                          nseg, ctl, w, cap, centre, partial);
-    else
-      hipLaunchKernelGGL((gram_chunk_kernel<NT, CENTRED, true>),
+    else  // plane lines re-read tiles through L2: plain loads
+      hipLaunchKernelGGL((gram_chunk_kernel<NT, CENTRED, true, 0, 2, false,
+                                            false, 0>),
                          dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab,
                          ss, n, pl.nt, seg_lo, seg_end, nseg, ctl, w, cap,
                          centre, partial);
   } else if constexpr (NT > kFullTiles) {
     // NT > 4 (one workgroup per CU, up to 256 VGPRs + AGPRs): the full-tile
     // stages — the compact form spilled there (n = 100: 0.99 against
-    // 0.89 ms, profiles/r06/gram_stages_ab.jsonl)
-    hipLaunchKernelGGL((gram_chunk_kernel<NT, CENTRED, false>),
-                       dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab,
-                       ss, n, pl.nt, seg_lo, seg_end, nseg, ctl, w, cap,
-                       centre, partial);
+    // 0.89 ms, profiles/r06/gram_stages_ab.jsonl); stages 4: plain loads
+    if (g_compact.load(std::memory_order_relaxed) == 4)
+      hipLaunchKernelGGL((gram_chunk_kernel<NT, CENTRED, false, 0, 2, false,
+                                            false, 0>),
+                         dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab,
+                         ss, n, pl.nt, seg_lo, seg_end, nseg, ctl, w, cap,
+                         centre, partial);
+    else
+      hipLaunchKernelGGL((gram_chunk_kernel<NT, CENTRED, false>),
+                         dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab,
+                         ss, n, pl.nt, seg_lo, seg_end, nseg, ctl, w, cap,
+                         centre, partial);
   } else if (g_compact.load(std::memory_order_relaxed) == 0) {
     // A/B: the round-5 full-tile stages (16·NT rows + the centre), one in
     // flight
@@ -1776,6 +1792,19 @@ void gram_pass(const float *const *tab, int64_t ss, int n,
     else
       hipLaunchKernelGGL(
           (gram_chunk_kernel<NT, CENTRED, false, 8 * NT, 2, false, true>),
+          dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab, ss, n, pl.nt,
+          seg_lo, seg_end, nseg, ctl, w, cap, centre, partial);
+  } else if (g_compact.load(std::memory_order_relaxed) == 4) {
+    // A/B: the default compact stages with plain (temporal) loads
+    if ((n + 1) / 2 <= compact_maxi3<NT>())
+      hipLaunchKernelGGL(
+          (gram_chunk_kernel<NT, CENTRED, false, compact_maxi3<NT>(), 3,
+                             false, false, 0>),
+          dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab, ss, n, pl.nt,
+          seg_lo, seg_end, nseg, ctl, w, cap, centre, partial);
+    else
+      hipLaunchKernelGGL(
+          (gram_chunk_kernel<NT, CENTRED, false, 8 * NT, 2, false, false, 0>),
           dim3(chunk_grid(pl, chunks)), dim3(kBlk), 0, st, tab, ss, n, pl.nt,
           seg_lo, seg_end, nseg, ctl, w, cap, centre, partial);
   } else if (g_compact.load(std::memory_order_relaxed) == 2) {
@@ -1868,7 +1897,7 @@ extern "C" int fsagg_pairgram_set_fused(int on) {
 }
 
 extern "C" int fsagg_pairgram_set_stages(int mode) {
-  return g_compact.exchange(mode < 0 ? 1 : (mode > 3 ? 3 : mode));
+  return g_compact.exchange(mode < 0 ? 1 : (mode > 4 ? 4 : mode));
 }
 
 extern "C" int fsagg_pairgram_set_desync(int mode) {
@@ -1882,10 +1911,10 @@ extern "C" int fsagg_pairgram_set_chunks(int chunks) {
 
 extern "C" int64_t fsagg_pairgram_knobs(void) {
   return int64_t(g_block8.load(std::memory_order_relaxed) & 3) |
-         (int64_t(g_compact.load(std::memory_order_relaxed) & 3) << 2) |
-         (int64_t(g_fused.load(std::memory_order_relaxed) & 1) << 4) |
-         (int64_t(g_desync.load(std::memory_order_relaxed) & 0xffff) << 5) |
-         (int64_t(g_main_chunks.load(std::memory_order_relaxed)) << 21);
+         (int64_t(g_compact.load(std::memory_order_relaxed) & 7) << 2) |
+         (int64_t(g_fused.load(std::memory_order_relaxed) & 1) << 5) |
+         (int64_t(g_desync.load(std::memory_order_relaxed) & 0xffff) << 6) |
+         (int64_t(g_main_chunks.load(std::memory_order_relaxed)) << 22);
 }
 
 extern "C" int fsagg_pairgram_block8(void) {

@@ -525,7 +525,7 @@ int fsagg_pairgram_set_block8(int on);
  * launch chains, whose kernels it selects). */
 int fsagg_pairgram_block8(void);
 /* Every Gram workgroup-form setting above in one value (block8 | stages << 2
- * | fused << 4 | desync << 5 | chunks << 21): the key of a captured launch
+ * | fused << 5 | desync << 6 | chunks << 22): the key of a captured launch
  * chain, read in one call. */
 int64_t fsagg_pairgram_knobs(void);
 /* The chunk kernel's LDS stages (n <= 112 forms): 1 (default) compact —
@@ -534,7 +534,9 @@ int64_t fsagg_pairgram_knobs(void);
  * flight); 2 the compact stages with early release (a stage's buffer is
  * refilled once every wave has read its fragments, so every buffer's stage
  * is in flight under the compute); 3 the compact stages with each MFMA
- * cluster at s_setprio 1; < 0 restores the default.  Returns the
+ * cluster at s_setprio 1; 4 the default stages with plain loads instead
+ * of non-temporal ones (the full-tile forms above 64 clients too);
+ * < 0 restores the default.  Returns the
  * previous setting.  For A/B measurements; the results are identical. */
 int fsagg_pairgram_set_stages(int mode);
 /* The main pass's target chunk count for the n <= 112 forms (default 1024,

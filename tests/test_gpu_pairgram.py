@@ -217,13 +217,13 @@ def test_pairgram_compact_stages(n):
     lay, _, keyed, stacked = _sets(clients)
     lib = L.load()
     res = {}
-    for mode in (0, 1, 2, 3):
+    for mode in (0, 1, 2, 3, 4):
         prev = lib.fsagg_pairgram_set_stages(mode)
         try:
             res[mode] = [_gram(keyed), _gram(stacked)]
         finally:
             lib.fsagg_pairgram_set_stages(prev)
-    for m in (1, 2, 3):
+    for m in (1, 2, 3, 4):
         for a, b in zip(res[0], res[m]):
             for x, y in zip(a, b):
                 assert np.asarray(x).tobytes() == np.asarray(y).tobytes(), \

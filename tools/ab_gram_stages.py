@@ -52,7 +52,7 @@ def main():
             bufs[mode] = ops.pairgram_rows_dist(rs, _GRAM_TOL)[0].cpu().numpy()
         same = bufs[ma].tobytes() == bufs[mb].tobytes()
         res = {ma: [], mb: []}
-        for rnd in range(4):
+        for rnd in range(int(os.environ.get('ROUNDS', '4'))):
             for mode in ((ma, mb) if rnd % 2 == 0 else (mb, ma)):
                 setk(mode)
                 for _ in range(5):
