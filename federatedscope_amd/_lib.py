@@ -91,6 +91,14 @@ SIGNATURES['fsagg_delta_sqnorm_keys_f32'] = (
     _c_i, [_c_p, _c_i, _c_i64, _c_p, _c_p, _c_i, _c_p, _c_p, _c_sz, _c_p])
 SIGNATURES['fsagg_delta_wsum_keys_f32'] = (
     _c_i, [_c_p, _c_p, _c_i, _c_i64, _c_p, _c_p, _c_i, _c_p, _c_p])
+SIGNATURES['fsagg_delta_sqnorm_wsum_workspace_bytes'] = (
+    _c_sz, [_c_i, _c_i64, _c_i])
+SIGNATURES['fsagg_delta_sqnorm_wsum_f32'] = (
+    _c_i, [_c_p, _c_p, _c_i, _c_i64, _c_p, _c_p, _c_i, _c_p, _c_p, _c_p,
+           _c_sz, _c_p])
+SIGNATURES['fsagg_delta_sqnorm_wsum_keys_f32'] = (
+    _c_i, [_c_p, _c_p, _c_i, _c_i64, _c_p, _c_p, _c_i, _c_p, _c_p, _c_p,
+           _c_sz, _c_p])
 FSAGG_STACK_CHUNK = 2048
 SIGNATURES['fsagg_gather_rows_f32'] = (
     _c_i, [_c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i, _c_p])

@@ -94,19 +94,20 @@ def calc_blocal_dissim(last_model, local_updated_models):
     weights = np.asarray([tp[0] for tp in local_updated_models])
     weights = weights / np.sum(weights)
     kt = _in_place(last_model, local_updated_models)
+    # the norms and the global update in one read of the clients
     if kt is not None:
         table, base, keys = kt
         segs = table.offsets
-        sq = ops.delta_sqnorm_keys(table, base=base).cpu().numpy()
         g = torch.empty(table.numel, dtype=torch.float32, device=table.device)
-        ops.delta_wsum_keys(table, [float(w) for w in weights], base, g)
+        sq = ops.delta_sqnorm_wsum_keys(table, [float(w) for w in weights],
+                                        base, g).cpu().numpy()
     else:
         lay, st, last, keys = _staged(last_model, local_updated_models)
         rows = st.rows(list(range(n)))
         segs = lay.segments()
-        sq = ops.delta_sqnorm(rows, segs, base=last).cpu().numpy()
         g = torch.empty(lay.numel, dtype=torch.float32, device=last.device)
-        ops.delta_wsum(rows, [float(w) for w in weights], last, g)
+        sq = ops.delta_sqnorm_wsum(rows, [float(w) for w in weights], segs,
+                                   last, g).cpu().numpy()
     gsq = ops.delta_sqnorm(ops.RowTable.from_tensors([g]), segs)
     gsq = gsq.cpu().numpy()[0]
     out = dict()

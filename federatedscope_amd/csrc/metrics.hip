@@ -259,6 +259,108 @@ __global__ __launch_bounds__(kBlock) void delta_wsum_kernel(
     if (live[e]) out[p[e]] = acc[e];
 }
 
+
+// calc_blocal_dissim's two client passes in ONE read of the clients: the
+// per-row, per-key Σ fl32(x − b)² of delta_partial_kernel and the weighted
+// sum out[p] = Σ_i fl32(w_i · fl32(x_i[p] − b[p])) of delta_wsum_kernel
+// (rows in order from +0: `out` is bit-identical to it).  One wave per
+// chunk of kFuseChunk coordinates that never straddles a key; lane l holds
+// coordinates 4l + 256j (j < 4): 16 base values and 16 wsum accumulators in
+// registers.  The wave walks the rows in order with the next row's loads
+// issued before the current row's arithmetic (16-B non-temporal loads when
+// the row's chunk is whole and 16-B aligned, else guarded 4-B loads), and
+// leaves each row's fp64 chunk sum (the lanes' sums, then the wave sum) in
+// partial[chunk][row]; delta_final_kernel adds a key's chunks in order.
+constexpr int kFuseChunk = 1024;
+constexpr int kFuseE = kFuseChunk / kWave;  // 16 values per lane
+typedef float f4x __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int fuse_idx(int lane, int k) {
+  return 4 * lane + 256 * (k >> 2) + (k & 3);
+}
+
+__device__ __forceinline__ void fuse_load(const float *x, bool vec, int len,
+                                          int lane, float (&v)[kFuseE]) {
+  if (vec) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f4x q = gld_nt(reinterpret_cast<const f4x *>(x + 4 * lane + 256 * j));
+      v[4 * j] = q.x;
+      v[4 * j + 1] = q.y;
+      v[4 * j + 2] = q.z;
+      v[4 * j + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kFuseE; ++k) {
+      const int idx = fuse_idx(lane, k);
+      v[k] = idx < len ? gload(x + idx) : 0.0f;
+    }
+  }
+}
+
+template <bool KEYS>
+__global__ __launch_bounds__(kWave) void delta_fused_kernel(
+    const float *const *__restrict__ rows, const float *__restrict__ w, int n,
+    const float *__restrict__ base, const float *const *__restrict__ base_keys,
+    const int64_t *__restrict__ seg_off, int nseg,
+    const int *__restrict__ prefix, double *__restrict__ partial,
+    float *__restrict__ out) {
+  const int c = blockIdx.x;
+  const int total = prefix[nseg];
+  if (c >= total) return;
+  int lo = 0, hi = nseg;  // segment: largest s with prefix[s] <= c
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (prefix[mid] <= c) lo = mid;
+    else hi = mid;
+  }
+  const int64_t start = seg_off[lo] + int64_t(c - prefix[lo]) * kFuseChunk;
+  int64_t end = start + kFuseChunk;
+  if (end > seg_off[lo + 1]) end = seg_off[lo + 1];
+  const int len = int(end - start);
+  const int lane = threadIdx.x;
+  const float *b = base_at<KEYS>(base, base_keys, lo, seg_off, start);
+  float bv[kFuseE], acc[kFuseE], xn[kFuseE];
+#pragma unroll
+  for (int k = 0; k < kFuseE; ++k) {
+    const int idx = fuse_idx(lane, k);
+    bv[k] = (b && idx < len) ? gload(b + idx) : 0.0f;
+    acc[k] = 0.0f;
+  }
+  const bool whole = len == kFuseChunk;
+  {
+    const float *x = row_at<KEYS>(rows, 0, nseg, lo, seg_off, start);
+    fuse_load(x, whole && (reinterpret_cast<uintptr_t>(x) & 15) == 0, len,
+              lane, xn);
+  }
+  for (int i = 0; i < n; ++i) {
+    float xv[kFuseE];
+#pragma unroll
+    for (int k = 0; k < kFuseE; ++k) xv[k] = xn[k];
+    if (i + 1 < n) {
+      const float *x = row_at<KEYS>(rows, i + 1, nseg, lo, seg_off, start);
+      fuse_load(x, whole && (reinterpret_cast<uintptr_t>(x) & 15) == 0, len,
+                lane, xn);
+    }
+    const float wi = w[i];
+    double sq = 0.0;
+#pragma unroll
+    for (int k = 0; k < kFuseE; ++k) {
+      const float d = __fsub_rn(xv[k], bv[k]);
+      acc[k] = add_rn(acc[k], mul_rn(wi, d));
+      sq = __fma_rn(double(d), double(d), sq);
+    }
+    sq = wave_sum(sq);
+    if (lane == 0) partial[int64_t(c) * n + i] = sq;
+  }
+#pragma unroll
+  for (int k = 0; k < kFuseE; ++k) {
+    const int idx = fuse_idx(lane, k);
+    if (idx < len) out[start + idx] = acc[k];
+  }
+}
+
 }  // namespace
 }  // namespace fsagg
 
@@ -373,4 +475,80 @@ extern "C" int fsagg_delta_sqnorm_keys_f32(
   return delta_sqnorm("fsagg_delta_sqnorm_keys_f32", true, keys, n, numel,
                       nullptr, base_keys, seg_off, nseg, sq, workspace,
                       workspace_bytes, stream);
+}
+
+namespace {
+
+int64_t fused_max_chunks(int64_t numel, int nseg) {
+  return numel / kFuseChunk + nseg + 1;
+}
+
+int delta_fused(const char *what, bool keys, const float *const *rows,
+                const float *weights, int n, int64_t numel, const float *base,
+                const float *const *base_keys, const int64_t *seg_off,
+                int nseg, double *sq, float *out, void *workspace,
+                size_t workspace_bytes, fsagg_stream_t stream) {
+  if (!rows || !weights || !seg_off || !sq || !out || n < 1 || nseg < 1 ||
+      numel < 0 || (keys ? !base_keys : !base) ||
+      fused_max_chunks(numel, nseg) > (int64_t(1) << 30)) {
+    set_error("%s: invalid argument (n=%d nseg=%d)", what, n, nseg);
+    return FSAGG_EINVAL;
+  }
+  const size_t need = fsagg_delta_sqnorm_wsum_workspace_bytes(n, numel, nseg);
+  if (!workspace || workspace_bytes < need) {
+    set_error("%s: workspace %zu < %zu bytes", what, workspace_bytes, need);
+    return FSAGG_ESPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  const int64_t chunks = fused_max_chunks(numel, nseg);
+  int *prefix = static_cast<int *>(workspace);
+  double *partial = reinterpret_cast<double *>(
+      static_cast<char *>(workspace) + align256(sizeof(int) * size_t(nseg + 1)));
+  hipLaunchKernelGGL(delta_prefix_kernel, dim3(1), dim3(1), 0, s, seg_off,
+                     nseg, int64_t(kFuseChunk), prefix);
+  if (keys)
+    hipLaunchKernelGGL(delta_fused_kernel<true>, dim3(unsigned(chunks)),
+                       dim3(kWave), 0, s, rows, weights, n, nullptr,
+                       base_keys, seg_off, nseg, prefix, partial, out);
+  else
+    hipLaunchKernelGGL(delta_fused_kernel<false>, dim3(unsigned(chunks)),
+                       dim3(kWave), 0, s, rows, weights, n, base, nullptr,
+                       seg_off, nseg, prefix, partial, out);
+  const int64_t waves = int64_t(n) * nseg;
+  const int64_t per = kBlock / kWave;
+  hipLaunchKernelGGL(delta_final_kernel,
+                     dim3(unsigned((waves + per - 1) / per)), dim3(kBlock), 0,
+                     s, partial, prefix, nseg, n, sq);
+  return check_launch(what);
+}
+
+}  // namespace
+
+extern "C" size_t fsagg_delta_sqnorm_wsum_workspace_bytes(int n,
+                                                          int64_t numel,
+                                                          int nseg) {
+  if (n < 1 || nseg < 1 || numel < 0) return 0;
+  return align256(sizeof(int) * size_t(nseg + 1)) +
+         align256(sizeof(double) * size_t(fused_max_chunks(numel, nseg)) *
+                  size_t(n));
+}
+
+extern "C" int fsagg_delta_sqnorm_wsum_f32(
+    const float *const *rows, const float *weights, int n, int64_t numel,
+    const float *base, const int64_t *seg_off, int nseg, double *sq,
+    float *out, void *workspace, size_t workspace_bytes,
+    fsagg_stream_t stream) {
+  return delta_fused("fsagg_delta_sqnorm_wsum_f32", false, rows, weights, n,
+                     numel, base, nullptr, seg_off, nseg, sq, out, workspace,
+                     workspace_bytes, stream);
+}
+
+extern "C" int fsagg_delta_sqnorm_wsum_keys_f32(
+    const float *const *keys, const float *weights, int n, int64_t numel,
+    const float *const *base_keys, const int64_t *seg_off, int nseg,
+    double *sq, float *out, void *workspace, size_t workspace_bytes,
+    fsagg_stream_t stream) {
+  return delta_fused("fsagg_delta_sqnorm_wsum_keys_f32", true, keys, weights,
+                     n, numel, nullptr, base_keys, seg_off, nseg, sq, out,
+                     workspace, workspace_bytes, stream);
 }

@@ -716,6 +716,35 @@ def delta_wsum(rows, weights, base, out):
     return out
 
 
+def delta_sqnorm_wsum(rows, weights, seg_offsets, base, out,
+                      workspace=None):
+    """:func:`delta_sqnorm` and :func:`delta_wsum` in one read of the rows
+    (calc_blocal_dissim's two passes): returns sq [n][nseg] (fp64, within
+    ~1e-15 relative of delta_sqnorm's order) and fills ``out``
+    (bit-identical to delta_wsum)."""
+    offs = [int(o) for o in seg_offsets]
+    if offs[0] != 0 or offs[-1] != rows.numel or \
+            any(b < a for a, b in zip(offs, offs[1:])):
+        raise ValueError('segment offsets must rise from 0 to numel')
+    _check_out(base, rows.numel, rows.device, what='base', align=4)
+    _check_out(out, rows.numel, rows.device, align=4)
+    if len(weights) != rows.n:
+        raise ValueError('%d weights for %d rows' % (len(weights), rows.n))
+    nseg = len(offs) - 1
+    lib = L.load()
+    need = lib.fsagg_delta_sqnorm_wsum_workspace_bytes(rows.n, rows.numel,
+                                                       nseg)
+    ws = (workspace or _WS).get(rows.device, need)
+    seg = _h2d(offs, torch.int64, rows.device)
+    w = _fp32_dev(weights, rows.device)
+    sq = torch.empty((rows.n, nseg), dtype=torch.float64, device=rows.device)
+    L.check(lib.fsagg_delta_sqnorm_wsum_f32(
+        rows.ptr(), w.data_ptr(), rows.n, rows.numel, base.data_ptr(),
+        seg.data_ptr(), nseg, sq.data_ptr(), out.data_ptr(), ws.data_ptr(),
+        ws.numel(), _stream(rows.device)), 'fsagg_delta_sqnorm_wsum_f32')
+    return sq
+
+
 class KeyTable:
     """Per-client, per-key device tensors addressed in place: an n x nseg
     pointer table (entry [i][s] = client i's fp32 tensor for key s) plus the
@@ -790,6 +819,28 @@ def delta_sqnorm_keys(keys, base=None, workspace=None):
         None if btab is None else btab.data_ptr(), keys.seg.data_ptr(),
         keys.nseg, sq.data_ptr(), ws.data_ptr(), ws.numel(),
         _stream(keys.device)), 'fsagg_delta_sqnorm_keys_f32')
+    return sq
+
+
+def delta_sqnorm_wsum_keys(keys, weights, base, out, workspace=None):
+    """:func:`delta_sqnorm_wsum` over a :class:`KeyTable` (``base``: per-key
+    tensors; ``out`` flat)."""
+    _check_out(out, keys.numel, keys.device, align=4)
+    if len(weights) != keys.n:
+        raise ValueError('%d weights for %d rows' % (len(weights), keys.n))
+    lib = L.load()
+    need = lib.fsagg_delta_sqnorm_wsum_workspace_bytes(keys.n, keys.numel,
+                                                       keys.nseg)
+    ws = (workspace or _WS).get(keys.device, need)
+    btab = keys.base_table(base)
+    w = _fp32_dev(weights, keys.device)
+    sq = torch.empty((keys.n, keys.nseg), dtype=torch.float64,
+                     device=keys.device)
+    L.check(lib.fsagg_delta_sqnorm_wsum_keys_f32(
+        keys.table.data_ptr(), w.data_ptr(), keys.n, keys.numel,
+        btab.data_ptr(), keys.seg.data_ptr(), keys.nseg, sq.data_ptr(),
+        out.data_ptr(), ws.data_ptr(), ws.numel(), _stream(keys.device)),
+        'fsagg_delta_sqnorm_wsum_keys_f32')
     return sq
 
 

@@ -354,6 +354,33 @@ int fsagg_delta_wsum_keys_f32(const float *const *keys, const float *weights,
                               fsagg_stream_t stream);
 
 /*
+ * calc_blocal_dissim's two client passes in one read of the clients: sq as
+ * fsagg_delta_sqnorm_f32 (per-row, per-key Σ fl32(x − base)² in fp64; a
+ * different fp64 summation order, so within ~1e-15 relative of it, not
+ * bit-identical) and out as fsagg_delta_wsum_f32 (bit-identical).  base is
+ * required.  The _keys form takes the key tables of the two key-table
+ * passes above.  Workspace: fsagg_delta_sqnorm_wsum_workspace_bytes.
+ * Reference: metric_calculator.py:309-357 (one loop over the clients'
+ * `local − last` for the norms, another for the global update).
+ */
+size_t fsagg_delta_sqnorm_wsum_workspace_bytes(int n, int64_t numel,
+                                               int nseg);
+int fsagg_delta_sqnorm_wsum_f32(const float *const *rows,
+                                const float *weights, int n, int64_t numel,
+                                const float *base, const int64_t *seg_off,
+                                int nseg, double *sq, float *out,
+                                void *workspace, size_t workspace_bytes,
+                                fsagg_stream_t stream);
+int fsagg_delta_sqnorm_wsum_keys_f32(const float *const *keys,
+                                     const float *weights, int n,
+                                     int64_t numel,
+                                     const float *const *base_keys,
+                                     const int64_t *seg_off, int nseg,
+                                     double *sq, float *out, void *workspace,
+                                     size_t workspace_bytes,
+                                     fsagg_stream_t stream);
+
+/*
  * Stage device-resident client updates into the client stack in ONE launch
  * (the per-key copies of ClientStack.load for GPU-resident state_dicts;
  * federatedscope/core/workers/server.py:966-970 stores the dicts that the

@@ -290,6 +290,54 @@ def test_delta_keys_match_flat_odd_layouts():
     assert out_f.cpu().numpy().tobytes() == want.tobytes()
 
 
+@pytest.mark.parametrize('shift', [0, 1])
+@pytest.mark.parametrize('n', [1, 13])
+def test_delta_sqnorm_wsum_fused(n, shift):
+    """calc_blocal_dissim's fused pass (one read of the clients): the global
+    update is bit-identical to delta_wsum, the norms agree with
+    delta_sqnorm to fp64 summation order, and the key-table and flat forms
+    agree bit for bit — on whole 16-B-aligned chunks (shift 0), rows one
+    element off alignment (shift 1: the guarded loads), chunk tails, empty
+    and single-element keys."""
+    from federatedscope_amd import ops
+    g = torch.Generator(device='cuda').manual_seed(11 + n + shift)
+    sizes = [1, 0, 1023, 5, 300_001, 0, 7, 65_537, 4096, 1024 * 37]
+    pool = torch.randn(n * (sum(sizes) + 8 * len(sizes)) + 8, device='cuda',
+                       generator=g)
+    clients, flat, off = [], [], shift
+    for i in range(n):
+        row = []
+        for sz in sizes:
+            row.append(pool[off:off + sz])
+            off += (sz + 3) // 4 * 4 + 4      # keys 16-B aligned + shift
+            assert row[-1].numel() == sz
+        clients.append(row)
+        flat.append(torch.cat(row))
+    base = [torch.randn(sz, device='cuda', generator=g) for sz in sizes]
+    kt = ops.KeyTable(clients, 'cuda')
+    rows = ops.RowTable.from_tensors(flat)
+    bflat = torch.cat(base)
+    w = [float(x) for x in np.random.default_rng(n).random(n)]
+    want_sq = ops.delta_sqnorm(rows, kt.offsets, base=bflat)
+    want_g = torch.empty(kt.numel, device='cuda')
+    ops.delta_wsum(rows, w, bflat, want_g)
+    out_k = torch.full((kt.numel, ), 7.0, device='cuda')
+    out_f = torch.full((kt.numel, ), 7.0, device='cuda')
+    sq_k = ops.delta_sqnorm_wsum_keys(kt, w, base, out_k)
+    sq_f = ops.delta_sqnorm_wsum(rows, w, kt.offsets, bflat, out_f)
+    assert torch.equal(out_k, want_g) and torch.equal(out_f, want_g)
+    assert torch.equal(sq_k, sq_f)
+    torch.testing.assert_close(sq_f, want_sq, rtol=1e-13, atol=0.0)
+    # fp64 norms against a float64 numpy restatement of fl32(x − b)²
+    x = torch.stack(flat).cpu().numpy()
+    d = (x - bflat.cpu().numpy()).astype(np.float64)
+    ref = np.add.reduceat(d * d, kt.offsets[:-1], axis=1)
+    for s, sz in enumerate(sizes):      # reduceat gives d[off] for empties
+        if sz == 0:
+            ref[:, s] = 0.0
+    np.testing.assert_allclose(sq_f.cpu().numpy(), ref, rtol=1e-12)
+
+
 def test_wire_unpack_skips_malformed_segments():
     """The segment table is device data: segments that overrun the packed
     input or the row, or name an unknown kind / scale, are skipped on the

@@ -175,6 +175,35 @@ def dissim_leg(n=100, P=6_000_000):
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         out[name + '_ms'] = round(min(ts) * 1e3, 2)
+    # kernels alone (HIP events): the fused B-local pass against the two
+    # passes it replaces, on the same key table
+    from federatedscope_amd import ops
+    kt = ops.KeyTable([list(m.values()) for _, m in clients], dev)
+    base = list(last.values())
+    w = [1.0 / n] * n
+    gbuf = torch.empty(kt.numel, device=dev)
+
+    def two_pass():
+        ops.delta_sqnorm_keys(kt, base=base)
+        ops.delta_wsum_keys(kt, w, base, gbuf)
+
+    def fused():
+        ops.delta_sqnorm_wsum_keys(kt, w, base, gbuf)
+    for name, fn in (('blocal_two_pass_kernels', two_pass),
+                     ('blocal_fused_kernels', fused),
+                     ('blocal_two_pass_kernels', two_pass),
+                     ('blocal_fused_kernels', fused)):
+        fn()
+        ts = []
+        for _ in range(10):
+            e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        out[name + '_ms'] = round(min(out.get(name + '_ms', 1e9),
+                                      sorted(ts)[len(ts) // 2]), 3)
     return dict(leg='dissim', clients=n, params=P, **out,
                 what='device-resident client dicts read in place (ops.KeyTable) + metric kernels')
 
