@@ -266,10 +266,11 @@ __global__ __launch_bounds__(kBlock) void delta_wsum_kernel(
 // (rows in order from +0: `out` is bit-identical to it).  One wave per
 // chunk of kFuseChunk coordinates that never straddles a key; lane l holds
 // coordinates 4l + 256j (j < 4): 16 base values and 16 wsum accumulators in
-// registers.  The wave walks the rows in order with the next row's loads
-// issued before the current row's arithmetic (16-B non-temporal loads when
-// the row's chunk is whole and 16-B aligned, else guarded 4-B loads), and
-// leaves each row's fp64 chunk sum (the lanes' sums, then the wave sum) in
+// registers.  The wave walks the rows in order: when the chunk is whole
+// and every row's piece 16-B aligned, three rows' 16-B non-temporal loads
+// stay in flight (fuse_rows_vec); else the next row's loads (16-B where
+// that row allows, guarded 4-B otherwise) are issued before the current
+// row's arithmetic.  It leaves each row's fp64 chunk sum (the lanes' sums, then the wave sum) in
 // partial[chunk][row]; delta_final_kernel adds a key's chunks in order.
 constexpr int kFuseChunk = 1024;
 constexpr int kFuseE = kFuseChunk / kWave;  // 16 values per lane
@@ -297,6 +298,76 @@ __device__ __forceinline__ void fuse_load(const float *x, bool vec, int len,
       v[k] = idx < len ? gload(x + idx) : 0.0f;
     }
   }
+}
+
+// One row of the fused pass: d = x − b into the wsum accumulators and the
+// row's fp64 sum of squares (wave sum) into part[i].
+__device__ __forceinline__ void fuse_row(const float (&xv)[kFuseE],
+                                         const float (&bv)[kFuseE], float wi,
+                                         float (&acc)[kFuseE], int lane,
+                                         double *part) {
+  double sq = 0.0;
+#pragma unroll
+  for (int k = 0; k < kFuseE; ++k) {
+    const float d = __fsub_rn(xv[k], bv[k]);
+    acc[k] = add_rn(acc[k], mul_rn(wi, d));
+    sq = __fma_rn(double(d), double(d), sq);
+  }
+  sq = wave_sum(sq);
+  // lane 0's total, stored by every lane (one address): no exec-masked
+  // store whose skip would blur the compiler's load counts
+  const uint64_t t = __double_as_longlong(sq);
+  const uint32_t tlo = __builtin_amdgcn_readfirstlane(uint32_t(t));
+  const uint32_t thi = __builtin_amdgcn_readfirstlane(uint32_t(t >> 32));
+  *part = __longlong_as_double(int64_t(uint64_t(tlo) | (uint64_t(thi) << 32)));
+}
+
+__device__ __forceinline__ void fuse_vec(const float *x, int lane,
+                                         float (&v)[kFuseE]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f4x q = gld_nt(reinterpret_cast<const f4x *>(x + 4 * lane + 256 * j));
+    v[4 * j] = q.x;
+    v[4 * j + 1] = q.y;
+    v[4 * j + 2] = q.z;
+    v[4 * j + 3] = q.w;
+  }
+}
+
+// Whole, aligned chunks: three rows' 16-B loads in flight while a row is
+// summed (buffers A, B, C in rotation).
+template <bool KEYS>
+__device__ __forceinline__ void fuse_rows_vec(
+    const float *const *__restrict__ rows, const float *__restrict__ w,
+    int n, int nseg, int lo, const int64_t *__restrict__ seg_off,
+    int64_t start, int lane, const float (&bv)[kFuseE],
+    float (&acc)[kFuseE], double *part) {
+  auto rp = [&](int i) {
+    return row_at<KEYS>(rows, i, nseg, lo, seg_off, start);
+  };
+  float xa[kFuseE], xb[kFuseE], xc[kFuseE];
+  fuse_vec(rp(0), lane, xa);
+  if (n > 1) fuse_vec(rp(1), lane, xb);
+  if (n > 2) fuse_vec(rp(2), lane, xc);
+  // steady state without branches (the compiler's load counts stay exact:
+  // a row's wait leaves the two later rows' loads in flight)
+  int i = 0;
+  for (; i + 5 < n; i += 3) {
+    fuse_row(xa, bv, w[i], acc, lane, part + i);
+    fuse_vec(rp(i + 3), lane, xa);
+    fuse_row(xb, bv, w[i + 1], acc, lane, part + i + 1);
+    fuse_vec(rp(i + 4), lane, xb);
+    fuse_row(xc, bv, w[i + 2], acc, lane, part + i + 2);
+    fuse_vec(rp(i + 5), lane, xc);
+  }
+  // the last <= 5 rows: i, i + 1, i + 2 are loaded (those < n)
+  if (i < n) fuse_row(xa, bv, w[i], acc, lane, part + i);
+  if (i + 3 < n) fuse_vec(rp(i + 3), lane, xa);
+  if (i + 1 < n) fuse_row(xb, bv, w[i + 1], acc, lane, part + i + 1);
+  if (i + 4 < n) fuse_vec(rp(i + 4), lane, xb);
+  if (i + 2 < n) fuse_row(xc, bv, w[i + 2], acc, lane, part + i + 2);
+  if (i + 3 < n) fuse_row(xa, bv, w[i + 3], acc, lane, part + i + 3);
+  if (i + 4 < n) fuse_row(xb, bv, w[i + 4], acc, lane, part + i + 4);
 }
 
 template <bool KEYS>
@@ -329,6 +400,17 @@ __global__ __launch_bounds__(kWave) void delta_fused_kernel(
     acc[k] = 0.0f;
   }
   const bool whole = len == kFuseChunk;
+  // every row's chunk whole and 16-B aligned (the lanes check the rows'
+  // pointers, then a ballot): the three-deep pipeline of 16-B loads
+  bool odd = false;
+  if (whole)
+    for (int i = lane; i < n; i += kWave)
+      odd |= (reinterpret_cast<uintptr_t>(
+                  row_at<KEYS>(rows, i, nseg, lo, seg_off, start)) & 15) != 0;
+  if (whole && !__any(odd)) {
+    fuse_rows_vec<KEYS>(rows, w, n, nseg, lo, seg_off, start, lane, bv, acc,
+                        partial + int64_t(c) * n);
+  } else {
   {
     const float *x = row_at<KEYS>(rows, 0, nseg, lo, seg_off, start);
     fuse_load(x, whole && (reinterpret_cast<uintptr_t>(x) & 15) == 0, len,
@@ -353,6 +435,7 @@ __global__ __launch_bounds__(kWave) void delta_fused_kernel(
     }
     sq = wave_sum(sq);
     if (lane == 0) partial[int64_t(c) * n + i] = sq;
+  }
   }
 #pragma unroll
   for (int k = 0; k < kFuseE; ++k) {
