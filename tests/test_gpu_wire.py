@@ -291,7 +291,7 @@ def test_delta_keys_match_flat_odd_layouts():
 
 
 @pytest.mark.parametrize('shift', [0, 1])
-@pytest.mark.parametrize('n', [1, 13])
+@pytest.mark.parametrize('n', [1, 2, 4, 5, 6, 13])
 def test_delta_sqnorm_wsum_fused(n, shift):
     """calc_blocal_dissim's fused pass (one read of the clients): the global
     update is bit-identical to delta_wsum, the norms agree with
