@@ -23,7 +23,7 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kPerThread = 4;
 // share rows loaded together (8 measured the same, 16 7 % slower)
-constexpr int kSsRows = 4;
+constexpr int kSsRows = 8;
 
 struct WireSeg {
   int64_t src;  // byte offset of the segment in the packed upload
@@ -192,16 +192,18 @@ __device__ __forceinline__ double py_mod(double a, double b) {
 typedef long long ll2v __attribute__((ext_vector_type(2)));
 typedef double d2v __attribute__((ext_vector_type(2)));
 
-// Two consecutive elements per lane (16-B loads of every share row), rows
-// taken four at a time so their loads are in flight together; the adds
-// stay in list order.
+// Two consecutive elements per lane (16-B non-temporal loads of every share
+// row), rows taken eight at a time so their loads are in flight together;
+// the adds stay in list order.  100 × 6M int64 shares: 0.786 ms against
+// 0.833–0.844 for four rows and plain loads (profiles/r06/ss_rows8_nt.jsonl;
+// sixteen rows 0.878, rejected/ss_rows16_nt.jsonl).
 __device__ __forceinline__ void ss_load2(const void *row, bool is_int,
                                          int64_t p, bool two, double &x0,
                                          double &x1) {
   if (is_int) {
     const int64_t *r = static_cast<const int64_t *>(row) + p;
     if (two) {
-      const ll2v v = gld(reinterpret_cast<const ll2v *>(r));
+      const ll2v v = gld_nt(reinterpret_cast<const ll2v *>(r));
       x0 = __ll2double_rn(v.x);
       x1 = __ll2double_rn(v.y);
     } else {
@@ -211,7 +213,7 @@ __device__ __forceinline__ void ss_load2(const void *row, bool is_int,
   } else {
     const double *r = static_cast<const double *>(row) + p;
     if (two) {
-      const d2v v = gld(reinterpret_cast<const d2v *>(r));
+      const d2v v = gld_nt(reinterpret_cast<const d2v *>(r));
       x0 = v.x;
       x1 = v.y;
     } else {
